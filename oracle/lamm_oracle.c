@@ -1,0 +1,511 @@
+/*
+ * lamm_oracle.c -- TEST INFRASTRUCTURE ONLY (the parity checker, never the thing
+ * measured or shipped).  Plain-C restatement of the reference arithmetic on the
+ * lamm_* mul_mat path:
+ *
+ *   * block formats            LC/ggml-common.h:144-225, 316-321
+ *   * weight quantizers        LC/ggml-quants.c:1002-1180 (q4_0..q5_1 *_reference,
+ *                              reached via ggml_quantize_chunk with imatrix==NULL,
+ *                              :3569-3583), :1182-1205 (q8_0), :2039-2114 (q2_K,
+ *                              with make_qkx2_quants :1945-2029, nearest_int :1767)
+ *   * activation quantizers    q8_0 :1182-1205 (ref) / :1280-1330 (AVX2 from_float),
+ *                              q8_1 :1396-1429 (ref) / :1505-1575 (AVX2),
+ *                              q8_K :3981-4018
+ *   * scalar vec_dot           q4_0 :4451-4469, q4_1 :4700-4718, q5_0 :4985-5008,
+ *                              q5_1 :5290-5313, q8_0 :5300-5313, q2_K :5820-5860,
+ *                              f32 LC/ggml.c:1576-1581 (double accumulation)
+ *   * mul_mat semantics        src/lamm_kernel_q4_0.hpp:21-37 (C[j*ldc+i], K blocks),
+ *                              computing ALL M rows (not inheriting SURVEY §8a defect 1)
+ *
+ * Floating-point expressions are written in the reference's evaluation order and
+ * compiled with -ffp-contract=off, so the results are bit-identical to a scalar
+ * (-march=x86-64) build of ggml: tests/test_oracle_golden.py checks exactly that.
+ */
+#include "lamm_oracle.h"
+
+#include <float.h>
+#include <math.h>
+#include <string.h>
+
+/* ---------------------------------------------------------------- fp16 */
+
+static inline uint32_t f2u(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
+static inline float u2f(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
+
+float lo_fp16_to_fp32(uint16_t h) {
+  const uint32_t sign = (uint32_t)(h & 0x8000u) << 16;
+  const uint32_t e = (h >> 10) & 0x1f, m = h & 0x3ffu;
+  if (e == 0) {                       /* zero / subnormal: m * 2^-24, exact */
+    float v = (float)m * 5.9604644775390625e-08f;
+    return u2f(f2u(v) | sign);
+  }
+  if (e == 31) return u2f(sign | 0x7f800000u | (m << 13));
+  return u2f(sign | ((e + 112u) << 23) | (m << 13));
+}
+
+uint16_t lo_fp32_to_fp16(float f) {   /* IEEE round-to-nearest-even */
+  uint32_t x = f2u(f);
+  const uint16_t sign = (uint16_t)((x >> 16) & 0x8000u);
+  uint32_t ax = x & 0x7fffffffu;
+  if (ax >= 0x7f800000u) return sign | (ax > 0x7f800000u ? 0x7e00u : 0x7c00u);
+  if (ax >= 0x477ff000u) return sign | 0x7c00u;           /* >= 65520 -> inf */
+  if (ax < 0x38800000u) {                                  /* below 2^-14 */
+    float r = rintf(u2f(ax) * 16777216.0f);                /* exact scale, RNE */
+    return sign | (uint16_t)r;
+  }
+  ax += 0xc8000fffu + ((ax >> 13) & 1u);                   /* rebias + RNE */
+  return sign | (uint16_t)(ax >> 13);
+}
+
+#define H2F(h) lo_fp16_to_fp32(h)
+#define F2H(f) lo_fp32_to_fp16(f)
+
+/* ------------------------------------------------------------ layout */
+
+int lo_block_elems(int t) {
+  switch (t) {
+  case LO_F32: return 1;
+  case LO_Q2_K: case LO_Q8_K: return 256;
+  default: return 32;
+  }
+}
+
+size_t lo_block_bytes(int t) {
+  switch (t) {
+  case LO_F32: return 4;
+  case LO_Q4_0: return 18;
+  case LO_Q4_1: return 20;
+  case LO_Q5_0: return 22;
+  case LO_Q5_1: return 24;
+  case LO_Q8_0: return 34;
+  case LO_Q8_1: return 36;
+  case LO_Q2_K: return 84;
+  case LO_Q8_K: return 292;
+  default: return 0;
+  }
+}
+
+int lo_vec_dot_type(int t) {
+  switch (t) {
+  case LO_F32: return LO_F32;
+  case LO_Q4_0: case LO_Q5_0: case LO_Q8_0: return LO_Q8_0;
+  case LO_Q4_1: case LO_Q5_1: return LO_Q8_1;
+  case LO_Q2_K: return LO_Q8_K;
+  default: return -1;
+  }
+}
+
+size_t lo_row_bytes(int t, int k) { return (size_t)(k / lo_block_elems(t)) * lo_block_bytes(t); }
+
+static inline uint16_t rd16(const uint8_t *p) { uint16_t v; memcpy(&v, p, 2); return v; }
+static inline void wr16(uint8_t *p, uint16_t v) { memcpy(p, &v, 2); }
+
+/* ------------------------------------------------------- quantizers */
+
+/* first element of largest magnitude, as the reference scans (strict <) */
+static void absmax_signed(const float *x, int n, float *amax, float *vmax) {
+  float a = 0.0f, m = 0.0f;
+  for (int j = 0; j < n; j++) {
+    if (a < fabsf(x[j])) { a = fabsf(x[j]); m = x[j]; }
+  }
+  *amax = a; *vmax = m;
+}
+
+static void minmax(const float *x, int n, float *mn, float *mx) {
+  float lo = FLT_MAX, hi = -FLT_MAX;
+  for (int j = 0; j < n; j++) {
+    if (x[j] < lo) lo = x[j];
+    if (x[j] > hi) hi = x[j];
+  }
+  *mn = lo; *mx = hi;
+}
+
+/* q4_0 / q5_0 : symmetric, d = max / -(2^(bits-1)) */
+static void quant_sym(const float *x, uint8_t *blk, int bits) {
+  float amax, vmax;
+  absmax_signed(x, 32, &amax, &vmax);
+  const float d = vmax / (bits == 4 ? -8 : -16);
+  const float id = d ? 1.0f / d : 0.0f;
+  wr16(blk, F2H(d));
+  uint32_t qh = 0;
+  uint8_t *qs = blk + (bits == 4 ? 2 : 6);
+  for (int j = 0; j < 16; j++) {
+    const float x0 = x[j] * id, x1 = x[16 + j] * id;
+    uint8_t v0, v1;
+    if (bits == 4) {
+      v0 = (uint8_t)((int8_t)(x0 + 8.5f)); if (v0 > 15) v0 = 15;
+      v1 = (uint8_t)((int8_t)(x1 + 8.5f)); if (v1 > 15) v1 = 15;
+    } else {
+      v0 = (uint8_t)((int8_t)(x0 + 16.5f)); if (v0 > 31) v0 = 31;
+      v1 = (uint8_t)((int8_t)(x1 + 16.5f)); if (v1 > 31) v1 = 31;
+      qh |= (uint32_t)((v0 >> 4) & 1) << j;
+      qh |= (uint32_t)((v1 >> 4) & 1) << (j + 16);
+    }
+    qs[j] = (uint8_t)((v0 & 0x0f) | ((v1 & 0x0f) << 4));
+  }
+  if (bits == 5) memcpy(blk + 2, &qh, 4);
+}
+
+/* q4_1 / q5_1 : affine, d = (max - min) / (2^bits - 1), m = min */
+static void quant_affine(const float *x, uint8_t *blk, int bits) {
+  float mn, mx;
+  minmax(x, 32, &mn, &mx);
+  const float d = (mx - mn) / ((1 << bits) - 1);
+  const float id = d ? 1.0f / d : 0.0f;
+  wr16(blk, F2H(d));
+  wr16(blk + 2, F2H(mn));
+  uint32_t qh = 0;
+  uint8_t *qs = blk + (bits == 4 ? 4 : 8);
+  for (int j = 0; j < 16; j++) {
+    const float x0 = (x[j] - mn) * id, x1 = (x[16 + j] - mn) * id;
+    uint8_t v0, v1;
+    if (bits == 4) {
+      v0 = (uint8_t)((int8_t)(x0 + 0.5f)); if (v0 > 15) v0 = 15;
+      v1 = (uint8_t)((int8_t)(x1 + 0.5f)); if (v1 > 15) v1 = 15;
+    } else {                            /* q5_1 reference has no clamp */
+      v0 = (uint8_t)(x0 + 0.5f);
+      v1 = (uint8_t)(x1 + 0.5f);
+      qh |= (uint32_t)((v0 >> 4) & 1) << j;
+      qh |= (uint32_t)((v1 >> 4) & 1) << (j + 16);
+    }
+    qs[j] = (uint8_t)((v0 & 0x0f) | ((v1 & 0x0f) << 4));
+  }
+  if (bits == 5) memcpy(blk + 4, &qh, 4);
+}
+
+/* q8_0 / q8_1 activations.  with_sum selects q8_1 (stores s = d*sum(q)). */
+static void quant_q8(const float *x, uint8_t *blk, int flavour, int with_sum) {
+  float amax = 0.0f;
+  for (int j = 0; j < 32; j++) amax = fmaxf(amax, fabsf(x[j]));
+  int8_t *qs = (int8_t *)(blk + (with_sum ? 4 : 2));
+  float d;
+  int sum = 0;
+  if (flavour == LO_QUANT_AVX) {
+    d = amax / 127.f;
+    const float id = (amax != 0.0f) ? 127.f / amax : 0.0f;
+    for (int j = 0; j < 32; j++) {
+      int v = (int)rintf(x[j] * id);     /* _mm256_round_ps(_MM_ROUND_NEAREST) */
+      if (v > 127) v = 127;              /* packs saturation */
+      if (v < -128) v = -128;
+      qs[j] = (int8_t)v;
+      sum += v;
+    }
+  } else {
+    d = amax / ((1 << 7) - 1);
+    const float id = d ? 1.0f / d : 0.0f;
+    for (int j = 0; j < 32; j++) {
+      qs[j] = (int8_t)roundf(x[j] * id);
+      sum += qs[j];
+    }
+  }
+  wr16(blk, F2H(d));
+  if (with_sum) wr16(blk + 2, F2H(sum * d));
+}
+
+static inline int nearest_int(float f) {
+  float v = f + 12582912.f;
+  int i; memcpy(&i, &v, 4);
+  return (i & 0x007fffff) - 0x00400000;
+}
+
+/* affine fit of n values to [0,nmax] minimising weighted |err| (use_mad) */
+static float fit_affine(int n, int nmax, const float *x, const float *w, uint8_t *L,
+                        float *the_min, uint8_t *Laux, float rmin, float rdelta,
+                        int nstep, int use_mad) {
+  float mn = x[0], mx = x[0];
+  float sum_w = w[0], sum_x = sum_w * x[0];
+  for (int i = 1; i < n; ++i) {
+    if (x[i] < mn) mn = x[i];
+    if (x[i] > mx) mx = x[i];
+    sum_w += w[i];
+    sum_x += w[i] * x[i];
+  }
+  if (mn > 0) mn = 0;
+  if (mx == mn) {
+    for (int i = 0; i < n; ++i) L[i] = 0;
+    *the_min = -mn;
+    return 0.f;
+  }
+  float iscale = nmax / (mx - mn);
+  float scale = 1 / iscale;
+  float best = 0;
+  for (int i = 0; i < n; ++i) {
+    int l = nearest_int(iscale * (x[i] - mn));
+    l = l < 0 ? 0 : (l > nmax ? nmax : l);
+    L[i] = (uint8_t)l;
+    float diff = scale * L[i] + mn - x[i];
+    diff = use_mad ? fabsf(diff) : diff * diff;
+    best += w[i] * diff;
+  }
+  if (nstep < 1) { *the_min = -mn; return scale; }
+  for (int is = 0; is <= nstep; ++is) {
+    iscale = (rmin + rdelta * is + nmax) / (mx - mn);
+    float sum_l = 0, sum_l2 = 0, sum_xl = 0;
+    for (int i = 0; i < n; ++i) {
+      int l = nearest_int(iscale * (x[i] - mn));
+      l = l < 0 ? 0 : (l > nmax ? nmax : l);
+      Laux[i] = (uint8_t)l;
+      sum_l += w[i] * l;
+      sum_l2 += w[i] * l * l;
+      sum_xl += w[i] * l * x[i];
+    }
+    float D = sum_w * sum_l2 - sum_l * sum_l;
+    if (D > 0) {
+      float this_scale = (sum_w * sum_xl - sum_x * sum_l) / D;
+      float this_min = (sum_l2 * sum_x - sum_l * sum_xl) / D;
+      if (this_min > 0) { this_min = 0; this_scale = sum_xl / sum_l2; }
+      float mad = 0;
+      for (int i = 0; i < n; ++i) {
+        float diff = this_scale * Laux[i] + this_min - x[i];
+        diff = use_mad ? fabsf(diff) : diff * diff;
+        mad += w[i] * diff;
+      }
+      if (mad < best) {
+        for (int i = 0; i < n; ++i) L[i] = Laux[i];
+        best = mad;
+        scale = this_scale;
+        mn = this_min;
+      }
+    }
+  }
+  *the_min = -mn;
+  return scale;
+}
+
+/* block_q2_K: scales[16] | qs[64] | d | dmin  (LC/ggml-common.h:199-209) */
+static void quant_q2_K(const float *x, uint8_t *blk) {
+  uint8_t L[256], Laux[16];
+  float w[16], mins[16], scales[16];
+  uint8_t *sc = blk, *qs = blk + 16;
+  float max_scale = 0, max_min = 0;
+  for (int j = 0; j < 16; ++j) {
+    for (int l = 0; l < 16; ++l) w[l] = fabsf(x[16 * j + l]);
+    scales[j] = fit_affine(16, 3, x + 16 * j, w, L + 16 * j, &mins[j], Laux, -0.5f, 0.1f, 15, 1);
+    if (scales[j] > max_scale) max_scale = scales[j];
+    if (mins[j] > max_min) max_min = mins[j];
+  }
+  if (max_scale > 0) {
+    float iscale = 15.f / max_scale;
+    for (int j = 0; j < 16; ++j) sc[j] = (uint8_t)nearest_int(iscale * scales[j]);
+    wr16(blk + 80, F2H(max_scale / 15.f));
+  } else {
+    for (int j = 0; j < 16; ++j) sc[j] = 0;
+    wr16(blk + 80, F2H(0.f));
+  }
+  if (max_min > 0) {
+    float iscale = 15.f / max_min;
+    for (int j = 0; j < 16; ++j) sc[j] |= (uint8_t)(nearest_int(iscale * mins[j]) << 4);
+    wr16(blk + 82, F2H(max_min / 15.f));
+  } else {
+    wr16(blk + 82, F2H(0.f));
+  }
+  for (int j = 0; j < 16; ++j) {
+    const float d = H2F(rd16(blk + 80)) * (sc[j] & 0xF);
+    if (!d) continue;
+    const float dm = H2F(rd16(blk + 82)) * (sc[j] >> 4);
+    for (int ii = 0; ii < 16; ++ii) {
+      int l = nearest_int((x[16 * j + ii] + dm) / d);
+      L[16 * j + ii] = (uint8_t)(l < 0 ? 0 : (l > 3 ? 3 : l));
+    }
+  }
+  for (int j = 0; j < 256; j += 128)
+    for (int l = 0; l < 32; ++l)
+      qs[j / 4 + l] = (uint8_t)(L[j + l] | (L[j + l + 32] << 2) | (L[j + l + 64] << 4) | (L[j + l + 96] << 6));
+}
+
+/* block_q8_K: f32 d | i8 qs[256] | i16 bsums[16] */
+static void quant_q8_K(const float *x, uint8_t *blk) {
+  float amax = 0, vmax = 0;
+  for (int j = 0; j < 256; ++j) {
+    float ax = fabsf(x[j]);
+    if (ax > amax) { amax = ax; vmax = x[j]; }
+  }
+  int8_t *qs = (int8_t *)(blk + 4);
+  if (!amax) {
+    float z = 0; memcpy(blk, &z, 4);
+    memset(qs, 0, 256);
+    memset(blk + 260, 0, 32);
+    return;
+  }
+  const float iscale = -127.f / vmax;
+  for (int j = 0; j < 256; ++j) {
+    int v = nearest_int(iscale * x[j]);
+    qs[j] = (int8_t)(v < 127 ? v : 127);
+  }
+  for (int j = 0; j < 16; ++j) {
+    int s = 0;
+    for (int i = 0; i < 16; ++i) s += qs[16 * j + i];
+    int16_t s16 = (int16_t)s;
+    memcpy(blk + 260 + 2 * j, &s16, 2);
+  }
+  float d = 1 / iscale;
+  memcpy(blk, &d, 4);
+}
+
+void lo_quantize_row(int type, int flavour, const float *x, void *y, int k) {
+  const int qk = lo_block_elems(type);
+  const size_t bb = lo_block_bytes(type);
+  uint8_t *out = (uint8_t *)y;
+  if (type == LO_F32) { memcpy(y, x, (size_t)k * 4); return; }
+  for (int b = 0; b < k / qk; b++) {
+    const float *xb = x + (size_t)b * qk;
+    uint8_t *yb = out + (size_t)b * bb;
+    switch (type) {
+    case LO_Q4_0: quant_sym(xb, yb, 4); break;
+    case LO_Q5_0: quant_sym(xb, yb, 5); break;
+    case LO_Q4_1: quant_affine(xb, yb, 4); break;
+    case LO_Q5_1: quant_affine(xb, yb, 5); break;
+    case LO_Q8_0: quant_q8(xb, yb, flavour, 0); break;
+    case LO_Q8_1: quant_q8(xb, yb, flavour, 1); break;
+    case LO_Q2_K: quant_q2_K(xb, yb); break;
+    case LO_Q8_K: quant_q8_K(xb, yb); break;
+    default: break;
+    }
+  }
+}
+
+/* --------------------------------------------------------- dequant */
+
+void lo_dequantize_row(int type, const void *vx, float *y, int k) {
+  const uint8_t *x = (const uint8_t *)vx;
+  const int qk = lo_block_elems(type);
+  const size_t bb = lo_block_bytes(type);
+  if (type == LO_F32) { memcpy(y, vx, (size_t)k * 4); return; }
+  for (int b = 0; b < k / qk; b++, x += bb, y += qk) {
+    switch (type) {
+    case LO_Q4_0: case LO_Q5_0: case LO_Q4_1: case LO_Q5_1: {
+      const int aff = (type == LO_Q4_1 || type == LO_Q5_1);
+      const int five = (type == LO_Q5_0 || type == LO_Q5_1);
+      const float d = H2F(rd16(x)), m = aff ? H2F(rd16(x + 2)) : 0.f;
+      uint32_t qh = 0;
+      if (five) memcpy(&qh, x + (aff ? 4 : 2), 4);
+      const uint8_t *qs = x + (aff ? 4 : 2) + (five ? 4 : 0);
+      for (int j = 0; j < 32; j++) {
+        int q = (j < 16) ? (qs[j] & 0xF) : (qs[j - 16] >> 4);
+        if (five) q |= ((qh >> j) & 1) << 4;
+        if (!aff) q -= five ? 16 : 8;
+        y[j] = aff ? d * q + m : d * q;
+      }
+    } break;
+    case LO_Q8_0: case LO_Q8_1: {
+      const float d = H2F(rd16(x));
+      const int8_t *qs = (const int8_t *)(x + (type == LO_Q8_1 ? 4 : 2));
+      for (int j = 0; j < 32; j++) y[j] = d * qs[j];
+    } break;
+    case LO_Q2_K: {
+      const float d = H2F(rd16(x + 80)), dmin = H2F(rd16(x + 82));
+      for (int e = 0; e < 256; e++) {
+        const int n = e / 128, j = (e % 128) / 32, l = e % 32;
+        const int is = 8 * n + 2 * j + (l >= 16);
+        const int q = (x[16 + 32 * n + l] >> (2 * j)) & 3;
+        y[e] = d * (x[is] & 0xF) * q - dmin * (x[is] >> 4);
+      }
+    } break;
+    case LO_Q8_K: {
+      float d; memcpy(&d, x, 4);
+      for (int j = 0; j < 256; j++) y[j] = d * ((const int8_t *)(x + 4))[j];
+    } break;
+    default: break;
+    }
+  }
+}
+
+/* --------------------------------------------------------- vec_dot */
+
+static float dot_f32(int k, const float *a, const float *b) {
+  double s = 0.0;
+  for (int i = 0; i < k; ++i) s += (double)(a[i] * b[i]);
+  return (float)s;
+}
+
+/* one 32-element block, (A, B) in the lamm pairs; returns the int dot */
+static int blk_idot(int type, const uint8_t *a, const int8_t *bq) {
+  int s = 0;
+  switch (type) {
+  case LO_Q4_0:
+    for (int j = 0; j < 16; ++j)
+      s += ((a[2 + j] & 0x0F) - 8) * bq[j] + ((a[2 + j] >> 4) - 8) * bq[j + 16];
+    break;
+  case LO_Q4_1:
+    for (int j = 0; j < 16; ++j)
+      s += (a[4 + j] & 0x0F) * bq[j] + (a[4 + j] >> 4) * bq[j + 16];
+    break;
+  case LO_Q5_0: {
+    uint32_t qh; memcpy(&qh, a + 2, 4);
+    for (int j = 0; j < 16; ++j) {
+      const int h0 = ((qh >> j) & 1) << 4, h1 = ((qh >> (j + 16)) & 1) << 4;
+      s += (((a[6 + j] & 0x0F) | h0) - 16) * bq[j] + (((a[6 + j] >> 4) | h1) - 16) * bq[j + 16];
+    }
+  } break;
+  case LO_Q5_1: {
+    uint32_t qh; memcpy(&qh, a + 4, 4);
+    for (int j = 0; j < 16; ++j) {
+      const int h0 = ((qh >> j) & 1) << 4, h1 = ((qh >> (j + 16)) & 1) << 4;
+      s += ((a[8 + j] & 0x0F) | h0) * bq[j] + ((a[8 + j] >> 4) | h1) * bq[j + 16];
+    }
+  } break;
+  case LO_Q8_0:
+    for (int j = 0; j < 32; ++j) s += ((const int8_t *)(a + 2))[j] * bq[j];
+    break;
+  default: break;
+  }
+  return s;
+}
+
+float lo_vec_dot(int type, int k, const void *va, const void *vb) {
+  const uint8_t *a = (const uint8_t *)va, *b = (const uint8_t *)vb;
+  if (type == LO_F32) return dot_f32(k, (const float *)va, (const float *)vb);
+  const size_t ab = lo_block_bytes(type), bb = lo_block_bytes(lo_vec_dot_type(type));
+  float sumf = 0.0f;
+  if (type == LO_Q2_K) {
+    for (int i = 0; i < k / 256; ++i, a += ab, b += bb) {
+      const uint8_t *sc = a, *q2 = a + 16;
+      float yd; memcpy(&yd, b, 4);
+      const int8_t *q8 = (const int8_t *)(b + 4);
+      int summs = 0;
+      for (int j = 0; j < 16; ++j) {
+        int16_t bs; memcpy(&bs, b + 260 + 2 * j, 2);
+        summs += bs * (sc[j] >> 4);
+      }
+      const float dall = yd * H2F(rd16(a + 80));
+      const float dmin = yd * H2F(rd16(a + 82));
+      int isum = 0, is = 0;
+      for (int n = 0; n < 2; ++n, q2 += 32) {
+        for (int j = 0, shift = 0; j < 4; ++j, shift += 2, q8 += 32) {
+          int d = sc[is++] & 0xF, part = 0;
+          for (int l = 0; l < 16; ++l) part += q8[l] * ((q2[l] >> shift) & 3);
+          isum += d * part;
+          d = sc[is++] & 0xF;
+          part = 0;
+          for (int l = 16; l < 32; ++l) part += q8[l] * ((q2[l] >> shift) & 3);
+          isum += d * part;
+        }
+      }
+      sumf += dall * isum - dmin * summs;
+    }
+    return sumf;
+  }
+  const int bq_off = (type == LO_Q4_1 || type == LO_Q5_1) ? 4 : 2;
+  for (int i = 0; i < k / 32; ++i, a += ab, b += bb) {
+    const int sumi = blk_idot(type, a, (const int8_t *)(b + bq_off));
+    const float da = H2F(rd16(a)), db = H2F(rd16(b));
+    switch (type) {
+    case LO_Q4_0: sumf += sumi * da * db; break;                 /* :4466 order */
+    case LO_Q8_0: sumf += sumi * (da * db); break;               /* :5310 order */
+    case LO_Q5_0: sumf += (da * db) * sumi; break;
+    case LO_Q4_1: case LO_Q5_1:
+      sumf += (da * db) * sumi + H2F(rd16(a + 2)) * H2F(rd16(b + 2));
+      break;
+    default: break;
+    }
+  }
+  return sumf;
+}
+
+void lo_mul_mat(int type, int M, int N, int K, const void *A, size_t lda_bytes,
+                const void *B, size_t ldb_bytes, float *C, size_t ldc) {
+  for (int j = 0; j < N; j++)
+    for (int i = 0; i < M; i++)
+      C[(size_t)j * ldc + i] = lo_vec_dot(type, K, (const uint8_t *)A + (size_t)i * lda_bytes,
+                                          (const uint8_t *)B + (size_t)j * ldb_bytes);
+}

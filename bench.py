@@ -1,0 +1,271 @@
+#!/usr/bin/env python3
+"""bench.py -- BASELINE.json metric for the MI355X lamm backend.
+
+metric: "Q4_0xQ8_0 GEMM effective GFLOPS @ K=4096; achieved HBM GB/s (GEMV)"
+
+Workload (BASELINE config 2, the decode GEMV): Q4_0 weights M=4096 x K=4096 against one
+Q8_0 activation row (N=1).  One *step* = one launch of the hot path over one batch of
+synthetic input: R distinct 4096x4096 weight slices (ggml batch dims ne02 = ne12 = R,
+src/loongarch_matmul.cpp:130-142) with one activation row each.  R is chosen so that the
+bytes streamed per launch (R x 9,457,920 B for q4_0) exceed the 256 MiB Infinity Cache:
+every byte comes from HBM and the launch is long enough (~60 us) that the event-timed
+per-launch duration is kernel time, not launch gaps.
+
+  value      = algorithmic GEMV bytes (A + B + C) of all ranks / max-over-ranks time  [GB/s]
+  roofline   = the GEMV kernel vs 8 TB/s HBM3E (MI355X_MICROARCH.md)
+  gemm       = BASELINE config 3 (M=4096, N=512, K=4096) effective GFLOPS (2MNK / t), vs the
+               dense MFMA-i8 peak (2x bf16 = 5.0 POP/s)
+  cpu_baseline = the reference itself (oracle/_ref/ref_driver_lamm3 = lamm opt-3 AVX2 build
+               of /root/reference, timed like la-benchmark-matmult) on this host's cores
+
+Multi-GPU (torchrun, one process per GPU): rows of A shard across ranks (weak scaling:
+each rank owns a 4096-row shard of every slice), then C is all-gathered over RCCL.
+
+Synthetic data: A bytes random with valid fp16 scales; B = the GPU activation quantizer
+applied to N(0,1) floats.  Inputs are resident in HBM before the timed region.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "la-llama.cpp_amd"))
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+I8_DENSE_PEAK_TOPS = 5000.0    # dense MFMA-i8 = 2x the 2.5 PF dense bf16 rate (MI355X_MICROARCH.md)
+MALL_BYTES = 256 << 20
+
+FP16_FIELDS = {  # byte offsets of fp16 scale fields inside one block (lamm_formats.h)
+    "q4_0": [0], "q4_1": [0, 2], "q5_0": [0], "q5_1": [0, 2], "q8_0": [0], "q2_k": [80, 82]}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def make_weights(torch, la, fmt, slices, M, K, gen):
+    t = la.BY_NAME[fmt]
+    rb = la.row_bytes(t, K)
+    assert rb % 16 == 0
+    if fmt == "f32":
+        w = torch.randn(slices * M * K, device="cuda", generator=gen).view(torch.uint8)
+        return w, rb
+    w = torch.randint(0, 256, (slices * M * rb,), dtype=torch.uint8, device="cuda", generator=gen)
+    bpb = la.type_size(t)
+    blocks = w.view(-1, bpb)
+    for off in FP16_FIELDS[fmt]:
+        d = (torch.rand(blocks.shape[0], device="cuda", generator=gen) * 0.02 + 1e-3).half()
+        blocks[:, off:off + 2].view(torch.float16)[:, 0] = d
+    return w, rb
+
+
+def make_activations(torch, la, fmt, rows, K, gen):
+    t = la.BY_NAME[fmt]
+    vt = la.vec_dot_type(t)
+    x = torch.randn(rows, K, device="cuda", generator=gen)
+    if vt == la.F32:
+        return x.view(torch.uint8).reshape(-1).clone()
+    y = torch.zeros(rows * la.row_bytes(vt, K) + 16, dtype=torch.uint8, device="cuda")
+    la.quantize_torch(vt, x, y, flavour=1)
+    return y
+
+
+def run_case(torch, la, dist, fmt, M, N, K, slices, steps, warmup, world):
+    """One batched launch per step; returns per-step seconds (max over ranks)."""
+    t = la.BY_NAME[fmt]
+    vt = la.vec_dot_type(t)
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(1234 + (dist.get_rank() if world > 1 else 0))
+    A, arow = make_weights(torch, la, fmt, slices, M, K, gen)
+    B = make_activations(torch, la, fmt, slices * N, K, gen)
+    C = torch.zeros(slices * N * M, dtype=torch.float32, device="cuda")
+    gathered = torch.zeros(world * C.numel(), dtype=torch.float32, device="cuda") if world > 1 else None
+    kb = K // la.blck_size(t)
+    brow = la.row_bytes(vt, K)
+    Am = la.Matrix(A.data_ptr(), t, M, kb, kb)
+    Bm = la.Matrix(B.data_ptr(), vt, kb, N, kb)
+    Cm = la.Matrix(C.data_ptr(), la.F32, M, N, M)
+    bt = la.Batch(slices, 1, slices, 1, M * arow, slices * M * arow, N * brow, slices * N * brow,
+                  4 * M * N, 4 * M * N * slices)
+    stream = torch.cuda.current_stream()
+
+    def step():
+        la.matmul_batched(Am, Bm, Cm, bt, stream.cuda_stream)
+        if world > 1:  # row shards -> every rank holds all of C (RCCL over xGMI)
+            dist.all_gather_into_tensor(gathered, C)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(steps):
+        step()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    ev = e0.elapsed_time(e1) / 1e3
+    per = torch.tensor([ev / steps, wall / steps], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(per, op=dist.ReduceOp.MAX)
+    # sanity: finite outputs
+    assert torch.isfinite(C).all().item(), "non-finite GEMV/GEMM output"
+    # kernel-only per-launch time (no collective) for the roofline
+    e2, e3 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e2.record(stream)
+    for _ in range(steps):
+        la.matmul_batched(Am, Bm, Cm, bt, stream.cuda_stream)
+    e3.record(stream)
+    torch.cuda.synchronize()
+    kern = e2.elapsed_time(e3) / 1e3 / steps
+    del A, B, C, gathered
+    torch.cuda.empty_cache()
+    return per[0].item(), per[1].item(), kern
+
+
+def gemv_bytes(la, fmt, M, K, N=1):
+    t = la.BY_NAME[fmt]
+    return M * la.row_bytes(t, K) + N * la.row_bytes(la.vec_dot_type(t), K) + 4 * M * N
+
+
+def cpu_baseline(fmt, M, N, K, budget_s, gemv_unit_bytes):
+    """The real reference (lamm opt=3, AVX2; Q8_0 uses opt=0 stock ggml because lamm's
+    AVX2 Q8_0 is numerically wrong) timed like la-benchmark-matmult."""
+    threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    threads = max(1, min(threads, 16))
+    variant = "lamm0" if fmt == "q8_0" else "lamm3"
+    exe = os.path.join(ROOT, "oracle", "_ref", f"ref_driver_{variant}")
+    if os.path.exists(exe):
+        out = subprocess.run([exe, "bench", fmt, str(M), str(N), str(K), str(threads), "100000", str(budget_s)],
+                             capture_output=True, text=True, timeout=budget_s * 4 + 120)
+        if out.returncode == 0:
+            r = json.loads(out.stdout.strip().splitlines()[-1])
+            us = r["median_us"]
+            return {"value": round(gemv_unit_bytes / (us * 1e-6) / 1e9, 3), "unit": "GB/s", "cores": threads,
+                    "kind": "reference", "median_us": us, "gflops": r["gflops"],
+                    "sample": f"{r['iters']} x {fmt} mul_mat M={M} N={N} K={K} via ggml_graph_compute "
+                              f"(ref_driver_{variant}: la-llama.cpp lamm opt {3 if variant == 'lamm3' else 0} "
+                              f"AVX2 build; INIT quantization of src1 included), median, ~{budget_s}s budget"}
+        log("reference baseline failed:", out.stderr[-500:])
+    # fallback: our scalar C port of the reference arithmetic, one thread
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import numpy as np
+    import oracle_lib as ol
+    o = ol.Oracle()
+    t = ol.BY_NAME[fmt]
+    rng = np.random.default_rng(0)
+    A = o.quantize(t, rng.standard_normal((M, K), dtype=np.float32))
+    B = o.quantize(o.vec_dot_type(t), rng.standard_normal((N, K), dtype=np.float32), ol.QUANT_AVX)
+    ts, t_end = [], time.perf_counter() + budget_s
+    while time.perf_counter() < t_end and len(ts) < 50:
+        t0 = time.perf_counter()
+        o.mul_mat(t, M, N, K, A, B)
+        ts.append(time.perf_counter() - t0)
+    med = sorted(ts)[len(ts) // 2]
+    return {"value": round(gemv_unit_bytes / med / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
+            "median_us": med * 1e6, "sample": f"{len(ts)} x scalar oracle mul_mat M={M} N={N} K={K}"}
+
+
+def read_traffic(tag):
+    p = os.path.join(ROOT, "profiles", f"traffic_{tag}.json")
+    if os.path.exists(p):
+        try:
+            return json.load(open(p))
+        except Exception:
+            return None
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--fmt", default="q4_0")
+    ap.add_argument("--M", type=int, default=4096)
+    ap.add_argument("--K", type=int, default=4096)
+    ap.add_argument("--gemm-N", type=int, default=512)
+    ap.add_argument("--no-gemm", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--sweep", action="store_true", help="also time every weight format (config 4)")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    import lamm_amd as la
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if la.device_count() == 0:
+        raise SystemExit("bench.py: no gfx950 device visible")
+
+    M, K = args.M, args.K
+    unit = gemv_bytes(la, args.fmt, M, K)
+    slices = max(8, -(-int(1.15 * MALL_BYTES) // unit))     # > MALL per launch
+    per_step, wall_step, kern = run_case(torch, la, dist, args.fmt, M, 1, K, slices, args.steps, args.warmup, world)
+    launch_bytes = slices * unit
+    value = world * launch_bytes / per_step / 1e9
+    achieved = launch_bytes / kern / 1e9
+    traffic = read_traffic(f"{args.fmt}_gemv")
+    out = {
+        "metric": "Q4_0xQ8_0 GEMM effective GFLOPS @ K=4096; achieved HBM GB/s (GEMV)",
+        "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(per_step * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "i8",
+        "data": "synthetic (random block bytes with valid fp16 scales; B = GPU q8 quantizer of N(0,1))",
+        "config": {"workload": f"{args.fmt.upper()}xQ8 GEMV M={M} N=1 K={K} (BASELINE config 2), "
+                               f"{slices} weight slices per launch (ggml ne02=ne12={slices}, "
+                               f"{launch_bytes / 1e6:.1f} MB/launch > 256 MiB MALL)",
+                   "fmt": args.fmt, "M_per_rank": M, "N": 1, "K": K, "slices": slices,
+                   "parallelism": f"rows of A sharded over {world} GPU(s)" + (" + RCCL all-gather of C" if world > 1 else "")},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": traffic.get("bytes_per_launch") if traffic else None,
+                     "kernel": "lamm::gemv_kernel<2,1>", "per_launch_us": round(kern * 1e6, 3),
+                     "algorithmic_bytes_per_launch": launch_bytes},
+    }
+    if not args.no_gemm:
+        gN = args.gemm_N
+        gslices = 4
+        g_step, _, g_kern = run_case(torch, la, dist, args.fmt, M, gN, K, gslices, max(3, args.steps // 4), 2, world)
+        ops = 2.0 * M * gN * K * gslices
+        out["gemm"] = {"workload": f"{args.fmt.upper()}xQ8 GEMM M={M} N={gN} K={K} (BASELINE config 3), "
+                                   f"{gslices} slices per launch",
+                       "value": round(world * ops / g_step / 1e9, 1), "unit": "GFLOPS",
+                       "roofline": {"bound": "mfma", "achieved": round(ops / g_kern / 1e12, 2),
+                                    "peak": I8_DENSE_PEAK_TOPS, "unit": "TFLOP/s",
+                                    "frac": round(ops / g_kern / 1e12 / I8_DENSE_PEAK_TOPS, 4),
+                                    "per_launch_us": round(g_kern * 1e6, 2)}}
+    if args.sweep:
+        sw = {}
+        for f in ["f32", "q4_0", "q4_1", "q5_0", "q5_1", "q8_0", "q2_k"]:
+            u = gemv_bytes(la, f, M, K)
+            sl = max(4, -(-int(1.15 * MALL_BYTES) // u))
+            _, _, kk = run_case(torch, la, dist, f, M, 1, K, sl, max(5, args.steps // 2), 2, world)
+            sw[f] = {"gemv_GBs": round(sl * u / kk / 1e9, 1), "gemv_us_per_slice": round(kk / sl * 1e6, 3)}
+        out["sweep"] = sw
+    if rank == 0 and world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(args.fmt, M, 1, K, args.cpu_budget, unit)
+    if world > 1:
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

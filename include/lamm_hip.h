@@ -1,0 +1,125 @@
+/*
+ * lamm_hip.h -- C ABI of the MI355X (gfx950) lamm backend: liblamm_hip.so
+ *
+ * Two entry layers, both plain C (no HIP / torch types in any signature):
+ *
+ *  1. The ggml operator boundary -- a drop-in for the reference plug-in
+ *     (AyiStar/la-llama.cpp src/loongarch_matmul.h:18-24), called from
+ *     ggml_compute_forward_mul_mat under #ifdef LA_LLAMA
+ *     (llama.cpp-b2430 ggml.c:10858-10863):
+ *
+ *        if (lamm_can_mul_mat(params, dst)) { lamm_mul_mat(params, dst); return; }
+ *
+ *     Same names, same argument meaning, same error behaviour: can_mul_mat returning
+ *     false is the only "error" (ggml falls back to its own CPU loop); lamm_mul_mat
+ *     aborts with a message on an internal failure (src/lamm_impl.hpp:100-103).
+ *     The structs are ggml's (b2430 layout); they stay opaque here.
+ *
+ *  2. The plug-in operator API on DEVICE memory, mirroring the reference's internal
+ *     interface LAMMImpl<T>::matmul(const Matrix &A, const Matrix &B, const Matrix &C)
+ *     (src/lamm_impl.hpp:20, Matrix = src/lamm_common.h:87-93): same struct layout,
+ *     same units (A.col = K in blocks, ld in elements of the matrix's own type,
+ *     C element (i,j) at c[j*ldc + i]).  Runs asynchronously on `hip_stream`.
+ */
+#ifndef LAMM_HIP_H
+#define LAMM_HIP_H
+
+#include <stdbool.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- 1. ggml boundary (replaces src/loongarch_matmul.h:18-24) ---------------- */
+struct ggml_compute_params;
+struct ggml_tensor;
+
+/* Replaces src/loongarch_matmul.cpp:10-62.  False outside the COMPUTE phase, for
+ * unsupported (src0, vec_dot_type) pairs, non-contiguous quantized src1, non-F32 dst,
+ * LAMM_OPT_LEVEL=0 in the environment, or when no gfx950 device is present. */
+bool lamm_can_mul_mat(const struct ggml_compute_params *params,
+                      const struct ggml_tensor *dst);
+
+/* Replaces src/loongarch_matmul.cpp:64-143.  Thread ith==0 of the ggml pool owns
+ * the GPU work (weights cached device-resident, B uploaded, C downloaded into
+ * dst with its strides, stream synchronised before return); other threads return
+ * at once and meet thread 0 at ggml's post-COMPUTE barrier.  Computes all M rows
+ * (the reference drops M % nth rows: SURVEY §8a defect 1). */
+void lamm_mul_mat(const struct ggml_compute_params *params,
+                  struct ggml_tensor *dst);
+
+/* Replaces src/loongarch_matmul.cpp:145.  3 when the GPU path is active,
+ * 0 when disabled by LAMM_OPT_LEVEL=0. */
+int lamm_get_opt_level(void);
+
+/* ---- 2. operator API on device memory ------------------------------------- */
+typedef struct lamm_matrix {   /* == struct Matrix, src/lamm_common.h:87-93 */
+  void *data;                  /* device pointer */
+  int type;                    /* ggml_type id: 0 f32, 2 q4_0, 3 q4_1, 6 q5_0,
+                                  7 q5_1, 8 q8_0, 9 q8_1, 10 q2_K, 15 q8_K */
+  int row;
+  int col;
+  int64_t ld;                  /* leading dimension, in blocks of `type` */
+} lamm_matrix;
+
+enum lamm_status {
+  LAMM_OK = 0,
+  LAMM_ERR_TYPE = 1,   /* unsupported (A.type, B.type, C.type) combination */
+  LAMM_ERR_SHAPE = 2,  /* M/N/K or leading dimensions inconsistent */
+  LAMM_ERR_ALIGN = 3,  /* A.data or A row pitch not 16-byte aligned */
+  LAMM_ERR_HIP = 4,    /* HIP runtime error (see lamm_hip_last_error) */
+  LAMM_ERR_NODEV = 5   /* no gfx950 device */
+};
+
+/* C[j*C.ld + i] = sum_k A[i,k] * B[k,j] for i < C.row (=A.row), j < C.col (=B.col).
+ * A: weights (f32/q4_0/q4_1/q5_0/q5_1/q8_0/q2_K), A.col = K/blck, A.ld >= A.col.
+ * B: activations of type vec_dot_type(A.type) (f32/q8_0/q8_1/q8_K), column j at
+ *    B.data + j*B.ld blocks, B.row = A.col.
+ * C: f32, C.ld >= C.row.   Returns a lamm_status.  Asynchronous on hip_stream.
+ * Loads are range-checked per dword: A and B must be readable up to the next
+ * 4-byte boundary past their last byte (always true for hipMalloc / torch memory). */
+int lamm_hip_matmul(const lamm_matrix *A, const lamm_matrix *B, const lamm_matrix *C,
+                    void *hip_stream);
+
+/* Batched form: the reference's per-slice loop over ne12 x ne13 with broadcast
+ * r2 = ne12/ne02, r3 = ne13/ne03 (src/loongarch_matmul.cpp:130-142) as ONE launch.
+ * Slice (i12, i13) multiplies A slice (i12/r2, i13/r3) by B slice (i12, i13) into
+ * C slice (i12, i13).  Strides are in bytes, like ggml's nb[2], nb[3].
+ * lamm_hip_matmul(A, B, C, s) == lamm_hip_matmul_batched(A, B, C, NULL, s). */
+typedef struct lamm_batch {
+  int64_t ne02, ne03;          /* A slices */
+  int64_t ne12, ne13;          /* B and C slices; multiples of ne02, ne03 */
+  size_t nba2, nba3;           /* A slice strides (bytes, multiples of 16) */
+  size_t nbb2, nbb3;           /* B slice strides (bytes) */
+  size_t nbc2, nbc3;           /* C slice strides (bytes, multiples of 4) */
+} lamm_batch;
+
+int lamm_hip_matmul_batched(const lamm_matrix *A, const lamm_matrix *B, const lamm_matrix *C,
+                            const lamm_batch *batch, void *hip_stream);
+
+/* Activation quantizer on device (ggml INIT phase, LC/ggml.c:10865-10887, run on
+ * the GPU): x[N][K] f32 (row j at x + j*ldx floats) -> y, N rows of `vec_type`
+ * blocks (row j at y + j*ldy blocks).  flavour 0 = *_reference rounding
+ * (roundf), 1 = the AVX2 from_float rounding (nearest-even, id = 127/amax). */
+int lamm_hip_quantize(int vec_type, int flavour, const float *x, int64_t ldx, void *y,
+                      int64_t ldy, int K, int N, void *hip_stream);
+
+const char *lamm_hip_last_error(void);
+int lamm_hip_device_count(void);
+
+/* ggml type traits for the supported types (LC/ggml.c:477-775). */
+int lamm_blck_size(int type);
+size_t lamm_type_size(int type);
+int lamm_vec_dot_type(int type);
+
+/* Device weight residency used by the ggml boundary (keyed by src0->data/type/
+ * shape/strides plus a sampled fingerprint of the bytes). */
+void lamm_hip_cache_clear(void);
+size_t lamm_hip_cache_bytes(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LAMM_HIP_H */

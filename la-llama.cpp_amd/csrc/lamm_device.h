@@ -1,0 +1,72 @@
+// lamm_device.h -- gfx950 device helpers shared by the lamm HIP kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <utility>
+
+#include "lamm_formats.h"
+
+namespace lamm {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ float h2f(uint32_t h16) {
+  return (float)__builtin_bit_cast(_Float16, (uint16_t)h16);
+}
+
+// Buffer resource over [base, base+bytes): loads past the end return 0 instead of
+// faulting (gfx950 raw buffer range check), which is how ragged tails are handled
+// without per-load branches (cdna_hip_programming.md §5.5 T8/T20).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ u32x4 bload16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+}
+__device__ __forceinline__ uint32_t bload4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+}
+__device__ __forceinline__ uint16_t bload2(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b16(r, off, 0, 0);
+}
+
+// dword starting at byte offset O of a register-resident byte string (O compile-time).
+template <int O, int NW>
+__device__ __forceinline__ uint32_t get32(const uint32_t (&w)[NW]) {
+  static_assert(O >= 0 && ((O & 3) == 0 ? (O >> 2) < NW : (O >> 2) + 1 < NW), "get32 range");
+  if constexpr ((O & 3) == 0) {
+    return w[O >> 2];
+  } else {
+    return __builtin_amdgcn_alignbit(w[(O >> 2) + 1], w[O >> 2], (O & 3) * 8);
+  }
+}
+template <int O, int NW>
+__device__ __forceinline__ uint32_t get16(const uint32_t (&w)[NW]) {
+  return (w[O >> 2] >> ((O & 3) * 8)) & 0xffffu;
+}
+
+// Compile-time unrolled loop: unroll<N>([&](auto I) { constexpr int i = I; ... });
+template <class Fn, int... I>
+__device__ __forceinline__ void unroll_impl(Fn& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class Fn>
+__device__ __forceinline__ void unroll(Fn&& f) {
+  unroll_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+__device__ __forceinline__ int dot4(uint32_t a, uint32_t b, int c) {
+  return __builtin_amdgcn_sdot4((int)a, (int)b, c, false);
+}
+
+// bit i (i<4) of x -> bit 4 of byte i  (the 5th quant bit of q5_0/q5_1)
+__device__ __forceinline__ uint32_t spread4_hi(uint32_t x4) {
+  return ((x4 * 0x00204081u) & 0x01010101u) << 4;
+}
+
+}  // namespace lamm

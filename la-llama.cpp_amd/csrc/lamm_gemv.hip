@@ -1,0 +1,401 @@
+// lamm_gemv.hip -- decode-shaped (N <= 8) quantized mat-vec for gfx950.
+//
+// Replaces the per-format block-dot kernels of the lamm plug-in
+// (src/lamm_kernel_{f32,q4_0,q4_1,q5_0,q5_1,q8_0,q2_k}.hpp, driven by
+// LAMMImpl<T>::matmul_simd_block, src/lamm_impl.hpp:90-147) for small N:
+//
+//   C[j*ldc + i] = sum_k A[i,k] * B[j,k]     (C stored N rows of M; lamm layout)
+//
+// Structure (one workgroup = 256 threads = 16 rows x 16 "chunks"):
+//   * A is streamed from HBM once, as raw block_q* bytes, with coalesced 16-byte
+//     buffer loads into LDS (AoS, no repack: 18/20/22/24/34/84-byte blocks are not
+//     dword aligned, so each thread then reads its chunk of G blocks from LDS).
+//   * B (the q8_0/q8_1/q8_K activation row(s)) is decoded once per workgroup into
+//     LDS as int8 words + fp32 scales (+ sum(q) / s / bsums), XOR-swizzled so the 16
+//     chunk-threads of a row read conflict-free.
+//   * Each thread unpacks its blocks' 2/4/5/8-bit quants to int8 in registers and
+//     accumulates exact per-block int32 dots with v_dot4_i32_i8, then applies the
+//     fp16 scales in fp32 (d_a*d_b*S [+ m_a*s_b]).  The 16 chunk partials of a row
+//     are reduced with wave shuffles in a fixed order (deterministic).
+//   * K larger than one segment (4096 elements; 1024 for f32) loops over segments.
+#include "lamm_device.h"
+#include "lamm_kernels.h"
+
+namespace lamm {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kSC = 16;                 // chunks per row per segment
+constexpr int kRows = kThreads / kSC;   // rows per workgroup
+
+template <int T> struct Fmt;
+// QK: elems/block, BPB: bytes/block, G: blocks per chunk (G*BPB % 16 == 0 or G=1),
+// VBPB: activation block bytes, VQK: activation elems/block
+template <> struct Fmt<kQ4_0> { static constexpr int QK = 32, BPB = 18, G = 8, VBPB = 34, VQK = 32; };
+template <> struct Fmt<kQ4_1> { static constexpr int QK = 32, BPB = 20, G = 8, VBPB = 36, VQK = 32; };
+template <> struct Fmt<kQ5_0> { static constexpr int QK = 32, BPB = 22, G = 8, VBPB = 34, VQK = 32; };
+template <> struct Fmt<kQ5_1> { static constexpr int QK = 32, BPB = 24, G = 8, VBPB = 36, VQK = 32; };
+template <> struct Fmt<kQ8_0> { static constexpr int QK = 32, BPB = 34, G = 8, VBPB = 34, VQK = 32; };
+template <> struct Fmt<kQ2_K> { static constexpr int QK = 256, BPB = 84, G = 1, VBPB = 292, VQK = 256; };
+template <> struct Fmt<kF32>  { static constexpr int QK = 1, BPB = 4, G = 64, VBPB = 4, VQK = 1; };
+
+template <int T> struct Geo {
+  using F = Fmt<T>;
+  static constexpr int CH_ELEMS = F::G * F::QK;          // 256 (64 for f32)
+  static constexpr int CH_BYTES = F::G * F::BPB;
+  static constexpr int CH_WORDS = (CH_BYTES + 3) / 4;
+  static constexpr int SEG_ELEMS = kSC * CH_ELEMS;       // 4096 (1024 for f32)
+  static constexpr int SEG_BLK = kSC * F::G;             // A blocks per row-segment
+  static constexpr int ROW_BYTES = kSC * CH_BYTES;       // LDS bytes per row-segment
+  static constexpr int A_PIECES = kRows * ROW_BYTES / 16;
+  static constexpr int A_NPT = (A_PIECES + kThreads - 1) / kThreads;
+  static constexpr int A_LDS = A_NPT * kThreads * 16;
+  static constexpr int VBLK = SEG_ELEMS / F::VQK;        // activation blocks per segment
+  static constexpr int BQ_WORDS = T == kF32 ? SEG_ELEMS : SEG_ELEMS / 4;  // int8 quads / f32 words
+};
+
+// XOR swizzle of B word index: the 16 chunk-threads of a row read 16-byte
+// piece p of chunk ch; piece p^ch spreads them over 16 bank slots.
+__device__ __forceinline__ int swz(int wi) {
+  return (wi & ~63) | ((((wi >> 2) & 15) ^ ((wi >> 6) & 15)) << 2) | (wi & 3);
+}
+
+template <int T, int NC>
+struct Smem {
+  using GG = Geo<T>;
+  uint32_t a[GG::A_LDS / 4];
+  uint32_t bq[NC][GG::BQ_WORDS];
+  float bd[NC][T == kF32 ? 1 : GG::VBLK];
+  float bx[NC][T == kF32 ? 1 : GG::VBLK];   // q8_0: sum(q) as float; q8_1: s
+  int bs[NC][T == kQ2_K ? GG::VBLK * 16 : 1];  // q8_K bsums
+};
+
+// ---- stage the activation segment (decoded) into LDS --------------------------
+template <int T, int NC>
+__device__ __forceinline__ void stage_b(Smem<T, NC>& sm, const GemvArgs& p, const unsigned char* Bz, int seg) {
+  using GG = Geo<T>;
+  using F = Fmt<T>;
+  const int t = threadIdx.x;
+  const int64_t bbytes = (int64_t)(p.N - 1) * p.ldb + (int64_t)(p.K / F::VQK) * F::VBPB;
+  // range-checked per dword: round up so a dword straddling the logical end is read
+  // (allocations are readable to the next 4-byte boundary: include/lamm_hip.h)
+  const auto rs = make_rsrc(Bz, (uint32_t)min((bbytes + 3) & ~int64_t(3), (int64_t)0x7fffffff));
+  if constexpr (T == kF32) {
+    // f32 activations: straight words
+    for (int it = t; it < NC * GG::BQ_WORDS; it += kThreads) {
+      const int j = it / GG::BQ_WORDS, w = it % GG::BQ_WORDS;
+      const int64_t e = (int64_t)seg * GG::SEG_ELEMS + w;
+      uint32_t v = 0;
+      if (j < p.N && e < p.K) v = bload4(rs, (uint32_t)(j * p.ldb + e * 4));
+      sm.bq[j][swz(w)] = v;
+    }
+  } else if constexpr (T == kQ2_K) {
+    // q8_K: f32 d | 256 x i8 | 16 x i16 bsums  = 73 dwords, dword aligned
+    for (int it = t; it < NC * GG::VBLK * 73; it += kThreads) {
+      const int j = it / (GG::VBLK * 73), r = it % (GG::VBLK * 73);
+      const int sb = r / 73, k = r % 73;
+      const int gsb = seg * GG::VBLK + sb;
+      uint32_t v = 0;
+      if (j < p.N && gsb * 256 < p.K) v = bload4(rs, (uint32_t)(j * p.ldb + gsb * 292 + 4 * k));
+      if (k == 0) {
+        sm.bd[j][sb] = __builtin_bit_cast(float, v);
+      } else if (k <= 64) {
+        sm.bq[j][swz(sb * 64 + k - 1)] = v;
+      } else {
+        sm.bs[j][sb * 16 + 2 * (k - 65)] = (int)(int16_t)(v & 0xffff);
+        sm.bs[j][sb * 16 + 2 * (k - 65) + 1] = (int)(int16_t)(v >> 16);
+      }
+    }
+  } else {
+    // q8_0 (34 B) / q8_1 (36 B): one block per item, 10 dword loads from the
+    // dword-aligned address at or below the block.
+    constexpr int VQS = F::VBPB == 36 ? 4 : 2;
+    for (int it = t; it < NC * GG::VBLK; it += kThreads) {
+      const int j = it / GG::VBLK, bi = it % GG::VBLK;
+      const int gb = seg * GG::VBLK + bi;
+      const bool ok = j < p.N && gb * 32 < p.K;
+      const uint32_t off = ok ? (uint32_t)(j * p.ldb + (int64_t)gb * F::VBPB) : 0xfffffff0u;
+      const uint32_t base = off & ~3u;
+      const int sh = (int)(off & 3u);
+      uint32_t w[10], m[10];
+#pragma unroll
+      for (int k = 0; k < 10; ++k) w[k] = bload4(rs, base + 4 * k);
+      // realign: m = the block's bytes as dwords from its first byte
+#pragma unroll
+      for (int k = 0; k < 9; ++k) m[k] = __builtin_amdgcn_alignbit(w[k + 1], w[k], sh * 8);
+      m[9] = 0;
+      const uint32_t h0 = m[0];
+      float sx = 0.f;
+      unroll<8>([&](auto K) {
+        constexpr int k = K;
+        const uint32_t q = get32<VQS + 4 * k>(m);
+        sm.bq[j][swz(bi * 8 + k)] = q;
+        if constexpr (VQS == 2) sx += (float)dot4(q, 0x01010101u, 0);
+      });
+      sm.bd[j][bi] = h2f(h0 & 0xffff);
+      if constexpr (VQS == 4) sx = h2f(h0 >> 16);
+      sm.bx[j][bi] = sx;
+    }
+  }
+}
+
+// ---- one A block (compile-time position G_IDX in the chunk) x NC columns -------
+template <int T, int NC, int GI>
+__device__ __forceinline__ void block_dot(const uint32_t (&w)[Geo<T>::CH_WORDS + 1], const Smem<T, NC>& sm,
+                                          int ch, int ncols, float (&acc)[NC]) {
+  using F = Fmt<T>;
+  constexpr int O = GI * F::BPB;
+  const int bi = ch * F::G + GI;                 // block index within segment
+  if constexpr (T == kQ2_K) {
+    // block_q2_K: scales[16] @0, qs[64] @16, d @80, dmin @82 ; B = q8_K
+    uint32_t sc[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) sc[k] = w[k];
+    const float da = h2f(w[20] & 0xffff), dm = h2f(w[20] >> 16);
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      if (j >= ncols) break;
+      const uint32_t* bq = sm.bq[j];
+      int isum = 0, summs = 0;
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int s = 8 * n + 2 * jj + h;
+            const int scv = (sc[s >> 2] >> (8 * (s & 3))) & 0xff;
+            const u32x4 b = *(const u32x4*)&bq[swz(ch * 64 + 32 * n + 8 * jj + 4 * h)];
+            int part = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const uint32_t q = (w[4 + 8 * n + 4 * h + k] >> (2 * jj)) & 0x03030303u;
+              part = dot4(q, b[k], part);
+            }
+            isum += (scv & 0xf) * part;
+            summs += sm.bs[j][ch * 16 + s] * (scv >> 4);
+          }
+        }
+      }
+      const float yd = sm.bd[j][ch];
+      acc[j] += (yd * da) * (float)isum - (yd * dm) * (float)summs;
+    }
+  } else {
+    // 32-element blocks.  Unpack to 8 int8 words (elements 0-15 = low nibbles,
+    // 16-31 = high nibbles; the 5th bit from qh), exact int32 dot with v_dot4.
+    uint32_t q[8];
+    float da, ma = 0.f;
+    if constexpr (T == kQ8_0) {
+      da = h2f(get16<O>(w));
+      unroll<8>([&](auto K) { q[K] = get32<O + 2 + 4 * K>(w); });
+    } else {
+      constexpr bool AFF = (T == kQ4_1 || T == kQ5_1);
+      constexpr bool FIVE = (T == kQ5_0 || T == kQ5_1);
+      constexpr int QS = (AFF ? 4 : 2) + (FIVE ? 4 : 0);
+      da = h2f(get16<O>(w));
+      if constexpr (AFF) ma = h2f(get16<O + 2>(w));
+      uint32_t qh = 0;
+      if constexpr (FIVE) qh = get32<O + (AFF ? 4 : 2)>(w);
+      unroll<4>([&](auto K) {
+        constexpr int k = K;
+        const uint32_t x = get32<O + QS + 4 * k>(w);
+        q[k] = x & 0x0f0f0f0fu;
+        q[4 + k] = (x >> 4) & 0x0f0f0f0fu;
+        if constexpr (FIVE) {
+          q[k] |= spread4_hi((qh >> (4 * k)) & 0xf);
+          q[4 + k] |= spread4_hi((qh >> (16 + 4 * k)) & 0xf);
+        }
+      });
+    }
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      if (j >= ncols) break;
+      const uint32_t* bq = sm.bq[j];
+      const u32x4 b0 = *(const u32x4*)&bq[swz(ch * 64 + 8 * GI)];
+      const u32x4 b1 = *(const u32x4*)&bq[swz(ch * 64 + 8 * GI + 4)];
+      int s = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s = dot4(q[k], b0[k], s);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s = dot4(q[4 + k], b1[k], s);
+      const float db = sm.bd[j][bi], bx = sm.bx[j][bi];
+      if constexpr (T == kQ4_0) {
+        acc[j] += (da * db) * ((float)s - 8.f * bx);     // sum (q-8) b = sum q b - 8 sum b
+      } else if constexpr (T == kQ5_0) {
+        acc[j] += (da * db) * ((float)s - 16.f * bx);
+      } else if constexpr (T == kQ8_0) {
+        acc[j] += (da * db) * (float)s;
+      } else {  // q4_1 / q5_1 against q8_1: d_a d_b S + m_a s_b
+        acc[j] += (da * db) * (float)s + ma * bx;
+      }
+    }
+  }
+}
+
+// f32: the chunk is 64 consecutive floats; elements past K (nvalid) are masked so
+// row padding (possibly NaN) never reaches the sum.
+template <int NC>
+__device__ __forceinline__ void chunk_dot_f32(const uint32_t (&w)[Geo<kF32>::CH_WORDS + 1],
+                                              const Smem<kF32, NC>& sm, int ch, int nvalid, int ncols,
+                                              float (&acc)[NC]) {
+  float a[64];
+#pragma unroll
+  for (int i = 0; i < 64; ++i) a[i] = i < nvalid ? __builtin_bit_cast(float, w[i]) : 0.f;
+#pragma unroll
+  for (int j = 0; j < NC; ++j) {
+    if (j >= ncols) break;
+    const uint32_t* bq = sm.bq[j];
+    float s = 0.f;
+#pragma unroll
+    for (int pc = 0; pc < 16; ++pc) {
+      const u32x4 b = *(const u32x4*)&bq[swz(ch * 64 + 4 * pc)];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s = __builtin_fmaf(a[4 * pc + k], __uint_as_float((uint32_t)b[k]), s);
+    }
+    acc[j] += s;
+  }
+}
+
+template <int T, int NC, int GI>
+__device__ __forceinline__ void chunk_dot(const uint32_t (&w)[Geo<T>::CH_WORDS + 1], const Smem<T, NC>& sm,
+                                          int ch, int nvalid, int ncols, float (&acc)[NC]) {
+  if constexpr (T == kF32) {
+    chunk_dot_f32<NC>(w, sm, ch, nvalid, ncols, acc);
+  } else if constexpr (GI < Fmt<T>::G) {
+    if (GI < nvalid) block_dot<T, NC, GI>(w, sm, ch, ncols, acc);
+    chunk_dot<T, NC, GI + 1>(w, sm, ch, nvalid, ncols, acc);
+  }
+}
+
+template <int T, int NC>
+__global__ __launch_bounds__(kThreads) void gemv_kernel(GemvArgs p) {
+  using GG = Geo<T>;
+  using F = Fmt<T>;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  Smem<T, NC>& sm = *reinterpret_cast<Smem<T, NC>*>(smem_raw);
+
+  const int t = threadIdx.x;
+  const int row = t / kSC, ch = t % kSC;
+  const int64_t r0 = (int64_t)blockIdx.x * kRows;
+  const int z = blockIdx.y, i12 = z % p.ne12, i13 = z / p.ne12;
+  const unsigned char* Az = p.A + (int64_t)(i12 / p.r2) * p.sa2 + (int64_t)(i13 / p.r3) * p.sa3;
+  const unsigned char* Bz = p.B + (int64_t)i12 * p.sb2 + (int64_t)i13 * p.sb3;
+  float* Cz = p.C + (int64_t)i12 * p.sc2 + (int64_t)i13 * p.sc3;
+  const int rows = (int)min((int64_t)kRows, (int64_t)p.M - r0);
+  const int row_bytes = p.nblk * F::BPB;                   // bytes of one A row
+  const int nseg = (p.nblk + GG::SEG_BLK - 1) / GG::SEG_BLK;
+  const int ncols = p.N < NC ? p.N : NC;
+
+  float acc[NC];
+#pragma unroll
+  for (int j = 0; j < NC; ++j) acc[j] = 0.f;
+
+  for (int seg = 0; seg < nseg; ++seg) {
+    // ---- issue the A segment loads (HBM stream) ----
+    const unsigned char* abase = Az + r0 * p.lda + (int64_t)seg * GG::ROW_BYTES;
+    const int64_t avail = (int64_t)(rows - 1) * p.lda + row_bytes - (int64_t)seg * GG::ROW_BYTES;
+    const auto ra = make_rsrc(abase, (uint32_t)min((avail + 3) & ~int64_t(3), (int64_t)0x7fffffff));
+    u32x4 v[GG::A_NPT];
+#pragma unroll
+    for (int k = 0; k < GG::A_NPT; ++k) {
+      const int pc = t + k * kThreads;
+      const int rr = pc / (GG::ROW_BYTES / 16), oo = pc % (GG::ROW_BYTES / 16);
+      const uint32_t off = (pc < GG::A_PIECES && rr < rows) ? (uint32_t)(rr * p.lda + 16 * oo) : 0x7ffffff0u;
+      v[k] = bload16(ra, off);
+    }
+    // ---- activations (L2-resident) decoded into LDS ----
+    stage_b<T, NC>(sm, p, Bz, seg);
+#pragma unroll
+    for (int k = 0; k < GG::A_NPT; ++k) *(u32x4*)&sm.a[4 * (t + k * kThreads)] = v[k];
+    __syncthreads();
+
+    // ---- compute this thread's chunk ----
+    const int cb0 = seg * GG::SEG_BLK + ch * F::G;           // first A block of chunk
+    if (row < rows && cb0 < p.nblk) {
+      uint32_t w[GG::CH_WORDS + 1];
+      const uint32_t* src = &sm.a[(row * GG::ROW_BYTES + ch * GG::CH_BYTES) / 4];
+      if constexpr (GG::CH_BYTES % 16 == 0) {
+#pragma unroll
+        for (int k = 0; k < GG::CH_WORDS / 4; ++k) {
+          const u32x4 x = *(const u32x4*)&src[4 * k];
+          w[4 * k] = x[0]; w[4 * k + 1] = x[1]; w[4 * k + 2] = x[2]; w[4 * k + 3] = x[3];
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < GG::CH_WORDS; ++k) w[k] = src[k];
+      }
+      w[GG::CH_WORDS] = 0;
+      const int nvalid = min(F::G, p.nblk - cb0);
+      chunk_dot<T, NC, 0>(w, sm, ch, nvalid, ncols, acc);
+    }
+    __syncthreads();
+  }
+
+  // ---- reduce the 16 chunk partials of each row (fixed order) ----
+#pragma unroll
+  for (int j = 0; j < NC; ++j) {
+    float x = acc[j];
+    x += __shfl_xor(x, 8);
+    x += __shfl_xor(x, 4);
+    x += __shfl_xor(x, 2);
+    x += __shfl_xor(x, 1);
+    acc[j] = x;
+  }
+  if (ch == 0 && row < rows) {
+#pragma unroll
+    for (int j = 0; j < NC; ++j)
+      if (j < ncols) Cz[(int64_t)j * p.ldc + r0 + row] = acc[j];
+  }
+}
+
+template <int T, int NC>
+hipError_t launch_t(const GemvArgs& p, hipStream_t s) {
+  const size_t lds = sizeof(Smem<T, NC>);
+  const int grid = (int)((p.M + kRows - 1) / kRows);
+  if (grid == 0) return hipSuccess;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)gemv_kernel<T, NC>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((gemv_kernel<T, NC>), dim3(grid, p.ne12 * p.ne13), dim3(kThreads), lds, s, p);
+  return hipGetLastError();
+}
+
+template <int T>
+hipError_t launch_nc(const GemvArgs& p, hipStream_t s) {
+  if (p.N <= 1) return launch_t<T, 1>(p, s);
+  if (p.N <= 2) return launch_t<T, 2>(p, s);
+  if (p.N <= 4) return launch_t<T, 4>(p, s);
+  return launch_t<T, 8>(p, s);
+}
+
+}  // namespace
+
+size_t gemv_lds_bytes(int type, int nc) {
+#define LDS_CASE(T)                                                            \
+  case T:                                                                      \
+    return nc <= 1 ? sizeof(Smem<T, 1>) : nc <= 2 ? sizeof(Smem<T, 2>)         \
+         : nc <= 4 ? sizeof(Smem<T, 4>) : sizeof(Smem<T, 8>);
+  switch (type) {
+    LDS_CASE(kQ4_0) LDS_CASE(kQ4_1) LDS_CASE(kQ5_0) LDS_CASE(kQ5_1)
+    LDS_CASE(kQ8_0) LDS_CASE(kQ2_K) LDS_CASE(kF32)
+    default: return 0;
+  }
+#undef LDS_CASE
+}
+
+hipError_t launch_gemv(int type, const GemvArgs& p, hipStream_t s) {
+  switch (type) {
+    case kQ4_0: return launch_nc<kQ4_0>(p, s);
+    case kQ4_1: return launch_nc<kQ4_1>(p, s);
+    case kQ5_0: return launch_nc<kQ5_0>(p, s);
+    case kQ5_1: return launch_nc<kQ5_1>(p, s);
+    case kQ8_0: return launch_nc<kQ8_0>(p, s);
+    case kQ2_K: return launch_nc<kQ2_K>(p, s);
+    case kF32:  return launch_nc<kF32>(p, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace lamm

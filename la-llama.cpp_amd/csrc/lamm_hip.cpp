@@ -1,0 +1,404 @@
+// lamm_hip.cpp -- host side of liblamm_hip.so: the C ABI of include/lamm_hip.h.
+//
+//   * lamm_hip_matmul  : the operator API on device memory (mirrors
+//                        LAMMImpl<T>::matmul, src/lamm_impl.hpp:20-29) -> kernel dispatch
+//   * lamm_can_mul_mat / lamm_mul_mat / lamm_get_opt_level : the ggml boundary
+//                        (src/loongarch_matmul.cpp:10-145) on top of it, with a
+//                        device-resident weight cache and strided B/C transfers.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <list>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+
+#include "../../include/lamm_hip.h"
+#include "ggml_b2430_abi.h"
+#include "lamm_formats.h"
+#include "lamm_kernels.h"
+
+namespace lamm {
+hipError_t launch_quantize(int vec_type, int flavour, const float* x, int64_t ldx, void* y,
+                           int64_t ldy_bytes, int K, int N, hipStream_t s);
+}
+
+using namespace lamm;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+struct DeviceProbe {
+  int count = 0;      // gfx950 devices visible
+  int device = 0;     // device used by the ggml boundary
+};
+
+const DeviceProbe& probe() {
+  static DeviceProbe p = [] {
+    DeviceProbe d;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) { (void)hipGetLastError(); return d; }
+    for (int i = 0; i < n; ++i) {
+      hipDeviceProp_t prop;
+      if (hipGetDeviceProperties(&prop, i) == hipSuccess && strncmp(prop.gcnArchName, "gfx950", 6) == 0) {
+        if (d.count == 0) d.device = i;
+        ++d.count;
+      }
+    }
+    const char* env = getenv("LAMM_HIP_DEVICE");
+    if (env && d.count) d.device = atoi(env);
+    return d;
+  }();
+  return p;
+}
+
+}  // namespace
+
+// =============================================================== traits
+extern "C" int lamm_blck_size(int type) { return block_bytes(type) ? block_elems(type) : 0; }
+extern "C" size_t lamm_type_size(int type) { return block_bytes(type); }
+extern "C" int lamm_vec_dot_type(int type) { return vec_dot_type(type); }
+extern "C" const char* lamm_hip_last_error(void) { return g_err.c_str(); }
+extern "C" int lamm_hip_device_count(void) { return probe().count; }
+
+// ======================================================== operator API
+extern "C" int lamm_hip_matmul_batched(const lamm_matrix* A, const lamm_matrix* B, const lamm_matrix* C,
+                                       const lamm_batch* batch, void* hip_stream) {
+  if (!A || !B || !C) return fail(LAMM_ERR_SHAPE, "null matrix");
+  if (!is_weight_type(A->type)) return fail(LAMM_ERR_TYPE, "unsupported A type %d", A->type);
+  if (B->type != vec_dot_type(A->type))
+    return fail(LAMM_ERR_TYPE, "B type %d is not vec_dot_type(%d)=%d", B->type, A->type, vec_dot_type(A->type));
+  if (C->type != kF32) return fail(LAMM_ERR_TYPE, "C must be f32");
+  const int M = A->row, N = B->col, Kb = A->col;
+  if (M < 0 || N < 0 || Kb < 0 || B->row != Kb || C->row != M || C->col != N)
+    return fail(LAMM_ERR_SHAPE, "shape mismatch A(%d,%d) B(%d,%d) C(%d,%d)", A->row, A->col, B->row, B->col,
+                C->row, C->col);
+  if (A->ld < Kb || (N > 1 && B->ld < Kb) || (N > 1 && C->ld < M))
+    return fail(LAMM_ERR_SHAPE, "leading dimension too small");
+  lamm_batch bt{1, 1, 1, 1, 0, 0, 0, 0, 0, 0};
+  if (batch) bt = *batch;
+  if (bt.ne02 < 1 || bt.ne03 < 1 || bt.ne12 < 1 || bt.ne13 < 1 || bt.ne12 % bt.ne02 || bt.ne13 % bt.ne03)
+    return fail(LAMM_ERR_SHAPE, "batch dims must be >= 1 and ne12 %% ne02 == ne13 %% ne03 == 0");
+  if (bt.ne12 * bt.ne13 > 65535) return fail(LAMM_ERR_SHAPE, "too many batch slices");
+  if (M == 0 || N == 0) return LAMM_OK;
+  const size_t abpb = block_bytes(A->type), bbpb = block_bytes(B->type);
+  const int64_t lda = A->ld * (int64_t)abpb, ldb = B->ld * (int64_t)bbpb;
+  if (((uintptr_t)A->data & 15) || (lda & 15) || (bt.nba2 & 15) || (bt.nba3 & 15))
+    return fail(LAMM_ERR_ALIGN, "A must be 16-byte aligned with 16-byte row/slice pitches (pitch %lld)",
+                (long long)lda);
+  if ((bt.nbc2 & 3) || (bt.nbc3 & 3) || ((uintptr_t)C->data & 3)) return fail(LAMM_ERR_ALIGN, "C must be f32-aligned");
+  if (B->type == kQ8_K && (((uintptr_t)B->data & 3) || (ldb & 3) || (bt.nbb2 & 3) || (bt.nbb3 & 3)))
+    return fail(LAMM_ERR_ALIGN, "q8_K B must be 4-byte aligned");
+  if (B->type == kF32 && (((uintptr_t)B->data & 3) || (bt.nbb2 & 3) || (bt.nbb3 & 3)))
+    return fail(LAMM_ERR_ALIGN, "f32 B must be 4-byte aligned");
+  if (probe().count == 0) return fail(LAMM_ERR_NODEV, "no gfx950 device");
+
+  hipStream_t s = static_cast<hipStream_t>(hip_stream);
+  GemvArgs p{static_cast<const unsigned char*>(A->data), lda, static_cast<const unsigned char*>(B->data), ldb,
+             static_cast<float*>(C->data), C->ld, M, N, Kb * block_elems(A->type), Kb};
+  p.ne12 = (int)bt.ne12;
+  p.ne13 = (int)bt.ne13;
+  p.r2 = (int)(bt.ne12 / bt.ne02);
+  p.r3 = (int)(bt.ne13 / bt.ne03);
+  p.sa2 = (int64_t)bt.nba2;
+  p.sa3 = (int64_t)bt.nba3;
+  p.sb2 = (int64_t)bt.nbb2;
+  p.sb3 = (int64_t)bt.nbb3;
+  p.sc2 = (int64_t)(bt.nbc2 / 4);
+  p.sc3 = (int64_t)(bt.nbc3 / 4);
+  hipError_t e;
+  if (N <= 8) {
+    e = launch_gemv(A->type, p, s);
+  } else if (gemm_supported(A->type)) {
+    e = launch_gemm(A->type, p, s);
+  } else {
+    e = hipSuccess;
+    for (int j0 = 0; j0 < N && e == hipSuccess; j0 += 8) {
+      GemvArgs q = p;
+      q.B = p.B + (int64_t)j0 * ldb;
+      q.C = p.C + (int64_t)j0 * p.ldc;
+      q.N = N - j0 < 8 ? N - j0 : 8;
+      e = launch_gemv(A->type, q, s);
+    }
+  }
+  if (e != hipSuccess) return fail(LAMM_ERR_HIP, "kernel launch: %s", hipGetErrorString(e));
+  return LAMM_OK;
+}
+
+extern "C" int lamm_hip_matmul(const lamm_matrix* A, const lamm_matrix* B, const lamm_matrix* C,
+                               void* hip_stream) {
+  return lamm_hip_matmul_batched(A, B, C, nullptr, hip_stream);
+}
+
+extern "C" int lamm_hip_quantize(int vec_type, int flavour, const float* x, int64_t ldx, void* y,
+                                 int64_t ldy, int K, int N, void* hip_stream) {
+  if (vec_type != kQ8_0 && vec_type != kQ8_1 && vec_type != kQ8_K)
+    return fail(LAMM_ERR_TYPE, "quantize: unsupported type %d", vec_type);
+  if (K % block_elems(vec_type)) return fail(LAMM_ERR_SHAPE, "quantize: K %% block != 0");
+  if (((uintptr_t)x & 15) || (ldx & 3)) return fail(LAMM_ERR_ALIGN, "quantize: x must be 16B aligned, ldx %% 4 == 0");
+  if (probe().count == 0) return fail(LAMM_ERR_NODEV, "no gfx950 device");
+  hipError_t e = launch_quantize(vec_type, flavour, x, ldx, y, ldy * (int64_t)block_bytes(vec_type), K, N,
+                                 static_cast<hipStream_t>(hip_stream));
+  if (e != hipSuccess) return fail(LAMM_ERR_HIP, "quantize launch: %s", hipGetErrorString(e));
+  return LAMM_OK;
+}
+
+// ===================================================== ggml boundary
+namespace {
+
+[[noreturn]] void die(const char* what, hipError_t e) {
+  fprintf(stderr, "lamm_hip: %s failed: %s\n", what, hipGetErrorString(e));
+  std::abort();
+}
+#define HIPCHK(x)                           \
+  do {                                      \
+    hipError_t _e = (x);                    \
+    if (_e != hipSuccess) die(#x, _e);      \
+  } while (0)
+
+// Device copy of one weight slice, keyed by the host slice it came from.
+struct WeightKey {
+  const void* host;
+  int type;
+  int64_t rows, kb;
+  size_t host_pitch;
+  bool operator==(const WeightKey& o) const {
+    return host == o.host && type == o.type && rows == o.rows && kb == o.kb && host_pitch == o.host_pitch;
+  }
+};
+struct WeightKeyHash {
+  size_t operator()(const WeightKey& k) const {
+    size_t h = std::hash<const void*>()(k.host);
+    h ^= std::hash<int64_t>()(k.rows * 1315423911ll + k.kb * 2654435761ll + k.type) + 0x9e3779b9 + (h << 6);
+    return h;
+  }
+};
+struct WeightEntry {
+  void* dev = nullptr;
+  int64_t dev_pitch = 0;
+  size_t bytes = 0;
+  uint64_t fingerprint = 0;
+  std::list<WeightKey>::iterator lru;
+};
+
+uint64_t fingerprint(const unsigned char* p, size_t pitch, size_t row_bytes, int64_t rows) {
+  // FNV-1a over 64 sampled 8-byte windows spread over the slice, plus the shape.
+  uint64_t h = 1469598103934665603ull ^ (row_bytes * 31 + (uint64_t)rows);
+  const size_t total = (size_t)(rows - 1) * pitch + row_bytes;
+  const size_t win = total < 8 ? total : 8;
+  for (int s = 0; s < 64; ++s) {
+    const size_t pos = (size_t)((double)(total - win) * s / 63.0);
+    uint64_t v = 0;
+    memcpy(&v, p + pos, win);
+    for (int b = 0; b < 8; ++b) { h ^= (v >> (8 * b)) & 0xff; h *= 1099511628211ull; }
+  }
+  return h;
+}
+
+class Runtime {
+ public:
+  static Runtime& get() {
+    static Runtime* r = new Runtime();  // leaked on purpose: no teardown-order issues
+    return *r;
+  }
+
+  std::mutex mu;
+
+  void ensure_init() {
+    if (stream_) return;
+    HIPCHK(hipSetDevice(probe().device));
+    HIPCHK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    const char* b = getenv("LAMM_HIP_CACHE_GB");
+    budget_ = (size_t)((b ? atof(b) : 64.0) * (1ull << 30));
+  }
+
+  // k.rows = ne01*ne02*ne03 device rows; host slices may be strided (nb[2], nb[3])
+  const WeightEntry& weights(const WeightKey& k, size_t row_bytes, const ggml::tensor* src0) {
+    const int64_t ne01 = src0->ne[1], ne02 = src0->ne[2], ne03 = src0->ne[3];
+    uint64_t fp = 0;
+    for (int64_t i3 = 0; i3 < ne03; ++i3)
+      for (int64_t i2 = 0; i2 < ne02; ++i2)
+        fp = fp * 1099511628211ull ^ fingerprint(static_cast<const unsigned char*>(k.host) + i2 * src0->nb[2] +
+                                                     i3 * src0->nb[3],
+                                                 k.host_pitch, row_bytes, ne01);
+    auto it = cache_.find(k);
+    if (it != cache_.end()) {
+      if (it->second.fingerprint == fp) {
+        lru_.splice(lru_.begin(), lru_, it->second.lru);
+        return it->second;
+      }
+      evict(it);
+    }
+    WeightEntry e;
+    // device row pitch: >= row_bytes, a whole number of blocks, a multiple of 16 B
+    const size_t bpb = block_bytes(k.type);
+    size_t pitch_blocks = (size_t)k.kb;
+    while ((pitch_blocks * bpb) % 16) ++pitch_blocks;
+    e.dev_pitch = (int64_t)(pitch_blocks * bpb);
+    e.bytes = (size_t)e.dev_pitch * k.rows + 64;
+    while (cached_bytes_ + e.bytes > budget_ && !lru_.empty()) evict(cache_.find(lru_.back()));
+    HIPCHK(hipMalloc(&e.dev, e.bytes));
+    for (int64_t i3 = 0; i3 < ne03; ++i3)
+      for (int64_t i2 = 0; i2 < ne02; ++i2)
+        HIPCHK(hipMemcpy2DAsync(static_cast<unsigned char*>(e.dev) + (i3 * ne02 + i2) * ne01 * e.dev_pitch,
+                                e.dev_pitch,
+                                static_cast<const unsigned char*>(k.host) + i2 * src0->nb[2] + i3 * src0->nb[3],
+                                k.host_pitch, row_bytes, ne01, hipMemcpyHostToDevice, stream_));
+    e.fingerprint = fp;
+    lru_.push_front(k);
+    e.lru = lru_.begin();
+    cached_bytes_ += e.bytes;
+    return cache_.emplace(k, e).first->second;
+  }
+
+  void* scratch(int which, size_t bytes) {
+    if (cap_[which] < bytes) {
+      if (buf_[which]) HIPCHK(hipFree(buf_[which]));
+      HIPCHK(hipMalloc(&buf_[which], bytes + 256));
+      cap_[which] = bytes;
+    }
+    return buf_[which];
+  }
+
+  void clear() {
+    while (!lru_.empty()) evict(cache_.find(lru_.back()));
+  }
+  size_t cached_bytes() const { return cached_bytes_; }
+  hipStream_t stream() const { return stream_; }
+
+ private:
+  void evict(std::unordered_map<WeightKey, WeightEntry, WeightKeyHash>::iterator it) {
+    if (it == cache_.end()) return;
+    (void)hipStreamSynchronize(stream_);
+    (void)hipFree(it->second.dev);
+    cached_bytes_ -= it->second.bytes;
+    lru_.erase(it->second.lru);
+    cache_.erase(it);
+  }
+
+  hipStream_t stream_ = nullptr;
+  size_t budget_ = 0, cached_bytes_ = 0;
+  std::unordered_map<WeightKey, WeightEntry, WeightKeyHash> cache_;
+  std::list<WeightKey> lru_;
+  void* buf_[2] = {nullptr, nullptr};
+  size_t cap_[2] = {0, 0};
+};
+
+int opt_level() {
+  static int lvl = [] {
+    const char* e = getenv("LAMM_OPT_LEVEL");
+    return e ? atoi(e) : 3;
+  }();
+  return lvl;
+}
+
+bool is_contiguous(const ggml::tensor* t) {
+  const size_t ts = block_bytes(t->type);
+  const int be = block_elems(t->type);
+  return t->nb[0] == ts && t->nb[1] == t->nb[0] * (size_t)(t->ne[0] / be) && t->nb[2] == t->nb[1] * (size_t)t->ne[1] &&
+         t->nb[3] == t->nb[2] * (size_t)t->ne[2];
+}
+
+}  // namespace
+
+extern "C" int lamm_get_opt_level(void) { return probe().count ? (opt_level() > 0 ? 3 : 0) : 0; }
+
+extern "C" bool lamm_can_mul_mat(const struct ggml_compute_params* vparams, const struct ggml_tensor* vdst) {
+  const auto* params = reinterpret_cast<const ggml::compute_params*>(vparams);
+  const auto* dst = reinterpret_cast<const ggml::tensor*>(vdst);
+  if (opt_level() == 0) return false;                       // :12-14
+  if (params->type != ggml::TASK_COMPUTE) return false;     // :15-17, INIT quantizes src1
+  const ggml::tensor* src0 = dst->src[0];
+  const ggml::tensor* src1 = dst->src[1];
+  if (!src0 || !src1) return false;
+  const int vdt = vec_dot_type(src0->type);
+  if (vdt < 0) return false;                                 // :37-52 supported pairs
+  if (src1->type == vdt && !is_contiguous(src1)) return false;  // :23-28
+  if (src1->nb[0] != block_bytes(src1->type)) return false;  // :29-31
+  if (dst->type != kF32) return false;                       // :34-36
+  if (src1->type != vdt && src1->type != kF32) return false; // wdata holds vdt rows
+  if (src0->ne[0] % block_elems(src0->type)) return false;
+  if (src0->nb[0] != block_bytes(src0->type)) return false;
+  if (dst->nb[0] != sizeof(float)) return false;
+  return probe().count > 0;                                  // no GPU: ggml's CPU loop
+}
+
+extern "C" void lamm_mul_mat(const struct ggml_compute_params* vparams, struct ggml_tensor* vdst) {
+  const auto* params = reinterpret_cast<const ggml::compute_params*>(vparams);
+  auto* dst = reinterpret_cast<ggml::tensor*>(vdst);
+  if (params->ith != 0) return;  // thread 0 owns the device work; ggml's barrier follows
+
+  const ggml::tensor* src0 = dst->src[0];
+  const ggml::tensor* src1 = dst->src[1];
+  const int t0 = src0->type, vdt = vec_dot_type(t0);
+  const int64_t ne00 = src0->ne[0], ne01 = src0->ne[1], ne02 = src0->ne[2], ne03 = src0->ne[3];
+  const int64_t ne11 = src1->ne[1], ne12 = src1->ne[2], ne13 = src1->ne[3];
+  const int qk = block_elems(t0);
+  const int64_t kb = ne00 / qk;                                 // K in blocks (A.col)
+  const size_t a_row = (size_t)kb * block_bytes(t0);
+  const size_t b_row = (size_t)kb * block_bytes(vdt);           // ggml_row_size(vdt, ne10)
+  const bool use_wdata = src1->type != vdt;
+  const int64_t M = ne01, N = ne11, nslices = ne12 * ne13;
+
+  Runtime& rt = Runtime::get();
+  std::lock_guard<std::mutex> lock(rt.mu);
+  rt.ensure_init();
+  hipStream_t s = rt.stream();
+
+  // weights: every (i02, i03) slice, device resident, rows re-pitched to 16 B
+  const WeightEntry& w = rt.weights(WeightKey{src0->data, t0, M * ne02 * ne03, kb, src0->nb[1]}, a_row, src0);
+  // activations: INIT-phase wdata (contiguous rows) or a contiguous vec_dot-typed src1
+  void* dB = rt.scratch(0, b_row * (size_t)(N * nslices) + 64);
+  if (use_wdata) {
+    HIPCHK(hipMemcpyAsync(dB, params->wdata, b_row * (size_t)(N * nslices), hipMemcpyHostToDevice, s));
+  } else {
+    HIPCHK(hipMemcpy2DAsync(dB, b_row, src1->data, src1->nb[1], b_row, (size_t)(N * nslices),
+                            hipMemcpyHostToDevice, s));
+  }
+  const size_t c_slice = (size_t)M * N * sizeof(float);
+  float* dC = static_cast<float*>(rt.scratch(1, c_slice * (size_t)nslices + 64));
+
+  lamm_matrix A{w.dev, t0, (int)M, (int)kb, w.dev_pitch / (int64_t)block_bytes(t0)};
+  lamm_matrix B{dB, vdt, (int)kb, (int)N, (int64_t)kb};
+  lamm_matrix C{dC, kF32, (int)M, (int)N, M};
+  lamm_batch bt{ne02, ne03, ne12, ne13, (size_t)(w.dev_pitch * M), (size_t)(w.dev_pitch * M * ne02),
+                b_row * (size_t)N, b_row * (size_t)(N * ne12), c_slice, c_slice * (size_t)ne12};
+  const int rc = lamm_hip_matmul_batched(&A, &B, &C, &bt, s);
+  if (rc != LAMM_OK) {
+    fprintf(stderr, "lamm_hip: lamm_hip_matmul_batched failed (%d): %s\n", rc, g_err.c_str());
+    std::abort();
+  }
+  for (int64_t i13 = 0; i13 < ne13; ++i13)
+    for (int64_t i12 = 0; i12 < ne12; ++i12) {
+      unsigned char* c_host = static_cast<unsigned char*>(dst->data) + i12 * dst->nb[2] + i13 * dst->nb[3];
+      HIPCHK(hipMemcpy2DAsync(c_host, dst->nb[1], dC + (i13 * ne12 + i12) * M * N, (size_t)M * sizeof(float),
+                              (size_t)M * sizeof(float), N, hipMemcpyDeviceToHost, s));
+    }
+  HIPCHK(hipStreamSynchronize(s));
+}
+
+extern "C" void lamm_hip_cache_clear(void) {
+  Runtime& rt = Runtime::get();
+  std::lock_guard<std::mutex> lock(rt.mu);
+  rt.clear();
+}
+
+extern "C" size_t lamm_hip_cache_bytes(void) {
+  Runtime& rt = Runtime::get();
+  std::lock_guard<std::mutex> lock(rt.mu);
+  return rt.cached_bytes();
+}

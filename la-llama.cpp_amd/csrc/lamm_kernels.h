@@ -1,0 +1,29 @@
+// lamm_kernels.h -- internal launch interface of the lamm HIP kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace lamm {
+
+// All strides in BYTES for A/B and in floats for C.  K in elements.
+// Row i of A starts at A + i*lda; column j of B at B + j*ldb; C[j*ldc + i].
+// Batch dims follow ggml's mul_mat (src/loongarch_matmul.cpp:130-142): slice
+// (i12, i13) uses A slice (i12/r2, i13/r3), B slice (i12, i13), C slice (i12, i13);
+// one launch covers all ne12*ne13 slices (blockIdx.y) instead of a host loop.
+struct GemvArgs {
+  const unsigned char* A; int64_t lda;
+  const unsigned char* B; int64_t ldb;
+  float* C; int64_t ldc;
+  int M, N, K, nblk;
+  int ne12 = 1, ne13 = 1, r2 = 1, r3 = 1;
+  int64_t sa2 = 0, sa3 = 0, sb2 = 0, sb3 = 0;   // bytes
+  int64_t sc2 = 0, sc3 = 0;                     // floats
+};
+
+hipError_t launch_gemv(int type, const GemvArgs& p, hipStream_t s);
+size_t gemv_lds_bytes(int type, int nc);
+
+hipError_t launch_gemm(int type, const GemvArgs& p, hipStream_t s);
+bool gemm_supported(int type);
+
+}  // namespace lamm

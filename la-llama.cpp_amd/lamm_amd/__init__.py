@@ -1,0 +1,187 @@
+"""lamm_amd -- Python view of liblamm_hip.so (the MI355X lamm backend).
+
+Thin ctypes binding over the C ABI in include/lamm_hip.h.  It mirrors the reference's
+operator surface for this path:
+
+* ``ggml_compute_params`` / ``ggml_tensor`` ctypes structs at the llama.cpp-b2430 binary
+  layout, so tests can drive ``lamm_can_mul_mat`` / ``lamm_mul_mat`` exactly as
+  ``ggml_compute_forward_mul_mat`` does (LC/ggml.c:10858-10863);
+* ``Matrix`` == ``struct Matrix`` (src/lamm_common.h:87-93) and ``matmul`` ==
+  ``LAMMImpl<T>::matmul(A, B, C)`` (src/lamm_impl.hpp:20) on device memory.
+
+There is no fallback: if the HIP library is missing this import fails loudly, and
+``matmul`` raises if the library reports an error.  PyTorch is only used by callers
+for device memory and streams.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "liblamm_hip.so")
+
+F32, Q4_0, Q4_1, Q5_0, Q5_1, Q8_0, Q8_1, Q2_K, Q8_K = 0, 2, 3, 6, 7, 8, 9, 10, 15
+NAMES = {F32: "f32", Q4_0: "q4_0", Q4_1: "q4_1", Q5_0: "q5_0", Q5_1: "q5_1",
+         Q8_0: "q8_0", Q8_1: "q8_1", Q2_K: "q2_k", Q8_K: "q8_k"}
+BY_NAME = {v: k for k, v in NAMES.items()}
+WEIGHT_TYPES = [F32, Q4_0, Q4_1, Q5_0, Q5_1, Q8_0, Q2_K]
+
+LAMM_OK, LAMM_ERR_TYPE, LAMM_ERR_SHAPE, LAMM_ERR_ALIGN, LAMM_ERR_HIP, LAMM_ERR_NODEV = range(6)
+
+TASK_INIT, TASK_COMPUTE, TASK_FINALIZE = 0, 1, 2
+OP_MUL_MAT = 23
+
+
+class LammError(RuntimeError):
+    pass
+
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(f"lamm_amd: {LIB_PATH} is missing -- build it with "
+                      f"`make -C la-llama.cpp_amd` (or __graft_entry__.build()); there is no fallback")
+
+lib = ctypes.CDLL(LIB_PATH)
+
+
+class Matrix(ctypes.Structure):
+    """struct lamm_matrix == struct Matrix (src/lamm_common.h:87-93)."""
+    _fields_ = [("data", ctypes.c_void_p), ("type", ctypes.c_int), ("row", ctypes.c_int),
+                ("col", ctypes.c_int), ("ld", ctypes.c_int64)]
+
+
+class Batch(ctypes.Structure):
+    """struct lamm_batch: ggml-style batch dims (src/loongarch_matmul.cpp:130-142)."""
+    _fields_ = [("ne02", ctypes.c_int64), ("ne03", ctypes.c_int64), ("ne12", ctypes.c_int64),
+                ("ne13", ctypes.c_int64), ("nba2", ctypes.c_size_t), ("nba3", ctypes.c_size_t),
+                ("nbb2", ctypes.c_size_t), ("nbb3", ctypes.c_size_t), ("nbc2", ctypes.c_size_t),
+                ("nbc3", ctypes.c_size_t)]
+
+
+class GgmlComputeParams(ctypes.Structure):
+    """struct ggml_compute_params, LC/ggml.h:668-677 (b2430)."""
+    _fields_ = [("type", ctypes.c_int32), ("ith", ctypes.c_int32), ("nth", ctypes.c_int32),
+                ("wsize", ctypes.c_size_t), ("wdata", ctypes.c_void_p)]
+
+
+class GgmlTensor(ctypes.Structure):
+    """struct ggml_tensor, LC/ggml.h:552-590 (b2430): 368 bytes."""
+
+
+GgmlTensor._fields_ = [
+    ("type", ctypes.c_int32), ("backend", ctypes.c_int32), ("buffer", ctypes.c_void_p),
+    ("ne", ctypes.c_int64 * 4), ("nb", ctypes.c_size_t * 4), ("op", ctypes.c_int32),
+    ("op_params", ctypes.c_int32 * 16), ("flags", ctypes.c_int32),
+    ("grad", ctypes.POINTER(GgmlTensor)), ("src", ctypes.POINTER(GgmlTensor) * 10),
+    ("perf_runs", ctypes.c_int32), ("perf_cycles", ctypes.c_int64), ("perf_time_us", ctypes.c_int64),
+    ("view_src", ctypes.POINTER(GgmlTensor)), ("view_offs", ctypes.c_size_t), ("data", ctypes.c_void_p),
+    ("name", ctypes.c_char * 64), ("extra", ctypes.c_void_p), ("padding", ctypes.c_char * 8)]
+
+lib.lamm_can_mul_mat.restype = ctypes.c_bool
+lib.lamm_can_mul_mat.argtypes = [ctypes.POINTER(GgmlComputeParams), ctypes.POINTER(GgmlTensor)]
+lib.lamm_mul_mat.restype = None
+lib.lamm_mul_mat.argtypes = [ctypes.POINTER(GgmlComputeParams), ctypes.POINTER(GgmlTensor)]
+lib.lamm_get_opt_level.restype = ctypes.c_int
+lib.lamm_hip_matmul.restype = ctypes.c_int
+lib.lamm_hip_matmul.argtypes = [ctypes.POINTER(Matrix)] * 3 + [ctypes.c_void_p]
+lib.lamm_hip_matmul_batched.restype = ctypes.c_int
+lib.lamm_hip_matmul_batched.argtypes = [ctypes.POINTER(Matrix)] * 3 + [ctypes.POINTER(Batch), ctypes.c_void_p]
+lib.lamm_hip_quantize.restype = ctypes.c_int
+lib.lamm_hip_quantize.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
+                                  ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+lib.lamm_hip_last_error.restype = ctypes.c_char_p
+lib.lamm_hip_device_count.restype = ctypes.c_int
+lib.lamm_blck_size.restype = ctypes.c_int
+lib.lamm_type_size.restype = ctypes.c_size_t
+lib.lamm_vec_dot_type.restype = ctypes.c_int
+lib.lamm_hip_cache_clear.restype = None
+lib.lamm_hip_cache_bytes.restype = ctypes.c_size_t
+
+
+def blck_size(t):
+    return lib.lamm_blck_size(t)
+
+
+def type_size(t):
+    return lib.lamm_type_size(t)
+
+
+def vec_dot_type(t):
+    return lib.lamm_vec_dot_type(t)
+
+
+def row_bytes(t, k):
+    return (k // blck_size(t)) * type_size(t)
+
+
+def last_error():
+    return lib.lamm_hip_last_error().decode()
+
+
+def device_count():
+    return lib.lamm_hip_device_count()
+
+
+def _check(rc, what):
+    if rc != LAMM_OK:
+        raise LammError(f"{what} failed ({rc}): {last_error()}")
+
+
+def matmul(A, B, C, stream=0):
+    """LAMMImpl<T>::matmul on device memory; A, B, C are ``Matrix`` (device pointers)."""
+    _check(lib.lamm_hip_matmul(ctypes.byref(A), ctypes.byref(B), ctypes.byref(C), ctypes.c_void_p(stream)),
+           "lamm_hip_matmul")
+
+
+def matmul_batched(A, B, C, batch, stream=0):
+    _check(lib.lamm_hip_matmul_batched(ctypes.byref(A), ctypes.byref(B), ctypes.byref(C), ctypes.byref(batch),
+                                       ctypes.c_void_p(stream)), "lamm_hip_matmul_batched")
+
+
+def mul_mat_torch(wtype, a, b, c, M, N, K, lda=None, ldb=None, ldc=None, stream=None, batch=None):
+    """C[j*ldc+i] = A_i . B_j for torch device tensors (uint8 blocks for A/B, f32 C).
+
+    lda/ldb in blocks (default: packed rows), ldc in floats (default M).
+    Runs on ``stream`` (default: torch's current stream)."""
+    import torch
+    vt = vec_dot_type(wtype)
+    kb = K // blck_size(wtype)
+    if stream is None:
+        stream = torch.cuda.current_stream().cuda_stream
+    A = Matrix(a.data_ptr(), wtype, M, kb, lda if lda is not None else kb)
+    B = Matrix(b.data_ptr(), vt, kb, N, ldb if ldb is not None else kb)
+    C = Matrix(c.data_ptr(), F32, M, N, ldc if ldc is not None else M)
+    if batch is None:
+        matmul(A, B, C, stream)
+    else:
+        matmul_batched(A, B, C, batch, stream)
+
+
+def quantize_torch(vtype, x, y, flavour=1, stream=None):
+    """GPU activation quantizer: x [N][K] f32 (torch, device) -> y blocks (uint8)."""
+    import torch
+    N, K = x.shape
+    if stream is None:
+        stream = torch.cuda.current_stream().cuda_stream
+    ldy = K // blck_size(vtype)
+    _check(lib.lamm_hip_quantize(vtype, flavour, ctypes.c_void_p(x.data_ptr()), x.stride(0),
+                                 ctypes.c_void_p(y.data_ptr()), ldy, K, N, ctypes.c_void_p(stream)),
+           "lamm_hip_quantize")
+
+
+def can_mul_mat(params, dst):
+    return bool(lib.lamm_can_mul_mat(ctypes.byref(params), ctypes.byref(dst)))
+
+
+def mul_mat(params, dst):
+    lib.lamm_mul_mat(ctypes.byref(params), ctypes.byref(dst))
+
+
+def get_opt_level():
+    return lib.lamm_get_opt_level()
+
+
+def cache_clear():
+    lib.lamm_hip_cache_clear()
+
+
+def cache_bytes():
+    return lib.lamm_hip_cache_bytes()

@@ -1,0 +1,173 @@
+"""GPU parity: the HIP path (called through the C ABI) vs the pinned oracle and the
+reference's own golden vectors.
+
+Tolerance (BASELINE.json north star): per output
+    |c_gpu - c_ref| <= 1e-3 * max(|c_ref|, sum_k |a_k b_k|)
+Per-block int32 dots are exact on both sides; only the fp32 accumulation order of
+the d_a*d_b*S terms differs, so observed errors are ~1e-7.
+"""
+import numpy as np
+import pytest
+
+from conftest import fixture_paths, load_fixture, load_inputs, rel_err
+import oracle_lib as ol
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-3
+
+torch = pytest.importorskip("torch")
+import lamm_amd as la  # noqa: E402
+
+ORACLE = ol.Oracle()
+FIXTURES = fixture_paths()
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available() or la.device_count() == 0:
+        pytest.fail("GPU tests need a gfx950 device (run with -m 'not gpu' on CPU)")
+    yield
+
+
+def pitch_blocks(t, kb):
+    """smallest lda (blocks) >= kb whose byte pitch is a multiple of 16"""
+    bpb = la.type_size(t)
+    lda = kb
+    while (lda * bpb) % 16:
+        lda += 1
+    return lda
+
+
+def dev_bytes(arr):
+    return torch.from_numpy(np.ascontiguousarray(arr).view(np.uint8).reshape(-1).copy()).cuda()
+
+
+def pitched_A(t, A_q, M, kb, lda):
+    rb = kb * la.type_size(t)
+    out = np.zeros(M * lda * la.type_size(t) + 64, np.uint8)
+    src = np.ascontiguousarray(A_q).reshape(M, rb)
+    out[:M * lda * la.type_size(t)].reshape(M, lda * la.type_size(t))[:, :rb] = src
+    return out
+
+
+def gpu_mul_mat(t, A_q, B_q, M, N, K, ldc=None, lda=None, ldb=None):
+    kb = K // la.blck_size(t)
+    vt = la.vec_dot_type(t)
+    lda = lda or pitch_blocks(t, kb)
+    A = dev_bytes(pitched_A(t, A_q, M, kb, lda))
+    if ldb is not None and ldb != kb:
+        rb = kb * la.type_size(vt)
+        Bp = np.zeros(N * ldb * la.type_size(vt), np.uint8)
+        Bp.reshape(N, -1)[:, :rb] = np.ascontiguousarray(B_q).reshape(N, rb)
+        B = dev_bytes(Bp)
+    else:
+        B = dev_bytes(B_q)
+    ldc = ldc or M
+    C = torch.full((N * ldc + 16,), float("nan"), dtype=torch.float32, device="cuda")
+    la.mul_mat_torch(t, A, B, C, M, N, K, lda=lda, ldb=ldb, ldc=ldc)
+    torch.cuda.synchronize()
+    c = C.cpu().numpy()
+    return np.stack([c[j * ldc:j * ldc + M] for j in range(N)]), c
+
+
+def absdot(t, A_q, B_q, M, N, K):
+    Ad = ORACLE.dequantize(t, A_q, M, K).astype(np.float64)
+    Bd = ORACLE.dequantize(la.vec_dot_type(t), B_q, N, K).astype(np.float64)
+    return np.abs(Bd) @ np.abs(Ad).T
+
+
+def _ids(paths):
+    return [p.rsplit("/", 1)[-1][:-4] for p in paths]
+
+
+@pytest.mark.parametrize("path", FIXTURES, ids=_ids(FIXTURES))
+def test_golden_vectors(path):
+    """Same bytes as the reference: C_scalar (from_float_reference B) and the
+    stock AVX2 vec_dot output (AVX2 from_float B)."""
+    z = load_fixture(path)
+    t, M, N, K = int(z["type"]), int(z["M"]), int(z["N"]), int(z["K"])
+    c_ref, _ = gpu_mul_mat(t, z["A_q"], z["B_ref"], M, N, K)
+    assert np.isfinite(c_ref).all()
+    e1 = rel_err(c_ref, z["C_scalar"], z["absdot"]).max()
+    c_avx, _ = gpu_mul_mat(t, z["A_q"], z["B_avx"], M, N, K)
+    e2 = rel_err(c_avx, z["C_vdot_avx"], z["absdot"]).max()
+    print(f"{z['name']}: max rel err vs scalar {e1:.2e}, vs avx2 {e2:.2e}")
+    assert e1 < TOL and e2 < TOL
+
+
+def random_case(t, M, N, K, seed, flavour=ol.QUANT_AVX):
+    rng = np.random.default_rng(seed)
+    a = rng.standard_normal((M, K), dtype=np.float32)
+    b = rng.standard_normal((N, K), dtype=np.float32)
+    vt = la.vec_dot_type(t)
+    A_q = ORACLE.quantize(t, a, ol.QUANT_REF)
+    fl = flavour if vt in (ol.Q8_0, ol.Q8_1) else ol.QUANT_REF
+    B_q = ORACLE.quantize(vt, b, fl)
+    return A_q, B_q
+
+
+SHAPES = [(1, 1, 256), (17, 3, 512), (31, 5, 768), (16, 8, 4096), (40, 7, 4096 + 256), (5, 9, 256),
+          (33, 17, 1024), (130, 2, 8192 + 512)]
+
+
+@pytest.mark.parametrize("t", ol.A_TYPES, ids=[ol.NAMES[t] for t in ol.A_TYPES])
+@pytest.mark.parametrize("shape", SHAPES, ids=[f"{m}x{n}x{k}" for m, n, k in SHAPES])
+def test_random_shapes_vs_oracle(t, shape):
+    """Ragged M (not a multiple of the 16-row tile), N across the GEMV (<=8) and
+    grouped/GEMM (>8) paths, K spanning several 4096-element segments."""
+    M, N, K = shape
+    A_q, B_q = random_case(t, M, N, K, seed=M * 1000 + N * 10 + K)
+    c, _ = gpu_mul_mat(t, A_q, B_q, M, N, K)
+    ref = ORACLE.mul_mat(t, M, N, K, A_q, B_q)
+    err = rel_err(c, ref, absdot(t, A_q, B_q, M, N, K)).max()
+    assert err < TOL, err
+
+
+@pytest.mark.parametrize("t", ol.A_TYPES, ids=[ol.NAMES[t] for t in ol.A_TYPES])
+def test_strided_operands(t):
+    """A rows padded (lda > K/blck), B columns padded (ldb), C rows padded (ldc > M);
+    bytes outside the logical C must stay untouched."""
+    M, N, K = 37, 6, 1024
+    kb = K // la.blck_size(t)
+    A_q, B_q = random_case(t, M, N, K, seed=7)
+    lda = pitch_blocks(t, kb + 5)
+    c, raw = gpu_mul_mat(t, A_q, B_q, M, N, K, ldc=M + 11, lda=lda, ldb=kb + 3)
+    ref = ORACLE.mul_mat(t, M, N, K, A_q, B_q)
+    assert rel_err(c, ref, absdot(t, A_q, B_q, M, N, K)).max() < TOL
+    gaps = np.concatenate([raw[j * (M + 11) + M:(j + 1) * (M + 11)] for j in range(N)])
+    assert np.isnan(gaps).all(), "kernel wrote outside the logical C"
+
+
+@pytest.mark.parametrize("t", ol.A_TYPES, ids=[ol.NAMES[t] for t in ol.A_TYPES])
+def test_known_answer_constant(t):
+    """src/la-benchmark-matmult.cpp:247-250: A=1, B=2 -> sum(C) = 2*K*M*N."""
+    M, N, K = 48, 3, 4096
+    vt = la.vec_dot_type(t)
+    A_q = ORACLE.quantize(t, np.ones((M, K), np.float32))
+    B_q = ORACLE.quantize(vt, np.full((N, K), 2.0, np.float32))
+    c, _ = gpu_mul_mat(t, A_q, B_q, M, N, K)
+    want = 2.0 * K * M * N
+    assert abs(c.sum(dtype=np.float64) - want) / want < 1e-2
+
+
+@pytest.mark.parametrize("t", [ol.Q4_0, ol.Q8_0, ol.Q2_K], ids=["q4_0", "q8_0", "q2_k"])
+def test_full_size_gemv_4096(t):
+    """BASELINE config 2 shape (M=4096, N=1, K=4096): every row vs the oracle."""
+    M, N, K = 4096, 1, 4096
+    A_q, B_q = random_case(t, M, N, K, seed=42)
+    c, _ = gpu_mul_mat(t, A_q, B_q, M, N, K)
+    ref = ORACLE.mul_mat(t, M, N, K, A_q, B_q)
+    assert rel_err(c, ref, absdot(t, A_q, B_q, M, N, K)).max() < TOL
+
+
+def test_extreme_quants():
+    """All-max / all-min quants (int8 -128/127 in B, nibble 0/15 in A): the exact
+    int32 block dots must not saturate (v_dot4 without clamp)."""
+    M, N, K = 16, 2, 4096
+    t = ol.Q4_0
+    A_q = ORACLE.quantize(t, np.full((M, K), -1.0, np.float32))
+    A_q.reshape(M, -1)[:, :] = A_q.reshape(M, -1)
+    B_q = ORACLE.quantize(ol.Q8_0, np.tile(np.where(np.arange(K) % 2 == 0, 1.0, -1.0).astype(np.float32), (N, 1)))
+    c, _ = gpu_mul_mat(t, A_q, B_q, M, N, K)
+    ref = ORACLE.mul_mat(t, M, N, K, A_q, B_q)
+    assert np.allclose(c, ref, rtol=0, atol=1e-3 * np.abs(ref).max() + 1e-6)

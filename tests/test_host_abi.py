@@ -1,0 +1,103 @@
+"""CPU tests of the C-ABI library: it loads, exports every symbol include/lamm_hip.h
+declares, its traits match the format contract, and argument validation behaves --
+no compute calls (there is no GPU here)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+import lamm_amd as la
+import oracle_lib as ol
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "lamm_hip.h")
+NO_GPU = la.device_count() == 0
+
+
+def declared_symbols():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(lamm_\w+)\s*\(", text)))
+
+
+def test_header_symbols_exported():
+    syms = declared_symbols()
+    assert {"lamm_can_mul_mat", "lamm_mul_mat", "lamm_get_opt_level", "lamm_hip_matmul"} <= set(syms)
+    for s in syms:
+        assert hasattr(la.lib, s), f"{s} declared in include/lamm_hip.h but not exported"
+
+
+def test_struct_layouts_match_b2430():
+    assert ctypes.sizeof(la.GgmlTensor) == 368
+    assert la.GgmlTensor.data.offset == 280 and la.GgmlTensor.src.offset == 160
+    assert la.GgmlTensor.ne.offset == 16 and la.GgmlTensor.nb.offset == 48
+    assert ctypes.sizeof(la.GgmlComputeParams) == 32 and la.GgmlComputeParams.wdata.offset == 24
+    assert ctypes.sizeof(la.Matrix) == 32 and la.Matrix.ld.offset == 24  # == struct Matrix
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference/llama.cpp-b2430"), reason="reference headers absent")
+def test_struct_layouts_against_reference_header(tmp_path):
+    src = tmp_path / "abi.c"
+    src.write_text(
+        '#include "ggml.h"\n#include <stdio.h>\n#include <stddef.h>\n'
+        'int main(){printf("%zu %zu %zu %zu %zu %zu\\n", sizeof(struct ggml_tensor),'
+        ' offsetof(struct ggml_tensor,data), offsetof(struct ggml_tensor,src), offsetof(struct ggml_tensor,nb),'
+        ' sizeof(struct ggml_compute_params), offsetof(struct ggml_compute_params,wdata));}\n')
+    exe = tmp_path / "abi"
+    import subprocess
+    subprocess.run(["gcc", "-I/root/reference/llama.cpp-b2430", str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()
+    assert list(map(int, out)) == [368, 280, 160, 48, 32, 24]
+
+
+def test_traits_match_oracle():
+    o = ol.Oracle()
+    for t in [ol.F32, ol.Q4_0, ol.Q4_1, ol.Q5_0, ol.Q5_1, ol.Q8_0, ol.Q8_1, ol.Q2_K, ol.Q8_K]:
+        assert la.blck_size(t) == o.block_elems(t)
+        assert la.type_size(t) == o.block_bytes(t)
+    for t in ol.A_TYPES:
+        assert la.vec_dot_type(t) == o.vec_dot_type(t)
+    assert la.vec_dot_type(1) == -1  # F16 is not on the lamm path (src/loongarch_matmul.cpp:37-52)
+
+
+def _mats(wtype=la.Q4_0, M=16, N=1, kb=128, lda=None):
+    vt = la.vec_dot_type(wtype)
+    A = la.Matrix(0x100000, wtype, M, kb, lda if lda is not None else kb)
+    B = la.Matrix(0x200000, vt, kb, N, kb)
+    C = la.Matrix(0x300000, la.F32, M, N, M)
+    return A, B, C
+
+
+def _rc(A, B, C):
+    return la.lib.lamm_hip_matmul(ctypes.byref(A), ctypes.byref(B), ctypes.byref(C), None)
+
+
+def test_validation_errors():
+    A, B, C = _mats()
+    B.type = la.Q8_1
+    assert _rc(A, B, C) == la.LAMM_ERR_TYPE
+    A, B, C = _mats()
+    A.type = 1  # F16 unsupported
+    assert _rc(A, B, C) == la.LAMM_ERR_TYPE
+    A, B, C = _mats()
+    B.row = 64
+    assert _rc(A, B, C) == la.LAMM_ERR_SHAPE
+    A, B, C = _mats(kb=3)          # q4_0 row of 3 blocks = 54 bytes: not a 16-byte pitch
+    assert _rc(A, B, C) == la.LAMM_ERR_ALIGN
+    A, B, C = _mats(kb=3, lda=8)   # pitched to 144 bytes: accepted
+    assert _rc(A, B, C) in (la.LAMM_OK, la.LAMM_ERR_NODEV)
+
+
+@pytest.mark.skipif(not NO_GPU, reason="checks the no-GPU behaviour")
+def test_no_gpu_behaviour():
+    A, B, C = _mats()
+    assert _rc(A, B, C) == la.LAMM_ERR_NODEV
+    assert la.get_opt_level() == 0
+    import ggml_emu
+    src0 = ggml_emu.Tensor(la.Q4_0, [64, 4], data=np.zeros(4 * 36, np.uint8))
+    src1 = ggml_emu.Tensor(la.F32, [64, 2], data=np.zeros(128, np.float32))
+    dst = ggml_emu.mul_mat_node(src0, src1)
+    # no GPU: the hook declines and ggml keeps its CPU loop
+    assert ggml_emu.compute(dst, nth=2) is False

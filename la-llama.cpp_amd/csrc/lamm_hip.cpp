@@ -123,7 +123,7 @@ extern "C" int lamm_hip_matmul_batched(const lamm_matrix* A, const lamm_matrix* 
   hipError_t e;
   if (N <= 8) {
     e = launch_gemv(A->type, p, s);
-  } else if (gemm_supported(A->type)) {
+  } else if (gemm_supported(A->type) && gemm_args_ok(A->type, p)) {
     e = launch_gemm(A->type, p, s);
   } else {
     e = hipSuccess;

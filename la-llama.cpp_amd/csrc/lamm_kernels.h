@@ -25,5 +25,6 @@ size_t gemv_lds_bytes(int type, int nc);
 
 hipError_t launch_gemm(int type, const GemvArgs& p, hipStream_t s);
 bool gemm_supported(int type);
+bool gemm_args_ok(int type, const GemvArgs& p);   // B pitch/alignment the GEMM staging needs
 
 }  // namespace lamm

@@ -44,18 +44,22 @@ template <> struct GF<kQ5_0> { static constexpr int ABPB = 22, VBPB = 34; };
 template <> struct GF<kQ5_1> { static constexpr int ABPB = 24, VBPB = 36; };
 template <> struct GF<kQ8_0> { static constexpr int ABPB = 34, VBPB = 34; };
 
+// ---- 32-element block formats ----------------------------------------------------
+// 512 threads = 8 waves laid out 4 (j) x 2 (i); each wave owns one 32x32 MFMA tile.
+constexpr int GT8 = 512;
+
 template <int T>
 struct GemmSmem {
   static constexpr int RA = TI * KBLK * GF<T>::ABPB;   // raw A bytes per K-step
   static constexpr int RB = TJ * KBLK * GF<T>::VBPB;   // raw B bytes per K-step
   static constexpr int RA_PIECES = RA / 16, RB_PIECES = RB / 16;
-  static constexpr int RA_NPT = (RA_PIECES + GT - 1) / GT, RB_NPT = (RB_PIECES + GT - 1) / GT;
-  uint32_t rawA[RA_NPT * GT * 4 + 4];
-  uint32_t rawB[RB_NPT * GT * 4 + 4];
+  static constexpr int RA_NPT = (RA_PIECES + GT8 - 1) / GT8, RB_NPT = (RB_PIECES + GT8 - 1) / GT8;
+  uint32_t rawA[RA_NPT * GT8 * 4 + 4];
+  uint32_t rawB[RB_NPT * GT8 * 4 + 4];
   uint32_t wt[TI * ROWB / 4];
   uint32_t act[TJ * ROWB / 4];
-  float da[KBLK][TI];
-  float db[KBLK][TJ];
+  _Float16 dah[KBLK][TI];       // fp16 scales, exactly as stored in the blocks
+  _Float16 dbh[KBLK][TJ];
   _Float16 mah[TI][KBLK];
   _Float16 sbh[TJ][KBLK];
 };
@@ -78,17 +82,13 @@ __device__ __forceinline__ void lds_block(const uint32_t* base, int byte_off, ui
 }
 
 template <int T>
-__device__ __forceinline__ void unpack_weight(const uint32_t (&m)[(GF<T>::ABPB + 3) / 4], uint32_t (&q)[8],
-                                              float& d, _Float16& mh) {
-  d = h2f(m[0] & 0xffff);
-  mh = (_Float16)0.f;
+__device__ __forceinline__ void unpack_weight(const uint32_t (&m)[(GF<T>::ABPB + 3) / 4], uint32_t (&q)[8]) {
   if constexpr (T == kQ8_0) {
     unroll<8>([&](auto K) { q[K] = get32<2 + 4 * K>(m); });
   } else {
     constexpr bool AFF = (T == kQ4_1 || T == kQ5_1);
     constexpr bool FIVE = (T == kQ5_0 || T == kQ5_1);
     constexpr int QS = (AFF ? 4 : 2) + (FIVE ? 4 : 0);
-    if constexpr (AFF) mh = __builtin_bit_cast(_Float16, (uint16_t)(m[0] >> 16));
     uint32_t qh = 0;
     if constexpr (FIVE) qh = get32<AFF ? 4 : 2>(m);
     unroll<4>([&](auto K) {
@@ -108,78 +108,80 @@ __device__ __forceinline__ void unpack_weight(const uint32_t (&m)[(GF<T>::ABPB +
 }
 
 template <int T>
-__global__ __launch_bounds__(GT) void gemm_kernel(GemvArgs p) {
+__global__ __launch_bounds__(GT8) void gemm_kernel(GemvArgs p) {
   using S = GemmSmem<T>;
   constexpr int ABPB = GF<T>::ABPB, VBPB = GF<T>::VBPB;
   constexpr bool AFF = (T == kQ4_1 || T == kQ5_1);
+  constexpr int APR = KBLK * ABPB / 16, BPR = KBLK * VBPB / 16;   // 16-byte pieces per row
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   S& sm = *reinterpret_cast<S*>(smem_raw);
 
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int lr = lane & 31, h = lane >> 5;
-  const int wj = w >> 1, wi = w & 1;
+  const int wj = w >> 1, wi = w & 1;             // wave tile: rows jb..jb+31, cols ib..ib+31
+  const int jb = 32 * wj, ib = 32 * wi;
   const int64_t i0 = (int64_t)blockIdx.x * TI, j0 = (int64_t)blockIdx.y * TJ;
   const int z = blockIdx.z, i12 = z % p.ne12, i13 = z / p.ne12;
-  const unsigned char* Az = p.A + (int64_t)(i12 / p.r2) * p.sa2 + (int64_t)(i13 / p.r3) * p.sa3;
-  const unsigned char* Bz = p.B + (int64_t)i12 * p.sb2 + (int64_t)i13 * p.sb3;
+  const unsigned char* Az = p.A + (int64_t)(i12 / p.r2) * p.sa2 + (int64_t)(i13 / p.r3) * p.sa3 + i0 * p.lda;
+  const unsigned char* Bz = p.B + (int64_t)i12 * p.sb2 + (int64_t)i13 * p.sb3 + j0 * p.ldb;
   float* Cz = p.C + (int64_t)i12 * p.sc2 + (int64_t)i13 * p.sc3;
   const int rowsA = (int)min((int64_t)TI, (int64_t)p.M - i0);
   const int rowsB = (int)min((int64_t)TJ, (int64_t)p.N - j0);
+  const int64_t a_end = (int64_t)(rowsA - 1) * p.lda + (int64_t)p.nblk * ABPB;   // bytes readable from Az
+  const int64_t b_end = (int64_t)(rowsB - 1) * p.ldb + (int64_t)p.nblk * VBPB;
 
-  f32x16 acc[2], macc[2];
+  // per-thread piece offsets within a K-step (constant over K)
+  uint32_t aoff[S::RA_NPT], boff[S::RB_NPT];
 #pragma unroll
-  for (int r = 0; r < 2; ++r)
+  for (int k = 0; k < S::RA_NPT; ++k) {
+    const int pc = t + k * GT8, rr = pc / APR, oo = pc % APR;
+    aoff[k] = (pc < S::RA_PIECES && rr < rowsA) ? (uint32_t)(rr * p.lda + 16 * oo) : 0x7ffffff0u;
+  }
 #pragma unroll
-    for (int e = 0; e < 16; ++e) { acc[r][e] = 0.f; macc[r][e] = 0.f; }
+  for (int k = 0; k < S::RB_NPT; ++k) {
+    const int pc = t + k * GT8, rr = pc / BPR, oo = pc % BPR;
+    boff[k] = (pc < S::RB_PIECES && rr < rowsB) ? (uint32_t)(rr * p.ldb + 16 * oo) : 0x7ffffff0u;
+  }
+
+  u32x4 va[S::RA_NPT], vb[S::RB_NPT];
+  auto issue = [&](int ks) {   // global -> registers for K-step ks (OOB reads return 0)
+    const int64_t ka = (int64_t)ks * KBLK * ABPB, kbb = (int64_t)ks * KBLK * VBPB;
+    const auto ra = make_rsrc(Az + ka, (uint32_t)min((a_end - ka + 3) & ~int64_t(3), (int64_t)0x7fffffff));
+    const auto rb = make_rsrc(Bz + kbb, (uint32_t)min((b_end - kbb + 3) & ~int64_t(3), (int64_t)0x7fffffff));
+#pragma unroll
+    for (int k = 0; k < S::RA_NPT; ++k) va[k] = bload16(ra, aoff[k]);
+#pragma unroll
+    for (int k = 0; k < S::RB_NPT; ++k) vb[k] = bload16(rb, boff[k]);
+  };
+
+  f32x16 acc, macc;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) { acc[e] = 0.f; macc[e] = 0.f; }
 
   const int nsteps = (p.nblk + KBLK - 1) / KBLK;
+  issue(0);
   for (int ks = 0; ks < nsteps; ++ks) {
     const int kb0 = ks * KBLK;
-    // ---- 1. raw tiles -> LDS (coalesced 16-byte buffer loads; OOB reads return 0) ----
-    {
-      const unsigned char* abase = Az + i0 * p.lda + (int64_t)kb0 * ABPB;
-      const int64_t avail = (int64_t)(rowsA - 1) * p.lda + (int64_t)(p.nblk - kb0) * ABPB;
-      const auto ra = make_rsrc(abase, (uint32_t)min((avail + 3) & ~int64_t(3), (int64_t)0x7fffffff));
-      const unsigned char* bbase = Bz + j0 * p.ldb + (int64_t)kb0 * VBPB;
-      const int64_t bavail = (int64_t)(rowsB - 1) * p.ldb + (int64_t)(p.nblk - kb0) * VBPB;
-      const auto rb = make_rsrc(bbase, (uint32_t)min((bavail + 3) & ~int64_t(3), (int64_t)0x7fffffff));
-      u32x4 va[S::RA_NPT], vb[S::RB_NPT];
+    // ---- registers (loaded during the previous step's MFMAs) -> raw LDS ----
 #pragma unroll
-      for (int k = 0; k < S::RA_NPT; ++k) {
-        const int pc = t + k * GT;
-        const int rr = pc / (KBLK * ABPB / 16), oo = pc % (KBLK * ABPB / 16);
-        const uint32_t off = (pc < S::RA_PIECES && rr < rowsA) ? (uint32_t)(rr * p.lda + 16 * oo) : 0x7ffffff0u;
-        va[k] = bload16(ra, off);
-      }
+    for (int k = 0; k < S::RA_NPT; ++k) *(u32x4*)&sm.rawA[4 * (t + k * GT8)] = va[k];
 #pragma unroll
-      for (int k = 0; k < S::RB_NPT; ++k) {
-        const int pc = t + k * GT;
-        const int rr = pc / (KBLK * VBPB / 16), oo = pc % (KBLK * VBPB / 16);
-        const uint32_t off = (pc < S::RB_PIECES && rr < rowsB) ? (uint32_t)(rr * p.ldb + 16 * oo) : 0x7ffffff0u;
-        vb[k] = bload16(rb, off);
-      }
-#pragma unroll
-      for (int k = 0; k < S::RA_NPT; ++k) *(u32x4*)&sm.rawA[4 * (t + k * GT)] = va[k];
-#pragma unroll
-      for (int k = 0; k < S::RB_NPT; ++k) *(u32x4*)&sm.rawB[4 * (t + k * GT)] = vb[k];
-    }
+    for (int k = 0; k < S::RB_NPT; ++k) *(u32x4*)&sm.rawB[4 * (t + k * GT8)] = vb[k];
     __syncthreads();
-    // ---- 2. unpack to int8 + scales ----
-    for (int it = t; it < TI * KBLK; it += GT) {
+    // ---- unpack to int8 + fp16 scales (one item = one (row, block)) ----
+    for (int it = t; it < TI * KBLK; it += GT8) {
       const int il = it / KBLK, b = it % KBLK;
       uint32_t m[(ABPB + 3) / 4], q[8];
       lds_block(sm.rawA, il * KBLK * ABPB + b * ABPB, m);
-      float d;
-      _Float16 mh;
-      unpack_weight<T>(m, q, d, mh);
+      unpack_weight<T>(m, q);
       const bool ok = il < rowsA && kb0 + b < p.nblk;
       u32x4* dst = (u32x4*)&sm.wt[(il * ROWB + 32 * b) / 4];
       dst[0] = ok ? u32x4{q[0], q[1], q[2], q[3]} : u32x4{0, 0, 0, 0};
       dst[1] = ok ? u32x4{q[4], q[5], q[6], q[7]} : u32x4{0, 0, 0, 0};
-      sm.da[b][il] = ok ? d : 0.f;
-      if constexpr (AFF) sm.mah[il][b] = ok ? mh : (_Float16)0.f;
+      sm.dah[b][il] = __builtin_bit_cast(_Float16, (uint16_t)(ok ? (m[0] & 0xffff) : 0));
+      if constexpr (AFF) sm.mah[il][b] = __builtin_bit_cast(_Float16, (uint16_t)(ok ? (m[0] >> 16) : 0));
     }
-    for (int it = t; it < TJ * KBLK; it += GT) {
+    for (int it = t; it < TJ * KBLK; it += GT8) {
       const int jl = it / KBLK, b = it % KBLK;
       uint32_t m[(VBPB + 3) / 4];
       lds_block(sm.rawB, jl * KBLK * VBPB + b * VBPB, m);
@@ -189,51 +191,43 @@ __global__ __launch_bounds__(GT) void gemm_kernel(GemvArgs p) {
       dst[0] = ok ? u32x4{get32<VQS>(m), get32<VQS + 4>(m), get32<VQS + 8>(m), get32<VQS + 12>(m)} : u32x4{0, 0, 0, 0};
       dst[1] = ok ? u32x4{get32<VQS + 16>(m), get32<VQS + 20>(m), get32<VQS + 24>(m), get32<VQS + 28>(m)}
                   : u32x4{0, 0, 0, 0};
-      sm.db[b][jl] = ok ? h2f(m[0] & 0xffff) : 0.f;
-      if constexpr (AFF) sm.sbh[jl][b] = ok ? __builtin_bit_cast(_Float16, (uint16_t)(m[0] >> 16)) : (_Float16)0.f;
+      sm.dbh[b][jl] = __builtin_bit_cast(_Float16, (uint16_t)(ok ? (m[0] & 0xffff) : 0));
+      if constexpr (AFF) sm.sbh[jl][b] = __builtin_bit_cast(_Float16, (uint16_t)(ok ? (m[0] >> 16) : 0));
     }
     __syncthreads();
-    // ---- 3. MFMA: exact int32 block dots, fp32 scale epilogue ----
-#pragma unroll
+    // ---- next step's global loads fly during this step's MFMAs ----
+    if (ks + 1 < nsteps) issue(ks + 1);
+    // ---- MFMA: exact int32 block dots; d_a*d_b on the fp16 MFMA; acc += P * S ----
+#pragma unroll 2
     for (int b = 0; b < KBLK; ++b) {
-      const i32x4 wf = *(const i32x4*)&sm.wt[((32 * wi + lr) * ROWB + 32 * b + 16 * h) / 4];
-      const float dai = sm.da[b][32 * wi + lr];
+      const i32x4 wf = *(const i32x4*)&sm.wt[((ib + lr) * ROWB + 32 * b + 16 * h) / 4];
+      const i32x4 af = *(const i32x4*)&sm.act[((jb + lr) * ROWB + 32 * b + 16 * h) / 4];
+      const i32x16 zero = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+      const i32x16 sdot = __builtin_amdgcn_mfma_i32_32x32x32_i8(af, wf, zero, 0, 0, 0);
+      // outer product d_b[j] * d_a[i] (k = 0 only): fp16 x fp16 is exact in fp32
+      const _Float16 hz = (_Float16)0.f;
+      const half8 dbv = {h == 0 ? sm.dbh[b][jb + lr] : hz, hz, hz, hz, hz, hz, hz, hz};
+      const half8 dav = {h == 0 ? sm.dah[b][ib + lr] : hz, hz, hz, hz, hz, hz, hz, hz};
+      const f32x16 fz = {};
+      const f32x16 sc = __builtin_amdgcn_mfma_f32_32x32x16_f16(dbv, dav, fz, 0, 0, 0);
 #pragma unroll
-      for (int rt = 0; rt < 2; ++rt) {
-        const int jb = 64 * wj + 32 * rt;
-        const i32x4 af = *(const i32x4*)&sm.act[((jb + lr) * ROWB + 32 * b + 16 * h) / 4];
-        i32x16 zero = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-        const i32x16 s = __builtin_amdgcn_mfma_i32_32x32x32_i8(af, wf, zero, 0, 0, 0);
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const f32x4 dbv = *(const f32x4*)&sm.db[b][jb + 8 * g + 4 * h];
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            acc[rt][4 * g + e] = __builtin_fmaf((float)s[4 * g + e], dai * dbv[e], acc[rt][4 * g + e]);
-        }
-      }
+      for (int r = 0; r < 16; ++r) acc[r] = __builtin_fmaf((float)sdot[r], sc[r], acc[r]);
     }
     if constexpr (AFF) {
       // sum_b m_a[i,b] * s_b[j,b] over this K-step's 8 blocks: one exact fp16 MFMA
-      const half4 mf = *(const half4*)&sm.mah[32 * wi + lr][4 * h];
-#pragma unroll
-      for (int rt = 0; rt < 2; ++rt) {
-        const half4 sf = *(const half4*)&sm.sbh[64 * wj + 32 * rt + lr][4 * h];
-        macc[rt] = __builtin_amdgcn_mfma_f32_32x32x8f16(sf, mf, macc[rt], 0, 0, 0);
-      }
+      const half4 mf = *(const half4*)&sm.mah[ib + lr][4 * h];
+      const half4 sf = *(const half4*)&sm.sbh[jb + lr][4 * h];
+      macc = __builtin_amdgcn_mfma_f32_32x32x8f16(sf, mf, macc, 0, 0, 0);
     }
     __syncthreads();
   }
 
   // ---- epilogue: C[j*ldc + i], lanes own i (128-byte segments) ----
-  const int64_t i = i0 + 32 * wi + lr;
+  const int64_t i = i0 + ib + lr;
 #pragma unroll
-  for (int rt = 0; rt < 2; ++rt) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int64_t j = j0 + 64 * wj + 32 * rt + (r & 3) + 8 * (r >> 2) + 4 * h;
-      if (i < p.M && j < p.N) Cz[j * p.ldc + i] = acc[rt][r] + (AFF ? macc[rt][r] : 0.f);
-    }
+  for (int r = 0; r < 16; ++r) {
+    const int64_t j = j0 + jb + (r & 3) + 8 * (r >> 2) + 4 * h;
+    if (i < p.M && j < p.N) Cz[j * p.ldc + i] = acc[r] + (AFF ? macc[r] : 0.f);
   }
 }
 
@@ -379,10 +373,10 @@ __global__ __launch_bounds__(GT) void gemm_q2k_kernel(GemvArgs p) {
 }
 
 template <class K>
-hipError_t launch_with(K kern, size_t lds, const GemvArgs& p, hipStream_t s) {
+hipError_t launch_with(K kern, size_t lds, int threads, const GemvArgs& p, hipStream_t s) {
   const dim3 grid((unsigned)((p.M + TI - 1) / TI), (unsigned)((p.N + TJ - 1) / TJ), (unsigned)(p.ne12 * p.ne13));
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(kern, grid, dim3(GT), lds, s, p);
+  hipLaunchKernelGGL(kern, grid, dim3(threads), lds, s, p);
   return hipGetLastError();
 }
 
@@ -400,12 +394,12 @@ bool gemm_args_ok(int type, const GemvArgs& p) {
 
 hipError_t launch_gemm(int type, const GemvArgs& p, hipStream_t s) {
   switch (type) {
-    case kQ4_0: return launch_with(gemm_kernel<kQ4_0>, sizeof(GemmSmem<kQ4_0>), p, s);
-    case kQ4_1: return launch_with(gemm_kernel<kQ4_1>, sizeof(GemmSmem<kQ4_1>), p, s);
-    case kQ5_0: return launch_with(gemm_kernel<kQ5_0>, sizeof(GemmSmem<kQ5_0>), p, s);
-    case kQ5_1: return launch_with(gemm_kernel<kQ5_1>, sizeof(GemmSmem<kQ5_1>), p, s);
-    case kQ8_0: return launch_with(gemm_kernel<kQ8_0>, sizeof(GemmSmem<kQ8_0>), p, s);
-    case kQ2_K: return launch_with(gemm_q2k_kernel, sizeof(Q2KSmem), p, s);
+    case kQ4_0: return launch_with(gemm_kernel<kQ4_0>, sizeof(GemmSmem<kQ4_0>), GT8, p, s);
+    case kQ4_1: return launch_with(gemm_kernel<kQ4_1>, sizeof(GemmSmem<kQ4_1>), GT8, p, s);
+    case kQ5_0: return launch_with(gemm_kernel<kQ5_0>, sizeof(GemmSmem<kQ5_0>), GT8, p, s);
+    case kQ5_1: return launch_with(gemm_kernel<kQ5_1>, sizeof(GemmSmem<kQ5_1>), GT8, p, s);
+    case kQ8_0: return launch_with(gemm_kernel<kQ8_0>, sizeof(GemmSmem<kQ8_0>), GT8, p, s);
+    case kQ2_K: return launch_with(gemm_q2k_kernel, sizeof(Q2KSmem), GT, p, s);
     default: return hipErrorInvalidValue;
   }
 }

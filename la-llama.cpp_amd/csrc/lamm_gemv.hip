@@ -21,6 +21,8 @@
 #include "lamm_device.h"
 #include "lamm_kernels.h"
 
+#include <cstdlib>
+
 namespace lamm {
 namespace {
 
@@ -71,8 +73,8 @@ struct Smem {
 };
 
 // ---- stage the activation segment (decoded) into LDS --------------------------
-template <int T, int NC>
-__device__ __forceinline__ void stage_b(Smem<T, NC>& sm, const GemvArgs& p, const unsigned char* Bz, int seg) {
+template <int T, int NC, class SM>
+__device__ __forceinline__ void stage_b(SM& sm, const GemvArgs& p, const unsigned char* Bz, int seg) {
   using GG = Geo<T>;
   using F = Fmt<T>;
   const int t = threadIdx.x;
@@ -140,8 +142,8 @@ __device__ __forceinline__ void stage_b(Smem<T, NC>& sm, const GemvArgs& p, cons
 }
 
 // ---- one A block (compile-time position G_IDX in the chunk) x NC columns -------
-template <int T, int NC, int GI>
-__device__ __forceinline__ void block_dot(const uint32_t (&w)[Geo<T>::CH_WORDS + 1], const Smem<T, NC>& sm,
+template <int T, int NC, int GI, class SM>
+__device__ __forceinline__ void block_dot(const uint32_t (&w)[Geo<T>::CH_WORDS + 1], const SM& sm,
                                           int ch, int ncols, float (&acc)[NC]) {
   using F = Fmt<T>;
   constexpr int O = GI * F::BPB;
@@ -234,9 +236,9 @@ __device__ __forceinline__ void block_dot(const uint32_t (&w)[Geo<T>::CH_WORDS +
 
 // f32: the chunk is 64 consecutive floats; elements past K (nvalid) are masked so
 // row padding (possibly NaN) never reaches the sum.
-template <int NC>
+template <int NC, class SM>
 __device__ __forceinline__ void chunk_dot_f32(const uint32_t (&w)[Geo<kF32>::CH_WORDS + 1],
-                                              const Smem<kF32, NC>& sm, int ch, int nvalid, int ncols,
+                                              const SM& sm, int ch, int nvalid, int ncols,
                                               float (&acc)[NC]) {
   float a[64];
 #pragma unroll
@@ -256,8 +258,8 @@ __device__ __forceinline__ void chunk_dot_f32(const uint32_t (&w)[Geo<kF32>::CH_
   }
 }
 
-template <int T, int NC, int GI>
-__device__ __forceinline__ void chunk_dot(const uint32_t (&w)[Geo<T>::CH_WORDS + 1], const Smem<T, NC>& sm,
+template <int T, int NC, int GI, class SM>
+__device__ __forceinline__ void chunk_dot(const uint32_t (&w)[Geo<T>::CH_WORDS + 1], const SM& sm,
                                           int ch, int nvalid, int ncols, float (&acc)[NC]) {
   if constexpr (T == kF32) {
     chunk_dot_f32<NC>(w, sm, ch, nvalid, ncols, acc);
@@ -267,7 +269,10 @@ __device__ __forceinline__ void chunk_dot(const uint32_t (&w)[Geo<T>::CH_WORDS +
   }
 }
 
-template <int T, int NC>
+// V (A staging variant): 0 = 16-byte buffer loads to VGPRs + ds_write;
+// 1 = LDS-DMA (buffer_load_dwordx4 ... lds) with the non-temporal policy (A is read
+// once); 2 = LDS-DMA, default policy; 3 = VGPR staging with non-temporal loads.
+template <int T, int NC, int V = 0>
 __global__ __launch_bounds__(kThreads) void gemv_kernel(GemvArgs p) {
   using GG = Geo<T>;
   using F = Fmt<T>;
@@ -295,23 +300,34 @@ __global__ __launch_bounds__(kThreads) void gemv_kernel(GemvArgs p) {
     const unsigned char* abase = Az + r0 * p.lda + (int64_t)seg * GG::ROW_BYTES;
     const int64_t avail = (int64_t)(rows - 1) * p.lda + row_bytes - (int64_t)seg * GG::ROW_BYTES;
     const auto ra = make_rsrc(abase, (uint32_t)min((avail + 3) & ~int64_t(3), (int64_t)0x7fffffff));
-    u32x4 v[GG::A_NPT];
+    [[maybe_unused]] u32x4 v[GG::A_NPT];
 #pragma unroll
     for (int k = 0; k < GG::A_NPT; ++k) {
       const int pc = t + k * kThreads;
       const int rr = pc / (GG::ROW_BYTES / 16), oo = pc % (GG::ROW_BYTES / 16);
       const uint32_t off = (pc < GG::A_PIECES && rr < rows) ? (uint32_t)(rr * p.lda + 16 * oo) : 0x7ffffff0u;
-      v[k] = bload16(ra, off);
+      if constexpr (V == 1 || V == 2 || V >= 4) {
+        // lane-linear LDS destination: wave-uniform base + 16 * lane
+        const int wbase = k * kThreads + (t & ~63);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            ra, (__attribute__((address_space(3))) void*)(sm.a + 4 * wbase), 16, off, 0, 0, V == 2 ? 0 : 2);
+      } else if constexpr (V == 3) {
+        v[k] = __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, 2);
+      } else {
+        v[k] = bload16(ra, off);
+      }
     }
     // ---- activations (L2-resident) decoded into LDS ----
-    stage_b<T, NC>(sm, p, Bz, seg);
+    if constexpr (V != 5) stage_b<T, NC>(sm, p, Bz, seg);
+    if constexpr (V == 0 || V == 3) {
 #pragma unroll
-    for (int k = 0; k < GG::A_NPT; ++k) *(u32x4*)&sm.a[4 * (t + k * kThreads)] = v[k];
+      for (int k = 0; k < GG::A_NPT; ++k) *(u32x4*)&sm.a[4 * (t + k * kThreads)] = v[k];
+    }
     __syncthreads();
 
     // ---- compute this thread's chunk ----
     const int cb0 = seg * GG::SEG_BLK + ch * F::G;           // first A block of chunk
-    if (row < rows && cb0 < p.nblk) {
+    if (V != 4 && row < rows && cb0 < p.nblk) {
       uint32_t w[GG::CH_WORDS + 1];
       const uint32_t* src = &sm.a[(row * GG::ROW_BYTES + ch * GG::CH_BYTES) / 4];
       if constexpr (GG::CH_BYTES % 16 == 0) {
@@ -348,18 +364,192 @@ __global__ __launch_bounds__(kThreads) void gemv_kernel(GemvArgs p) {
   }
 }
 
+// ---- wave-streaming single-segment kernel (K <= one segment: 4096 elements) --------
+// Each WAVE owns groups of 4 rows (its 64 lanes = 4 rows x 16 chunks).  Group g+1 is
+// loaded HBM -> VGPRs (non-temporal 16-byte buffer loads) while group g is computed
+// from the wave's private LDS slot, so every wave keeps a group in flight during its
+// compute and the register file (3x the LDS) is the landing zone.  A wave reads only
+// the LDS bytes it wrote itself: no workgroup barrier in the loop, the waves of a CU
+// desynchronise.  B is decoded once per workgroup and reused by all its groups.
+constexpr int kWRows = 4;   // rows per wave group
+
+template <int T> struct WGeo {
+  using GG = Geo<T>;
+  static constexpr int BYTES = kWRows * GG::ROW_BYTES;    // one wave group
+  static constexpr int NPW = (BYTES + 1023) / 1024;       // 16-byte loads per lane
+  static constexpr int SLOT = NPW * 1024;
+};
+
+template <int T, int NC, int WAVES>
+struct SmemStream {
+  using GG = Geo<T>;
+  uint32_t a[WAVES][WGeo<T>::SLOT / 4];
+  uint32_t bq[NC][GG::BQ_WORDS];
+  float bd[NC][T == kF32 ? 1 : GG::VBLK];
+  float bx[NC][T == kF32 ? 1 : GG::VBLK];
+  int bs[NC][T == kQ2_K ? GG::VBLK * 16 : 1];
+};
+
+template <int T, int NC, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void gemv_stream_kernel(GemvArgs p) {
+  using GG = Geo<T>;
+  using WG = WGeo<T>;
+  using F = Fmt<T>;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  SmemStream<T, NC, WAVES>& sm = *reinterpret_cast<SmemStream<T, NC, WAVES>*>(smem_raw);
+
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int row = lane / kSC, ch = lane % kSC;
+  const int z = blockIdx.y, i12 = z % p.ne12, i13 = z / p.ne12;
+  const unsigned char* Az = p.A + (int64_t)(i12 / p.r2) * p.sa2 + (int64_t)(i13 / p.r3) * p.sa3;
+  const unsigned char* Bz = p.B + (int64_t)i12 * p.sb2 + (int64_t)i13 * p.sb3;
+  float* Cz = p.C + (int64_t)i12 * p.sc2 + (int64_t)i13 * p.sc3;
+  const int ngroups = (p.M + kWRows - 1) / kWRows;
+  const int row_bytes = p.nblk * F::BPB;
+  const int ncols = p.N < NC ? p.N : NC;
+  const int stride = gridDim.x * WAVES;
+
+  u32x4 v[WG::NPW];
+  auto load = [&](int q) {
+    const int64_t r0 = (int64_t)q * kWRows;
+    const int rows = (int)min((int64_t)kWRows, (int64_t)p.M - r0);
+    const int64_t avail = (int64_t)(rows - 1) * p.lda + row_bytes;
+    const auto ra = make_rsrc(Az + r0 * p.lda, (uint32_t)min((avail + 3) & ~int64_t(3), (int64_t)0x7fffffff));
+#pragma unroll
+    for (int k = 0; k < WG::NPW; ++k) {
+      const int pc = lane + 64 * k;
+      const int rr = pc / (GG::ROW_BYTES / 16), oo = pc % (GG::ROW_BYTES / 16);
+      const uint32_t off = (pc * 16 < WG::BYTES && rr < rows) ? (uint32_t)(rr * p.lda + 16 * oo) : 0x7ffffff0u;
+      v[k] = __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, 2);   // nt: streamed once
+    }
+  };
+
+  int q = blockIdx.x * WAVES + w;
+  if (q < ngroups) load(q);
+  stage_b<T, NC>(sm, p, Bz, 0);
+  __syncthreads();   // B visible to every wave
+
+  for (; q < ngroups; q += stride) {
+#pragma unroll
+    for (int k = 0; k < WG::NPW; ++k) *(u32x4*)&sm.a[w][4 * (lane + 64 * k)] = v[k];
+    const int qn = q + stride;
+    if (qn < ngroups) load(qn);      // in flight during this group's compute
+
+    const int64_t r0 = (int64_t)q * kWRows;
+    const int rows = (int)min((int64_t)kWRows, (int64_t)p.M - r0);
+    float acc[NC];
+#pragma unroll
+    for (int j = 0; j < NC; ++j) acc[j] = 0.f;
+    const int cb0 = ch * F::G;
+    if (row < rows && cb0 < p.nblk) {
+      uint32_t wv[GG::CH_WORDS + 1];
+      const uint32_t* src = &sm.a[w][(row * GG::ROW_BYTES + ch * GG::CH_BYTES) / 4];
+      if constexpr (GG::CH_BYTES % 16 == 0) {
+#pragma unroll
+        for (int c = 0; c < GG::CH_WORDS / 4; ++c) {
+          const u32x4 x = *(const u32x4*)&src[4 * c];
+          wv[4 * c] = x[0]; wv[4 * c + 1] = x[1]; wv[4 * c + 2] = x[2]; wv[4 * c + 3] = x[3];
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < GG::CH_WORDS; ++c) wv[c] = src[c];
+      }
+      wv[GG::CH_WORDS] = 0;
+      chunk_dot<T, NC, 0>(wv, sm, ch, min(F::G, p.nblk - cb0), ncols, acc);
+    }
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      float x = acc[j];
+      x += __shfl_xor(x, 8);
+      x += __shfl_xor(x, 4);
+      x += __shfl_xor(x, 2);
+      x += __shfl_xor(x, 1);
+      acc[j] = x;
+    }
+    if (ch == 0 && row < rows) {
+#pragma unroll
+      for (int j = 0; j < NC; ++j)
+        if (j < ncols) Cz[(int64_t)j * p.ldc + r0 + row] = acc[j];
+    }
+  }
+}
+
+template <int T, int NC, int WAVES>
+constexpr bool stream_fits() { return sizeof(SmemStream<T, NC, WAVES>) <= 160 * 1024; }
+
+template <int T, int NC, int WAVES>
+hipError_t launch_stream_w(const GemvArgs& p, hipStream_t s, int gx) {
+  const size_t lds = sizeof(SmemStream<T, NC, WAVES>);
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)gemv_stream_kernel<T, NC, WAVES>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((gemv_stream_kernel<T, NC, WAVES>), dim3(gx, p.ne12 * p.ne13), dim3(64 * WAVES), lds, s, p);
+  return hipGetLastError();
+}
+
 template <int T, int NC>
-hipError_t launch_t(const GemvArgs& p, hipStream_t s) {
+hipError_t launch_stream(const GemvArgs& p, hipStream_t s) {
+  const int ngroups = (p.M + kWRows - 1) / kWRows;
+  const int slices = p.ne12 * p.ne13;
+  // 8-wave workgroups when there is enough work for >= 2 per CU, else 4-wave ones
+  constexpr bool fit8 = stream_fits<T, NC, 8>();
+  const bool big = fit8 && (int64_t)ngroups * slices >= 2 * 256 * 8 * 2;
+  const int waves = big ? 8 : 4;
+  const size_t lds = big ? sizeof(SmemStream<T, NC, 8>) : sizeof(SmemStream<T, NC, 4>);
+  int per_cu = (int)((160 * 1024) / lds);
+  per_cu = per_cu < 1 ? 1 : (per_cu > 4 ? 4 : per_cu);
+  // all workgroups resident in ONE round (no tail round): floor, not ceil
+  int gx = (256 * per_cu) / slices;
+  const int gmax = (ngroups + waves - 1) / waves;
+  gx = gx < 1 ? 1 : (gx > gmax ? gmax : gx);
+  if constexpr (fit8) {
+    if (big) return launch_stream_w<T, NC, 8>(p, s, gx);
+  }
+  return launch_stream_w<T, NC, 4>(p, s, gx);
+}
+
+template <int T, int NC, int V = 0>
+hipError_t launch_v(const GemvArgs& p, hipStream_t s) {
   const size_t lds = sizeof(Smem<T, NC>);
   const int grid = (int)((p.M + kRows - 1) / kRows);
   if (grid == 0) return hipSuccess;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)gemv_kernel<T, NC>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute((const void*)gemv_kernel<T, NC, V>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
     attr_set = true;
   }
-  hipLaunchKernelGGL((gemv_kernel<T, NC>), dim3(grid, p.ne12 * p.ne13), dim3(kThreads), lds, s, p);
+  hipLaunchKernelGGL((gemv_kernel<T, NC, V>), dim3(grid, p.ne12 * p.ne13), dim3(kThreads), lds, s, p);
   return hipGetLastError();
+}
+
+int variant() {
+  const char* e = getenv("LAMM_GEMV_VARIANT");
+  return e ? atoi(e) : 0;
+}
+
+template <int T, int NC>
+hipError_t launch_t(const GemvArgs& p, hipStream_t s) {
+  const int v = variant();
+  if constexpr (stream_fits<T, NC, 4>()) {
+    if (p.nblk <= Geo<T>::SEG_BLK && v == 0) return launch_stream<T, NC>(p, s);
+  }
+  if constexpr (T == kQ4_0 && NC == 1) {
+    switch (v) {
+      case 1: return launch_v<T, NC, 1>(p, s);
+      case 2: return launch_v<T, NC, 2>(p, s);
+      case 3: return launch_v<T, NC, 3>(p, s);
+      case 4: return launch_v<T, NC, 4>(p, s);   // ablation: no compute (timing only)
+      case 5: return launch_v<T, NC, 5>(p, s);   // ablation: no B staging (timing only)
+      case 7: return launch_v<T, NC, 0>(p, s);   // force the segmented kernel
+      default: break;
+    }
+  }
+  return launch_v<T, NC, 0>(p, s);
 }
 
 template <int T>

@@ -48,22 +48,6 @@ template <> struct GF<kQ8_0> { static constexpr int ABPB = 34, VBPB = 34; };
 // 512 threads = 8 waves laid out 4 (j) x 2 (i); each wave owns one 32x32 MFMA tile.
 constexpr int GT8 = 512;
 
-template <int T>
-struct GemmSmem {
-  static constexpr int RA = TI * KBLK * GF<T>::ABPB;   // raw A bytes per K-step
-  static constexpr int RB = TJ * KBLK * GF<T>::VBPB;   // raw B bytes per K-step
-  static constexpr int RA_PIECES = RA / 16, RB_PIECES = RB / 16;
-  static constexpr int RA_NPT = (RA_PIECES + GT8 - 1) / GT8, RB_NPT = (RB_PIECES + GT8 - 1) / GT8;
-  uint32_t rawA[RA_NPT * GT8 * 4 + 4];
-  uint32_t rawB[RB_NPT * GT8 * 4 + 4];
-  uint32_t wt[TI * ROWB / 4];
-  uint32_t act[TJ * ROWB / 4];
-  _Float16 dah[KBLK][TI];       // fp16 scales, exactly as stored in the blocks
-  _Float16 dbh[KBLK][TJ];
-  _Float16 mah[TI][KBLK];
-  _Float16 sbh[TJ][KBLK];
-};
-
 __device__ __forceinline__ uint32_t sub_bytes(uint32_t x, uint32_t off4) {
   // per-byte x - off (x < 0x80 per byte): no borrow crosses a byte
   return ((x | 0x80808080u) - off4) ^ 0x80808080u;
@@ -107,128 +91,278 @@ __device__ __forceinline__ void unpack_weight(const uint32_t (&m)[(GF<T>::ABPB +
   }
 }
 
+// ================================================================== 32-block GEMM
+// Activations are decoded ONCE per call by prep_act_kernel into a workspace (per slice z):
+//   act [j][Kpad]       int8 quants, Kpad = nsteps * 256 (zero padded)
+//   d8  [ks][j][8]      the 8 block scales d_b of K-step ks as 8-byte {d_b, 0, 0, 0} fp16
+//                       quads: a ready-made v_mfma_f32_32x32x8_f16 operand (0 for pad blocks)
+//   s   [ks][j][8]      fp16 s_b (q8_1 only)
+// so a K-step's activation tile is 128 x 256 contiguous int8 bytes + 8 KiB of scale
+// operands, moved HBM/L2 -> LDS by LDS-DMA (buffer_load ... lds).  The weight tile stays
+// AoS in HBM, arrives by LDS-DMA and is unpacked to int8 in LDS once per K-step.
+//
+// Scale product: both lane halves (k = 0 and k = 4) of the 32x32x8 f16 MFMA carry the same
+// {d, 0, 0, 0} quad, so it yields exactly 2 * d_b * d_a (fp16 x fp16 products and their
+// doubling are exact in fp32); the final 0.5 is exact too, so no per-block VALU work is
+// spent on building scale operands.
+constexpr int KSTEP = KBLK * 32;    // 256 elements
+
+struct PrepLayout {
+  int nsteps, kpad;
+  int64_t act_bytes, d8_bytes, s_bytes, slice_bytes;
+  __host__ __device__ static PrepLayout of(const GemvArgs& p) {
+    PrepLayout L;
+    L.nsteps = (p.nblk + KBLK - 1) / KBLK;
+    L.kpad = L.nsteps * KSTEP;
+    L.act_bytes = (int64_t)p.N * L.kpad;
+    L.d8_bytes = (int64_t)L.nsteps * p.N * KBLK * 8;
+    L.s_bytes = ((int64_t)L.nsteps * p.N * KBLK * 2 + 15) & ~int64_t(15);
+    L.slice_bytes = L.act_bytes + L.d8_bytes + L.s_bytes;
+    return L;
+  }
+};
+
+template <int VBPB>   // 34 = q8_0, 36 = q8_1
+__global__ __launch_bounds__(256) void prep_act_kernel(GemvArgs p, unsigned char* ws) {
+  const PrepLayout L = PrepLayout::of(p);
+  const int z = blockIdx.y, i12 = z % p.ne12, i13 = z / p.ne12;
+  const unsigned char* Bz = p.B + (int64_t)i12 * p.sb2 + (int64_t)i13 * p.sb3;
+  unsigned char* act = ws + (int64_t)z * L.slice_bytes;
+  uint2* d8 = (uint2*)(act + L.act_bytes);
+  _Float16* ssc = (_Float16*)(act + L.act_bytes + L.d8_bytes);
+  const int64_t it = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t nb_pad = (int64_t)L.nsteps * KBLK;
+  if (it >= (int64_t)p.N * nb_pad) return;
+  const int j = (int)(it / nb_pad), b = (int)(it % nb_pad);
+  const int64_t bbytes = (int64_t)(p.N - 1) * p.ldb + (int64_t)p.nblk * VBPB;
+  const auto rs = make_rsrc(Bz, (uint32_t)min((bbytes + 3) & ~int64_t(3), (int64_t)0x7fffffff));
+  constexpr int VQS = VBPB == 36 ? 4 : 2;
+  const bool ok = b < p.nblk;
+  const uint32_t off = ok ? (uint32_t)(j * p.ldb + (int64_t)b * VBPB) : 0xfffffff0u;
+  const uint32_t base = off & ~3u;
+  const int sh = (int)(off & 3u);
+  uint32_t w[10], m[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) w[k] = bload4(rs, base + 4 * k);
+#pragma unroll
+  for (int k = 0; k < 9; ++k) m[k] = __builtin_amdgcn_alignbit(w[k + 1], w[k], sh * 8);
+  m[9] = 0;
+  u32x4* dst = (u32x4*)(act + (int64_t)j * L.kpad + 32 * b);
+  dst[0] = ok ? u32x4{get32<VQS>(m), get32<VQS + 4>(m), get32<VQS + 8>(m), get32<VQS + 12>(m)} : u32x4{0, 0, 0, 0};
+  dst[1] = ok ? u32x4{get32<VQS + 16>(m), get32<VQS + 20>(m), get32<VQS + 24>(m), get32<VQS + 28>(m)}
+              : u32x4{0, 0, 0, 0};
+  const int ks = b / KBLK, bb = b % KBLK;
+  const int64_t si = ((int64_t)ks * p.N + j) * KBLK + bb;
+  d8[si] = uint2{ok ? (m[0] & 0xffffu) : 0u, 0u};
+  if constexpr (VBPB == 36) ssc[si] = __builtin_bit_cast(_Float16, (uint16_t)(ok ? (m[0] >> 16) : 0));
+}
+
+template <int N_>
+__device__ __forceinline__ void wait_vm() {   // s_waitcnt vmcnt(N) lgkmcnt(0)
+  static_assert(N_ >= 0 && N_ < 64, "vmcnt");
+  __builtin_amdgcn_s_waitcnt((N_ & 0xF) | ((N_ >> 4) << 14) | (0x7 << 4));
+  asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, const void* lds, uint32_t off) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, off, 0, 0, 0);
+}
+__device__ __forceinline__ void dma4(__amdgpu_buffer_rsrc_t r, const void* lds, uint32_t off) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 4, off, 0, 0, 0);
+}
+
 template <int T>
-__global__ __launch_bounds__(GT8) void gemm_kernel(GemvArgs p) {
-  using S = GemmSmem<T>;
-  constexpr int ABPB = GF<T>::ABPB, VBPB = GF<T>::VBPB;
-  constexpr bool AFF = (T == kQ4_1 || T == kQ5_1);
-  constexpr int APR = KBLK * ABPB / 16, BPR = KBLK * VBPB / 16;   // 16-byte pieces per row
+struct G3 {
+  static constexpr bool AFF = (T == kQ4_1 || T == kQ5_1);
+  static constexpr int ABPB = GF<T>::ABPB;
+  static constexpr int A_BYTES = TI * KBLK * ABPB;                 // raw weight tile bytes
+  static_assert((KBLK * ABPB) % 16 == 0, "a K-step of a weight row is whole 16-byte pieces");
+  static constexpr int A_PIECES = A_BYTES / 16;
+  static_assert(A_PIECES % 64 == 0, "whole waves of weight pieces");
+  static constexpr int A_NDW = (A_PIECES + GT8 - 1) / GT8;         // 16-byte DMA rounds
+  static constexpr bool A_RAGGED = (A_PIECES % GT8) != 0;          // last round: some waves only
+  static constexpr int ACT_N = TJ * KSTEP / 16 / GT8;              // 16-byte DMAs per thread (4)
+  static_assert(TJ * KBLK * 8 == GT8 * 16, "one 16-byte DMA per thread moves the d8 tile");
+  static constexpr int OPS = ACT_N + 1 + (AFF ? 1 : 0);            // + this wave's A rounds
+};
+
+template <int T, int NBUF>
+struct Smem3 {
+  using C = G3<T>;
+  uint32_t act[NBUF][TJ * KSTEP / 4];  // swizzled int8 activation tiles
+  uint32_t araw[NBUF][C::A_BYTES / 4]; // raw AoS weight tiles
+  uint2 db8[NBUF][TJ][KBLK];           // {d_b, 0, 0, 0} fp16 quads
+  _Float16 sbh[NBUF][TJ][KBLK];        // s_b (q8_1)
+  uint32_t wt[TI * ROWB / 4];          // unpacked int8 weight tile
+  uint2 da8[KBLK][TI];                 // {d_a, 0, 0, 0} fp16 quads
+  _Float16 mah[TI][KBLK];              // m_a (q4_1 / q5_1)
+};
+
+// NBUF = 2: the next K-step's DMA is in flight during this one's unpack + MFMA.
+// V: ablations (1 no MFMA phase, 2 no unpack, 3 no DMA) for tools/ab_gemm.py.
+template <int T, int NBUF, int V>
+__device__ __forceinline__ void gemm3_body(const GemvArgs& p, const unsigned char* ws) {
+  using C = G3<T>;
+  using S = Smem3<T, NBUF>;
+  constexpr int ABPB = C::ABPB;
+  constexpr bool AFF = C::AFF;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   S& sm = *reinterpret_cast<S*>(smem_raw);
+  const PrepLayout L = PrepLayout::of(p);
 
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int lr = lane & 31, h = lane >> 5;
-  const int wj = w >> 1, wi = w & 1;             // wave tile: rows jb..jb+31, cols ib..ib+31
+  const int wj = w >> 1, wi = w & 1;
   const int jb = 32 * wj, ib = 32 * wi;
   const int64_t i0 = (int64_t)blockIdx.x * TI, j0 = (int64_t)blockIdx.y * TJ;
   const int z = blockIdx.z, i12 = z % p.ne12, i13 = z / p.ne12;
   const unsigned char* Az = p.A + (int64_t)(i12 / p.r2) * p.sa2 + (int64_t)(i13 / p.r3) * p.sa3 + i0 * p.lda;
-  const unsigned char* Bz = p.B + (int64_t)i12 * p.sb2 + (int64_t)i13 * p.sb3 + j0 * p.ldb;
+  const unsigned char* wsz = ws + (int64_t)z * L.slice_bytes;
   float* Cz = p.C + (int64_t)i12 * p.sc2 + (int64_t)i13 * p.sc3;
   const int rowsA = (int)min((int64_t)TI, (int64_t)p.M - i0);
   const int rowsB = (int)min((int64_t)TJ, (int64_t)p.N - j0);
-  const int64_t a_end = (int64_t)(rowsA - 1) * p.lda + (int64_t)p.nblk * ABPB;   // bytes readable from Az
-  const int64_t b_end = (int64_t)(rowsB - 1) * p.ldb + (int64_t)p.nblk * VBPB;
 
-  // per-thread piece offsets within a K-step (constant over K)
-  uint32_t aoff[S::RA_NPT], boff[S::RB_NPT];
+  // -- per-thread DMA source offsets (relative to the step's rsrc bases) --
+  const int wbase = t & ~63;
+  uint32_t act_off[C::ACT_N];
 #pragma unroll
-  for (int k = 0; k < S::RA_NPT; ++k) {
-    const int pc = t + k * GT8, rr = pc / APR, oo = pc % APR;
-    aoff[k] = (pc < S::RA_PIECES && rr < rowsA) ? (uint32_t)(rr * p.lda + 16 * oo) : 0x7ffffff0u;
+  for (int k = 0; k < C::ACT_N; ++k) {
+    const int pc = k * GT8 + t;                  // LDS piece (row r, slot c')
+    const int r = pc >> 4, cs = pc & 15;
+    const int c = cs ^ (r & 15);                 // source piece: XOR swizzle on the SOURCE
+    act_off[k] = r < rowsB ? (uint32_t)(r * L.kpad + 16 * c) : 0x7ffffff0u;
   }
+  uint32_t a_off[C::A_NDW];
 #pragma unroll
-  for (int k = 0; k < S::RB_NPT; ++k) {
-    const int pc = t + k * GT8, rr = pc / BPR, oo = pc % BPR;
-    boff[k] = (pc < S::RB_PIECES && rr < rowsB) ? (uint32_t)(rr * p.ldb + 16 * oo) : 0x7ffffff0u;
+  for (int k = 0; k < C::A_NDW; ++k) {
+    const int d = k * GT8 + t;                   // 16-byte piece of the packed [TI][KBLK*ABPB] image
+    const int r = d / (KBLK * ABPB / 16), o = d % (KBLK * ABPB / 16);
+    a_off[k] = (d < C::A_PIECES && r < rowsA) ? (uint32_t)(r * p.lda + 16 * o) : 0x7ffffff0u;
   }
+  const bool a_last = !C::A_RAGGED || (C::A_NDW - 1) * GT8 + wbase < C::A_PIECES;   // wave-uniform
 
-  u32x4 va[S::RA_NPT], vb[S::RB_NPT];
-  auto issue = [&](int ks) {   // global -> registers for K-step ks (OOB reads return 0)
-    const int64_t ka = (int64_t)ks * KBLK * ABPB, kbb = (int64_t)ks * KBLK * VBPB;
-    const auto ra = make_rsrc(Az + ka, (uint32_t)min((a_end - ka + 3) & ~int64_t(3), (int64_t)0x7fffffff));
-    const auto rb = make_rsrc(Bz + kbb, (uint32_t)min((b_end - kbb + 3) & ~int64_t(3), (int64_t)0x7fffffff));
+  auto issue = [&](int ks, int buf) {
+    const unsigned char* ab = Az + (int64_t)ks * KBLK * ABPB;
+    const int64_t aend = (int64_t)(rowsA - 1) * p.lda + (int64_t)(p.nblk - ks * KBLK) * ABPB;
+    const auto ra = make_rsrc(ab, (uint32_t)max((int64_t)0, min((aend + 3) & ~int64_t(3), (int64_t)0x7fffffff)));
 #pragma unroll
-    for (int k = 0; k < S::RA_NPT; ++k) va[k] = bload16(ra, aoff[k]);
+    for (int k = 0; k < C::A_NDW; ++k)
+      if (k + 1 < C::A_NDW || a_last) dma16(ra, &sm.araw[buf][4 * (k * GT8 + wbase)], a_off[k]);
+    const unsigned char* xb = wsz + j0 * L.kpad + (int64_t)ks * KSTEP;
+    const auto rx = make_rsrc(xb, (uint32_t)((int64_t)(rowsB - 1) * L.kpad + KSTEP));
 #pragma unroll
-    for (int k = 0; k < S::RB_NPT; ++k) vb[k] = bload16(rb, boff[k]);
+    for (int k = 0; k < C::ACT_N; ++k) dma16(rx, &sm.act[buf][4 * (k * GT8 + wbase)], act_off[k]);
+    const int64_t soff = ((int64_t)ks * p.N + j0) * KBLK;
+    const auto rd = make_rsrc(wsz + L.act_bytes + 8 * soff, (uint32_t)(rowsB * KBLK * 8));
+    dma16(rd, &sm.db8[buf][0][0] + 2 * wbase, 16 * t);
+    if constexpr (AFF) {
+      const auto rss = make_rsrc(wsz + L.act_bytes + L.d8_bytes + 2 * soff, (uint32_t)(rowsB * KBLK * 2));
+      dma4(rss, &sm.sbh[buf][0][0] + 2 * wbase, 4 * t);
+    }
+  };
+  auto wait_step = [&](bool one_in_flight) {   // this wave's DMA for the current step landed
+    if (NBUF == 2 && one_in_flight) {
+      if (a_last) wait_vm<C::OPS + C::A_NDW>(); else wait_vm<C::OPS + C::A_NDW - 1>();
+    } else {
+      wait_vm<0>();
+    }
   };
 
   f32x16 acc, macc;
 #pragma unroll
   for (int e = 0; e < 16; ++e) { acc[e] = 0.f; macc[e] = 0.f; }
 
-  const int nsteps = (p.nblk + KBLK - 1) / KBLK;
-  issue(0);
+  const int nsteps = L.nsteps;
+  if (V != 3) issue(0, 0);
+  if (NBUF == 2 && V != 3 && nsteps > 1) issue(1, 1);
   for (int ks = 0; ks < nsteps; ++ks) {
-    const int kb0 = ks * KBLK;
-    // ---- registers (loaded during the previous step's MFMAs) -> raw LDS ----
-#pragma unroll
-    for (int k = 0; k < S::RA_NPT; ++k) *(u32x4*)&sm.rawA[4 * (t + k * GT8)] = va[k];
-#pragma unroll
-    for (int k = 0; k < S::RB_NPT; ++k) *(u32x4*)&sm.rawB[4 * (t + k * GT8)] = vb[k];
-    __syncthreads();
-    // ---- unpack to int8 + fp16 scales (one item = one (row, block)) ----
-    for (int it = t; it < TI * KBLK; it += GT8) {
-      const int il = it / KBLK, b = it % KBLK;
+    const int buf = NBUF == 2 ? (ks & 1) : 0;
+    wait_step(ks + 1 < nsteps);
+    raw_barrier();                                   // step ks's DMA visible to all waves
+    // ---- unpack the weight tile (one (row, block) item per thread) ----
+    if (V != 2) {
+      const int il = t / KBLK, b = t % KBLK;         // 512 threads = 64 rows x 8 blocks
       uint32_t m[(ABPB + 3) / 4], q[8];
-      lds_block(sm.rawA, il * KBLK * ABPB + b * ABPB, m);
+      lds_block(sm.araw[buf], il * KBLK * ABPB + b * ABPB, m);
       unpack_weight<T>(m, q);
-      const bool ok = il < rowsA && kb0 + b < p.nblk;
+      const bool ok = il < rowsA && ks * KBLK + b < p.nblk;
       u32x4* dst = (u32x4*)&sm.wt[(il * ROWB + 32 * b) / 4];
       dst[0] = ok ? u32x4{q[0], q[1], q[2], q[3]} : u32x4{0, 0, 0, 0};
       dst[1] = ok ? u32x4{q[4], q[5], q[6], q[7]} : u32x4{0, 0, 0, 0};
-      sm.dah[b][il] = __builtin_bit_cast(_Float16, (uint16_t)(ok ? (m[0] & 0xffff) : 0));
+      sm.da8[b][il] = uint2{ok ? (m[0] & 0xffffu) : 0u, 0u};
       if constexpr (AFF) sm.mah[il][b] = __builtin_bit_cast(_Float16, (uint16_t)(ok ? (m[0] >> 16) : 0));
     }
-    for (int it = t; it < TJ * KBLK; it += GT8) {
-      const int jl = it / KBLK, b = it % KBLK;
-      uint32_t m[(VBPB + 3) / 4];
-      lds_block(sm.rawB, jl * KBLK * VBPB + b * VBPB, m);
-      constexpr int VQS = VBPB == 36 ? 4 : 2;
-      const bool ok = jl < rowsB && kb0 + b < p.nblk;
-      u32x4* dst = (u32x4*)&sm.act[(jl * ROWB + 32 * b) / 4];
-      dst[0] = ok ? u32x4{get32<VQS>(m), get32<VQS + 4>(m), get32<VQS + 8>(m), get32<VQS + 12>(m)} : u32x4{0, 0, 0, 0};
-      dst[1] = ok ? u32x4{get32<VQS + 16>(m), get32<VQS + 20>(m), get32<VQS + 24>(m), get32<VQS + 28>(m)}
-                  : u32x4{0, 0, 0, 0};
-      sm.dbh[b][jl] = __builtin_bit_cast(_Float16, (uint16_t)(ok ? (m[0] & 0xffff) : 0));
-      if constexpr (AFF) sm.sbh[jl][b] = __builtin_bit_cast(_Float16, (uint16_t)(ok ? (m[0] >> 16) : 0));
-    }
-    __syncthreads();
-    // ---- next step's global loads fly during this step's MFMAs ----
-    if (ks + 1 < nsteps) issue(ks + 1);
-    // ---- MFMA: exact int32 block dots; d_a*d_b on the fp16 MFMA; acc += P * S ----
-#pragma unroll 2
-    for (int b = 0; b < KBLK; ++b) {
-      const i32x4 wf = *(const i32x4*)&sm.wt[((ib + lr) * ROWB + 32 * b + 16 * h) / 4];
-      const i32x4 af = *(const i32x4*)&sm.act[((jb + lr) * ROWB + 32 * b + 16 * h) / 4];
+    __builtin_amdgcn_s_waitcnt(0xC07F);              // lgkmcnt(0)
+    raw_barrier();
+    // ---- MFMA: exact int32 block dots (i8) + 2 d_b d_a (f16); acc += float(S) * P ----
+    // Two blocks per trip: block b's MFMAs are in flight while block b-1's epilogue runs.
+    if constexpr (V != 1) {
+      const int r = jb + lr;
+      const uint32_t* wrow = &sm.wt[((ib + lr) * ROWB + 16 * h) / 4];
+      const uint32_t* arow = &sm.act[buf][r * KSTEP / 4];
+      const int sw = r & 15;
+      struct Ops { i32x4 af, wf; half4 db, da; };
+      auto ld = [&](int b, Ops& o) {
+        o.wf = *(const i32x4*)&wrow[8 * b];
+        o.af = *(const i32x4*)&arow[4 * ((2 * b + h) ^ sw)];
+        o.db = *(const half4*)&sm.db8[buf][r][b];
+        o.da = *(const half4*)&sm.da8[b][ib + lr];
+      };
       const i32x16 zero = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-      const i32x16 sdot = __builtin_amdgcn_mfma_i32_32x32x32_i8(af, wf, zero, 0, 0, 0);
-      // outer product d_b[j] * d_a[i] (k = 0 only): fp16 x fp16 is exact in fp32
-      const _Float16 hz = (_Float16)0.f;
-      const half8 dbv = {h == 0 ? sm.dbh[b][jb + lr] : hz, hz, hz, hz, hz, hz, hz, hz};
-      const half8 dav = {h == 0 ? sm.dah[b][ib + lr] : hz, hz, hz, hz, hz, hz, hz, hz};
       const f32x16 fz = {};
-      const f32x16 sc = __builtin_amdgcn_mfma_f32_32x32x16_f16(dbv, dav, fz, 0, 0, 0);
+      auto epi = [&](const i32x16& sd, const f32x16& sc) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[r] = __builtin_fmaf((float)sdot[r], sc[r], acc[r]);
+        for (int e = 0; e < 16; ++e) acc[e] = __builtin_fmaf((float)sd[e], sc[e], acc[e]);
+      };
+      Ops o0, o1;
+      ld(0, o0);
+      ld(1, o1);
+      i32x16 sp = __builtin_amdgcn_mfma_i32_32x32x32_i8(o0.af, o0.wf, zero, 0, 0, 0);
+      f32x16 pp = __builtin_amdgcn_mfma_f32_32x32x8f16(o0.db, o0.da, fz, 0, 0, 0);
+#pragma unroll 1
+      for (int b = 1; b < KBLK - 1; b += 2) {
+        ld(b + 1, o0);
+        const i32x16 sa = __builtin_amdgcn_mfma_i32_32x32x32_i8(o1.af, o1.wf, zero, 0, 0, 0);
+        const f32x16 pa = __builtin_amdgcn_mfma_f32_32x32x8f16(o1.db, o1.da, fz, 0, 0, 0);
+        epi(sp, pp);
+        ld(b + 2, o1);
+        sp = __builtin_amdgcn_mfma_i32_32x32x32_i8(o0.af, o0.wf, zero, 0, 0, 0);
+        pp = __builtin_amdgcn_mfma_f32_32x32x8f16(o0.db, o0.da, fz, 0, 0, 0);
+        epi(sa, pa);
+      }
+      {  // block KBLK-1 (o1) and the tail
+        const i32x16 sa = __builtin_amdgcn_mfma_i32_32x32x32_i8(o1.af, o1.wf, zero, 0, 0, 0);
+        const f32x16 pa = __builtin_amdgcn_mfma_f32_32x32x8f16(o1.db, o1.da, fz, 0, 0, 0);
+        epi(sp, pp);
+        epi(sa, pa);
+      }
     }
     if constexpr (AFF) {
-      // sum_b m_a[i,b] * s_b[j,b] over this K-step's 8 blocks: one exact fp16 MFMA
       const half4 mf = *(const half4*)&sm.mah[ib + lr][4 * h];
-      const half4 sf = *(const half4*)&sm.sbh[jb + lr][4 * h];
+      const half4 sf = *(const half4*)&sm.sbh[buf][jb + lr][4 * h];
       macc = __builtin_amdgcn_mfma_f32_32x32x8f16(sf, mf, macc, 0, 0, 0);
     }
-    __syncthreads();
+    __builtin_amdgcn_s_waitcnt(0xC07F);              // this wave's LDS reads are done
+    raw_barrier();                                   // nobody reads buf / wt any more
+    if (V != 3 && ks + NBUF < nsteps) issue(ks + NBUF, buf);
   }
 
-  // ---- epilogue: C[j*ldc + i], lanes own i (128-byte segments) ----
   const int64_t i = i0 + ib + lr;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int64_t j = j0 + jb + (r & 3) + 8 * (r >> 2) + 4 * h;
-    if (i < p.M && j < p.N) Cz[j * p.ldc + i] = acc[r] + (AFF ? macc[r] : 0.f);
+  for (int e = 0; e < 16; ++e) {
+    const int64_t j = j0 + jb + (e & 3) + 8 * (e >> 2) + 4 * h;
+    if (i < p.M && j < p.N) Cz[j * p.ldc + i] = 0.5f * acc[e] + (AFF ? macc[e] : 0.f);
   }
+}
+
+template <int T, int NBUF, int V = 0>
+__global__ __launch_bounds__(GT8) void gemm3_kernel(GemvArgs p, const unsigned char* ws) {
+  gemm3_body<T, NBUF, V>(p, ws);
 }
 
 // ------------------------------------------------------------------ q2_K x q8_K
@@ -380,6 +514,37 @@ hipError_t launch_with(K kern, size_t lds, int threads, const GemvArgs& p, hipSt
   return hipGetLastError();
 }
 
+int gemm_variant() {   // A/B and ablation switch for tools/ab_gemm.py; 0 in production
+  const char* e = getenv("LAMM_GEMM_VARIANT");
+  return e ? atoi(e) : 0;
+}
+
+template <int T>
+hipError_t launch_v3(const GemvArgs& p, void* ws, hipStream_t s) {
+  constexpr int VBPB = GF<T>::VBPB;
+  const PrepLayout L = PrepLayout::of(p);
+  const int64_t items = (int64_t)p.N * L.nsteps * KBLK;
+  hipLaunchKernelGGL((prep_act_kernel<VBPB>), dim3((unsigned)((items + 255) / 256), p.ne12 * p.ne13), dim3(256), 0,
+                     s, p, static_cast<unsigned char*>(ws));
+  constexpr int NB = 2;
+  const dim3 grid((unsigned)((p.M + TI - 1) / TI), (unsigned)((p.N + TJ - 1) / TJ), (unsigned)(p.ne12 * p.ne13));
+  const auto* wsc = static_cast<const unsigned char*>(ws);
+  auto go = [&](auto kern, size_t lds_bytes = 0) {
+    const size_t lds = lds_bytes ? lds_bytes : sizeof(Smem3<T, NB>);
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, grid, dim3(GT8), lds, s, p, wsc);
+  };
+  switch (gemm_variant()) {
+    case 1: go(gemm3_kernel<T, NB, 1>); break;
+    case 2: go(gemm3_kernel<T, NB, 2>); break;
+    case 3: go(gemm3_kernel<T, NB, 3>); break;
+    case 4: break;   // prep pass only
+    case 5: go(gemm3_kernel<T, 1, 0>, sizeof(Smem3<T, 1>)); break;   // single-buffered
+    default: go(gemm3_kernel<T, NB, 0>);
+  }
+  return hipGetLastError();
+}
+
 }  // namespace
 
 bool gemm_supported(int type) {
@@ -387,18 +552,25 @@ bool gemm_supported(int type) {
 }
 
 bool gemm_args_ok(int type, const GemvArgs& p) {
-  // B rows are staged with 16-byte (32-block formats) or 4-byte (q8_K) loads
-  const int64_t a = type == kQ2_K ? 4 : 16;
-  return (p.ldb % a) == 0 && ((uintptr_t)p.B % a) == 0 && (p.sb2 % a) == 0 && (p.sb3 % a) == 0;
+  // q2_K stages B rows with 4-byte loads; the 32-block path reads B through the prep pass
+  // and A by 16-byte LDS-DMA pieces (lda and the slice strides are validated multiples of 16)
+  if (type == kQ2_K) return (p.ldb % 4) == 0 && ((uintptr_t)p.B % 4) == 0 && (p.sb2 % 4) == 0 && (p.sb3 % 4) == 0;
+  return ((uintptr_t)p.A % 16) == 0 && (p.lda % 16) == 0 && (p.sa2 % 16) == 0 && (p.sa3 % 16) == 0;
 }
 
-hipError_t launch_gemm(int type, const GemvArgs& p, hipStream_t s) {
+size_t gemm_workspace_bytes(int type, const GemvArgs& p) {
+  if (type == kQ2_K) return 0;
+  const PrepLayout L = PrepLayout::of(p);
+  return (size_t)(p.ne12 * p.ne13) * (size_t)L.slice_bytes + 256;
+}
+
+hipError_t launch_gemm(int type, const GemvArgs& p, void* ws, hipStream_t s) {
   switch (type) {
-    case kQ4_0: return launch_with(gemm_kernel<kQ4_0>, sizeof(GemmSmem<kQ4_0>), GT8, p, s);
-    case kQ4_1: return launch_with(gemm_kernel<kQ4_1>, sizeof(GemmSmem<kQ4_1>), GT8, p, s);
-    case kQ5_0: return launch_with(gemm_kernel<kQ5_0>, sizeof(GemmSmem<kQ5_0>), GT8, p, s);
-    case kQ5_1: return launch_with(gemm_kernel<kQ5_1>, sizeof(GemmSmem<kQ5_1>), GT8, p, s);
-    case kQ8_0: return launch_with(gemm_kernel<kQ8_0>, sizeof(GemmSmem<kQ8_0>), GT8, p, s);
+    case kQ4_0: return launch_v3<kQ4_0>(p, ws, s);
+    case kQ4_1: return launch_v3<kQ4_1>(p, ws, s);
+    case kQ5_0: return launch_v3<kQ5_0>(p, ws, s);
+    case kQ5_1: return launch_v3<kQ5_1>(p, ws, s);
+    case kQ8_0: return launch_v3<kQ8_0>(p, ws, s);
     case kQ2_K: return launch_with(gemm_q2k_kernel, sizeof(Q2KSmem), GT, p, s);
     default: return hipErrorInvalidValue;
   }

@@ -66,6 +66,31 @@ const DeviceProbe& probe() {
   return p;
 }
 
+// Device scratch for the GEMM's decoded activations: grow-only, one per process and
+// device.  Growing synchronises `s` before the old buffer is released.
+std::mutex g_ws_mu;
+void* g_ws = nullptr;
+size_t g_ws_bytes = 0;
+int g_ws_dev = -1;
+
+void* workspace(size_t bytes, hipStream_t s) {
+  std::lock_guard<std::mutex> lock(g_ws_mu);
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (g_ws && g_ws_bytes >= bytes && g_ws_dev == dev) return g_ws;
+  if (g_ws) {
+    (void)hipStreamSynchronize(s);
+    (void)hipDeviceSynchronize();
+    (void)hipFree(g_ws);
+    g_ws = nullptr;
+  }
+  const size_t want = bytes + bytes / 4;
+  if (hipMalloc(&g_ws, want) != hipSuccess) { g_ws = nullptr; g_ws_bytes = 0; return nullptr; }
+  g_ws_bytes = want;
+  g_ws_dev = dev;
+  return g_ws;
+}
+
 }  // namespace
 
 // =============================================================== traits
@@ -124,7 +149,10 @@ extern "C" int lamm_hip_matmul_batched(const lamm_matrix* A, const lamm_matrix* 
   if (N <= 8) {
     e = launch_gemv(A->type, p, s);
   } else if (gemm_supported(A->type) && gemm_args_ok(A->type, p)) {
-    e = launch_gemm(A->type, p, s);
+    void* ws = nullptr;
+    const size_t wsb = gemm_workspace_bytes(A->type, p);
+    if (wsb && !(ws = workspace(wsb, s))) return fail(LAMM_ERR_HIP, "workspace allocation of %zu bytes failed", wsb);
+    e = launch_gemm(A->type, p, ws, s);
   } else {
     e = hipSuccess;
     for (int j0 = 0; j0 < N && e == hipSuccess; j0 += 8) {

@@ -23,7 +23,8 @@ struct GemvArgs {
 hipError_t launch_gemv(int type, const GemvArgs& p, hipStream_t s);
 size_t gemv_lds_bytes(int type, int nc);
 
-hipError_t launch_gemm(int type, const GemvArgs& p, hipStream_t s);
+hipError_t launch_gemm(int type, const GemvArgs& p, void* workspace, hipStream_t s);
+size_t gemm_workspace_bytes(int type, const GemvArgs& p);   // device scratch launch_gemm needs
 bool gemm_supported(int type);
 bool gemm_args_ok(int type, const GemvArgs& p);   // B pitch/alignment the GEMM staging needs
 

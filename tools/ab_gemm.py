@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""Interleaved A/B timing of GEMM variants (LAMM_GEMM_VARIANT) in ONE process.
+
+Variant 0 is production; 1 = no MFMA phase, 2 = no weight unpack, 3 = no DMA, 4 = the
+activation prep pass alone (ablations: outputs differ, only variant 0's are checked)."""
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "la-llama.cpp_amd"))
+sys.path.insert(0, ROOT)
+import lamm_amd as la  # noqa: E402
+import bench  # noqa: E402
+
+
+def main():
+    variants = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "0,1,2,3,4").split(",")]
+    fmt = os.environ.get("FMT", "q4_0")
+    M, K, N = 4096, 4096, int(os.environ.get("NCOL", "512"))
+    slices = int(os.environ.get("SLICES", "4"))
+    t = la.BY_NAME[fmt]
+    vt = la.vec_dot_type(t)
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(7)
+    A, arow = bench.make_weights(torch, la, fmt, slices, M, K, gen)
+    B = bench.make_activations(torch, la, fmt, slices * N, K, gen)
+    kb = K // la.blck_size(t)
+    brow = la.row_bytes(vt, K)
+    res = {v: [] for v in variants}
+    stream = torch.cuda.current_stream()
+    C = torch.zeros(slices * N * M, dtype=torch.float32, device="cuda")
+    Am = la.Matrix(A.data_ptr(), t, M, kb, kb)
+    Bm = la.Matrix(B.data_ptr(), vt, kb, N, kb)
+    Cm = la.Matrix(C.data_ptr(), la.F32, M, N, M)
+    bt = la.Batch(slices, 1, slices, 1, M * arow, slices * M * arow, N * brow, slices * N * brow,
+                  4 * M * N, 4 * M * N * slices)
+    for rnd in range(5):
+        for v in variants:
+            os.environ["LAMM_GEMM_VARIANT"] = str(v)
+            for _ in range(2):
+                la.matmul_batched(Am, Bm, Cm, bt, stream.cuda_stream)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(10):
+                la.matmul_batched(Am, Bm, Cm, bt, stream.cuda_stream)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            res[v].append(e0.elapsed_time(e1) * 1e3 / 10)
+    flops = 2.0 * M * N * K * slices
+    summary = {}
+    for v in variants:
+        med = sorted(res[v])[len(res[v]) // 2]
+        summary[v] = {"median_us": round(med, 2), "TOPs": round(flops / (med * 1e-6) / 1e12, 1)}
+    print(json.dumps({"fmt": fmt, "M": M, "N": N, "K": K, "slices": slices, "variants": summary}))
+
+
+if __name__ == "__main__":
+    main()

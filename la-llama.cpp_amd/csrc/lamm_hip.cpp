@@ -91,6 +91,17 @@ void* workspace(size_t bytes, hipStream_t s) {
   return g_ws;
 }
 
+// GEMM engine for the q4_0 / q4_1 / q5_0 prefill path: 0 = block-scaled fp6 MFMA
+// (lamm_gemm_fp6.hip), 1 = MFMA-i8 (lamm_gemm.hip).  The fp6 kernel's 256x128 tiles only pay
+// off once they fill the chip (>= one tile per CU); smaller calls take the i8 kernel's
+// 128x64 tiles.  LAMM_GEMM_PATH=fp6 / i8 forces one (A/B measurements).
+int gemm_path(const GemvArgs& p) {
+  const char* e = getenv("LAMM_GEMM_PATH");
+  if (e && (!strcmp(e, "i8") || !strcmp(e, "1"))) return 1;
+  if (e && (!strcmp(e, "fp6") || !strcmp(e, "0"))) return 0;
+  return gemm_fp6_tiles(p) >= 256 ? 0 : 1;
+}
+
 }  // namespace
 
 // =============================================================== traits
@@ -148,6 +159,11 @@ extern "C" int lamm_hip_matmul_batched(const lamm_matrix* A, const lamm_matrix* 
   hipError_t e;
   if (N <= 8) {
     e = launch_gemv(A->type, p, s);
+  } else if (gemm_fp6_supported(A->type) && gemm_path(p) == 0) {
+    const size_t wsb = gemm_fp6_workspace_bytes(A->type, p);
+    void* ws = workspace(wsb, s);
+    if (!ws) return fail(LAMM_ERR_HIP, "workspace allocation of %zu bytes failed", wsb);
+    e = launch_gemm_fp6(A->type, p, ws, s);
   } else if (gemm_supported(A->type) && gemm_args_ok(A->type, p)) {
     void* ws = nullptr;
     const size_t wsb = gemm_workspace_bytes(A->type, p);

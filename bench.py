@@ -33,6 +33,7 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "la-llama.cpp_amd"))
+from lamm_amd.shard import RowGather  # noqa: E402  (pure Python; the HIP library loads in main())
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 I8_DENSE_PEAK_TOPS = 5000.0    # dense MFMA-i8 = 2x the 2.5 PF dense bf16 rate (MI355X_MICROARCH.md)
@@ -84,7 +85,9 @@ def run_case(torch, la, dist, fmt, M, N, K, slices, steps, warmup, world, warm_f
     A, arow = make_weights(torch, la, fmt, slices, M, K, gen)
     B = make_activations(torch, la, fmt, slices * N, K, gen)
     C = torch.zeros(slices * N * M, dtype=torch.float32, device="cuda")
-    gathered = torch.zeros(world * C.numel(), dtype=torch.float32, device="cuda") if world > 1 else None
+    # rows of A shard across ranks (weak scaling: each rank owns an M-row slab of every
+    # slice); the slabs of C meet in one RCCL all-gather + one interleaving copy
+    gather = RowGather(dist, slices * N, M, world, torch.float32, "cuda") if world > 1 else None
     kb = K // la.blck_size(t)
     brow = la.row_bytes(vt, K)
     Am = la.Matrix(A.data_ptr(), t, M, kb, kb)
@@ -97,7 +100,7 @@ def run_case(torch, la, dist, fmt, M, N, K, slices, steps, warmup, world, warm_f
     def step():
         la.matmul_batched(Am, Bm, Cm, bt, stream.cuda_stream)
         if world > 1:  # row shards -> every rank holds all of C (RCCL over xGMI)
-            dist.all_gather_into_tensor(gathered, C)
+            gather(C)
 
     if warm_first:
         skip = os.environ.pop("LAMM_GEMM_SKIP_PREP", None)
@@ -138,7 +141,7 @@ def run_case(torch, la, dist, fmt, M, N, K, slices, steps, warmup, world, warm_f
     e3.record(stream)
     torch.cuda.synchronize()
     kern = e2.elapsed_time(e3) / 1e3 / steps
-    del A, B, C, gathered
+    del A, B, C, gather
     torch.cuda.empty_cache()
     return per[0].item(), per[1].item(), kern
 

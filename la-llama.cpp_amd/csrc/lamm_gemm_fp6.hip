@@ -44,7 +44,6 @@ typedef _Float16 half4 __attribute__((ext_vector_type(4)));
 constexpr int F6_KB = 2;        // 32-element blocks per K-step
 constexpr int F6_TI = 256;      // weight rows per tile
 constexpr int F6_TJ = 128;      // activation rows per tile
-constexpr int F6_NT = 512;      // threads per workgroup (8 waves, 2 per SIMD)
 constexpr int F6_PIECE = 1024;  // bytes one wave moves per LDS-DMA instruction (64 lanes x 16 B)
 constexpr int F6_NBUF = 4;      // LDS stages (3 K-steps of DMA in flight)
 constexpr int SCALE_W = 130, SCALE_HI = 134, SCALE_LO = 130;   // E8M0: 2^(s-127)
@@ -62,9 +61,6 @@ template <> struct F6<kQ5_0> { static constexpr int ABPB = 22, VBPB = 34; static
 constexpr int F6_A_BYTES = 2 * F6_KB * F6_TI * 16;
 constexpr int F6_B_BYTES = 2 * F6_KB * 2 * F6_TJ * 16;
 constexpr int F6_STAGE = F6_A_BYTES + F6_B_BYTES;
-constexpr int F6_NW = F6_NT / 64;
-static_assert(F6_STAGE % (F6_NW * F6_PIECE) == 0, "every wave moves the same number of DMA pieces");
-constexpr int F6_PPW = F6_STAGE / F6_PIECE / F6_NW;   // DMA pieces per wave per stage
 constexpr int F6_PA = F6_A_BYTES / F6_PIECE;
 
 // byte offset of plane p (16 bytes) of the fragment of (block b, [k-group h,] row r).  Planes
@@ -290,9 +286,18 @@ __device__ __forceinline__ half4 f6_dq(const F6Frag& f) {   // {d, 0, 0, 0}
 
 // V: ablations for tools/ab_gemm.py (0 production, 1 no compute, 2 no DMA, 3 no epilogue FMAs,
 //    4 no DMA + no LDS fragment reads (operands from registers), 5 no DMA + no barrier)
-template <int T, int V>
-__global__ __launch_bounds__(F6_NT) void gemm_fp6_kernel(GemvArgs p, const unsigned char* ws) {
+// WJ: 32-row activation sub-tiles per wave (2: 8 waves of 64x64; 1: 16 waves of 32x64)
+template <int WJ> struct F6Waves {
+  static constexpr int NWJ = F6_TJ / (32 * WJ), NWI = F6_TI / 64, NW = NWJ * NWI, NT = 64 * NW;
+  static_assert(F6_STAGE % (NW * F6_PIECE) == 0, "every wave moves the same number of DMA pieces");
+  static constexpr int PPW = F6_STAGE / F6_PIECE / NW;   // DMA pieces per wave per stage
+};
+
+template <int T, int V, int WJ>
+__global__ __launch_bounds__(F6Waves<WJ>::NT) void gemm_fp6_kernel(GemvArgs p, const unsigned char* ws) {
   using F = F6<T>;
+  using WV = F6Waves<WJ>;
+  constexpr int F6_NW = WV::NW, F6_PPW = WV::PPW, UPB = 2 * WJ;   // UPB: units per block
   constexpr bool AFF = F::AFF;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const F6Layout L = F6Layout::of(p);
@@ -300,7 +305,7 @@ __global__ __launch_bounds__(F6_NT) void gemm_fp6_kernel(GemvArgs p, const unsig
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int lr = lane & 31, h = lane >> 5;
-  const int wj = w & 1, wi = w >> 1;   // 2 (j) x 4 (i) waves
+  const int wj = w % WV::NWJ, wi = w / WV::NWJ;   // NWJ (j) x 4 (i) waves
   // XCD-aware tile order: workgroup id -> tile index so that the workgroups one XCD runs at
   // once are neighbouring tiles of one slice (their DMA chunks meet in that XCD's L2).
   int it, jt, z;
@@ -340,9 +345,9 @@ __global__ __launch_bounds__(F6_NT) void gemm_fp6_kernel(GemvArgs p, const unsig
   };
 
   const int sc_a = h ? SCALE_LO : SCALE_HI;   // MFMA A operand = activations (k-group h)
-  f32x16 acc[2][2];   // [jt][it]: 2 * sum d_a d_b S (+ 2 * sum m_a s_b)
+  f32x16 acc[WJ][2];   // [jt][it]: 2 * sum d_a d_b S (+ 2 * sum m_a s_b)
 #pragma unroll
-  for (int x = 0; x < 2; ++x)
+  for (int x = 0; x < WJ; ++x)
 #pragma unroll
     for (int y = 0; y < 2; ++y)
 #pragma unroll
@@ -352,7 +357,7 @@ __global__ __launch_bounds__(F6_NT) void gemm_fp6_kernel(GemvArgs p, const unsig
   constexpr bool NODMA = V == 2 || V == 4 || V == 5;
   if (!NODMA)
     for (int k = 0; k < F6_NBUF - 1 && k < nsteps; ++k) issue(k);
-  F6Frag fb[2][2], fa[2][2];   // [block][sub-tile]
+  F6Frag fb[2][WJ], fa[2][2];   // [block slot][sub-tile]
   F6Res rr[2];
   for (int ks = 0; ks < nsteps; ++ks) {
     if (!NODMA) {   // this wave's pieces of stage ks landed (younger stages may stay in flight)
@@ -374,7 +379,7 @@ __global__ __launch_bounds__(F6_NT) void gemm_fp6_kernel(GemvArgs p, const unsig
       if constexpr (V == 4) {
         if (ks > 0) return;
       }
-      const int r = 64 * wj + 32 * x + lr;
+      const int r = 32 * WJ * wj + 32 * x + lr;
       f6_load(fb[b & 1][x], sB + f6_boff(0, b, h, r), sB + f6_boff(1, b, h, r));
     };
     auto ldA = [&](int b, int y) {
@@ -384,21 +389,21 @@ __global__ __launch_bounds__(F6_NT) void gemm_fp6_kernel(GemvArgs p, const unsig
       const int r = 64 * wi + 32 * y + lr;
       f6_load(fa[b & 1][y], sA + f6_aoff(0, b, r), sA + f6_aoff(1, b, r));
     };
+    // unit n = (block n / UPB, j sub-tile (n / 2) % WJ, i sub-tile n % 2)
     auto ld_unit = [&](int n) {   // the fragments unit n uses first
-      const int b = n >> 2, x = (n >> 1) & 1, y = n & 1;
-      if ((n & 3) == 0) { ldB(b, 0); ldA(b, 0); }
-      else if ((n & 3) == 1) ldA(b, y);
-      else if ((n & 3) == 2) ldB(b, x);
+      const int b = n / UPB, u = n % UPB, x = (n / 2) % WJ;
+      if (u == 0) { ldB(b, 0); ldA(b, 0); }
+      else if (u == 1) ldA(b, 1);
+      else if ((u & 1) == 0) ldB(b, x);
     };
-    // unit n = (block n >> 2, j sub-tile (n >> 1) & 1, i sub-tile n & 1)
     auto mfmas = [&](int n, F6Res& R) {
-      const F6Frag& fB = fb[(n >> 2) & 1][(n >> 1) & 1];
-      const F6Frag& fA = fa[(n >> 2) & 1][n & 1];
+      const F6Frag& fB = fb[(n / UPB) & 1][(n / 2) % WJ];
+      const F6Frag& fA = fa[(n / UPB) & 1][n & 1];
       R.s = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fB.v, fA.v, fz, 2, 2, 0, sc_a, 0, SCALE_W);
       R.pr = __builtin_amdgcn_mfma_f32_32x32x8f16(f6_dq<AFF>(fB), f6_dq<AFF>(fA), fz, 0, 0, 0);
     };
     auto epi = [&](int n, const F6Res& R) {
-      f32x16& c = acc[(n >> 1) & 1][n & 1];
+      f32x16& c = acc[(n / 2) % WJ][n & 1];
       if constexpr (V == 3) {
         c[0] += R.s[0] + R.pr[0];
       } else {
@@ -406,25 +411,24 @@ __global__ __launch_bounds__(F6_NT) void gemm_fp6_kernel(GemvArgs p, const unsig
         for (int e = 0; e < 16; ++e) c[e] = __builtin_fmaf(R.s[e], R.pr[e], c[e]);
       }
     };
-    uint32_t msA[2][2] = {{0, 0}, {0, 0}}, msB[2][2] = {{0, 0}, {0, 0}};   // q4_1: m_a / s_b per block
+    uint32_t msA[2][2] = {{0, 0}, {0, 0}}, msB[WJ][2] = {};   // q4_1: m_a / s_b per block
     auto keep_ms = [&](int b) {
       if constexpr (AFF) {
 #pragma unroll
-        for (int x = 0; x < 2; ++x) {
-          msA[x][b >> 1] |= ((uint32_t)fa[b & 1][x].v[7] & 0xffffu) << (16 * (b & 1));
-          msB[x][b >> 1] |= ((uint32_t)fb[b & 1][x].v[7] & 0xffffu) << (16 * (b & 1));
-        }
+        for (int y = 0; y < 2; ++y) msA[y][b >> 1] |= ((uint32_t)fa[b & 1][y].v[7] & 0xffffu) << (16 * (b & 1));
+#pragma unroll
+        for (int x = 0; x < WJ; ++x) msB[x][b >> 1] |= ((uint32_t)fb[b & 1][x].v[7] & 0xffffu) << (16 * (b & 1));
       }
     };
 
     static_assert(F6_KB == 2 || F6_KB == 4, "the m*s rank-KB MFMA packs <= 4 blocks per k half");
-    constexpr int NU = 4 * F6_KB;   // units per K-step
-    constexpr int LDA = 4;          // fragment prefetch distance in units (one block)
+    constexpr int NU = UPB * F6_KB;   // units per K-step
+    constexpr int LDA = UPB;          // fragment prefetch distance in units (one block)
     unroll<LDA>([&](auto NN) { ld_unit(NN); });
     mfmas(0, rr[0]);
     unroll<NU>([&](auto NN) {
       constexpr int n = NN;
-      if constexpr ((n & 3) == 3) keep_ms(n >> 2);
+      if constexpr (n % UPB == UPB - 1) keep_ms(n / UPB);
       if constexpr (n + LDA < NU) ld_unit(n + LDA);
       if constexpr (n + 1 < NU) mfmas(n + 1, rr[(n + 1) & 1]);
       __builtin_amdgcn_sched_barrier(0);
@@ -433,7 +437,7 @@ __global__ __launch_bounds__(F6_NT) void gemm_fp6_kernel(GemvArgs p, const unsig
     });
     if constexpr (AFF) {   // sum_b m_a * s_b: rank-KB per K-step, both k halves carry it (x2 like P)
 #pragma unroll
-      for (int x = 0; x < 2; ++x) {
+      for (int x = 0; x < WJ; ++x) {
         const half4 sf = __builtin_bit_cast(half4, uint2{msB[x][0], msB[x][1]});
 #pragma unroll
         for (int y = 0; y < 2; ++y) {
@@ -446,13 +450,13 @@ __global__ __launch_bounds__(F6_NT) void gemm_fp6_kernel(GemvArgs p, const unsig
 
   float* Cz = p.C + (int64_t)i12 * p.sc2 + (int64_t)i13 * p.sc3;
 #pragma unroll
-  for (int x = 0; x < 2; ++x)
+  for (int x = 0; x < WJ; ++x)
 #pragma unroll
     for (int y = 0; y < 2; ++y) {
       const int64_t i = (int64_t)it * F6_TI + 64 * wi + 32 * y + lr;
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
-        const int64_t j = (int64_t)jt * F6_TJ + 64 * wj + 32 * x + (e & 3) + 8 * (e >> 2) + 4 * h;
+        const int64_t j = (int64_t)jt * F6_TJ + 32 * WJ * wj + 32 * x + (e & 3) + 8 * (e >> 2) + 4 * h;
         if (i < p.M && j < p.N) Cz[j * p.ldc + i] = 0.5f * acc[x][y][e];
       }
     }
@@ -475,19 +479,25 @@ hipError_t launch_fp6_t(const GemvArgs& p, void* ws, hipStream_t s) {
                      dim3(PREP_NT), 0, s, p, w);
   }
   const size_t lds = (size_t)F6_NBUF * F6_STAGE;
-  auto go = [&](auto kern) {
+  auto go = [&](auto kern, int nt) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(kern, dim3((unsigned)(L.nit * L.njt * p.ne12 * p.ne13)), dim3(F6_NT), lds, s, p,
+    hipLaunchKernelGGL(kern, dim3((unsigned)(L.nit * L.njt * p.ne12 * p.ne13)), dim3(nt), lds, s, p,
                        static_cast<const unsigned char*>(ws));
   };
   const char* ev = getenv("LAMM_GEMM_VARIANT");
+  const char* ew = getenv("LAMM_FP6_WJ");   // A/B: 1 = 16 waves of 32x64
+  const int wjv = ew ? atoi(ew) : 2;
+  if (wjv == 1) {
+    go(gemm_fp6_kernel<T, 0, 1>, F6Waves<1>::NT);
+    return hipGetLastError();
+  }
+  constexpr int NT2 = F6Waves<2>::NT;
   switch (ev ? atoi(ev) : 0) {
-    case 1: go(gemm_fp6_kernel<T, 1>); break;
-    case 2: go(gemm_fp6_kernel<T, 2>); break;
-    case 3: go(gemm_fp6_kernel<T, 3>); break;
-    case 4: go(gemm_fp6_kernel<T, 4>); break;
-    case 5: go(gemm_fp6_kernel<T, 5>); break;
-    default: go(gemm_fp6_kernel<T, 0>);
+    case 1: go(gemm_fp6_kernel<T, 1, 2>, NT2); break;
+    case 2: go(gemm_fp6_kernel<T, 2, 2>, NT2); break;
+    case 3: go(gemm_fp6_kernel<T, 3, 2>, NT2); break;
+    case 5: go(gemm_fp6_kernel<T, 5, 2>, NT2); break;
+    default: go(gemm_fp6_kernel<T, 0, 2>, NT2);
   }
   return hipGetLastError();
 }

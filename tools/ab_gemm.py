@@ -40,9 +40,14 @@ def main():
                   4 * M * N, 4 * M * N * slices)
     for rnd in range(5):
         for v in variants:
+            os.environ.pop("LAMM_FP6_WJ", None)
             if v in ("fp6", "i8"):
                 os.environ["LAMM_GEMM_PATH"] = v
                 os.environ["LAMM_GEMM_VARIANT"] = "0"
+            elif v.startswith("fp6w"):   # fp6 wave-tile width: fp6w1 = 16 waves of 32x64
+                os.environ["LAMM_GEMM_PATH"] = "fp6"
+                os.environ["LAMM_GEMM_VARIANT"] = "0"
+                os.environ["LAMM_FP6_WJ"] = v[4:]
             elif v.startswith("fp6-"):   # fp6 ablations: fp6-1 no compute, fp6-2 no DMA, fp6-3 no FMAs
                 os.environ["LAMM_GEMM_PATH"] = "fp6"
                 os.environ["LAMM_GEMM_VARIANT"] = v[4:]

@@ -40,7 +40,8 @@ I8_DENSE_PEAK_TOPS = 5000.0    # dense MFMA-i8 = 2x the 2.5 PF dense bf16 rate (
 MALL_BYTES = 256 << 20
 
 FP16_FIELDS = {  # byte offsets of fp16 scale fields inside one block (lamm_formats.h)
-    "q4_0": [0], "q4_1": [0, 2], "q5_0": [0], "q5_1": [0, 2], "q8_0": [0], "q2_k": [80, 82]}
+    "q4_0": [0], "q4_1": [0, 2], "q5_0": [0], "q5_1": [0, 2], "q8_0": [0], "q2_k": [80, 82],
+    "q4_k": [0, 2], "q5_k": [0, 2], "q6_k": [208]}
 
 
 def log(*a):
@@ -283,7 +284,7 @@ def main():
                              "per_launch_us": round(g_main * 1e6, 2)}}
     if args.sweep:
         sw = {}
-        for f in ["f32", "q4_0", "q4_1", "q5_0", "q5_1", "q8_0", "q2_k"]:
+        for f in ["f32", "q4_0", "q4_1", "q5_0", "q5_1", "q8_0", "q2_k", "q4_k", "q5_k", "q6_k"]:
             u = gemv_bytes(la, f, M, K)
             sl = max(4, -(-int(1.15 * MALL_BYTES) // u))
             _, _, kk = run_case(torch, la, dist, f, M, 1, K, sl, max(5, args.steps // 2), 2, world)

@@ -39,6 +39,9 @@ template <> struct Fmt<kQ5_0> { static constexpr int QK = 32, BPB = 22, G = 8, V
 template <> struct Fmt<kQ5_1> { static constexpr int QK = 32, BPB = 24, G = 8, VBPB = 36, VQK = 32; };
 template <> struct Fmt<kQ8_0> { static constexpr int QK = 32, BPB = 34, G = 8, VBPB = 34, VQK = 32; };
 template <> struct Fmt<kQ2_K> { static constexpr int QK = 256, BPB = 84, G = 1, VBPB = 292, VQK = 256; };
+template <> struct Fmt<kQ4_K> { static constexpr int QK = 256, BPB = 144, G = 1, VBPB = 292, VQK = 256; };
+template <> struct Fmt<kQ5_K> { static constexpr int QK = 256, BPB = 176, G = 1, VBPB = 292, VQK = 256; };
+template <> struct Fmt<kQ6_K> { static constexpr int QK = 256, BPB = 210, G = 1, VBPB = 292, VQK = 256; };
 template <> struct Fmt<kF32>  { static constexpr int QK = 1, BPB = 4, G = 64, VBPB = 4, VQK = 1; };
 
 template <int T> struct Geo {
@@ -69,7 +72,7 @@ struct Smem {
   uint32_t bq[NC][GG::BQ_WORDS];
   float bd[NC][T == kF32 ? 1 : GG::VBLK];
   float bx[NC][T == kF32 ? 1 : GG::VBLK];   // q8_0: sum(q) as float; q8_1: s
-  int bs[NC][T == kQ2_K ? GG::VBLK * 16 : 1];  // q8_K bsums
+  int bs[NC][Fmt<T>::VQK == 256 ? GG::VBLK * 16 : 1];  // q8_K bsums
 };
 
 // ---- stage the activation segment (decoded) into LDS --------------------------
@@ -91,7 +94,7 @@ __device__ __forceinline__ void stage_b(SM& sm, const GemvArgs& p, const unsigne
       if (j < p.N && e < p.K) v = bload4(rs, (uint32_t)(j * p.ldb + e * 4));
       sm.bq[j][swz(w)] = v;
     }
-  } else if constexpr (T == kQ2_K) {
+  } else if constexpr (F::VQK == 256) {
     // q8_K: f32 d | 256 x i8 | 16 x i16 bsums  = 73 dwords, dword aligned
     for (int it = t; it < NC * GG::VBLK * 73; it += kThreads) {
       const int j = it / (GG::VBLK * 73), r = it % (GG::VBLK * 73);
@@ -181,6 +184,81 @@ __device__ __forceinline__ void block_dot(const uint32_t (&w)[Geo<T>::CH_WORDS +
       }
       const float yd = sm.bd[j][ch];
       acc[j] += (yd * da) * (float)isum - (yd * dm) * (float)summs;
+    }
+  } else if constexpr (T == kQ4_K || T == kQ5_K) {
+    // block_q4_K: d, dmin @0 | scales[12] @4 | qs[128] @16 ; block_q5_K: qh[32] @16, qs @48.
+    // 6-bit scales / mins: the utmp shuffle of LC/ggml-quants.c:7324-7330.  Element
+    // 32*sb + l: nibble (sb & 1) of qs[32*(sb >> 1) + l] (+16 if bit sb of qh[l]).
+    static_assert(O == 0, "k-quant chunks hold one super-block");
+    constexpr bool Q5 = T == kQ5_K;
+    constexpr int QS = Q5 ? 12 : 4;   // dword index of qs
+    uint32_t u0 = w[1], u1 = w[2], u2 = w[3];
+    const uint32_t u3 = ((u2 >> 4) & 0x0f0f0f0fu) | (((u1 >> 6) & 0x03030303u) << 4);
+    const uint32_t uaux = u1 & 0x3f3f3f3fu;
+    u1 = (u2 & 0x0f0f0f0fu) | (((u0 >> 6) & 0x03030303u) << 4);
+    u2 = uaux;
+    u0 &= 0x3f3f3f3fu;
+    const float da = h2f(w[0] & 0xffff), dm = h2f(w[0] >> 16);
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      if (j >= ncols) break;
+      const uint32_t* bq = sm.bq[j];
+      int isum = 0, summ = 0;
+#pragma unroll
+      for (int sb = 0; sb < 8; ++sb) {
+        const int sc = (int)(((sb < 4 ? u0 : u1) >> (8 * (sb & 3))) & 0xffu);
+        const int mn = (int)(((sb < 4 ? u2 : u3) >> (8 * (sb & 3))) & 0xffu);
+        int part = 0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const u32x4 b = *(const u32x4*)&bq[swz(ch * 64 + 8 * sb + 4 * h)];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            uint32_t q = (w[QS + 8 * (sb >> 1) + 4 * h + k] >> (4 * (sb & 1))) & 0x0f0f0f0fu;
+            if constexpr (Q5) q |= ((w[4 + 4 * h + k] >> sb) & 0x01010101u) << 4;
+            part = dot4(q, b[k], part);
+          }
+        }
+        isum += sc * part;
+        summ += mn * (sm.bs[j][ch * 16 + 2 * sb] + sm.bs[j][ch * 16 + 2 * sb + 1]);
+      }
+      const float yd = sm.bd[j][ch];
+      acc[j] += (yd * da) * (float)isum - (yd * dm) * (float)summ;
+    }
+  } else if constexpr (T == kQ6_K) {
+    // block_q6_K: ql[128] @0 | qh[64] @128 | scales[16] (int8) @192 | d @208.  Element
+    // 128*hf + 32*part + l = (nibble (part >> 1) of ql[64*hf + 32*(part & 1) + l]
+    //   | ((qh[32*hf + l] >> 2*part) & 3) << 4) - 32     (LC/ggml-quants.c:8710-8720)
+    static_assert(O == 0, "k-quant chunks hold one super-block");
+    const float da = h2f(w[52] & 0xffff);
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      if (j >= ncols) break;
+      const uint32_t* bq = sm.bq[j];
+      int isum = 0;
+#pragma unroll
+      for (int sb = 0; sb < 8; ++sb) {
+        const int hf = sb >> 2, part = sb & 3;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const u32x4 b = *(const u32x4*)&bq[swz(ch * 64 + 8 * sb + 4 * h)];
+          int s16 = 0;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int kk = 4 * h + k;
+            const uint32_t nw = w[16 * hf + 8 * (part & 1) + kk];
+            const uint32_t nib = (part < 2 ? nw : (nw >> 4)) & 0x0f0f0f0fu;
+            const uint32_t hb = ((w[32 + 8 * hf + kk] >> (2 * part)) & 0x03030303u) << 4;
+            // per byte (q - 32) with q = nib | hb in [0, 63]: no borrow crosses a byte
+            const uint32_t q = (((nib | hb) | 0x80808080u) - 0x20202020u) ^ 0x80808080u;
+            s16 = dot4(q, b[k], s16);
+          }
+          const int si = 2 * sb + h;
+          const int scale = (int)(int8_t)((w[48 + (si >> 2)] >> (8 * (si & 3))) & 0xffu);
+          isum += scale * s16;
+        }
+      }
+      acc[j] += (sm.bd[j][ch] * da) * (float)isum;
     }
   } else {
     // 32-element blocks.  Unpack to 8 int8 words (elements 0-15 = low nibbles,
@@ -329,8 +407,13 @@ __global__ __launch_bounds__(kThreads) void gemv_kernel(GemvArgs p) {
     const int cb0 = seg * GG::SEG_BLK + ch * F::G;           // first A block of chunk
     if (V != 4 && row < rows && cb0 < p.nblk) {
       uint32_t w[GG::CH_WORDS + 1];
-      const uint32_t* src = &sm.a[(row * GG::ROW_BYTES + ch * GG::CH_BYTES) / 4];
-      if constexpr (GG::CH_BYTES % 16 == 0) {
+      const int cbyte = row * GG::ROW_BYTES + ch * GG::CH_BYTES;
+      const uint32_t* src = &sm.a[cbyte / 4];
+      if constexpr (GG::CH_BYTES % 4 != 0) {   // q6_K: 210-byte chunks, 2-byte aligned
+        const int sh = (cbyte & 3) * 8;
+#pragma unroll
+        for (int k = 0; k < GG::CH_WORDS; ++k) w[k] = __builtin_amdgcn_alignbit(src[k + 1], src[k], sh);
+      } else if constexpr (GG::CH_BYTES % 16 == 0) {
 #pragma unroll
         for (int k = 0; k < GG::CH_WORDS / 4; ++k) {
           const u32x4 x = *(const u32x4*)&src[4 * k];
@@ -387,7 +470,7 @@ struct SmemStream {
   uint32_t bq[NC][GG::BQ_WORDS];
   float bd[NC][T == kF32 ? 1 : GG::VBLK];
   float bx[NC][T == kF32 ? 1 : GG::VBLK];
-  int bs[NC][T == kQ2_K ? GG::VBLK * 16 : 1];
+  int bs[NC][Fmt<T>::VQK == 256 ? GG::VBLK * 16 : 1];
 };
 
 template <int T, int NC, int WAVES>
@@ -444,8 +527,13 @@ __global__ __launch_bounds__(64 * WAVES) void gemv_stream_kernel(GemvArgs p) {
     const int cb0 = ch * F::G;
     if (row < rows && cb0 < p.nblk) {
       uint32_t wv[GG::CH_WORDS + 1];
-      const uint32_t* src = &sm.a[w][(row * GG::ROW_BYTES + ch * GG::CH_BYTES) / 4];
-      if constexpr (GG::CH_BYTES % 16 == 0) {
+      const int cbyte = row * GG::ROW_BYTES + ch * GG::CH_BYTES;
+      const uint32_t* src = &sm.a[w][cbyte / 4];
+      if constexpr (GG::CH_BYTES % 4 != 0) {   // q6_K: 210-byte chunks, 2-byte aligned
+        const int sh = (cbyte & 3) * 8;
+#pragma unroll
+        for (int c = 0; c < GG::CH_WORDS; ++c) wv[c] = __builtin_amdgcn_alignbit(src[c + 1], src[c], sh);
+      } else if constexpr (GG::CH_BYTES % 16 == 0) {
 #pragma unroll
         for (int c = 0; c < GG::CH_WORDS / 4; ++c) {
           const u32x4 x = *(const u32x4*)&src[4 * c];
@@ -535,7 +623,10 @@ int variant() {
 template <int T, int NC>
 hipError_t launch_t(const GemvArgs& p, hipStream_t s) {
   const int v = variant();
-  if constexpr (stream_fits<T, NC, 4>()) {
+  // the 256-element super-block formats decode a whole super-block per lane: with more than
+  // one activation column their stream kernel outgrows 256 VGPRs (spills), so only NC == 1
+  // (the decode GEMV) streams; wider N takes the LDS-staged segment kernel
+  if constexpr (stream_fits<T, NC, 4>() && (Fmt<T>::VQK != 256 || NC == 1)) {
     if (p.nblk <= Geo<T>::SEG_BLK && v == 0) return launch_stream<T, NC>(p, s);
   }
   if constexpr (T == kQ4_0 && NC == 1) {
@@ -569,7 +660,7 @@ size_t gemv_lds_bytes(int type, int nc) {
          : nc <= 4 ? sizeof(Smem<T, 4>) : sizeof(Smem<T, 8>);
   switch (type) {
     LDS_CASE(kQ4_0) LDS_CASE(kQ4_1) LDS_CASE(kQ5_0) LDS_CASE(kQ5_1)
-    LDS_CASE(kQ8_0) LDS_CASE(kQ2_K) LDS_CASE(kF32)
+    LDS_CASE(kQ8_0) LDS_CASE(kQ2_K) LDS_CASE(kQ4_K) LDS_CASE(kQ5_K) LDS_CASE(kQ6_K) LDS_CASE(kF32)
     default: return 0;
   }
 #undef LDS_CASE
@@ -583,6 +674,9 @@ hipError_t launch_gemv(int type, const GemvArgs& p, hipStream_t s) {
     case kQ5_1: return launch_nc<kQ5_1>(p, s);
     case kQ8_0: return launch_nc<kQ8_0>(p, s);
     case kQ2_K: return launch_nc<kQ2_K>(p, s);
+    case kQ4_K: return launch_nc<kQ4_K>(p, s);
+    case kQ5_K: return launch_nc<kQ5_K>(p, s);
+    case kQ6_K: return launch_nc<kQ6_K>(p, s);
     case kF32:  return launch_nc<kF32>(p, s);
     default: return hipErrorInvalidValue;
   }

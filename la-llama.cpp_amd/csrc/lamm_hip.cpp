@@ -357,6 +357,11 @@ bool is_contiguous(const ggml::tensor* t) {
          t->nb[3] == t->nb[2] * (size_t)t->ne[2];
 }
 
+bool kquants_enabled() {
+  const char* e = getenv("LAMM_HIP_KQUANTS");
+  return !(e && e[0] == '0');
+}
+
 }  // namespace
 
 extern "C" int lamm_get_opt_level(void) { return probe().count ? (opt_level() > 0 ? 3 : 0) : 0; }
@@ -371,6 +376,9 @@ extern "C" bool lamm_can_mul_mat(const struct ggml_compute_params* vparams, cons
   if (!src0 || !src1) return false;
   const int vdt = vec_dot_type(src0->type);
   if (vdt < 0) return false;                                 // :37-52 supported pairs
+  // q4_K / q5_K / q6_K are beyond the reference's lamm set (e.g. a Q4_0
+  // model's Q6_K output.weight); LAMM_HIP_KQUANTS=0 restores the reference's exact set
+  if ((src0->type == kQ4_K || src0->type == kQ5_K || src0->type == kQ6_K) && !kquants_enabled()) return false;
   if (src1->type == vdt && !is_contiguous(src1)) return false;  // :23-28
   if (src1->nb[0] != block_bytes(src1->type)) return false;  // :29-31
   if (dst->type != kF32) return false;                       // :34-36

@@ -13,6 +13,10 @@
  *                              q8_K :3981-4018
  *   * scalar vec_dot           q4_0 :4451-4469, q4_1 :4700-4718, q5_0 :4985-5008,
  *                              q5_1 :5290-5313, q8_0 :5300-5313, q2_K :5820-5860,
+ *                              q4_K :7301-7358, q5_K :7968-8029, q6_K :8695-8738
+ *                              (the SURVEY §8f "next" formats; no quantizer restated:
+ *                              their test inputs are the reference's own bytes or
+ *                              random bytes, for which vec_dot is equally defined)
  *                              f32 LC/ggml.c:1576-1581 (double accumulation)
  *   * mul_mat semantics        src/lamm_kernel_q4_0.hpp:21-37 (C[j*ldc+i], K blocks),
  *                              computing ALL M rows (not inheriting SURVEY §8a defect 1)
@@ -65,7 +69,7 @@ uint16_t lo_fp32_to_fp16(float f) {   /* IEEE round-to-nearest-even */
 int lo_block_elems(int t) {
   switch (t) {
   case LO_F32: return 1;
-  case LO_Q2_K: case LO_Q8_K: return 256;
+  case LO_Q2_K: case LO_Q4_K: case LO_Q5_K: case LO_Q6_K: case LO_Q8_K: return 256;
   default: return 32;
   }
 }
@@ -80,6 +84,9 @@ size_t lo_block_bytes(int t) {
   case LO_Q8_0: return 34;
   case LO_Q8_1: return 36;
   case LO_Q2_K: return 84;
+  case LO_Q4_K: return 144;
+  case LO_Q5_K: return 176;
+  case LO_Q6_K: return 210;
   case LO_Q8_K: return 292;
   default: return 0;
   }
@@ -90,7 +97,7 @@ int lo_vec_dot_type(int t) {
   case LO_F32: return LO_F32;
   case LO_Q4_0: case LO_Q5_0: case LO_Q8_0: return LO_Q8_0;
   case LO_Q4_1: case LO_Q5_1: return LO_Q8_1;
-  case LO_Q2_K: return LO_Q8_K;
+  case LO_Q2_K: case LO_Q4_K: case LO_Q5_K: case LO_Q6_K: return LO_Q8_K;
   default: return -1;
   }
 }
@@ -364,6 +371,40 @@ void lo_quantize_row(int type, int flavour, const float *x, void *y, int k) {
   }
 }
 
+/* ------------------------------------------------ k-quant element access */
+
+/* 6-bit scales / mins of q4_K / q5_K from the 12 packed bytes: the utmp shuffle of
+ * LC/ggml-quants.c:7324-7330 (kmask1 = 0x3f3f3f3f, kmask2 = 0x0f0f0f0f, kmask3 = 0x03030303) */
+static void kq_scale_min(const uint8_t *s12, uint8_t sc[8], uint8_t mn[8]) {
+  uint32_t u[4];
+  memcpy(u, s12, 12);
+  u[3] = ((u[2] >> 4) & 0x0f0f0f0fu) | (((u[1] >> 6) & 0x03030303u) << 4);
+  const uint32_t uaux = u[1] & 0x3f3f3f3fu;
+  u[1] = (u[2] & 0x0f0f0f0fu) | (((u[0] >> 6) & 0x03030303u) << 4);
+  u[2] = uaux;
+  u[0] &= 0x3f3f3f3fu;
+  memcpy(sc, u, 8);
+  memcpy(mn, u + 2, 8);
+}
+
+/* quant of element e (0..255) of a q4_K / q5_K block: :7316-7322 / :7983-7992 */
+static int kq_nibble(const uint8_t *x, int type, int e) {
+  const int g = e / 64, hi = (e % 64) >= 32, l = e % 32;
+  const uint8_t *qs = x + (type == LO_Q5_K ? 48 : 16);
+  int q = hi ? (qs[32 * g + l] >> 4) : (qs[32 * g + l] & 0xF);
+  if (type == LO_Q5_K) q += (x[16 + l] >> (e / 32)) & 1 ? 16 : 0;
+  return q;
+}
+
+/* q6_K element e: (ql | qh << 4) - 32, :8710-8720 */
+static int q6_value(const uint8_t *x, int e) {
+  const int hf = e / 128, r = e % 128, part = r / 32, l = r % 32;
+  const uint8_t *ql = x + 64 * hf, *qh = x + 128 + 32 * hf;
+  const int nib = (part & 1) ? ql[32 + l] : ql[l];
+  const int q = (part < 2 ? (nib & 0xF) : (nib >> 4)) | (((qh[l] >> (2 * part)) & 3) << 4);
+  return q - 32;
+}
+
 /* --------------------------------------------------------- dequant */
 
 void lo_dequantize_row(int type, const void *vx, float *y, int k) {
@@ -400,6 +441,21 @@ void lo_dequantize_row(int type, const void *vx, float *y, int k) {
         const int q = (x[16 + 32 * n + l] >> (2 * j)) & 3;
         y[e] = d * (x[is] & 0xF) * q - dmin * (x[is] >> 4);
       }
+    } break;
+    case LO_Q4_K: case LO_Q5_K: {   /* LC/ggml-quants.c dequantize_row_q4_K / q5_K */
+      uint8_t sc[8], mn[8];
+      kq_scale_min(x + 4, sc, mn);
+      const float d = H2F(rd16(x)), dmin = H2F(rd16(x + 2));
+      for (int e = 0; e < 256; e++) {
+        const int j = e / 32, l = e % 32;
+        int q = kq_nibble(x, type, e);
+        y[e] = d * sc[j] * q - dmin * mn[j];
+        (void)l;
+      }
+    } break;
+    case LO_Q6_K: {                  /* dequantize_row_q6_K */
+      const float d = H2F(rd16(x + 208));
+      for (int e = 0; e < 256; e++) y[e] = d * (int8_t)x[192 + e / 16] * q6_value(x, e);
     } break;
     case LO_Q8_K: {
       float d; memcpy(&d, x, 4);
@@ -483,6 +539,44 @@ float lo_vec_dot(int type, int k, const void *va, const void *vb) {
       }
       sumf += dall * isum - dmin * summs;
     }
+    return sumf;
+  }
+  if (type == LO_Q4_K || type == LO_Q5_K || type == LO_Q6_K) {
+    /* the reference's 8-lane order: aux32[l] (int) per super-block, sums[l] += d*aux32[l],
+     * sumf -= dmin*sumi per super-block, then sumf += sums[l] (:7301-7358, :8695-8738) */
+    float sums[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int i = 0; i < k / 256; ++i, a += ab, b += bb) {
+      float yd; memcpy(&yd, b, 4);
+      const int8_t *q8 = (const int8_t *)(b + 4);
+      int32_t aux32[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      int8_t av[256];
+      for (int e = 0; e < 256; ++e) av[e] = (int8_t)(type == LO_Q6_K ? q6_value(a, e) : kq_nibble(a, type, e));
+      if (type == LO_Q6_K) {
+        for (int j = 0; j < 16; ++j) {
+          const int scale = (int8_t)a[192 + j];
+          for (int l = 0; l < 16; ++l) aux32[l % 8] += scale * (int16_t)(q8[16 * j + l] * av[16 * j + l]);
+        }
+        const float d = H2F(rd16(a + 208)) * yd;
+        for (int l = 0; l < 8; ++l) sums[l] += d * aux32[l];
+      } else {
+        uint8_t sc[8], mn[8];
+        kq_scale_min(a + 4, sc, mn);
+        int sumi = 0;
+        for (int j = 0; j < 16; ++j) {
+          int16_t bs; memcpy(&bs, b + 260 + 2 * j, 2);
+          sumi += bs * mn[j / 2];
+        }
+        for (int j = 0; j < 8; ++j) {
+          const int32_t scale = sc[j];
+          for (int l = 0; l < 32; ++l) aux32[l % 8] += scale * (int16_t)(q8[32 * j + l] * av[32 * j + l]);
+        }
+        const float d = H2F(rd16(a)) * yd;
+        for (int l = 0; l < 8; ++l) sums[l] += d * aux32[l];
+        const float dmin = H2F(rd16(a + 2)) * yd;
+        sumf -= dmin * sumi;
+      }
+    }
+    for (int l = 0; l < 8; ++l) sumf += sums[l];
     return sumf;
   }
   const int bq_off = (type == LO_Q4_1 || type == LO_Q5_1) ? 4 : 2;

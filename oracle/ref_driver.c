@@ -20,7 +20,7 @@
  * Usage:
  *   ref_driver gen   <type> <M> <N> <K> <nthreads> <A_f32.bin> <B_f32.bin> <out_prefix>
  *   ref_driver bench <type> <M> <N> <K> <nthreads> <iters> <budget_seconds>
- * type is a ggml type name: f32 q4_0 q4_1 q5_0 q5_1 q8_0 q2_k
+ * type is a ggml type name: f32 q4_0 q4_1 q5_0 q5_1 q8_0 q2_k (+ q4_k q5_k q6_k)
  */
 #include "ggml.h"
 
@@ -40,6 +40,9 @@ static enum ggml_type parse_type(const char *s) {
   if (!strcasecmp(s, "q5_1")) return GGML_TYPE_Q5_1;
   if (!strcasecmp(s, "q8_0")) return GGML_TYPE_Q8_0;
   if (!strcasecmp(s, "q2_k")) return GGML_TYPE_Q2_K;
+  if (!strcasecmp(s, "q4_k")) return GGML_TYPE_Q4_K;   /* SURVEY §8f "next" formats */
+  if (!strcasecmp(s, "q5_k")) return GGML_TYPE_Q5_K;
+  if (!strcasecmp(s, "q6_k")) return GGML_TYPE_Q6_K;
   fprintf(stderr, "unknown type %s\n", s);
   exit(2);
 }

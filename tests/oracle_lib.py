@@ -13,11 +13,29 @@ ORACLE_DIR = os.path.join(ROOT, "oracle")
 ORACLE_SO = os.path.join(ORACLE_DIR, "liblamm_oracle.so")
 
 F32, Q4_0, Q4_1, Q5_0, Q5_1, Q8_0, Q8_1, Q2_K, Q8_K = 0, 2, 3, 6, 7, 8, 9, 10, 15
+Q4_K, Q5_K, Q6_K = 12, 13, 14
 QUANT_REF, QUANT_AVX = 0, 1
 NAMES = {F32: "f32", Q4_0: "q4_0", Q4_1: "q4_1", Q5_0: "q5_0", Q5_1: "q5_1",
-         Q8_0: "q8_0", Q8_1: "q8_1", Q2_K: "q2_k", Q8_K: "q8_k"}
+         Q8_0: "q8_0", Q8_1: "q8_1", Q2_K: "q2_k", Q8_K: "q8_k",
+         Q4_K: "q4_k", Q5_K: "q5_k", Q6_K: "q6_k"}
 BY_NAME = {v: k for k, v in NAMES.items()}
-A_TYPES = [F32, Q4_0, Q4_1, Q5_0, Q5_1, Q8_0, Q2_K]
+A_TYPES = [F32, Q4_0, Q4_1, Q5_0, Q5_1, Q8_0, Q2_K]   # the lamm formats (quantizers restated)
+KQ_TYPES = [Q4_K, Q5_K, Q6_K]                        # vec_dot only, no quantizer
+# byte offsets of the fp16 scale fields of a block (random-byte test inputs keep them finite)
+FP16_FIELDS = {Q4_K: [0, 2], Q5_K: [0, 2], Q6_K: [208]}
+
+
+def random_kq_blocks(t, rows, k, rng):
+    """Random bytes for `rows` x `k` elements of k-quant type t, with finite positive fp16
+    scales (vec_dot is defined for every byte pattern; this is how the GPU tests feed the
+    formats the oracle has no quantizer for)."""
+    bpb = {Q4_K: 144, Q5_K: 176, Q6_K: 210}[t]
+    nb = rows * (k // 256)
+    blk = rng.integers(0, 256, size=(nb, bpb), dtype=np.uint8)
+    for off in FP16_FIELDS[t]:
+        d = (rng.random(nb) * 0.02 + 1e-3).astype(np.float16)
+        blk[:, off:off + 2] = d.view(np.uint8).reshape(nb, 2)
+    return blk.reshape(-1)
 
 
 def _ensure_built():

@@ -123,6 +123,25 @@ def test_random_shapes_vs_oracle(t, shape):
     assert err < TOL, err
 
 
+KQ_SHAPES = [(1, 1, 256), (17, 3, 512), (40, 7, 4096 + 256), (33, 17, 1024), (130, 2, 8192 + 512), (4096, 1, 4096)]
+
+
+@pytest.mark.parametrize("t", ol.KQ_TYPES, ids=[ol.NAMES[t] for t in ol.KQ_TYPES])
+@pytest.mark.parametrize("shape", KQ_SHAPES, ids=[f"{m}x{n}x{k}" for m, n, k in KQ_SHAPES])
+def test_kquants_random_bytes_vs_oracle(t, shape):
+    """SURVEY §8f q4_K / q5_K / q6_K (beyond the reference's lamm set): random block bytes
+    (finite fp16 scales) against q8_K rows from the oracle's quantizer; GEMV (N <= 8), the
+    grouped-GEMV path (N > 8), K spanning several 4096-element segments."""
+    M, N, K = shape
+    rng = np.random.default_rng(M * 31 + N * 7 + K + t)
+    A_q = ol.random_kq_blocks(t, M, K, rng)
+    B_q = ORACLE.quantize(ol.Q8_K, rng.standard_normal((N, K), dtype=np.float32))
+    c, _ = gpu_mul_mat(t, A_q, B_q, M, N, K)
+    ref = ORACLE.mul_mat(t, M, N, K, A_q, B_q)
+    err = rel_err(c, ref, absdot(t, A_q, B_q, M, N, K)).max()
+    assert err < TOL, err
+
+
 FP6_TYPES = [ol.Q4_0, ol.Q4_1, ol.Q5_0]
 GEMM_SHAPES = [(33, 17, 1024), (130, 9, 8192 + 512), (257, 129, 4096 + 64), (300, 40, 96)]
 

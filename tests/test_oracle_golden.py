@@ -21,6 +21,8 @@ def _ids(paths):
 def test_weight_quantizer_bit_exact(path):
     z = load_fixture(path)
     t, M, N, K = int(z["type"]), int(z["M"]), int(z["N"]), int(z["K"])
+    if t in ol.KQ_TYPES:
+        pytest.skip("no quantizer restated for the §8f k-quants (inputs are reference bytes)")
     a, _ = load_inputs(M, N, K)
     q = ORACLE.quantize(t, a, ol.QUANT_REF)
     assert np.array_equal(q, z["A_q"]), "ggml_quantize_chunk restatement differs"

@@ -33,6 +33,9 @@ REF = os.path.join(ROOT, "oracle", "_ref")
 FORMATS = {  # name -> (ggml type id, vec_dot type id)
     "f32": (0, 0), "q4_0": (2, 8), "q4_1": (3, 9), "q5_0": (6, 8),
     "q5_1": (7, 9), "q8_0": (8, 8), "q2_k": (10, 15),
+    # SURVEY §8f "next" formats (not lamm's: the reference routes them to stock ggml, so
+    # C_lamm3 is ggml's own AVX2 vec_dot there)
+    "q4_k": (12, 15), "q5_k": (13, 15), "q6_k": (14, 15),
 }
 # (M, N, K): tile remainders; the reference's own LAMM_DEBUG shape
 # (src/la-benchmark-matmult.cpp:176-178); a decode-shaped GEMV.
@@ -64,7 +67,9 @@ def run_gen(binary, fmt, M, N, K, a, b, tmp):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(ROOT, "tests", "golden"))
+    ap.add_argument("--formats", default=",".join(FORMATS), help="comma-separated subset")
     args = ap.parse_args()
+    wanted = args.formats.split(",")
     os.makedirs(args.out, exist_ok=True)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib  # our restatement, used only for the fp64 dequantized reference
@@ -76,6 +81,8 @@ def main():
                             seed=np.int64(1000 + 17 * si), input_sha256=np.array(sha(a, b)))
     with tempfile.TemporaryDirectory() as tmp:
         for fmt, (t, vt) in FORMATS.items():
+            if fmt not in wanted:
+                continue
             for si, (M, N, K) in enumerate(SHAPES):
                 seed = 1000 + 17 * si
                 a, b = inputs(seed, M, N, K)

@@ -38,7 +38,9 @@ struct ggml_tensor;
 
 /* Replaces src/loongarch_matmul.cpp:10-62.  False outside the COMPUTE phase, for
  * unsupported (src0, vec_dot_type) pairs, non-contiguous quantized src1, non-F32 dst,
- * LAMM_OPT_LEVEL=0 in the environment, or when no gfx950 device is present. */
+ * LAMM_OPT_LEVEL=0 in the environment, or when no gfx950 device is present.
+ * Accepts the reference's 7 pairs plus f16 / q4_K / q5_K / q6_K;
+ * LAMM_HIP_EXTRA_TYPES=0 restricts it to the reference's exact set. */
 bool lamm_can_mul_mat(const struct ggml_compute_params *params,
                       const struct ggml_tensor *dst);
 
@@ -58,7 +60,8 @@ int lamm_get_opt_level(void);
 typedef struct lamm_matrix {   /* == struct Matrix, src/lamm_common.h:87-93 */
   void *data;                  /* device pointer */
   int type;                    /* ggml_type id: 0 f32, 2 q4_0, 3 q4_1, 6 q5_0,
-                                  7 q5_1, 8 q8_0, 9 q8_1, 10 q2_K, 15 q8_K */
+                                  7 q5_1, 8 q8_0, 9 q8_1, 10 q2_K, 15 q8_K;
+                                  SURVEY §8f additions: 1 f16, 12 q4_K, 13 q5_K, 14 q6_K */
   int row;
   int col;
   int64_t ld;                  /* leading dimension, in blocks of `type` */
@@ -74,8 +77,9 @@ enum lamm_status {
 };
 
 /* C[j*C.ld + i] = sum_k A[i,k] * B[k,j] for i < C.row (=A.row), j < C.col (=B.col).
- * A: weights (f32/q4_0/q4_1/q5_0/q5_1/q8_0/q2_K), A.col = K/blck, A.ld >= A.col.
- * B: activations of type vec_dot_type(A.type) (f32/q8_0/q8_1/q8_K), column j at
+ * A: weights (f32/q4_0/q4_1/q5_0/q5_1/q8_0/q2_K, + f16/q4_K/q5_K/q6_K), A.col = K/blck,
+ *    A.ld >= A.col.
+ * B: activations of type vec_dot_type(A.type) (f32/q8_0/q8_1/q8_K/f16), column j at
  *    B.data + j*B.ld blocks, B.row = A.col.
  * C: f32, C.ld >= C.row.   Returns a lamm_status.  Asynchronous on hip_stream.
  * Loads are range-checked per dword: A and B must be readable up to the next
@@ -102,7 +106,8 @@ int lamm_hip_matmul_batched(const lamm_matrix *A, const lamm_matrix *B, const la
 /* Activation quantizer on device (ggml INIT phase, LC/ggml.c:10865-10887, run on
  * the GPU): x[N][K] f32 (row j at x + j*ldx floats) -> y, N rows of `vec_type`
  * blocks (row j at y + j*ldy blocks).  flavour 0 = *_reference rounding
- * (roundf), 1 = the AVX2 from_float rounding (nearest-even, id = 127/amax). */
+ * (roundf), 1 = the AVX2 from_float rounding (nearest-even, id = 127/amax).
+ * vec_type: q8_0, q8_1, q8_K, or f16 (ggml_fp32_to_fp16_row, nearest-even). */
 int lamm_hip_quantize(int vec_type, int flavour, const float *x, int64_t ldx, void *y,
                       int64_t ldy, int K, int N, void *hip_stream);
 

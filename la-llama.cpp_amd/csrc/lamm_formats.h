@@ -12,7 +12,7 @@
 namespace lamm {
 
 enum Type : int {
-  kF32 = 0, kQ4_0 = 2, kQ4_1 = 3, kQ5_0 = 6, kQ5_1 = 7,
+  kF32 = 0, kF16 = 1, kQ4_0 = 2, kQ4_1 = 3, kQ5_0 = 6, kQ5_1 = 7,
   kQ8_0 = 8, kQ8_1 = 9, kQ2_K = 10, kQ4_K = 12, kQ5_K = 13, kQ6_K = 14, kQ8_K = 15,
 };
 
@@ -45,10 +45,10 @@ static_assert(offsetof(block_q5_K, qs) == 48 && offsetof(block_q6_K, d) == 208, 
 
 // Host-side traits, indexed by ggml type id.
 inline bool is_kquant256(int t) { return t == kQ2_K || t == kQ4_K || t == kQ5_K || t == kQ6_K || t == kQ8_K; }
-inline int block_elems(int t) { return t == kF32 ? 1 : is_kquant256(t) ? 256 : 32; }
+inline int block_elems(int t) { return (t == kF32 || t == kF16) ? 1 : is_kquant256(t) ? 256 : 32; }
 inline size_t block_bytes(int t) {
   switch (t) {
-    case kF32: return 4;   case kQ4_0: return 18; case kQ4_1: return 20;
+    case kF32: return 4;   case kF16: return 2;   case kQ4_0: return 18; case kQ4_1: return 20;
     case kQ5_0: return 22; case kQ5_1: return 24; case kQ8_0: return 34;
     case kQ8_1: return 36; case kQ2_K: return 84; case kQ8_K: return 292;
     case kQ4_K: return 144; case kQ5_K: return 176; case kQ6_K: return 210;
@@ -58,6 +58,7 @@ inline size_t block_bytes(int t) {
 inline int vec_dot_type(int t) {
   switch (t) {
     case kF32: return kF32;
+    case kF16: return kF16;   // F16 weights (KV cache) x F16 rows, ggml_vec_dot_f16
     case kQ4_0: case kQ5_0: case kQ8_0: return kQ8_0;
     case kQ4_1: case kQ5_1: return kQ8_1;
     case kQ2_K: case kQ4_K: case kQ5_K: case kQ6_K: return kQ8_K;

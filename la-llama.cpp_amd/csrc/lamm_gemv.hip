@@ -43,6 +43,7 @@ template <> struct Fmt<kQ4_K> { static constexpr int QK = 256, BPB = 144, G = 1,
 template <> struct Fmt<kQ5_K> { static constexpr int QK = 256, BPB = 176, G = 1, VBPB = 292, VQK = 256; };
 template <> struct Fmt<kQ6_K> { static constexpr int QK = 256, BPB = 210, G = 1, VBPB = 292, VQK = 256; };
 template <> struct Fmt<kF32>  { static constexpr int QK = 1, BPB = 4, G = 64, VBPB = 4, VQK = 1; };
+template <> struct Fmt<kF16>  { static constexpr int QK = 1, BPB = 2, G = 128, VBPB = 2, VQK = 1; };
 
 template <int T> struct Geo {
   using F = Fmt<T>;
@@ -56,7 +57,7 @@ template <int T> struct Geo {
   static constexpr int A_NPT = (A_PIECES + kThreads - 1) / kThreads;
   static constexpr int A_LDS = A_NPT * kThreads * 16;
   static constexpr int VBLK = SEG_ELEMS / F::VQK;        // activation blocks per segment
-  static constexpr int BQ_WORDS = T == kF32 ? SEG_ELEMS : SEG_ELEMS / 4;  // int8 quads / f32 words
+  static constexpr int BQ_WORDS = T == kF32 ? SEG_ELEMS : T == kF16 ? SEG_ELEMS / 2 : SEG_ELEMS / 4;  // int8 quads / f32 words / f16 pairs
 };
 
 // XOR swizzle of B word index: the 16 chunk-threads of a row read 16-byte
@@ -70,8 +71,8 @@ struct Smem {
   using GG = Geo<T>;
   uint32_t a[GG::A_LDS / 4];
   uint32_t bq[NC][GG::BQ_WORDS];
-  float bd[NC][T == kF32 ? 1 : GG::VBLK];
-  float bx[NC][T == kF32 ? 1 : GG::VBLK];   // q8_0: sum(q) as float; q8_1: s
+  float bd[NC][(T == kF32 || T == kF16) ? 1 : GG::VBLK];
+  float bx[NC][(T == kF32 || T == kF16) ? 1 : GG::VBLK];   // q8_0: sum(q) as float; q8_1: s
   int bs[NC][Fmt<T>::VQK == 256 ? GG::VBLK * 16 : 1];  // q8_K bsums
 };
 
@@ -93,6 +94,17 @@ __device__ __forceinline__ void stage_b(SM& sm, const GemvArgs& p, const unsigne
       uint32_t v = 0;
       if (j < p.N && e < p.K) v = bload4(rs, (uint32_t)(j * p.ldb + e * 4));
       sm.bq[j][swz(w)] = v;
+    }
+  } else if constexpr (T == kF16) {
+    // f16 rows (ggml INIT converted src1 with ggml_fp32_to_fp16_row): pairs of halves,
+    // read with 2-byte loads (F16 rows need not be dword aligned); past K -> 0
+    for (int it = t; it < NC * GG::BQ_WORDS; it += kThreads) {
+      const int j = it / GG::BQ_WORDS, w = it % GG::BQ_WORDS;
+      const int64_t e = (int64_t)seg * GG::SEG_ELEMS + 2 * w;
+      uint32_t lo = 0, hi = 0;
+      if (j < p.N && e < p.K) lo = bload2(rs, (uint32_t)(j * p.ldb + e * 2));
+      if (j < p.N && e + 1 < p.K) hi = bload2(rs, (uint32_t)(j * p.ldb + e * 2 + 2));
+      sm.bq[j][swz(w)] = lo | (hi << 16);
     }
   } else if constexpr (F::VQK == 256) {
     // q8_K: f32 d | 256 x i8 | 16 x i16 bsums  = 73 dwords, dword aligned
@@ -336,11 +348,43 @@ __device__ __forceinline__ void chunk_dot_f32(const uint32_t (&w)[Geo<kF32>::CH_
   }
 }
 
+// f16 (e.g. the F16 KV cache of the attention matmuls): 128 halves per chunk,
+// exact fp16 x fp16 products with fp32 accumulation (v_dot2_f32_f16); halves past K masked.
+template <int NC, class SM>
+__device__ __forceinline__ void chunk_dot_f16(const uint32_t (&w)[Geo<kF16>::CH_WORDS + 1],
+                                              const SM& sm, int ch, int nvalid, int ncols,
+                                              float (&acc)[NC]) {
+  typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+  uint32_t a[64];
+#pragma unroll
+  for (int i = 0; i < 64; ++i) {
+    const uint32_t m = 2 * i + 1 < nvalid ? 0xffffffffu : (2 * i < nvalid ? 0x0000ffffu : 0u);
+    a[i] = w[i] & m;
+  }
+#pragma unroll
+  for (int j = 0; j < NC; ++j) {
+    if (j >= ncols) break;
+    const uint32_t* bq = sm.bq[j];
+    float s = 0.f;
+#pragma unroll
+    for (int pc = 0; pc < 16; ++pc) {
+      const u32x4 b = *(const u32x4*)&bq[swz(ch * 64 + 4 * pc)];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        s = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2, a[4 * pc + k]), __builtin_bit_cast(h2, (uint32_t)b[k]), s,
+                                   false);
+    }
+    acc[j] += s;
+  }
+}
+
 template <int T, int NC, int GI, class SM>
 __device__ __forceinline__ void chunk_dot(const uint32_t (&w)[Geo<T>::CH_WORDS + 1], const SM& sm,
                                           int ch, int nvalid, int ncols, float (&acc)[NC]) {
   if constexpr (T == kF32) {
     chunk_dot_f32<NC>(w, sm, ch, nvalid, ncols, acc);
+  } else if constexpr (T == kF16) {
+    chunk_dot_f16<NC>(w, sm, ch, nvalid, ncols, acc);
   } else if constexpr (GI < Fmt<T>::G) {
     if (GI < nvalid) block_dot<T, NC, GI>(w, sm, ch, ncols, acc);
     chunk_dot<T, NC, GI + 1>(w, sm, ch, nvalid, ncols, acc);
@@ -468,8 +512,8 @@ struct SmemStream {
   using GG = Geo<T>;
   uint32_t a[WAVES][WGeo<T>::SLOT / 4];
   uint32_t bq[NC][GG::BQ_WORDS];
-  float bd[NC][T == kF32 ? 1 : GG::VBLK];
-  float bx[NC][T == kF32 ? 1 : GG::VBLK];
+  float bd[NC][(T == kF32 || T == kF16) ? 1 : GG::VBLK];
+  float bx[NC][(T == kF32 || T == kF16) ? 1 : GG::VBLK];
   int bs[NC][Fmt<T>::VQK == 256 ? GG::VBLK * 16 : 1];
 };
 
@@ -660,7 +704,7 @@ size_t gemv_lds_bytes(int type, int nc) {
          : nc <= 4 ? sizeof(Smem<T, 4>) : sizeof(Smem<T, 8>);
   switch (type) {
     LDS_CASE(kQ4_0) LDS_CASE(kQ4_1) LDS_CASE(kQ5_0) LDS_CASE(kQ5_1)
-    LDS_CASE(kQ8_0) LDS_CASE(kQ2_K) LDS_CASE(kQ4_K) LDS_CASE(kQ5_K) LDS_CASE(kQ6_K) LDS_CASE(kF32)
+    LDS_CASE(kQ8_0) LDS_CASE(kQ2_K) LDS_CASE(kQ4_K) LDS_CASE(kQ5_K) LDS_CASE(kQ6_K) LDS_CASE(kF32) LDS_CASE(kF16)
     default: return 0;
   }
 #undef LDS_CASE
@@ -678,6 +722,7 @@ hipError_t launch_gemv(int type, const GemvArgs& p, hipStream_t s) {
     case kQ5_K: return launch_nc<kQ5_K>(p, s);
     case kQ6_K: return launch_nc<kQ6_K>(p, s);
     case kF32:  return launch_nc<kF32>(p, s);
+    case kF16:  return launch_nc<kF16>(p, s);
     default: return hipErrorInvalidValue;
   }
 }

@@ -190,7 +190,7 @@ extern "C" int lamm_hip_matmul(const lamm_matrix* A, const lamm_matrix* B, const
 
 extern "C" int lamm_hip_quantize(int vec_type, int flavour, const float* x, int64_t ldx, void* y,
                                  int64_t ldy, int K, int N, void* hip_stream) {
-  if (vec_type != kQ8_0 && vec_type != kQ8_1 && vec_type != kQ8_K)
+  if (vec_type != kQ8_0 && vec_type != kQ8_1 && vec_type != kQ8_K && vec_type != kF16)
     return fail(LAMM_ERR_TYPE, "quantize: unsupported type %d", vec_type);
   if (K % block_elems(vec_type)) return fail(LAMM_ERR_SHAPE, "quantize: K %% block != 0");
   if (((uintptr_t)x & 15) || (ldx & 3)) return fail(LAMM_ERR_ALIGN, "quantize: x must be 16B aligned, ldx %% 4 == 0");
@@ -357,8 +357,8 @@ bool is_contiguous(const ggml::tensor* t) {
          t->nb[3] == t->nb[2] * (size_t)t->ne[2];
 }
 
-bool kquants_enabled() {
-  const char* e = getenv("LAMM_HIP_KQUANTS");
+bool extra_types_enabled() {
+  const char* e = getenv("LAMM_HIP_EXTRA_TYPES");
   return !(e && e[0] == '0');
 }
 
@@ -376,9 +376,12 @@ extern "C" bool lamm_can_mul_mat(const struct ggml_compute_params* vparams, cons
   if (!src0 || !src1) return false;
   const int vdt = vec_dot_type(src0->type);
   if (vdt < 0) return false;                                 // :37-52 supported pairs
-  // q4_K / q5_K / q6_K are beyond the reference's lamm set (e.g. a Q4_0
-  // model's Q6_K output.weight); LAMM_HIP_KQUANTS=0 restores the reference's exact set
-  if ((src0->type == kQ4_K || src0->type == kQ5_K || src0->type == kQ6_K) && !kquants_enabled()) return false;
+  // q4_K / q5_K / q6_K / f16 are beyond the reference's lamm set (a Q4_0
+  // model's Q6_K output.weight, the F16 KV-cache attention matmuls);
+  // LAMM_HIP_EXTRA_TYPES=0 restores the reference's exact set
+  if ((src0->type == kQ4_K || src0->type == kQ5_K || src0->type == kQ6_K || src0->type == kF16) &&
+      !extra_types_enabled())
+    return false;
   if (src1->type == vdt && !is_contiguous(src1)) return false;  // :23-28
   if (src1->nb[0] != block_bytes(src1->type)) return false;  // :29-31
   if (dst->type != kF32) return false;                       // :34-36

@@ -125,6 +125,17 @@ __global__ __launch_bounds__(256) void quant_q8_K(const float* __restrict__ x, i
   if (lane == 0) *reinterpret_cast<float*>(blkp) = d;
 }
 
+// F16 activations: ggml_fp32_to_fp16_row (LC/ggml.c), round-to-nearest-even per
+// element -- v_cvt_f16_f32 in the default round mode, subnormals kept
+__global__ __launch_bounds__(256) void cvt_f16(const float* __restrict__ x, int64_t ldx, unsigned char* __restrict__ y,
+                                               int64_t ldy_bytes, int K, int N) {
+  const int64_t it = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (it >= (int64_t)K * N) return;
+  const int64_t j = it / K, e = it % K;
+  const _Float16 h = (_Float16)x[j * ldx + e];
+  *reinterpret_cast<_Float16*>(y + j * ldy_bytes + 2 * e) = h;
+}
+
 }  // namespace
 
 hipError_t launch_quantize(int vec_type, int flavour, const float* x, int64_t ldx, void* y,
@@ -145,6 +156,12 @@ hipError_t launch_quantize(int vec_type, int flavour, const float* x, int64_t ld
     const int grid = (int)((threads + 255) / 256);
     if (grid == 0) return hipSuccess;
     hipLaunchKernelGGL(quant_q8_K, dim3(grid), dim3(256), 0, s, x, ldx, yb, ldy_bytes, K, N);
+    return hipGetLastError();
+  }
+  if (vec_type == kF16) {
+    const int64_t n = (int64_t)K * N;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(cvt_f16, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, ldx, yb, ldy_bytes, K, N);
     return hipGetLastError();
   }
   return hipErrorInvalidValue;

@@ -21,11 +21,12 @@ LIB_PATH = os.path.join(os.path.dirname(_HERE), "liblamm_hip.so")
 
 F32, Q4_0, Q4_1, Q5_0, Q5_1, Q8_0, Q8_1, Q2_K, Q8_K = 0, 2, 3, 6, 7, 8, 9, 10, 15
 Q4_K, Q5_K, Q6_K = 12, 13, 14   # SURVEY §8f "next" formats (beyond the reference's lamm set)
+F16 = 1                         # F16 x F16 (attention / KV cache)
 NAMES = {F32: "f32", Q4_0: "q4_0", Q4_1: "q4_1", Q5_0: "q5_0", Q5_1: "q5_1",
          Q8_0: "q8_0", Q8_1: "q8_1", Q2_K: "q2_k", Q8_K: "q8_k",
-         Q4_K: "q4_k", Q5_K: "q5_k", Q6_K: "q6_k"}
+         Q4_K: "q4_k", Q5_K: "q5_k", Q6_K: "q6_k", F16: "f16"}
 BY_NAME = {v: k for k, v in NAMES.items()}
-WEIGHT_TYPES = [F32, Q4_0, Q4_1, Q5_0, Q5_1, Q8_0, Q2_K, Q4_K, Q5_K, Q6_K]
+WEIGHT_TYPES = [F32, Q4_0, Q4_1, Q5_0, Q5_1, Q8_0, Q2_K, Q4_K, Q5_K, Q6_K, F16]
 
 LAMM_OK, LAMM_ERR_TYPE, LAMM_ERR_SHAPE, LAMM_ERR_ALIGN, LAMM_ERR_HIP, LAMM_ERR_NODEV = range(6)
 

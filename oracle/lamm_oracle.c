@@ -17,7 +17,8 @@
  *                              (the SURVEY §8f "next" formats; no quantizer restated:
  *                              their test inputs are the reference's own bytes or
  *                              random bytes, for which vec_dot is equally defined)
- *                              f32 LC/ggml.c:1576-1581 (double accumulation)
+ *                              f32 LC/ggml.c:1576-1581 (double accumulation),
+ *                              f16 LC/ggml.c:1589-1629 (scalar branch: double accumulation)
  *   * mul_mat semantics        src/lamm_kernel_q4_0.hpp:21-37 (C[j*ldc+i], K blocks),
  *                              computing ALL M rows (not inheriting SURVEY §8a defect 1)
  *
@@ -68,7 +69,7 @@ uint16_t lo_fp32_to_fp16(float f) {   /* IEEE round-to-nearest-even */
 
 int lo_block_elems(int t) {
   switch (t) {
-  case LO_F32: return 1;
+  case LO_F32: case LO_F16: return 1;
   case LO_Q2_K: case LO_Q4_K: case LO_Q5_K: case LO_Q6_K: case LO_Q8_K: return 256;
   default: return 32;
   }
@@ -77,6 +78,7 @@ int lo_block_elems(int t) {
 size_t lo_block_bytes(int t) {
   switch (t) {
   case LO_F32: return 4;
+  case LO_F16: return 2;
   case LO_Q4_0: return 18;
   case LO_Q4_1: return 20;
   case LO_Q5_0: return 22;
@@ -95,6 +97,7 @@ size_t lo_block_bytes(int t) {
 int lo_vec_dot_type(int t) {
   switch (t) {
   case LO_F32: return LO_F32;
+  case LO_F16: return LO_F16;
   case LO_Q4_0: case LO_Q5_0: case LO_Q8_0: return LO_Q8_0;
   case LO_Q4_1: case LO_Q5_1: return LO_Q8_1;
   case LO_Q2_K: case LO_Q4_K: case LO_Q5_K: case LO_Q6_K: return LO_Q8_K;
@@ -354,6 +357,10 @@ void lo_quantize_row(int type, int flavour, const float *x, void *y, int k) {
   const size_t bb = lo_block_bytes(type);
   uint8_t *out = (uint8_t *)y;
   if (type == LO_F32) { memcpy(y, x, (size_t)k * 4); return; }
+  if (type == LO_F16) {   /* ggml_fp32_to_fp16_row (LC/ggml.c): per element, round-to-nearest-even */
+    for (int i = 0; i < k; i++) wr16(out + 2 * (size_t)i, lo_fp32_to_fp16(x[i]));
+    return;
+  }
   for (int b = 0; b < k / qk; b++) {
     const float *xb = x + (size_t)b * qk;
     uint8_t *yb = out + (size_t)b * bb;
@@ -412,6 +419,10 @@ void lo_dequantize_row(int type, const void *vx, float *y, int k) {
   const int qk = lo_block_elems(type);
   const size_t bb = lo_block_bytes(type);
   if (type == LO_F32) { memcpy(y, vx, (size_t)k * 4); return; }
+  if (type == LO_F16) {
+    for (int i = 0; i < k; i++) y[i] = H2F(rd16(x + 2 * (size_t)i));
+    return;
+  }
   for (int b = 0; b < k / qk; b++, x += bb, y += qk) {
     switch (type) {
     case LO_Q4_0: case LO_Q5_0: case LO_Q4_1: case LO_Q5_1: {
@@ -511,6 +522,11 @@ static int blk_idot(int type, const uint8_t *a, const int8_t *bq) {
 float lo_vec_dot(int type, int k, const void *va, const void *vb) {
   const uint8_t *a = (const uint8_t *)va, *b = (const uint8_t *)vb;
   if (type == LO_F32) return dot_f32(k, (const float *)va, (const float *)vb);
+  if (type == LO_F16) {   /* ggml_vec_dot_f16 scalar branch: ggml_float (double) sum of f32 products */
+    double s = 0.0;
+    for (int i = 0; i < k; ++i) s += (double)(H2F(rd16(a + 2 * (size_t)i)) * H2F(rd16(b + 2 * (size_t)i)));
+    return (float)s;
+  }
   const size_t ab = lo_block_bytes(type), bb = lo_block_bytes(lo_vec_dot_type(type));
   float sumf = 0.0f;
   if (type == LO_Q2_K) {

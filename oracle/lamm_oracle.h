@@ -19,7 +19,7 @@ extern "C" {
 
 /* Type ids are ggml's enum values (LC/ggml.h:341-368). */
 enum {
-  LO_F32 = 0, LO_Q4_0 = 2, LO_Q4_1 = 3, LO_Q5_0 = 6, LO_Q5_1 = 7,
+  LO_F32 = 0, LO_F16 = 1, LO_Q4_0 = 2, LO_Q4_1 = 3, LO_Q5_0 = 6, LO_Q5_1 = 7,
   LO_Q8_0 = 8, LO_Q8_1 = 9, LO_Q2_K = 10, LO_Q4_K = 12, LO_Q5_K = 13, LO_Q6_K = 14, LO_Q8_K = 15
 };
 

@@ -34,6 +34,7 @@
 
 static enum ggml_type parse_type(const char *s) {
   if (!strcasecmp(s, "f32")) return GGML_TYPE_F32;
+  if (!strcasecmp(s, "f16")) return GGML_TYPE_F16;   /* SURVEY §8f */
   if (!strcasecmp(s, "q4_0")) return GGML_TYPE_Q4_0;
   if (!strcasecmp(s, "q4_1")) return GGML_TYPE_Q4_1;
   if (!strcasecmp(s, "q5_0")) return GGML_TYPE_Q5_0;

@@ -14,12 +14,13 @@ ORACLE_SO = os.path.join(ORACLE_DIR, "liblamm_oracle.so")
 
 F32, Q4_0, Q4_1, Q5_0, Q5_1, Q8_0, Q8_1, Q2_K, Q8_K = 0, 2, 3, 6, 7, 8, 9, 10, 15
 Q4_K, Q5_K, Q6_K = 12, 13, 14
+F16 = 1
 QUANT_REF, QUANT_AVX = 0, 1
 NAMES = {F32: "f32", Q4_0: "q4_0", Q4_1: "q4_1", Q5_0: "q5_0", Q5_1: "q5_1",
          Q8_0: "q8_0", Q8_1: "q8_1", Q2_K: "q2_k", Q8_K: "q8_k",
-         Q4_K: "q4_k", Q5_K: "q5_k", Q6_K: "q6_k"}
+         Q4_K: "q4_k", Q5_K: "q5_k", Q6_K: "q6_k", F16: "f16"}
 BY_NAME = {v: k for k, v in NAMES.items()}
-A_TYPES = [F32, Q4_0, Q4_1, Q5_0, Q5_1, Q8_0, Q2_K]   # the lamm formats (quantizers restated)
+A_TYPES = [F32, Q4_0, Q4_1, Q5_0, Q5_1, Q8_0, Q2_K, F16]   # quantizers restated (F16: §8f)
 KQ_TYPES = [Q4_K, Q5_K, Q6_K]                        # vec_dot only, no quantizer
 # byte offsets of the fp16 scale fields of a block (random-byte test inputs keep them finite)
 FP16_FIELDS = {Q4_K: [0, 2], Q5_K: [0, 2], Q6_K: [208]}

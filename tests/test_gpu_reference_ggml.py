@@ -17,7 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EXE = os.path.join(ROOT, "oracle", "_ref", "ref_driver_hip")
 FIXTURES = fixture_paths()
 NAMES = {0: "f32", 2: "q4_0", 3: "q4_1", 6: "q5_0", 7: "q5_1", 8: "q8_0", 10: "q2_k",
-         12: "q4_k", 13: "q5_k", 14: "q6_k"}
+         12: "q4_k", 13: "q5_k", 14: "q6_k", 1: "f16"}
 
 
 @pytest.fixture(scope="module")

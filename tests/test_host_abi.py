@@ -54,12 +54,14 @@ def test_struct_layouts_against_reference_header(tmp_path):
 
 def test_traits_match_oracle():
     o = ol.Oracle()
-    for t in [ol.F32, ol.Q4_0, ol.Q4_1, ol.Q5_0, ol.Q5_1, ol.Q8_0, ol.Q8_1, ol.Q2_K, ol.Q8_K]:
+    for t in [ol.F32, ol.Q4_0, ol.Q4_1, ol.Q5_0, ol.Q5_1, ol.Q8_0, ol.Q8_1, ol.Q2_K, ol.Q8_K] + ol.KQ_TYPES + [ol.F16]:
         assert la.blck_size(t) == o.block_elems(t)
         assert la.type_size(t) == o.block_bytes(t)
-    for t in ol.A_TYPES:
+    for t in ol.A_TYPES + ol.KQ_TYPES:
         assert la.vec_dot_type(t) == o.vec_dot_type(t)
-    assert la.vec_dot_type(1) == -1  # F16 is not on the lamm path (src/loongarch_matmul.cpp:37-52)
+    # F16 and the k-quants are SURVEY §8f additions beyond the reference's lamm pairs
+    # (src/loongarch_matmul.cpp:37-52); Q3_K (11) stays unsupported
+    assert la.vec_dot_type(1) == 1 and la.vec_dot_type(11) == -1
 
 
 def _mats(wtype=la.Q4_0, M=16, N=1, kb=128, lda=None):

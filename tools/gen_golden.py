@@ -35,7 +35,7 @@ FORMATS = {  # name -> (ggml type id, vec_dot type id)
     "q5_1": (7, 9), "q8_0": (8, 8), "q2_k": (10, 15),
     # SURVEY §8f "next" formats (not lamm's: the reference routes them to stock ggml, so
     # C_lamm3 is ggml's own AVX2 vec_dot there)
-    "q4_k": (12, 15), "q5_k": (13, 15), "q6_k": (14, 15),
+    "q4_k": (12, 15), "q5_k": (13, 15), "q6_k": (14, 15), "f16": (1, 1),
 }
 # (M, N, K): tile remainders; the reference's own LAMM_DEBUG shape
 # (src/la-benchmark-matmult.cpp:176-178); a decode-shaped GEMV.

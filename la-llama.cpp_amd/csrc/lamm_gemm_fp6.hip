@@ -47,6 +47,9 @@ constexpr int F6_TJ = 128;      // activation rows per tile
 constexpr int F6_PIECE = 1024;  // bytes one wave moves per LDS-DMA instruction (64 lanes x 16 B)
 constexpr int F6_NBUF = 4;      // LDS stages (3 K-steps of DMA in flight)
 constexpr int SCALE_W = 130, SCALE_HI = 134, SCALE_LO = 130;   // E8M0: 2^(s-127)
+#ifndef F6_PD
+#define F6_PD 1   // MFMA pipeline depth: unit n+PD's MFMAs are issued before unit n's FMAs (2: no gain, +20 VGPRs)
+#endif
 
 template <int T> struct F6;
 template <> struct F6<kQ4_0> { static constexpr int ABPB = 18, VBPB = 34; static constexpr bool AFF = false; };
@@ -285,7 +288,8 @@ __device__ __forceinline__ half4 f6_dq(const F6Frag& f) {   // {d, 0, 0, 0}
 }
 
 // V: ablations for tools/ab_gemm.py (0 production, 1 no compute, 2 no DMA, 3 no epilogue FMAs,
-//    4 no DMA + no LDS fragment reads (operands from registers), 5 no DMA + no barrier)
+//    4 no DMA + no LDS fragment reads (operands from registers), 5 no DMA + no barrier,
+//    6 no P-MFMA, 7 no S-MFMA)
 // WJ: 32-row activation sub-tiles per wave (2: 8 waves of 64x64; 1: 16 waves of 32x64)
 template <int WJ> struct F6Waves {
   static constexpr int NWJ = F6_TJ / (32 * WJ), NWI = F6_TI / 64, NW = NWJ * NWI, NT = 64 * NW;
@@ -358,7 +362,7 @@ __global__ __launch_bounds__(F6Waves<WJ>::NT) void gemm_fp6_kernel(GemvArgs p, c
   if (!NODMA)
     for (int k = 0; k < F6_NBUF - 1 && k < nsteps; ++k) issue(k);
   F6Frag fb[2][WJ], fa[2][2];   // [block slot][sub-tile]
-  F6Res rr[2];
+  F6Res rr[F6_PD + 1];   // results of the units in flight
   for (int ks = 0; ks < nsteps; ++ks) {
     if (!NODMA) {   // this wave's pieces of stage ks landed (younger stages may stay in flight)
       const int ahead = min(F6_NBUF - 2, nsteps - 1 - ks);
@@ -399,8 +403,12 @@ __global__ __launch_bounds__(F6Waves<WJ>::NT) void gemm_fp6_kernel(GemvArgs p, c
     auto mfmas = [&](int n, F6Res& R) {
       const F6Frag& fB = fb[(n / UPB) & 1][(n / 2) % WJ];
       const F6Frag& fA = fa[(n / UPB) & 1][n & 1];
-      R.s = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fB.v, fA.v, fz, 2, 2, 0, sc_a, 0, SCALE_W);
-      R.pr = __builtin_amdgcn_mfma_f32_32x32x8f16(f6_dq<AFF>(fB), f6_dq<AFF>(fA), fz, 0, 0, 0);
+      if constexpr (V != 7)
+        R.s = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fB.v, fA.v, fz, 2, 2, 0, sc_a, 0, SCALE_W);
+      if constexpr (V != 6)
+        R.pr = __builtin_amdgcn_mfma_f32_32x32x8f16(f6_dq<AFF>(fB), f6_dq<AFF>(fA), fz, 0, 0, 0);
+      if constexpr (V == 6) R.pr = R.s;   // ablation: no P-MFMA
+      if constexpr (V == 7) R.s = R.pr;   // ablation: no S-MFMA
     };
     auto epi = [&](int n, const F6Res& R) {
       f32x16& c = acc[(n / 2) % WJ][n & 1];
@@ -425,14 +433,14 @@ __global__ __launch_bounds__(F6Waves<WJ>::NT) void gemm_fp6_kernel(GemvArgs p, c
     constexpr int NU = UPB * F6_KB;   // units per K-step
     constexpr int LDA = UPB;          // fragment prefetch distance in units (one block)
     unroll<LDA>([&](auto NN) { ld_unit(NN); });
-    mfmas(0, rr[0]);
+    unroll<F6_PD>([&](auto NN) { mfmas(NN, rr[NN]); });
     unroll<NU>([&](auto NN) {
       constexpr int n = NN;
       if constexpr (n % UPB == UPB - 1) keep_ms(n / UPB);
       if constexpr (n + LDA < NU) ld_unit(n + LDA);
-      if constexpr (n + 1 < NU) mfmas(n + 1, rr[(n + 1) & 1]);
+      if constexpr (n + F6_PD < NU) mfmas(n + F6_PD, rr[(n + F6_PD) % (F6_PD + 1)]);
       __builtin_amdgcn_sched_barrier(0);
-      epi(n, rr[n & 1]);
+      epi(n, rr[n % (F6_PD + 1)]);
       __builtin_amdgcn_sched_barrier(0);
     });
     if constexpr (AFF) {   // sum_b m_a * s_b: rank-KB per K-step, both k halves carry it (x2 like P)
@@ -497,6 +505,8 @@ hipError_t launch_fp6_t(const GemvArgs& p, void* ws, hipStream_t s) {
     case 2: go(gemm_fp6_kernel<T, 2, 2>, NT2); break;
     case 3: go(gemm_fp6_kernel<T, 3, 2>, NT2); break;
     case 5: go(gemm_fp6_kernel<T, 5, 2>, NT2); break;
+    case 6: go(gemm_fp6_kernel<T, 6, 2>, NT2); break;
+    case 7: go(gemm_fp6_kernel<T, 7, 2>, NT2); break;
     default: go(gemm_fp6_kernel<T, 0, 2>, NT2);
   }
   return hipGetLastError();

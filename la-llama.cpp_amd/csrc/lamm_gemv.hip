@@ -721,8 +721,10 @@ hipError_t launch_gemv(int type, const GemvArgs& p, hipStream_t s) {
     case kQ4_K: return launch_nc<kQ4_K>(p, s);
     case kQ5_K: return launch_nc<kQ5_K>(p, s);
     case kQ6_K: return launch_nc<kQ6_K>(p, s);
-    case kF32:  return launch_nc<kF32>(p, s);
-    case kF16:  return launch_nc<kF16>(p, s);
+    // unquantized rows stream through lamm_gemv_dense.hip (LAMM_GEMV_VARIANT=7: this file's
+    // segmented kernel, kept for A/B)
+    case kF32:  return variant() == 7 ? launch_nc<kF32>(p, s) : launch_gemv_dense(kF32, p, s);
+    case kF16:  return variant() == 7 ? launch_nc<kF16>(p, s) : launch_gemv_dense(kF16, p, s);
     default: return hipErrorInvalidValue;
   }
 }

@@ -22,6 +22,7 @@ struct GemvArgs {
 
 hipError_t launch_gemv(int type, const GemvArgs& p, hipStream_t s);
 size_t gemv_lds_bytes(int type, int nc);
+hipError_t launch_gemv_dense(int type, const GemvArgs& p, hipStream_t s);   // F32 / F16 rows
 
 hipError_t launch_gemm(int type, const GemvArgs& p, void* workspace, hipStream_t s);
 size_t gemm_workspace_bytes(int type, const GemvArgs& p);   // device scratch launch_gemm needs

@@ -237,3 +237,33 @@ def test_extreme_quants():
     c, _ = gpu_mul_mat(t, A_q, B_q, M, N, K)
     ref = ORACLE.mul_mat(t, M, N, K, A_q, B_q)
     assert np.allclose(c, ref, rtol=0, atol=1e-3 * np.abs(ref).max() + 1e-6)
+
+
+DENSE_SHAPES = [(1, 1, 1), (37, 1, 3), (300, 2, 257), (33, 5, 1001), (70, 8, 4099), (19, 3, 9000), (5, 11, 2050)]
+
+
+@pytest.mark.parametrize("t", [ol.F32, ol.F16], ids=["f32", "f16"])
+@pytest.mark.parametrize("shape", DENSE_SHAPES, ids=[f"{m}x{n}x{k}" for m, n, k in DENSE_SHAPES])
+def test_dense_rows_ragged_k(t, shape):
+    """F32 / F16 rows of any length K (ggml allows it; lamm_gemv_dense.hip): the row pitch
+    is padded to 16 bytes with NaN bit patterns, which the ragged-tail masking must keep out
+    of the sums; K spans several activation segments for N up to 8 and beyond (grouped)."""
+    M, N, K = shape
+    rng = np.random.default_rng(M * 7 + N * 3 + K)
+    vt = la.vec_dot_type(t)
+    A_q = ORACLE.quantize(t, rng.standard_normal((M, K), dtype=np.float32))
+    B_q = ORACLE.quantize(vt, rng.standard_normal((N, K), dtype=np.float32))
+    eb = la.type_size(t)
+    lda = pitch_blocks(t, K) + 16 // eb          # at least one padded 16-byte piece
+    nan = np.array([0x7fc00000 if eb == 4 else 0x7e00], dtype=np.uint32 if eb == 4 else np.uint16)
+    Ap = np.tile(nan, M * lda).view(np.uint8).reshape(M, lda * eb).copy()
+    Ap[:, :K * eb] = A_q.reshape(M, K * eb)
+    A = dev_bytes(np.concatenate([Ap.reshape(-1), np.zeros(64, np.uint8)]))
+    B = dev_bytes(B_q)
+    C = torch.full((N * M + 16,), float("nan"), dtype=torch.float32, device="cuda")
+    la.mul_mat_torch(t, A, B, C, M, N, K, lda=lda)
+    torch.cuda.synchronize()
+    c = C.cpu().numpy()[:N * M].reshape(N, M)
+    ref = ORACLE.mul_mat(t, M, N, K, A_q, B_q)
+    assert np.isfinite(c).all()
+    assert rel_err(c, ref, absdot(t, A_q, B_q, M, N, K)).max() < TOL

@@ -363,6 +363,25 @@ __global__ __launch_bounds__(F6Waves<WJ>::NT) void gemm_fp6_kernel(GemvArgs p, c
     for (int k = 0; k < F6_NBUF - 1 && k < nsteps; ++k) issue(k);
   F6Frag fb[2][WJ], fa[2][2];   // [block slot][sub-tile]
   F6Res rr[F6_PD + 1];   // results of the units in flight
+  constexpr int NU = UPB * F6_KB;   // units per K-step
+  auto epi = [&](int n, const F6Res& R) {
+    f32x16& c = acc[(n / 2) % WJ][n & 1];
+    if constexpr (V == 3) {
+      c[0] += R.s[0] + R.pr[0];
+    } else {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) c[e] = __builtin_fmaf(R.s[e], R.pr[e], c[e]);
+    }
+  };
+  // Every wave defers its last unit's FMAs of a K-step across the barrier: they run while the
+  // next step's first fragments load (-2.7 % main-kernel time, profiles/r01/ab_sched.txt).
+  // A/B variants: 8 = + waves 4-7 at s_setprio 1 (no gain); 10 = only waves 4-7 defer (a
+  // stagger: two code paths, 256 VGPRs, +65 %); 12 = no deferral (the previous schedule)
+  const bool defer = V != 12 && (V != 10 || w >= 4);
+  if constexpr (V == 8) {
+    if (w >= 4) __builtin_amdgcn_s_setprio(1);
+  }
+  bool pend = false;
   for (int ks = 0; ks < nsteps; ++ks) {
     if (!NODMA) {   // this wave's pieces of stage ks landed (younger stages may stay in flight)
       const int ahead = min(F6_NBUF - 2, nsteps - 1 - ks);
@@ -410,15 +429,6 @@ __global__ __launch_bounds__(F6Waves<WJ>::NT) void gemm_fp6_kernel(GemvArgs p, c
       if constexpr (V == 6) R.pr = R.s;   // ablation: no P-MFMA
       if constexpr (V == 7) R.s = R.pr;   // ablation: no S-MFMA
     };
-    auto epi = [&](int n, const F6Res& R) {
-      f32x16& c = acc[(n / 2) % WJ][n & 1];
-      if constexpr (V == 3) {
-        c[0] += R.s[0] + R.pr[0];
-      } else {
-#pragma unroll
-        for (int e = 0; e < 16; ++e) c[e] = __builtin_fmaf(R.s[e], R.pr[e], c[e]);
-      }
-    };
     uint32_t msA[2][2] = {{0, 0}, {0, 0}}, msB[WJ][2] = {};   // q4_1: m_a / s_b per block
     auto keep_ms = [&](int b) {
       if constexpr (AFF) {
@@ -430,9 +440,14 @@ __global__ __launch_bounds__(F6Waves<WJ>::NT) void gemm_fp6_kernel(GemvArgs p, c
     };
 
     static_assert(F6_KB == 2 || F6_KB == 4, "the m*s rank-KB MFMA packs <= 4 blocks per k half");
-    constexpr int NU = UPB * F6_KB;   // units per K-step
     constexpr int LDA = UPB;          // fragment prefetch distance in units (one block)
+    static_assert((NU - 1) % (F6_PD + 1) >= F6_PD, "deferred unit's result slot is reused too early");
     unroll<LDA>([&](auto NN) { ld_unit(NN); });
+    if (pend) {   // previous step's last unit, under this step's first LDS reads
+      __builtin_amdgcn_sched_barrier(0);
+      epi(NU - 1, rr[(NU - 1) % (F6_PD + 1)]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
     unroll<F6_PD>([&](auto NN) { mfmas(NN, rr[NN]); });
     unroll<NU>([&](auto NN) {
       constexpr int n = NN;
@@ -440,9 +455,10 @@ __global__ __launch_bounds__(F6Waves<WJ>::NT) void gemm_fp6_kernel(GemvArgs p, c
       if constexpr (n + LDA < NU) ld_unit(n + LDA);
       if constexpr (n + F6_PD < NU) mfmas(n + F6_PD, rr[(n + F6_PD) % (F6_PD + 1)]);
       __builtin_amdgcn_sched_barrier(0);
-      epi(n, rr[n % (F6_PD + 1)]);
+      if (n != NU - 1 || !defer) epi(n, rr[n % (F6_PD + 1)]);
       __builtin_amdgcn_sched_barrier(0);
     });
+    pend = defer;
     if constexpr (AFF) {   // sum_b m_a * s_b: rank-KB per K-step, both k halves carry it (x2 like P)
 #pragma unroll
       for (int x = 0; x < WJ; ++x) {
@@ -456,6 +472,7 @@ __global__ __launch_bounds__(F6Waves<WJ>::NT) void gemm_fp6_kernel(GemvArgs p, c
     }
   }
 
+  if (pend) epi(NU - 1, rr[(NU - 1) % (F6_PD + 1)]);
   float* Cz = p.C + (int64_t)i12 * p.sc2 + (int64_t)i13 * p.sc3;
 #pragma unroll
   for (int x = 0; x < WJ; ++x)
@@ -507,6 +524,9 @@ hipError_t launch_fp6_t(const GemvArgs& p, void* ws, hipStream_t s) {
     case 5: go(gemm_fp6_kernel<T, 5, 2>, NT2); break;
     case 6: go(gemm_fp6_kernel<T, 6, 2>, NT2); break;
     case 7: go(gemm_fp6_kernel<T, 7, 2>, NT2); break;
+    case 8: go(gemm_fp6_kernel<T, 8, 2>, NT2); break;
+    case 10: go(gemm_fp6_kernel<T, 10, 2>, NT2); break;
+    case 12: go(gemm_fp6_kernel<T, 12, 2>, NT2); break;
     default: go(gemm_fp6_kernel<T, 0, 2>, NT2);
   }
   return hipGetLastError();

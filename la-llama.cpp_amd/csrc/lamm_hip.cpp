@@ -95,6 +95,12 @@ void* workspace(size_t bytes, hipStream_t s) {
 // (lamm_gemm_fp6.hip), 1 = MFMA-i8 (lamm_gemm.hip).  The fp6 kernel's 256x128 tiles only pay
 // off once they fill the chip (>= one tile per CU); smaller calls take the i8 kernel's
 // 128x64 tiles.  LAMM_GEMM_PATH=fp6 / i8 forces one (A/B measurements).
+// env var set to "0" (A/B switches that turn a default path off)
+bool getenv_flag0(const char* name) {
+  const char* e = getenv(name);
+  return e && !strcmp(e, "0");
+}
+
 int gemm_path(const GemvArgs& p) {
   const char* e = getenv("LAMM_GEMM_PATH");
   if (e && (!strcmp(e, "i8") || !strcmp(e, "1"))) return 1;
@@ -159,6 +165,8 @@ extern "C" int lamm_hip_matmul_batched(const lamm_matrix* A, const lamm_matrix* 
   hipError_t e;
   if (N <= 8) {
     e = launch_gemv(A->type, p, s);
+  } else if (gemm_dense_supported(A->type) && !getenv_flag0("LAMM_DENSE_GEMM")) {
+    e = launch_gemm_dense(A->type, p, s);
   } else if (gemm_fp6_supported(A->type) && gemm_path(p) == 0) {
     const size_t wsb = gemm_fp6_workspace_bytes(A->type, p);
     void* ws = workspace(wsb, s);

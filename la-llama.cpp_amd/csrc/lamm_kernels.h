@@ -23,6 +23,9 @@ struct GemvArgs {
 hipError_t launch_gemv(int type, const GemvArgs& p, hipStream_t s);
 size_t gemv_lds_bytes(int type, int nc);
 hipError_t launch_gemv_dense(int type, const GemvArgs& p, hipStream_t s);   // F32 / F16 rows
+// F32 / F16 prefill GEMM on the matrix cores (lamm_gemm_dense.hip)
+hipError_t launch_gemm_dense(int type, const GemvArgs& p, hipStream_t s);
+bool gemm_dense_supported(int type);
 
 hipError_t launch_gemm(int type, const GemvArgs& p, void* workspace, hipStream_t s);
 size_t gemm_workspace_bytes(int type, const GemvArgs& p);   // device scratch launch_gemm needs

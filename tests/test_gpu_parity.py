@@ -267,3 +267,68 @@ def test_dense_rows_ragged_k(t, shape):
     ref = ORACLE.mul_mat(t, M, N, K, A_q, B_q)
     assert np.isfinite(c).all()
     assert rel_err(c, ref, absdot(t, A_q, B_q, M, N, K)).max() < TOL
+
+
+DGEMM_SHAPES = [(130, 129, 1000), (257, 300, 4096 + 8), (64, 33, 77), (128, 128, 128), (9, 700, 3)]
+
+
+def _dense_case(t, M, N, K, seed, ldb_extra=0):
+    rng = np.random.default_rng(seed)
+    vt = la.vec_dot_type(t)
+    A_q = ORACLE.quantize(t, rng.standard_normal((M, K), dtype=np.float32))
+    B_q = ORACLE.quantize(vt, rng.standard_normal((N, K), dtype=np.float32))
+    eb = la.type_size(t)
+    lda = pitch_blocks(t, K) + 16 // eb
+    nan = np.array([0x7fc00000 if eb == 4 else 0x7e00], dtype=np.uint32 if eb == 4 else np.uint16)
+    Ap = np.tile(nan, M * lda).view(np.uint8).reshape(M, lda * eb).copy()
+    Ap[:, :K * eb] = A_q.reshape(M, K * eb)
+    ldb = K + ldb_extra
+    Bp = np.tile(nan, N * ldb).view(np.uint8).reshape(N, ldb * eb).copy()
+    Bp[:, :K * eb] = B_q.reshape(N, K * eb)
+    return A_q, B_q, Ap, Bp, lda, ldb
+
+
+@pytest.mark.parametrize("t", [ol.F32, ol.F16], ids=["f32", "f16"])
+@pytest.mark.parametrize("shape", DGEMM_SHAPES, ids=[f"{m}x{n}x{k}" for m, n, k in DGEMM_SHAPES])
+@pytest.mark.parametrize("bal", [True, False], ids=["b16", "bunaligned"])
+def test_dense_gemm_vs_oracle(t, shape, bal):
+    """F32 / F16 prefill GEMM on the matrix cores (lamm_gemm_dense.hip): ragged M / N / K
+    against the 128x128 tile and 128-byte K-step, NaN row padding on both operands (masked),
+    B rows 16-byte aligned (b128 loads) or not (element loads: F16 rows 2-byte aligned)."""
+    M, N, K = shape
+    eb = la.type_size(t)
+    extra = (-K) % (16 // eb) if bal else (1 if (K * eb) % 16 == 0 else 0)
+    A_q, B_q, Ap, Bp, lda, ldb = _dense_case(t, M, N, K, M * 7 + N * 3 + K, extra)
+    assert ((ldb * eb) % 16 == 0) == bal
+    A = dev_bytes(np.concatenate([Ap.reshape(-1), np.zeros(64, np.uint8)]))
+    B = dev_bytes(np.concatenate([Bp.reshape(-1), np.zeros(64, np.uint8)]))
+    C = torch.full((N * M + 16,), float("nan"), dtype=torch.float32, device="cuda")
+    la.mul_mat_torch(t, A, B, C, M, N, K, lda=lda, ldb=ldb)
+    torch.cuda.synchronize()
+    c = C.cpu().numpy()[:N * M].reshape(N, M)
+    ref = ORACLE.mul_mat(t, M, N, K, A_q, B_q)
+    assert np.isfinite(c).all()
+    assert rel_err(c, ref, absdot(t, A_q, B_q, M, N, K)).max() < TOL
+
+
+@pytest.mark.parametrize("t", [ol.F32, ol.F16], ids=["f32", "f16"])
+def test_dense_gemm_batched_broadcast(t):
+    """ggml batch dims on the dense GEMM: 2 weight slices broadcast over 2x3 activation slices
+    (r2 = 1, r3 = 3 -- the GQA-style sharing of a KV-cache slice by several query heads)."""
+    M, N, K = 70, 40, 200
+    eb = la.type_size(t)
+    cases = [_dense_case(t, M, N, K, 100 + s) for s in range(6)]
+    lda, ldb = cases[0][4], cases[0][5]
+    abytes, bbytes = M * lda * eb, N * ldb * eb
+    A = dev_bytes(np.concatenate([cases[s][2].reshape(-1) for s in range(2)] + [np.zeros(64, np.uint8)]))
+    B = dev_bytes(np.concatenate([cases[s][3].reshape(-1) for s in range(6)] + [np.zeros(64, np.uint8)]))
+    C = torch.full((6 * N * M,), float("nan"), dtype=torch.float32, device="cuda")
+    # ne02=2, ne03=1, ne12=2, ne13=3: slice (i12, i13) uses A slice (i12, i13 / 3)
+    bt = la.Batch(2, 1, 2, 3, abytes, 2 * abytes, bbytes, 2 * bbytes, 4 * M * N, 4 * M * N * 2)
+    la.mul_mat_torch(t, A, B, C, M, N, K, lda=lda, ldb=ldb, batch=bt)
+    torch.cuda.synchronize()
+    c = C.cpu().numpy().reshape(6, N, M)
+    for z in range(6):
+        a = cases[z % 2][0]
+        ref = ORACLE.mul_mat(t, M, N, K, a, cases[z][1])
+        assert rel_err(c[z], ref, absdot(t, a, cases[z][1], M, N, K)).max() < TOL, z

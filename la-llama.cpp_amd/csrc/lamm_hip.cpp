@@ -346,8 +346,8 @@ class Runtime {
   size_t budget_ = 0, cached_bytes_ = 0;
   std::unordered_map<WeightKey, WeightEntry, WeightKeyHash> cache_;
   std::list<WeightKey> lru_;
-  void* buf_[2] = {nullptr, nullptr};
-  size_t cap_[2] = {0, 0};
+  void* buf_[3] = {nullptr, nullptr, nullptr};
+  size_t cap_[3] = {0, 0, 0};
 };
 
 int opt_level() {
@@ -370,6 +370,25 @@ bool extra_types_enabled() {
   return !(e && e[0] == '0');
 }
 
+// quantize src1 on the GPU instead of in ggml's INIT phase
+// (LC/ggml.c:10865-10887: serial on thread 0).  The hook then claims the INIT phase too (and
+// does nothing in it), uploads the F32 rows and runs lamm_hip_quantize -- the AVX2 flavour
+// of the x86 reference build, bit-exact, so C is unchanged.  LAMM_HIP_GPU_QUANT=0: ggml's
+// CPU INIT as in the reference, =1: always on the GPU; unset: on the GPU from 8 activation
+// rows up (e2e through the unchanged ggml, profiles/r01/e2e_gpu_quant.txt: Q4_0 4096x512x4096
+// 528 -> 376 us, N=8 44 -> 42 us, but N=1 26 -> 31 us: the extra H2D + launch outweigh
+// quantizing 4096 floats on the host).
+bool gpu_quantizes(const ggml::tensor* src0, const ggml::tensor* src1) {
+  const char* e = getenv("LAMM_HIP_GPU_QUANT");
+  const int64_t rows = src1->ne[1] * src1->ne[2] * src1->ne[3];
+  if (e && e[0] == '0') return false;
+  if (!(e && e[0] == '1') && rows < 8) return false;
+  const int vdt = vec_dot_type(src0->type);
+  return src1->type == kF32 && vdt != kF32 &&
+         (vdt == kQ8_0 || vdt == kQ8_1 || vdt == kQ8_K || vdt == kF16) && src1->nb[0] == sizeof(float) &&
+         (src1->nb[1] & 3) == 0 && (src1->nb[2] & 3) == 0 && (src1->nb[3] & 3) == 0;
+}
+
 }  // namespace
 
 extern "C" int lamm_get_opt_level(void) { return probe().count ? (opt_level() > 0 ? 3 : 0) : 0; }
@@ -378,10 +397,16 @@ extern "C" bool lamm_can_mul_mat(const struct ggml_compute_params* vparams, cons
   const auto* params = reinterpret_cast<const ggml::compute_params*>(vparams);
   const auto* dst = reinterpret_cast<const ggml::tensor*>(vdst);
   if (opt_level() == 0) return false;                       // :12-14
-  if (params->type != ggml::TASK_COMPUTE) return false;     // :15-17, INIT quantizes src1
   const ggml::tensor* src0 = dst->src[0];
   const ggml::tensor* src1 = dst->src[1];
   if (!src0 || !src1) return false;
+  // :15-17: INIT belongs to ggml (it quantizes src1) unless the GPU quantizes it; the INIT
+  // and COMPUTE answers must agree, so INIT re-runs every COMPUTE check below
+  if (params->type == ggml::TASK_INIT) {
+    if (!gpu_quantizes(src0, src1)) return false;
+  } else if (params->type != ggml::TASK_COMPUTE) {
+    return false;
+  }
   const int vdt = vec_dot_type(src0->type);
   if (vdt < 0) return false;                                 // :37-52 supported pairs
   // q4_K / q5_K / q6_K / f16 are beyond the reference's lamm set (a Q4_0
@@ -403,6 +428,7 @@ extern "C" bool lamm_can_mul_mat(const struct ggml_compute_params* vparams, cons
 extern "C" void lamm_mul_mat(const struct ggml_compute_params* vparams, struct ggml_tensor* vdst) {
   const auto* params = reinterpret_cast<const ggml::compute_params*>(vparams);
   auto* dst = reinterpret_cast<ggml::tensor*>(vdst);
+  if (params->type != ggml::TASK_COMPUTE) return;  // INIT claimed for the GPU quantizer: nothing to do
   if (params->ith != 0) return;  // thread 0 owns the device work; ggml's barrier follows
 
   const ggml::tensor* src0 = dst->src[0];
@@ -426,7 +452,23 @@ extern "C" void lamm_mul_mat(const struct ggml_compute_params* vparams, struct g
   const WeightEntry& w = rt.weights(WeightKey{src0->data, t0, M * ne02 * ne03, kb, src0->nb[1]}, a_row, src0);
   // activations: INIT-phase wdata (contiguous rows) or a contiguous vec_dot-typed src1
   void* dB = rt.scratch(0, b_row * (size_t)(N * nslices) + 64);
-  if (use_wdata) {
+  if (use_wdata && gpu_quantizes(src0, src1)) {
+    // F32 rows -> device (contiguous [slice][N][K]) -> vec_dot_type blocks on the GPU
+    const int64_t ldx = (ne00 + 3) & ~int64_t(3);   // the quantizer reads rows as float4
+    const size_t xrow = (size_t)ne00 * sizeof(float);
+    float* dX = static_cast<float*>(rt.scratch(2, (size_t)ldx * sizeof(float) * (size_t)(N * nslices) + 64));
+    for (int64_t i13 = 0; i13 < ne13; ++i13)
+      for (int64_t i12 = 0; i12 < ne12; ++i12) {
+        const unsigned char* x = static_cast<const unsigned char*>(src1->data) + i12 * src1->nb[2] + i13 * src1->nb[3];
+        HIPCHK(hipMemcpy2DAsync(dX + (i13 * ne12 + i12) * N * ldx, (size_t)ldx * sizeof(float), x, src1->nb[1], xrow,
+                                (size_t)N, hipMemcpyHostToDevice, s));
+      }
+    const int qrc = lamm_hip_quantize(vdt, /*AVX2 flavour*/ 1, dX, ldx, dB, kb, (int)ne00, (int)(N * nslices), s);
+    if (qrc != LAMM_OK) {
+      fprintf(stderr, "lamm_hip: lamm_hip_quantize failed (%d): %s\n", qrc, g_err.c_str());
+      std::abort();
+    }
+  } else if (use_wdata) {
     HIPCHK(hipMemcpyAsync(dB, params->wdata, b_row * (size_t)(N * nslices), hipMemcpyHostToDevice, s));
   } else {
     HIPCHK(hipMemcpy2DAsync(dB, b_row, src1->data, src1->nb[1], b_row, (size_t)(N * nslices),

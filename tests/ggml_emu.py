@@ -4,10 +4,13 @@ Builds b2430-layout ``ggml_tensor`` structs over numpy host buffers and replays 
 control flow of ``ggml_compute_forward_mul_mat`` (LC/ggml.c:10736-10891) for one
 mul_mat node:
 
-  INIT    : lamm_can_mul_mat must say no (params->type != COMPUTE); thread 0 then
+  INIT    : the hook is asked first (LC/ggml.c:10858-10863 precedes the INIT branch).
+            The reference's hook says no (params->type != COMPUTE) and thread 0 then
             quantizes src1 into wdata with traits[vec_dot_type].from_float
             (LC/ggml.c:10865-10887) -- here the oracle's AVX2-flavour quantizer, i.e.
-            what an x86 AVX2 build of ggml runs;
+            what an x86 AVX2 build of ggml runs.  liblamm_hip claims INIT when it
+            quantizes src1 on the GPU (LAMM_HIP_GPU_QUANT, default on): every worker
+            calls the hook, which returns at once, and wdata stays untouched;
   COMPUTE : every worker ith in [0, nth) calls the hook (LC/ggml.c:10858-10863).
 """
 import ctypes
@@ -68,8 +71,13 @@ def compute(dst, nth=4, oracle=None, flavour=ol.QUANT_AVX):
     params.wsize, params.wdata = wdata.size, wdata.ctypes.data
 
     params.type = la.TASK_INIT
-    assert not la.can_mul_mat(params, dst.t), "hook must not claim the INIT phase"
-    if src1.t.type != vt:  # thread 0 quantizes src1 -> wdata (contiguous F32 src1 assumed)
+    if la.can_mul_mat(params, dst.t):   # GPU quantizes src1 in COMPUTE
+        for ith in range(nth):
+            params.ith = ith
+            la.mul_mat(params, dst.t)
+        params.ith = 0
+        wdata[:] = 0xA5                  # poison: COMPUTE must not read wdata
+    elif src1.t.type != vt:  # thread 0 quantizes src1 -> wdata (contiguous F32 src1 assumed)
         x = src1.buf.view(np.float32).reshape(nrows, K)
         wdata[:] = oracle.quantize(vt, x, flavour)
 

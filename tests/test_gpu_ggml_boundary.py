@@ -46,14 +46,23 @@ def expected(t, A_q, b, M, N, K, ne2, ne3):
 
 
 @pytest.mark.parametrize("t", ol.A_TYPES, ids=[ol.NAMES[t] for t in ol.A_TYPES])
-def test_boundary_matches_oracle(t):
+def test_boundary_matches_oracle(t, monkeypatch):
+    """Both INIT modes: src1 quantized on the GPU (default) and by ggml's CPU INIT
+    (LAMM_HIP_GPU_QUANT=0).  The GPU quantizer is bit-exact with the AVX2 from_float the
+    CPU path uses, so the two outputs must be identical bit for bit."""
     M, N, K = 67, 9, 512
-    src0, src1, A_q, b = make_node(t, M, N, K, seed=t)
-    dst = ggml_emu.mul_mat_node(src0, src1)
-    assert ggml_emu.compute(dst, nth=3) is True
-    got = dst.buf.view(np.float32).reshape(N, M)
-    want = expected(t, A_q, b, M, N, K, (1, 1), (1, 1))[0, 0]
-    assert rel_err(got, want, np.abs(want) + 1.0).max() < 1e-3
+    outs = []
+    for mode in ("1", "0"):
+        monkeypatch.setenv("LAMM_HIP_GPU_QUANT", mode)
+        src0, src1, A_q, b = make_node(t, M, N, K, seed=t)
+        dst = ggml_emu.mul_mat_node(src0, src1)
+        assert ggml_emu.compute(dst, nth=3) is True
+        got = dst.buf.view(np.float32).reshape(N, M)
+        want = expected(t, A_q, b, M, N, K, (1, 1), (1, 1))[0, 0]
+        assert rel_err(got, want, np.abs(want) + 1.0).max() < 1e-3
+        outs.append(got.copy())
+    if t not in (ol.F32,):
+        np.testing.assert_array_equal(outs[0], outs[1])
     assert la.get_opt_level() == 3
 
 
@@ -92,15 +101,24 @@ def test_weight_cache_reuse_and_invalidation():
     assert la.cache_bytes() == 0
 
 
-def test_non_compute_phases_and_unsupported():
+def test_non_compute_phases_and_unsupported(monkeypatch):
     t, M, N, K = ol.Q4_0, 16, 1, 256
     src0, src1, _, _ = make_node(t, M, N, K)
     dst = ggml_emu.mul_mat_node(src0, src1)
     p = la.GgmlComputeParams()
     p.ith, p.nth = 0, 1
-    for phase in (la.TASK_INIT, la.TASK_FINALIZE):
-        p.type = phase
-        assert not la.can_mul_mat(p, dst.t)
+    p.type = la.TASK_FINALIZE
+    assert not la.can_mul_mat(p, dst.t)
+    p.type = la.TASK_INIT        # claimed only when src1 is quantized on the GPU
+    assert not la.can_mul_mat(p, dst.t)          # default: N = 1 stays on ggml's CPU INIT
+    monkeypatch.setenv("LAMM_HIP_GPU_QUANT", "1")
+    assert la.can_mul_mat(p, dst.t)
+    monkeypatch.setenv("LAMM_HIP_GPU_QUANT", "0")
+    assert not la.can_mul_mat(p, dst.t)
+    monkeypatch.delenv("LAMM_HIP_GPU_QUANT")
+    src0b, src1b, _, _ = make_node(t, M, 8, K)   # from 8 activation rows: GPU quantizer
+    dstb = ggml_emu.mul_mat_node(src0b, src1b)
+    assert la.can_mul_mat(p, dstb.t)
     p.type = la.TASK_COMPUTE
     assert la.can_mul_mat(p, dst.t)
     src0.t.type = 1  # F16 src0 (KV cache matmuls): not on the lamm path

@@ -1,9 +1,10 @@
 """The drop-in proof: the reference's own, unchanged ggml (llama.cpp-b2430 ggml.c built
 from /root/reference with -DLA_LLAMA, its hook LC/ggml.c:10858-10863 resolved to our
 include/loongarch_matmul.h, linked against liblamm_hip.so -- oracle/Makefile target
-ref_driver_hip) runs ggml_graph_compute(ggml_mul_mat(A, B)) on the golden inputs.  Its
-INIT phase quantizes B on the CPU exactly as always; COMPUTE goes to the GPU.  The graph
-output must match the reference's own CPU outputs for the same inputs."""
+ref_driver_hip) runs ggml_graph_compute(ggml_mul_mat(A, B)) on the golden inputs.  By
+default the hook claims INIT and quantizes B on the GPU; with LAMM_HIP_GPU_QUANT=0 ggml's
+INIT quantizes it on the CPU as always.  The graph output must match the reference's own
+CPU outputs for the same inputs, and both modes must agree bit for bit."""
 import os
 import subprocess
 
@@ -44,3 +45,9 @@ def test_unchanged_ggml_graph_through_lamm_hip(exe, path, tmp_path):
     # the hook computed all M rows (no M % nth drop) and matches the reference CPU paths
     assert np.isfinite(c).all()
     assert rel_err(c, z["C_vdot_avx"], z["absdot"]).max() < 1e-3
+    # the CPU-INIT mode (the reference's own flow) gives the same bytes
+    out0 = str(tmp_path / "o0")
+    r = subprocess.run([exe, "gen", NAMES[t], str(M), str(N), str(K), "4", str(pa), str(pb), out0],
+                       capture_output=True, text=True, timeout=120, env=dict(os.environ, LAMM_HIP_GPU_QUANT="0"))
+    assert r.returncode == 0, r.stderr[-2000:]
+    np.testing.assert_array_equal(np.fromfile(out0 + ".C.bin", np.float32).reshape(N, M), c)

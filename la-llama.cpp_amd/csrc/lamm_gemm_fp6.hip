@@ -297,8 +297,13 @@ template <int WJ> struct F6Waves {
   static constexpr int PPW = F6_STAGE / F6_PIECE / NW;   // DMA pieces per wave per stage
 };
 
+// Split-K (grids with too few 256x128 tiles to fill 256 CUs, e.g. ONE 4096x512 GEMM = 64
+// tiles): split s of nsplit runs K-steps [s*nsteps/nsplit, (s+1)*nsteps/nsplit) and writes its
+// partial tile to part[s][z][j][i]; f6_reduce then sums the splits in order 0..nsplit-1
+// (deterministic).  nsplit == 1 writes C directly.
 template <int T, int V, int WJ>
-__global__ __launch_bounds__(F6Waves<WJ>::NT) void gemm_fp6_kernel(GemvArgs p, const unsigned char* ws) {
+__global__ __launch_bounds__(F6Waves<WJ>::NT) void gemm_fp6_kernel(GemvArgs p, const unsigned char* ws, int nsplit,
+                                                                    float* part) {
   using F = F6<T>;
   using WV = F6Waves<WJ>;
   constexpr int F6_NW = WV::NW, F6_PPW = WV::PPW, UPB = 2 * WJ;   // UPB: units per block
@@ -312,11 +317,14 @@ __global__ __launch_bounds__(F6Waves<WJ>::NT) void gemm_fp6_kernel(GemvArgs p, c
   const int wj = w % WV::NWJ, wi = w / WV::NWJ;   // NWJ (j) x 4 (i) waves
   // XCD-aware tile order: workgroup id -> tile index so that the workgroups one XCD runs at
   // once are neighbouring tiles of one slice (their DMA chunks meet in that XCD's L2).
-  int it, jt, z;
+  int it, jt, z, sp;
   {
-    const int nwg = L.nit * L.njt * p.ne12 * p.ne13;
+    const int ntile = L.nit * L.njt * p.ne12 * p.ne13;
+    const int nwg = ntile * nsplit;
     const int id = blockIdx.x, x = id & 7, k = id >> 3, q = nwg >> 3, rmd = nwg & 7;
-    const int wv = x < rmd ? x * (q + 1) + k : rmd * (q + 1) + (x - rmd) * q + k;
+    int wv = x < rmd ? x * (q + 1) + k : rmd * (q + 1) + (x - rmd) * q + k;
+    sp = wv / ntile;   // split-major: one XCD's neighbouring tiles share a K range
+    wv %= ntile;
     const int per = L.nit * L.njt;
     z = wv / per;
     const int ws_ = wv % per, ib = ws_ / (8 * L.njt), rem = ws_ % (8 * L.njt);
@@ -329,6 +337,7 @@ __global__ __launch_bounds__(F6Waves<WJ>::NT) void gemm_fp6_kernel(GemvArgs p, c
   const unsigned char* wa = ws + (int64_t)a * L.a_slice + (int64_t)it * L.nsteps * F6_A_BYTES;
   const unsigned char* wb = ws + L.a_bytes + (int64_t)z * L.b_slice + (int64_t)jt * L.nsteps * F6_B_BYTES;
   const int nsteps = L.nsteps;
+  const int k0 = (int)((int64_t)sp * nsteps / nsplit), k1 = (int)((int64_t)(sp + 1) * nsteps / nsplit);
 
   // ---- LDS-DMA: piece pc = k*NW + w of a stage (A chunk pieces first, then B) ----
   const auto ra = make_rsrc(wa, (uint32_t)(nsteps * F6_A_BYTES));
@@ -360,7 +369,7 @@ __global__ __launch_bounds__(F6Waves<WJ>::NT) void gemm_fp6_kernel(GemvArgs p, c
 
   constexpr bool NODMA = V == 2 || V == 4 || V == 5;
   if (!NODMA)
-    for (int k = 0; k < F6_NBUF - 1 && k < nsteps; ++k) issue(k);
+    for (int k = k0; k < k0 + F6_NBUF - 1 && k < k1; ++k) issue(k);
   F6Frag fb[2][WJ], fa[2][2];   // [block slot][sub-tile]
   F6Res rr[F6_PD + 1];   // results of the units in flight
   constexpr int NU = UPB * F6_KB;   // units per K-step
@@ -382,15 +391,15 @@ __global__ __launch_bounds__(F6Waves<WJ>::NT) void gemm_fp6_kernel(GemvArgs p, c
     if (w >= 4) __builtin_amdgcn_s_setprio(1);
   }
   bool pend = false;
-  for (int ks = 0; ks < nsteps; ++ks) {
+  for (int ks = k0; ks < k1; ++ks) {
     if (!NODMA) {   // this wave's pieces of stage ks landed (younger stages may stay in flight)
-      const int ahead = min(F6_NBUF - 2, nsteps - 1 - ks);
+      const int ahead = min(F6_NBUF - 2, k1 - 1 - ks);
       if (ahead >= 2) f6_wait_vm<2 * F6_PPW>();
       else if (ahead == 1) f6_wait_vm<F6_PPW>();
       else f6_wait_vm<0>();
     }
     if (V != 5) f6_barrier();   // stage ks visible to all waves; stage ks-1 no longer read
-    if (!NODMA && ks + F6_NBUF - 1 < nsteps) issue(ks + F6_NBUF - 1);
+    if (!NODMA && ks + F6_NBUF - 1 < k1) issue(ks + F6_NBUF - 1);
     if constexpr (V == 1) continue;
     const unsigned char* sA = smem + (ks % F6_NBUF) * F6_STAGE;
     const unsigned char* sB = sA + F6_A_BYTES;
@@ -400,14 +409,14 @@ __global__ __launch_bounds__(F6Waves<WJ>::NT) void gemm_fp6_kernel(GemvArgs p, c
     // in front of every wave's first MFMA).  Block b lives in register slot b & 1.
     auto ldB = [&](int b, int x) {
       if constexpr (V == 4) {
-        if (ks > 0) return;
+        if (ks > k0) return;
       }
       const int r = 32 * WJ * wj + 32 * x + lr;
       f6_load(fb[b & 1][x], sB + f6_boff(0, b, h, r), sB + f6_boff(1, b, h, r));
     };
     auto ldA = [&](int b, int y) {
       if constexpr (V == 4) {
-        if (ks > 0) return;
+        if (ks > k0) return;
       }
       const int r = 64 * wi + 32 * y + lr;
       f6_load(fa[b & 1][y], sA + f6_aoff(0, b, r), sA + f6_aoff(1, b, r));
@@ -473,7 +482,15 @@ __global__ __launch_bounds__(F6Waves<WJ>::NT) void gemm_fp6_kernel(GemvArgs p, c
   }
 
   if (pend) epi(NU - 1, rr[(NU - 1) % (F6_PD + 1)]);
-  float* Cz = p.C + (int64_t)i12 * p.sc2 + (int64_t)i13 * p.sc3;
+  float* Cz;
+  int64_t ldc;
+  if (nsplit == 1) {
+    Cz = p.C + (int64_t)i12 * p.sc2 + (int64_t)i13 * p.sc3;
+    ldc = p.ldc;
+  } else {
+    Cz = part + ((int64_t)sp * p.ne12 * p.ne13 + z) * p.N * p.M;
+    ldc = p.M;
+  }
 #pragma unroll
   for (int x = 0; x < WJ; ++x)
 #pragma unroll
@@ -482,9 +499,35 @@ __global__ __launch_bounds__(F6Waves<WJ>::NT) void gemm_fp6_kernel(GemvArgs p, c
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int64_t j = (int64_t)jt * F6_TJ + 32 * WJ * wj + 32 * x + (e & 3) + 8 * (e >> 2) + 4 * h;
-        if (i < p.M && j < p.N) Cz[j * p.ldc + i] = 0.5f * acc[x][y][e];
+        if (i < p.M && j < p.N) Cz[j * ldc + i] = 0.5f * acc[x][y][e];
       }
     }
+}
+
+// C[z][j][i] = sum_{s < nsplit} part[s][z][j][i], in split order
+__global__ __launch_bounds__(256) void f6_reduce(GemvArgs p, int nsplit, const float* __restrict__ part) {
+  const int64_t per = (int64_t)p.N * p.M, slices = (int64_t)p.ne12 * p.ne13;
+  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (g >= per * slices) return;
+  const int64_t z = g / per, r = g % per, j = r / p.M, i = r % p.M;
+  float acc = part[g];
+  for (int s = 1; s < nsplit; ++s) acc += part[(int64_t)s * per * slices + g];
+  const int i12 = (int)(z % p.ne12), i13 = (int)(z / p.ne12);
+  p.C[(int64_t)i12 * p.sc2 + (int64_t)i13 * p.sc3 + j * p.ldc + i] = acc;
+}
+
+// K-splits for a grid of `tiles` workgroups: double until 256 CUs have one each, keeping
+// >= 8 K-steps per split.  LAMM_FP6_SPLIT=n forces n (A/B).
+int f6_nsplit(const GemvArgs& p, const F6Layout& L) {
+  const char* e = getenv("LAMM_FP6_SPLIT");
+  const int tiles = L.nit * L.njt * p.ne12 * p.ne13;
+  int n = 1;
+  if (e && atoi(e) > 0) {
+    n = atoi(e);
+  } else {
+    while (tiles * n < 256 && n < 8 && L.nsteps / (2 * n) >= 8) n *= 2;
+  }
+  return n < 1 ? 1 : (n > L.nsteps ? L.nsteps : n);
 }
 
 template <int T>
@@ -504,20 +547,19 @@ hipError_t launch_fp6_t(const GemvArgs& p, void* ws, hipStream_t s) {
                      dim3(PREP_NT), 0, s, p, w);
   }
   const size_t lds = (size_t)F6_NBUF * F6_STAGE;
+  const int nsplit = f6_nsplit(p, L);
+  float* part = reinterpret_cast<float*>(w + L.a_bytes + (size_t)(p.ne12 * p.ne13) * (size_t)L.b_slice);
   auto go = [&](auto kern, int nt) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(kern, dim3((unsigned)(L.nit * L.njt * p.ne12 * p.ne13)), dim3(nt), lds, s, p,
-                       static_cast<const unsigned char*>(ws));
+    hipLaunchKernelGGL(kern, dim3((unsigned)(L.nit * L.njt * p.ne12 * p.ne13 * nsplit)), dim3(nt), lds, s, p,
+                       static_cast<const unsigned char*>(ws), nsplit, part);
   };
   const char* ev = getenv("LAMM_GEMM_VARIANT");
   const char* ew = getenv("LAMM_FP6_WJ");   // A/B: 1 = 16 waves of 32x64
   const int wjv = ew ? atoi(ew) : 2;
-  if (wjv == 1) {
-    go(gemm_fp6_kernel<T, 0, 1>, F6Waves<1>::NT);
-    return hipGetLastError();
-  }
   constexpr int NT2 = F6Waves<2>::NT;
-  switch (ev ? atoi(ev) : 0) {
+  switch (wjv == 1 ? -1 : ev ? atoi(ev) : 0) {
+    case -1: go(gemm_fp6_kernel<T, 0, 1>, F6Waves<1>::NT); break;
     case 1: go(gemm_fp6_kernel<T, 1, 2>, NT2); break;
     case 2: go(gemm_fp6_kernel<T, 2, 2>, NT2); break;
     case 3: go(gemm_fp6_kernel<T, 3, 2>, NT2); break;
@@ -528,6 +570,11 @@ hipError_t launch_fp6_t(const GemvArgs& p, void* ws, hipStream_t s) {
     case 10: go(gemm_fp6_kernel<T, 10, 2>, NT2); break;
     case 12: go(gemm_fp6_kernel<T, 12, 2>, NT2); break;
     default: go(gemm_fp6_kernel<T, 0, 2>, NT2);
+  }
+  if (nsplit > 1) {
+    const int64_t n = (int64_t)p.N * p.M * p.ne12 * p.ne13;
+    hipLaunchKernelGGL(f6_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, p, nsplit,
+                       static_cast<const float*>(part));
   }
   return hipGetLastError();
 }
@@ -544,7 +591,9 @@ int gemm_fp6_tiles(const GemvArgs& p) {
 size_t gemm_fp6_workspace_bytes(int type, const GemvArgs& p) {
   (void)type;
   const F6Layout L = F6Layout::of(p);
-  return (size_t)L.a_bytes + (size_t)(p.ne12 * p.ne13) * (size_t)L.b_slice + 256;
+  const int nsplit = f6_nsplit(p, L);
+  const size_t part = nsplit > 1 ? (size_t)nsplit * p.ne12 * p.ne13 * (size_t)p.N * p.M * sizeof(float) : 0;
+  return (size_t)L.a_bytes + (size_t)(p.ne12 * p.ne13) * (size_t)L.b_slice + part + 256;
 }
 
 hipError_t launch_gemm_fp6(int type, const GemvArgs& p, void* ws, hipStream_t s) {

@@ -36,6 +36,6 @@ bool gemm_args_ok(int type, const GemvArgs& p);   // B pitch/alignment the GEMM 
 hipError_t launch_gemm_fp6(int type, const GemvArgs& p, void* workspace, hipStream_t s);
 size_t gemm_fp6_workspace_bytes(int type, const GemvArgs& p);
 bool gemm_fp6_supported(int type);
-int gemm_fp6_tiles(const GemvArgs& p);   // workgroups of its main kernel (one 256x128 tile each)
+int gemm_fp6_tiles(const GemvArgs& p);   // 256x128 output tiles of the fp6 GEMM (before K-splits)
 
 }  // namespace lamm

@@ -180,8 +180,8 @@ def quantize_torch(vtype, x, y, flavour=1, stream=None):
 
 def gemm_engine(fmt, M, N, K, slices=1):
     """Which prefill engine lamm_hip_matmul* picks for N > 8 (mirrors gemm_path() in
-    csrc/lamm_hip.cpp): "fp6" (q4_0/q4_1/q5_0 when its 256x128 tiles fill >= 256 CUs),
-    "i8" otherwise; LAMM_GEMM_PATH overrides."""
+    csrc/lamm_hip.cpp): "fp6" (q4_0/q4_1/q5_0 when its 256x128 tiles fill >= 256 CUs;
+    forced onto smaller grids it splits K), "i8" otherwise; LAMM_GEMM_PATH overrides."""
     t = BY_NAME[fmt] if isinstance(fmt, str) else fmt
     if N <= 8:
         return "gemv"

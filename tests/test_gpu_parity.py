@@ -162,11 +162,29 @@ def test_gemm_engines_vs_oracle(t, shape, engine, monkeypatch):
     assert err < TOL, err
 
 
+@pytest.mark.parametrize("split", [1, 3, 8])
 @pytest.mark.parametrize("t", FP6_TYPES, ids=[ol.NAMES[t] for t in FP6_TYPES])
-def test_gemm_fp6_batched_broadcast(t, monkeypatch):
-    """fp6 engine with ggml batch dims: 2 weight slices broadcast over 4 activation slices
-    (r2 = 2), the unique-A-slice prep indexing of lamm_gemm_fp6.hip."""
+def test_gemm_fp6_split_k(t, split, monkeypatch):
+    """fp6 engine with K split over workgroups (LAMM_FP6_SPLIT; auto for grids < 256 tiles):
+    uneven splits of 65 K-steps, partial tiles summed in split order by f6_reduce."""
     monkeypatch.setenv("LAMM_GEMM_PATH", "fp6")
+    monkeypatch.setenv("LAMM_FP6_SPLIT", str(split))
+    M, N, K = 300, 140, 4096 + 64
+    A_q, B_q = random_case(t, M, N, K, seed=split)
+    c, raw = gpu_mul_mat(t, A_q, B_q, M, N, K, ldc=M + 3)
+    ref = ORACLE.mul_mat(t, M, N, K, A_q, B_q)
+    assert rel_err(c, ref, absdot(t, A_q, B_q, M, N, K)).max() < TOL
+    assert np.isnan(np.concatenate([raw[j * (M + 3) + M:(j + 1) * (M + 3)] for j in range(N)])).all()
+
+
+@pytest.mark.parametrize("split", ["0", "4"])
+@pytest.mark.parametrize("t", FP6_TYPES, ids=[ol.NAMES[t] for t in FP6_TYPES])
+def test_gemm_fp6_batched_broadcast(t, split, monkeypatch):
+    """fp6 engine with ggml batch dims: 2 weight slices broadcast over 4 activation slices
+    (r2 = 2), the unique-A-slice prep indexing of lamm_gemm_fp6.hip; split-K partials
+    indexed per slice."""
+    monkeypatch.setenv("LAMM_GEMM_PATH", "fp6")
+    monkeypatch.setenv("LAMM_FP6_SPLIT", split)
     M, N, K = 70, 20, 512
     kb = K // la.blck_size(t)
     vt = la.vec_dot_type(t)

@@ -41,7 +41,12 @@ def main():
     for rnd in range(5):
         for v in variants:
             os.environ.pop("LAMM_FP6_WJ", None)
-            if v in ("fp6", "i8"):
+            os.environ.pop("LAMM_FP6_SPLIT", None)
+            if v.startswith("fp6s"):     # fp6 with a forced K-split count: fp6s4
+                os.environ["LAMM_GEMM_PATH"] = "fp6"
+                os.environ["LAMM_GEMM_VARIANT"] = "0"
+                os.environ["LAMM_FP6_SPLIT"] = v[4:]
+            elif v in ("fp6", "i8"):
                 os.environ["LAMM_GEMM_PATH"] = v
                 os.environ["LAMM_GEMM_VARIANT"] = "0"
             elif v.startswith("fp6w"):   # fp6 wave-tile width: fp6w1 = 16 waves of 32x64

@@ -111,6 +111,23 @@ int lamm_hip_matmul_batched(const lamm_matrix *A, const lamm_matrix *B, const la
 int lamm_hip_quantize(int vec_type, int flavour, const float *x, int64_t ldx, void *y,
                       int64_t ldy, int K, int N, void *hip_stream);
 
+/* Weight-stationary form (weight residency).  Inference multiplies the
+ * same weights by new activations on every call; a lamm_weights handle records A (whose
+ * device blocks must stay valid and unchanged while the handle lives) and its ggml slice
+ * dims, and for the formats the prefill GEMM repacks (q4_0 / q4_1 / q5_0) keeps that packed
+ * form device-resident (lamm_hip_weights_bytes), so a call skips the per-call weight
+ * repack.  lamm_hip_matmul_weights(W, B, C, batch, s) computes exactly what
+ * lamm_hip_matmul_batched(&A, B, C, batch, s) computes; batch may be NULL (one slice per A
+ * slice) and, if given, must repeat W's ne02 / ne03 / nba2 / nba3.  Creation runs on
+ * hip_stream; destroy synchronises the device before freeing. */
+typedef struct lamm_weights lamm_weights;
+int lamm_hip_weights_create(const lamm_matrix *A, int64_t ne02, int64_t ne03, size_t nba2, size_t nba3,
+                            void *hip_stream, lamm_weights **out);
+int lamm_hip_matmul_weights(const lamm_weights *W, const lamm_matrix *B, const lamm_matrix *C,
+                            const lamm_batch *batch, void *hip_stream);
+size_t lamm_hip_weights_bytes(const lamm_weights *W);
+void lamm_hip_weights_destroy(lamm_weights *W);
+
 const char *lamm_hip_last_error(void);
 int lamm_hip_device_count(void);
 

@@ -91,21 +91,25 @@ void* workspace(size_t bytes, hipStream_t s) {
   return g_ws;
 }
 
-// GEMM engine for the q4_0 / q4_1 / q5_0 prefill path: 0 = block-scaled fp6 MFMA
-// (lamm_gemm_fp6.hip), 1 = MFMA-i8 (lamm_gemm.hip).  The fp6 kernel's 256x128 tiles only pay
-// off once they fill the chip (>= one tile per CU); smaller calls take the i8 kernel's
-// 128x64 tiles.  LAMM_GEMM_PATH=fp6 / i8 forces one (A/B measurements).
 // env var set to "0" (A/B switches that turn a default path off)
 bool getenv_flag0(const char* name) {
   const char* e = getenv(name);
   return e && !strcmp(e, "0");
 }
 
-int gemm_path(const GemvArgs& p) {
+// GEMM engine for the q4_0 / q4_1 / q5_0 prefill path: 0 = block-scaled fp6 MFMA
+// (lamm_gemm_fp6.hip), 1 = MFMA-i8 (lamm_gemm.hip).  The fp6 kernel's 256x128 tiles only pay
+// off once they fill the chip (>= one tile per CU); smaller calls take the i8 kernel's
+// 128x64 tiles.  With weight-stationary callers (lamm_hip_weights: the packed weights are
+// resident) the fp6 kernel's K-split fills the chip from 64 tiles up and wins there too
+// (profiles/r01/ab_stationary.txt: one 4096x512x4096 slice 44.4 us at 4 splits vs 48.2 us
+// on i8; two slices 65.1 vs 88.1); per call, re-packing the weights costs it that margin on
+// a single slice (53.8 vs 47.9).  LAMM_GEMM_PATH=fp6 / i8 forces one (A/B measurements).
+int gemm_path(const GemvArgs& p, bool stationary) {
   const char* e = getenv("LAMM_GEMM_PATH");
   if (e && (!strcmp(e, "i8") || !strcmp(e, "1"))) return 1;
   if (e && (!strcmp(e, "fp6") || !strcmp(e, "0"))) return 0;
-  return gemm_fp6_tiles(p) >= 256 ? 0 : 1;
+  return (stationary ? gemm_fp6_grid(p) : gemm_fp6_tiles(p)) >= 256 ? 0 : 1;
 }
 
 }  // namespace
@@ -118,8 +122,28 @@ extern "C" const char* lamm_hip_last_error(void) { return g_err.c_str(); }
 extern "C" int lamm_hip_device_count(void) { return probe().count; }
 
 // ======================================================== operator API
-extern "C" int lamm_hip_matmul_batched(const lamm_matrix* A, const lamm_matrix* B, const lamm_matrix* C,
-                                       const lamm_batch* batch, void* hip_stream) {
+struct lamm_weights {
+  lamm_matrix A;
+  int64_t ne02, ne03;
+  size_t nba2, nba3;
+  void* packed = nullptr;    // fp6 GEMM form of A (q4_0 / q4_1 / q5_0), null otherwise
+  size_t packed_bytes = 0;
+};
+
+namespace {
+
+GemvArgs weight_args(const lamm_matrix* A, int64_t ne02, int64_t ne03, size_t nba2, size_t nba3) {
+  GemvArgs p{static_cast<const unsigned char*>(A->data), A->ld * (int64_t)block_bytes(A->type), nullptr, 0,
+             nullptr, 0, A->row, 1, A->col * block_elems(A->type), A->col};
+  p.ne12 = (int)ne02;
+  p.ne13 = (int)ne03;
+  p.sa2 = (int64_t)nba2;
+  p.sa3 = (int64_t)nba3;
+  return p;
+}
+
+int matmul_impl(const lamm_matrix* A, const lamm_matrix* B, const lamm_matrix* C, const lamm_batch* batch,
+                void* hip_stream, const lamm_weights* W) {
   if (!A || !B || !C) return fail(LAMM_ERR_SHAPE, "null matrix");
   if (!is_weight_type(A->type)) return fail(LAMM_ERR_TYPE, "unsupported A type %d", A->type);
   if (B->type != vec_dot_type(A->type))
@@ -167,11 +191,12 @@ extern "C" int lamm_hip_matmul_batched(const lamm_matrix* A, const lamm_matrix* 
     e = launch_gemv(A->type, p, s);
   } else if (gemm_dense_supported(A->type) && !getenv_flag0("LAMM_DENSE_GEMM")) {
     e = launch_gemm_dense(A->type, p, s);
-  } else if (gemm_fp6_supported(A->type) && gemm_path(p) == 0) {
-    const size_t wsb = gemm_fp6_workspace_bytes(A->type, p);
+  } else if (gemm_fp6_supported(A->type) && gemm_path(p, W && W->packed) == 0) {
+    const void* prepA = W ? W->packed : nullptr;
+    const size_t wsb = gemm_fp6_workspace_bytes(A->type, p, prepA != nullptr);
     void* ws = workspace(wsb, s);
     if (!ws) return fail(LAMM_ERR_HIP, "workspace allocation of %zu bytes failed", wsb);
-    e = launch_gemm_fp6(A->type, p, ws, s);
+    e = launch_gemm_fp6(A->type, p, prepA, ws, s);
   } else if (gemm_supported(A->type) && gemm_args_ok(A->type, p)) {
     void* ws = nullptr;
     const size_t wsb = gemm_workspace_bytes(A->type, p);
@@ -189,6 +214,66 @@ extern "C" int lamm_hip_matmul_batched(const lamm_matrix* A, const lamm_matrix* 
   }
   if (e != hipSuccess) return fail(LAMM_ERR_HIP, "kernel launch: %s", hipGetErrorString(e));
   return LAMM_OK;
+}
+
+}  // namespace
+
+extern "C" int lamm_hip_matmul_batched(const lamm_matrix* A, const lamm_matrix* B, const lamm_matrix* C,
+                                       const lamm_batch* batch, void* hip_stream) {
+  return matmul_impl(A, B, C, batch, hip_stream, nullptr);
+}
+
+extern "C" int lamm_hip_weights_create(const lamm_matrix* A, int64_t ne02, int64_t ne03, size_t nba2, size_t nba3,
+                                       void* hip_stream, lamm_weights** out) {
+  if (!A || !out) return fail(LAMM_ERR_SHAPE, "null argument");
+  *out = nullptr;
+  if (!is_weight_type(A->type)) return fail(LAMM_ERR_TYPE, "unsupported A type %d", A->type);
+  if (A->row < 0 || A->col < 0 || A->ld < A->col) return fail(LAMM_ERR_SHAPE, "bad A shape");
+  if (ne02 < 1 || ne03 < 1 || ne02 * ne03 > 65535) return fail(LAMM_ERR_SHAPE, "bad A slice counts");
+  const int64_t lda = A->ld * (int64_t)block_bytes(A->type);
+  if (((uintptr_t)A->data & 15) || (lda & 15) || (nba2 & 15) || (nba3 & 15))
+    return fail(LAMM_ERR_ALIGN, "A must be 16-byte aligned with 16-byte row/slice pitches");
+  if (probe().count == 0) return fail(LAMM_ERR_NODEV, "no gfx950 device");
+  auto* W = new lamm_weights{*A, ne02, ne03, nba2, nba3};
+  if (gemm_fp6_supported(A->type) && A->row > 0 && A->col > 0) {
+    const GemvArgs p = weight_args(A, ne02, ne03, nba2, nba3);
+    W->packed_bytes = gemm_fp6_weight_bytes(A->type, p);
+    if (hipMalloc(&W->packed, W->packed_bytes) != hipSuccess) {
+      delete W;
+      return fail(LAMM_ERR_HIP, "hipMalloc of %zu packed weight bytes failed", W->packed_bytes);
+    }
+    const hipError_t e = prepare_fp6_weights(A->type, p, W->packed, static_cast<hipStream_t>(hip_stream));
+    if (e != hipSuccess) {
+      (void)hipFree(W->packed);
+      delete W;
+      return fail(LAMM_ERR_HIP, "weight packing: %s", hipGetErrorString(e));
+    }
+  }
+  *out = W;
+  return LAMM_OK;
+}
+
+extern "C" int lamm_hip_matmul_weights(const lamm_weights* W, const lamm_matrix* B, const lamm_matrix* C,
+                                       const lamm_batch* batch, void* hip_stream) {
+  if (!W) return fail(LAMM_ERR_SHAPE, "null weights");
+  lamm_batch bt{W->ne02, W->ne03, W->ne02, W->ne03, W->nba2, W->nba3, 0, 0, 0, 0};
+  if (batch) {
+    if (batch->ne02 != W->ne02 || batch->ne03 != W->ne03 || batch->nba2 != W->nba2 || batch->nba3 != W->nba3)
+      return fail(LAMM_ERR_SHAPE, "batch A dims differ from the prepared weights'");
+    bt = *batch;
+  }
+  return matmul_impl(&W->A, B, C, &bt, hip_stream, W);
+}
+
+extern "C" size_t lamm_hip_weights_bytes(const lamm_weights* W) { return W ? W->packed_bytes : 0; }
+
+extern "C" void lamm_hip_weights_destroy(lamm_weights* W) {
+  if (!W) return;
+  if (W->packed) {
+    (void)hipDeviceSynchronize();   // no launch may still read the packed form
+    (void)hipFree(W->packed);
+  }
+  delete W;
 }
 
 extern "C" int lamm_hip_matmul(const lamm_matrix* A, const lamm_matrix* B, const lamm_matrix* C,
@@ -243,6 +328,7 @@ struct WeightEntry {
   void* dev = nullptr;
   int64_t dev_pitch = 0;
   size_t bytes = 0;
+  lamm_weights* prepared = nullptr;   // packed GEMM form, made on the first prefill call
   uint64_t fingerprint = 0;
   std::list<WeightKey>::iterator lru;
 };
@@ -279,7 +365,7 @@ class Runtime {
   }
 
   // k.rows = ne01*ne02*ne03 device rows; host slices may be strided (nb[2], nb[3])
-  const WeightEntry& weights(const WeightKey& k, size_t row_bytes, const ggml::tensor* src0) {
+  WeightEntry& weights(const WeightKey& k, size_t row_bytes, const ggml::tensor* src0) {
     const int64_t ne01 = src0->ne[1], ne02 = src0->ne[2], ne03 = src0->ne[3];
     uint64_t fp = 0;
     for (int64_t i3 = 0; i3 < ne03; ++i3)
@@ -317,6 +403,19 @@ class Runtime {
     return cache_.emplace(k, e).first->second;
   }
 
+  // the entry's weight-stationary handle (packed fp6 GEMM form), created on first use
+  lamm_weights* prepared(WeightEntry& e, const lamm_matrix& A, int64_t ne02, int64_t ne03) {
+    if (!e.prepared) {
+      const size_t pitch = (size_t)e.dev_pitch * A.row;
+      if (lamm_hip_weights_create(&A, ne02, ne03, pitch, pitch * ne02, stream_, &e.prepared) != LAMM_OK) {
+        fprintf(stderr, "lamm_hip: lamm_hip_weights_create failed: %s\n", g_err.c_str());
+        std::abort();
+      }
+      cached_bytes_ += lamm_hip_weights_bytes(e.prepared);
+    }
+    return e.prepared;
+  }
+
   void* scratch(int which, size_t bytes) {
     if (cap_[which] < bytes) {
       if (buf_[which]) HIPCHK(hipFree(buf_[which]));
@@ -337,6 +436,10 @@ class Runtime {
     if (it == cache_.end()) return;
     (void)hipStreamSynchronize(stream_);
     (void)hipFree(it->second.dev);
+    if (it->second.prepared) {
+      cached_bytes_ -= lamm_hip_weights_bytes(it->second.prepared);
+      lamm_hip_weights_destroy(it->second.prepared);
+    }
     cached_bytes_ -= it->second.bytes;
     lru_.erase(it->second.lru);
     cache_.erase(it);
@@ -449,7 +552,7 @@ extern "C" void lamm_mul_mat(const struct ggml_compute_params* vparams, struct g
   hipStream_t s = rt.stream();
 
   // weights: every (i02, i03) slice, device resident, rows re-pitched to 16 B
-  const WeightEntry& w = rt.weights(WeightKey{src0->data, t0, M * ne02 * ne03, kb, src0->nb[1]}, a_row, src0);
+  WeightEntry& w = rt.weights(WeightKey{src0->data, t0, M * ne02 * ne03, kb, src0->nb[1]}, a_row, src0);
   // activations: INIT-phase wdata (contiguous rows) or a contiguous vec_dot-typed src1
   void* dB = rt.scratch(0, b_row * (size_t)(N * nslices) + 64);
   if (use_wdata && gpu_quantizes(src0, src1)) {
@@ -482,7 +585,16 @@ extern "C" void lamm_mul_mat(const struct ggml_compute_params* vparams, struct g
   lamm_matrix C{dC, kF32, (int)M, (int)N, M};
   lamm_batch bt{ne02, ne03, ne12, ne13, (size_t)(w.dev_pitch * M), (size_t)(w.dev_pitch * M * ne02),
                 b_row * (size_t)N, b_row * (size_t)(N * ne12), c_slice, c_slice * (size_t)ne12};
-  const int rc = lamm_hip_matmul_batched(&A, &B, &C, &bt, s);
+  // prefill calls on the fp6 engine reuse the weights' packed form (weight-stationary)
+  GemvArgs pa = weight_args(&A, ne02, ne03, bt.nba2, bt.nba3);
+  pa.N = (int)N;
+  pa.ne12 = (int)ne12;
+  pa.ne13 = (int)ne13;
+  pa.r2 = (int)(ne12 / ne02);
+  pa.r3 = (int)(ne13 / ne03);
+  const bool stationary = N > 8 && gemm_fp6_supported(t0) && gemm_path(pa, true) == 0;
+  const int rc = stationary ? lamm_hip_matmul_weights(rt.prepared(w, A, ne02, ne03), &B, &C, &bt, s)
+                            : lamm_hip_matmul_batched(&A, &B, &C, &bt, s);
   if (rc != LAMM_OK) {
     fprintf(stderr, "lamm_hip: lamm_hip_matmul_batched failed (%d): %s\n", rc, g_err.c_str());
     std::abort();

@@ -98,6 +98,16 @@ lib.lamm_hip_matmul_batched.argtypes = [ctypes.POINTER(Matrix)] * 3 + [ctypes.PO
 lib.lamm_hip_quantize.restype = ctypes.c_int
 lib.lamm_hip_quantize.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
                                   ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+lib.lamm_hip_weights_create.restype = ctypes.c_int
+lib.lamm_hip_weights_create.argtypes = [ctypes.POINTER(Matrix), ctypes.c_int64, ctypes.c_int64, ctypes.c_size_t,
+                                        ctypes.c_size_t, ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]
+lib.lamm_hip_matmul_weights.restype = ctypes.c_int
+lib.lamm_hip_matmul_weights.argtypes = [ctypes.c_void_p, ctypes.POINTER(Matrix), ctypes.POINTER(Matrix),
+                                        ctypes.POINTER(Batch), ctypes.c_void_p]
+lib.lamm_hip_weights_bytes.restype = ctypes.c_size_t
+lib.lamm_hip_weights_bytes.argtypes = [ctypes.c_void_p]
+lib.lamm_hip_weights_destroy.restype = None
+lib.lamm_hip_weights_destroy.argtypes = [ctypes.c_void_p]
 lib.lamm_hip_last_error.restype = ctypes.c_char_p
 lib.lamm_hip_device_count.restype = ctypes.c_int
 lib.lamm_blck_size.restype = ctypes.c_int
@@ -166,6 +176,52 @@ def mul_mat_torch(wtype, a, b, c, M, N, K, lda=None, ldb=None, ldc=None, stream=
         matmul_batched(A, B, C, batch, stream)
 
 
+class Weights:
+    """Weight-stationary handle (lamm_hip_weights_create): A stays where it is and must not
+    change; q4_0 / q4_1 / q5_0 additionally keep their packed prefill-GEMM form on device.
+    ``a`` is a torch device tensor of A blocks; lda in blocks; slice strides in bytes."""
+
+    def __init__(self, wtype, a, M, K, lda=None, ne02=1, ne03=1, nba2=0, nba3=0, stream=None):
+        import torch
+        kb = K // blck_size(wtype)
+        if stream is None:
+            stream = torch.cuda.current_stream().cuda_stream
+        self.wtype, self.M, self.K, self.kb = wtype, M, K, kb
+        self.ne02, self.ne03, self.nba2, self.nba3 = ne02, ne03, nba2, nba3
+        self._a = a   # keep the blocks alive
+        self.A = Matrix(a.data_ptr(), wtype, M, kb, lda if lda is not None else kb)
+        h = ctypes.c_void_p()
+        _check(lib.lamm_hip_weights_create(ctypes.byref(self.A), ne02, ne03, nba2, nba3, ctypes.c_void_p(stream),
+                                           ctypes.byref(h)), "lamm_hip_weights_create")
+        self.h = h
+
+    @property
+    def packed_bytes(self):
+        return lib.lamm_hip_weights_bytes(self.h)
+
+    def matmul_torch(self, b, c, N, ldb=None, ldc=None, batch=None, stream=None):
+        import torch
+        if stream is None:
+            stream = torch.cuda.current_stream().cuda_stream
+        vt = vec_dot_type(self.wtype)
+        B = Matrix(b.data_ptr(), vt, self.kb, N, ldb if ldb is not None else self.kb)
+        C = Matrix(c.data_ptr(), F32, self.M, N, ldc if ldc is not None else self.M)
+        _check(lib.lamm_hip_matmul_weights(self.h, ctypes.byref(B), ctypes.byref(C),
+                                           ctypes.byref(batch) if batch is not None else None,
+                                           ctypes.c_void_p(stream)), "lamm_hip_matmul_weights")
+
+    def close(self):
+        if self.h:
+            lib.lamm_hip_weights_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def quantize_torch(vtype, x, y, flavour=1, stream=None):
     """GPU activation quantizer: x [N][K] f32 (torch, device) -> y blocks (uint8)."""
     import torch
@@ -178,10 +234,10 @@ def quantize_torch(vtype, x, y, flavour=1, stream=None):
            "lamm_hip_quantize")
 
 
-def gemm_engine(fmt, M, N, K, slices=1):
+def gemm_engine(fmt, M, N, K, slices=1, stationary=False):
     """Which prefill engine lamm_hip_matmul* picks for N > 8 (mirrors gemm_path() in
-    csrc/lamm_hip.cpp): "fp6" (q4_0/q4_1/q5_0 when its 256x128 tiles fill >= 256 CUs;
-    forced onto smaller grids it splits K), "i8" otherwise; LAMM_GEMM_PATH overrides."""
+    csrc/lamm_hip.cpp): "fp6" (q4_0/q4_1/q5_0 when its 256x128 tiles fill >= 256 CUs -- or,
+    for stationary weights (la.Weights), its tiles x K-splits do), "i8" otherwise; LAMM_GEMM_PATH overrides."""
     t = BY_NAME[fmt] if isinstance(fmt, str) else fmt
     if N <= 8:
         return "gemv"
@@ -193,6 +249,14 @@ def gemm_engine(fmt, M, N, K, slices=1):
     if env in ("fp6", "0"):
         return "fp6"
     tiles = -(-M // 256) * -(-N // 128) * slices
+    if stationary:   # f6_nsplit(): double until 256 workgroups, >= 8 K-steps per split
+        nsteps = -(-(K // 32) // 2)
+        split = int(os.environ.get("LAMM_FP6_SPLIT", "0") or 0)
+        if split <= 0:
+            split = 1
+            while tiles * split < 256 and split < 8 and nsteps // (2 * split) >= 8:
+                split *= 2
+        tiles *= max(1, min(split, nsteps))
     return "fp6" if tiles >= 256 else "i8"
 
 

@@ -350,3 +350,42 @@ def test_dense_gemm_batched_broadcast(t):
         a = cases[z % 2][0]
         ref = ORACLE.mul_mat(t, M, N, K, a, cases[z][1])
         assert rel_err(c[z], ref, absdot(t, a, cases[z][1], M, N, K)).max() < TOL, z
+
+
+@pytest.mark.parametrize("t", [ol.Q4_0, ol.Q4_1, ol.Q5_0, ol.Q8_0, ol.F16], ids=["q4_0", "q4_1", "q5_0", "q8_0", "f16"])
+def test_weights_stationary_matches_per_call(t, monkeypatch):
+    """lamm_hip_weights_create / matmul_weights (packed prefill-GEMM weights kept on device)
+    give the same bytes as the per-call path, on both the fp6 GEMM (forced, with a batched
+    broadcast) and the GEMV; batch A dims other than the handle's are refused."""
+    monkeypatch.setenv("LAMM_GEMM_PATH", "fp6")
+    M, N, K = 300, 140, 1024
+    eb = la.type_size(t)
+    kb = K // la.blck_size(t)
+    lda = pitch_blocks(t, kb)
+    vt = la.vec_dot_type(t)
+    As = [random_case(t, M, N, K, seed=40 + s)[0] for s in range(2)]
+    Bs = [random_case(t, M, N, K, seed=50 + s)[1] for s in range(4)]
+    abytes = M * lda * eb
+    A = dev_bytes(np.concatenate([pitched_A(t, a, M, kb, lda)[:abytes] for a in As] + [np.zeros(64, np.uint8)]))
+    bbytes = N * kb * la.type_size(vt)
+    B = dev_bytes(np.concatenate([np.ascontiguousarray(b).view(np.uint8).reshape(-1)[:bbytes] for b in Bs]))
+    bt = la.Batch(2, 1, 4, 1, abytes, 2 * abytes, bbytes, 4 * bbytes, 4 * M * N, 4 * M * N * 4)
+    W = la.Weights(t, A, M, K, lda=lda, ne02=2, ne03=1, nba2=abytes, nba3=2 * abytes)
+    assert (W.packed_bytes > 0) == (t in FP6_TYPES)
+    for n in (N, 3):   # GEMM and GEMV
+        C0 = torch.full((4 * n * M,), float("nan"), dtype=torch.float32, device="cuda")
+        C1 = torch.full_like(C0, float("nan"))
+        btn = la.Batch(2, 1, 4, 1, abytes, 2 * abytes, bbytes, 4 * bbytes, 4 * M * n, 4 * M * n * 4)
+        la.mul_mat_torch(t, A, B, C0, M, n, K, lda=lda, batch=btn)
+        W.matmul_torch(B, C1, n, batch=btn)
+        torch.cuda.synchronize()
+        assert torch.equal(C0, C1)
+        c = C1.cpu().numpy().reshape(4, n, M)
+        for z in range(4):
+            Bz = np.ascontiguousarray(Bs[z]).view(np.uint8).reshape(-1)[:n * kb * la.type_size(vt)]
+            ref = ORACLE.mul_mat(t, M, n, K, As[z // 2], Bz)
+            assert rel_err(c[z], ref, absdot(t, As[z // 2], Bz, M, n, K)).max() < TOL
+    bad = la.Batch(1, 1, 4, 1, abytes, abytes, bbytes, 4 * bbytes, 4 * M * N, 4 * M * N * 4)
+    with pytest.raises(la.LammError):
+        W.matmul_torch(B, C1, N, batch=bad)
+    W.close()

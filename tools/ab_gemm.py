@@ -38,6 +38,15 @@ def main():
     Cm = la.Matrix(C.data_ptr(), la.F32, M, N, M)
     bt = la.Batch(slices, 1, slices, 1, M * arow, slices * M * arow, N * brow, slices * N * brow,
                   4 * M * N, 4 * M * N * slices)
+    W = None
+    if os.environ.get("STATIONARY") == "1":   # weights as a lamm_hip_weights handle (packed once)
+        W = la.Weights(t, A, M, K, ne02=slices, ne03=1, nba2=M * arow, nba3=slices * M * arow)
+
+    def run():
+        if W is not None:
+            W.matmul_torch(B, C, N, batch=bt, stream=stream.cuda_stream)
+        else:
+            la.matmul_batched(Am, Bm, Cm, bt, stream.cuda_stream)
     for rnd in range(5):
         for v in variants:
             os.environ.pop("LAMM_FP6_WJ", None)
@@ -60,11 +69,11 @@ def main():
                 os.environ["LAMM_GEMM_PATH"] = "i8"
                 os.environ["LAMM_GEMM_VARIANT"] = v
             for _ in range(2):
-                la.matmul_batched(Am, Bm, Cm, bt, stream.cuda_stream)
+                run()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
             for _ in range(10):
-                la.matmul_batched(Am, Bm, Cm, bt, stream.cuda_stream)
+                run()
             e1.record(stream)
             torch.cuda.synchronize()
             res[v].append(e0.elapsed_time(e1) * 1e3 / 10)

@@ -234,7 +234,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if world > 1 and os.environ.get("LAMM_BENCH_REHEARSE") == "1":
+        # rehearsal of the N>1 code path on a one-GPU box: every rank on cuda:0, gloo for the
+        # collectives (numbers meaningless; the driver's multi-GPU runs use RCCL, below)
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo")
+    elif world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     if la.device_count() == 0:

@@ -67,7 +67,12 @@ class RowGather:
         self.out = torch.empty((R, world * m), dtype=dtype, device=device)
 
     def __call__(self, c_shard):
-        if self.world > 1:
+        if self.world > 1 and self.recv.is_cuda and self.dist.get_backend() == "gloo":
+            # gloo is a host backend: stage device slabs through host memory (bench rehearsal)
+            recv = self.recv.cpu()
+            self.dist.all_gather_into_tensor(recv.view(-1), c_shard.reshape(-1).cpu())
+            self.recv.copy_(recv)
+        elif self.world > 1:
             self.dist.all_gather_into_tensor(self.recv.view(-1), c_shard.reshape(-1))
         else:
             self.recv[0].copy_(c_shard.view(self.R, self.m))

@@ -55,6 +55,9 @@ def make_weights(torch, la, fmt, slices, M, K, gen):
     if fmt == "f32":
         w = torch.randn(slices * M * K, device="cuda", generator=gen).view(torch.uint8)
         return w, rb
+    if fmt == "f16":
+        w = torch.randn(slices * M * K, device="cuda", generator=gen).half().view(torch.uint8)
+        return w, rb
     w = torch.randint(0, 256, (slices * M * rb,), dtype=torch.uint8, device="cuda", generator=gen)
     bpb = la.type_size(t)
     blocks = w.view(-1, bpb)
@@ -306,12 +309,23 @@ def main():
                              "frac": round(ops / g_main / 1e12 / I8_DENSE_PEAK_TOPS, 4),
                              "per_launch_us": round(g_main * 1e6, 2)}}
     if args.sweep:
+        # BASELINE config 4: every weight format, GEMV (HBM GB/s, > MALL per launch) and the
+        # single-slice M=4096 N=512 K=4096 GEMM (effective GFLOPS, stationary weights)
         sw = {}
-        for f in ["f32", "q4_0", "q4_1", "q5_0", "q5_1", "q8_0", "q2_k", "q4_k", "q5_k", "q6_k"]:
+        for f in ["f32", "f16", "q4_0", "q4_1", "q5_0", "q5_1", "q8_0", "q2_k", "q4_k", "q5_k", "q6_k"]:
             u = gemv_bytes(la, f, M, K)
             sl = max(4, -(-int(1.15 * MALL_BYTES) // u))
             _, _, kk = run_case(torch, la, dist, f, M, 1, K, sl, max(5, args.steps // 2), 2, world)
             sw[f] = {"gemv_GBs": round(sl * u / kk / 1e9, 1), "gemv_us_per_slice": round(kk / sl * 1e6, 3)}
+            if not args.no_gemm:
+                gN = args.gemm_N
+                _, _, gk = run_case(torch, la, dist, f, M, gN, K, 1, max(3, args.steps // 4), 2, world)
+                t = la.BY_NAME[f]
+                engine = ("dense-mfma" if t in (la.F32, la.F16) else
+                          la.gemm_engine(f, M, gN, K, 1, stationary=True) if t in (la.Q4_0, la.Q4_1, la.Q5_0) else
+                          "i8" if t in (la.Q5_1, la.Q8_0, la.Q2_K) else "kq-i8")
+                sw[f].update({"gemm_GFLOPS": round(2.0 * M * gN * K / gk / 1e9, 1), "gemm_us": round(gk * 1e6, 2),
+                              "gemm_engine": engine})
         out["sweep"] = sw
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.fmt, M, 1, K, args.cpu_budget, unit)

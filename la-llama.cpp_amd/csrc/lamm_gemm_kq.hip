@@ -1,0 +1,274 @@
+// lamm_gemm_kq.hip -- prefill GEMM (N > 8) for the §8f k-quant weights q4_K / q5_K / q6_K
+// against q8_K activations (vec_dot LC/ggml-quants.c:7301-7358 q4_K, :7968-8029 q5_K,
+// :8695-8738 q6_K).  Without it these shapes ran as N/8 grouped GEMV launches (~30x slower).
+//
+// Per 256-element super-block the reference computes exact integer sub-block dots, scales
+// them by the INTEGER 6-bit (q4_K/q5_K) or int8 (q6_K) sub-block scales, and applies the fp16
+// super-block scale(s) once:
+//   q4_K/q5_K:  d_b * ( d_a * sum_e sc(e) q(e) b(e)  -  dmin_a * sum_s m_s * bsum_s )
+//   q6_K:       d_b *   d_a * sum_e sc(e) (q(e) - 32) b(e)
+// Folding the integer scale into the weight operand makes the whole super-block ONE exact
+// integer dot: A'(e) = sc(e) * q(e) (<= 1953) or sc(e) * (q(e) - 32) (|.| <= 4096).  A' does
+// not fit int8, so it is split exactly as A' = 128 * hi + lo, lo = A' & 127 in [0, 127],
+// hi = A' >> 7 in [-32, 31]: two chains of 8 v_mfma_i32_32x32x32_i8 (K = 32 each) per 32x32
+// tile and super-block give S = 128 * S_hi + S_lo bit-exactly (|S| < 2^28).  The min term is
+// one v_mfma_f32_32x32x16_f16 over the 16 q8_K bsums (|bsum| <= 2048 and m <= 63: exact in
+// fp16, products and sums exact in fp32).  Only the final fp32 scaling differs in rounding
+// order from the reference (d_b is f32, d_a / dmin fp16).
+//
+// Structure (like the q2_K kernel in lamm_gemm.hip): 256 threads = 4 waves as 2 (j) x 2 (i),
+// tile 128 (j) x 64 (i), one super-block per step: raw A rows and raw q8_K rows are staged
+// into LDS with dword loads, unpacked once per step into int8 planes (A lo / hi, B quants),
+// then each wave runs its 2 tiles' MFMA chains.
+#include "lamm_device.h"
+#include "lamm_kernels.h"
+
+namespace lamm {
+namespace {
+
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+
+constexpr int KQ_T = 256;              // threads
+constexpr int KQ_TI = 64, KQ_TJ = 128;
+constexpr int KQ_ROWB = 256 + 16;      // int8 plane row pitch: conflict-free b128 reads
+
+template <int T> struct KQ;
+template <> struct KQ<kQ4_K> { static constexpr int ABPB = 144; static constexpr bool MIN = true; };
+template <> struct KQ<kQ5_K> { static constexpr int ABPB = 176; static constexpr bool MIN = true; };
+template <> struct KQ<kQ6_K> { static constexpr int ABPB = 210; static constexpr bool MIN = false; };
+
+template <int T>
+struct KQSmem {
+  static constexpr int RAWW = KQ<T>::ABPB / 4 + 1;           // dwords per staged A row (+1: q6_K is 2-aligned)
+  uint32_t rawA[((KQ_TI * RAWW + KQ_T - 1) / KQ_T) * KQ_T];
+  uint32_t rawB[((KQ_TJ * 73 + KQ_T - 1) / KQ_T) * KQ_T];  // q8_K: f32 d | 256 x i8 | 16 x i16 = 73 dwords
+  uint32_t wlo[KQ_TI * KQ_ROWB / 4];
+  uint32_t whi[KQ_TI * KQ_ROWB / 4];
+  uint32_t act[KQ_TJ * KQ_ROWB / 4];
+  float da[KQ_TI], dmn[KQ_TI], yd[KQ_TJ];
+  _Float16 mn[KQ_TI][16];   // m of the 32-sub-block each 16-element bsum belongs to
+  _Float16 bs[KQ_TJ][16];
+};
+
+// scales / mins of sub-block j (0..7) from the 12 packed bytes (LC/ggml-quants.c
+// get_scale_min_k4, as the utmp shuffle of the vec_dot)
+__device__ __forceinline__ void kq_sm(const uint32_t (&u)[3], int j, int& sc, int& m) {
+  auto byte = [&](int b) { return (int)((u[b >> 2] >> (8 * (b & 3))) & 0xffu); };
+  if (j < 4) {
+    sc = byte(j) & 63;
+    m = byte(j + 4) & 63;
+  } else {
+    sc = (byte(j + 4) & 0xF) | ((byte(j - 4) >> 6) << 4);
+    m = (byte(j + 4) >> 4) | ((byte(j) >> 6) << 4);
+  }
+}
+
+template <int T>
+__global__ __launch_bounds__(KQ_T) void gemm_kq_kernel(GemvArgs p) {
+  using F = KQ<T>;
+  using S = KQSmem<T>;
+  constexpr int ABPB = F::ABPB, RAWW = S::RAWW;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  S& sm = *reinterpret_cast<S*>(smem_raw);
+
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int lr = lane & 31, h = lane >> 5;
+  const int wj = w >> 1, wi = w & 1;
+  const int64_t i0 = (int64_t)blockIdx.x * KQ_TI, j0 = (int64_t)blockIdx.y * KQ_TJ;
+  const int z = blockIdx.z, i12 = z % p.ne12, i13 = z / p.ne12;
+  const unsigned char* Az = p.A + (int64_t)(i12 / p.r2) * p.sa2 + (int64_t)(i13 / p.r3) * p.sa3;
+  const unsigned char* Bz = p.B + (int64_t)i12 * p.sb2 + (int64_t)i13 * p.sb3;
+  float* Cz = p.C + (int64_t)i12 * p.sc2 + (int64_t)i13 * p.sc3;
+  const int rowsA = (int)min((int64_t)KQ_TI, (int64_t)p.M - i0);
+  const int rowsB = (int)min((int64_t)KQ_TJ, (int64_t)p.N - j0);
+
+  f32x16 acc[2];
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[r][e] = 0.f;
+
+  for (int sb = 0; sb < p.nblk; ++sb) {
+    // ---- stage raw A (row r: dwords from the 4-aligned address at or below its block) and B
+    const int ash = (sb * ABPB) & 3;   // lda is a multiple of 16: same shift for every row
+    {
+      const unsigned char* abase = Az + i0 * p.lda + (((int64_t)sb * ABPB) & ~int64_t(3));
+      const int64_t avail = (int64_t)(rowsA - 1) * p.lda + (int64_t)p.nblk * ABPB - (((int64_t)sb * ABPB) & ~int64_t(3));
+      const auto ra = make_rsrc(abase, (uint32_t)min((avail + 3) & ~int64_t(3), (int64_t)0x7fffffff));
+      const unsigned char* bbase = Bz + j0 * p.ldb + (int64_t)sb * 292;
+      const int64_t bavail = (int64_t)(rowsB - 1) * p.ldb + (int64_t)(p.nblk - sb) * 292;
+      const auto rb = make_rsrc(bbase, (uint32_t)min((bavail + 3) & ~int64_t(3), (int64_t)0x7fffffff));
+      constexpr int NA = sizeof(sm.rawA) / 4 / KQ_T, NB = sizeof(sm.rawB) / 4 / KQ_T;
+      uint32_t va[NA], vb[NB];
+#pragma unroll
+      for (int k = 0; k < NA; ++k) {
+        const int dw = t + k * KQ_T, rr = dw / RAWW, oo = dw % RAWW;
+        const uint32_t off = (dw < KQ_TI * RAWW && rr < rowsA) ? (uint32_t)(rr * p.lda + 4 * oo) : 0x7ffffff0u;
+        va[k] = bload4(ra, off);
+      }
+#pragma unroll
+      for (int k = 0; k < NB; ++k) {
+        const int dw = t + k * KQ_T, rr = dw / 73, oo = dw % 73;
+        const uint32_t off = (dw < KQ_TJ * 73 && rr < rowsB) ? (uint32_t)(rr * p.ldb + 4 * oo) : 0x7ffffff0u;
+        vb[k] = bload4(rb, off);
+      }
+#pragma unroll
+      for (int k = 0; k < NA; ++k) sm.rawA[t + k * KQ_T] = va[k];
+#pragma unroll
+      for (int k = 0; k < NB; ++k) sm.rawB[t + k * KQ_T] = vb[k];
+    }
+    __syncthreads();
+
+    // ---- unpack A: 64 rows x 16 groups of 16 elements; A' = sc * q split into lo / hi ----
+    for (int it = t; it < KQ_TI * 16; it += KQ_T) {
+      const int il = it / 16, g = it % 16;
+      const uint32_t* row = &sm.rawA[il * RAWW];
+      auto rd8 = [&](int b) { const int o = b + ash; return (int)((row[o >> 2] >> (8 * (o & 3))) & 0xffu); };
+      int aval[16];
+      if constexpr (T == kQ6_K) {
+        const int sc = (int)(int8_t)rd8(192 + g);
+        const int hf = g / 8, part = (g % 8) / 2, l0 = (g % 2) * 16;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          const int l = l0 + k;
+          const int nib = (part & 1) ? rd8(64 * hf + 32 + l) : rd8(64 * hf + l);
+          const int q = (part < 2 ? (nib & 0xF) : (nib >> 4)) | (((rd8(128 + 32 * hf + l) >> (2 * part)) & 3) << 4);
+          aval[k] = sc * (q - 32);
+        }
+      } else {
+        uint32_t u[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) u[k] = (uint32_t)rd8(4 + 4 * k) | ((uint32_t)rd8(5 + 4 * k) << 8) |
+                                           ((uint32_t)rd8(6 + 4 * k) << 16) | ((uint32_t)rd8(7 + 4 * k) << 24);
+        int sc, m;
+        kq_sm(u, g / 2, sc, m);
+        const int e0 = 16 * g, G = e0 / 64, hi = (e0 % 64) >= 32, l0 = e0 % 32;
+        constexpr int QS = T == kQ5_K ? 48 : 16;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          const int l = l0 + k;
+          const int b = rd8(QS + 32 * G + l);
+          int q = hi ? (b >> 4) : (b & 0xF);
+          if constexpr (T == kQ5_K) q += ((rd8(16 + l) >> (e0 / 32)) & 1) << 4;
+          aval[k] = sc * q;
+        }
+        if (il < rowsA) sm.mn[il][g] = (_Float16)(float)m;
+        else sm.mn[il][g] = (_Float16)0.f;
+      }
+      uint32_t lo[4], hi8[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        lo[k] = 0;
+        hi8[k] = 0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int a = aval[4 * k + c];
+          lo[k] |= (uint32_t)(a & 127) << (8 * c);
+          hi8[k] |= ((uint32_t)(a >> 7) & 0xffu) << (8 * c);
+        }
+      }
+      const bool ok = il < rowsA;
+      *(u32x4*)&sm.wlo[(il * KQ_ROWB + 16 * g) / 4] = ok ? u32x4{lo[0], lo[1], lo[2], lo[3]} : u32x4{0, 0, 0, 0};
+      *(u32x4*)&sm.whi[(il * KQ_ROWB + 16 * g) / 4] = ok ? u32x4{hi8[0], hi8[1], hi8[2], hi8[3]} : u32x4{0, 0, 0, 0};
+      if (g == 0) {
+        if constexpr (T == kQ6_K) {
+          sm.da[il] = ok ? h2f((uint32_t)rd8(208) | ((uint32_t)rd8(209) << 8)) : 0.f;
+          sm.dmn[il] = 0.f;
+        } else {
+          sm.da[il] = ok ? h2f((uint32_t)rd8(0) | ((uint32_t)rd8(1) << 8)) : 0.f;
+          sm.dmn[il] = ok ? h2f((uint32_t)rd8(2) | ((uint32_t)rd8(3) << 8)) : 0.f;
+        }
+      }
+    }
+    // ---- unpack B: 128 rows x 16 pieces of 16 quants; bsums to fp16 (exact), d_b f32 ----
+    for (int it = t; it < KQ_TJ * 16; it += KQ_T) {
+      const int jl = it / 16, q16 = it % 16;
+      const uint32_t* blk = &sm.rawB[jl * 73];
+      const bool ok = jl < rowsB;
+      *(u32x4*)&sm.act[(jl * KQ_ROWB + 16 * q16) / 4] =
+          ok ? u32x4{blk[1 + 4 * q16], blk[2 + 4 * q16], blk[3 + 4 * q16], blk[4 + 4 * q16]} : u32x4{0, 0, 0, 0};
+      if constexpr (F::MIN) {
+        const uint32_t bw = blk[65 + (q16 >> 1)];
+        sm.bs[jl][q16] = ok ? (_Float16)(float)(int16_t)((q16 & 1) ? (bw >> 16) : (bw & 0xffff)) : (_Float16)0.f;
+      }
+      if (q16 == 0) sm.yd[jl] = ok ? __uint_as_float(blk[0]) : 0.f;
+    }
+    __syncthreads();
+
+    // ---- 2 x 8 chained i8 MFMAs per tile: S = 128 S_hi + S_lo; mins by one f16 MFMA ----
+    const int ia = 32 * wi + lr;
+    const float dai = sm.da[ia], dmi = sm.dmn[ia];
+    half8 mnf = {};
+    if constexpr (F::MIN) mnf = *(const half8*)&sm.mn[ia][8 * h];
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+      const int jb = 64 * wj + 32 * rt;
+      i32x16 slo = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, shi = slo;
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) {
+        const int o = (32 * kk + 16 * h) / 4;
+        const i32x4 af = *(const i32x4*)&sm.act[(jb + lr) * KQ_ROWB / 4 + o];
+        const i32x4 wl = *(const i32x4*)&sm.wlo[ia * KQ_ROWB / 4 + o];
+        const i32x4 wh = *(const i32x4*)&sm.whi[ia * KQ_ROWB / 4 + o];
+        slo = __builtin_amdgcn_mfma_i32_32x32x32_i8(af, wl, slo, 0, 0, 0);
+        shi = __builtin_amdgcn_mfma_i32_32x32x32_i8(af, wh, shi, 0, 0, 0);
+      }
+      f32x16 mins = {};
+      if constexpr (F::MIN) {
+        const half8 bsf = *(const half8*)&sm.bs[jb + lr][8 * h];
+        mins = __builtin_amdgcn_mfma_f32_32x32x16_f16(bsf, mnf, mins, 0, 0, 0);
+      }
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const f32x4 ydv = *(const f32x4*)&sm.yd[jb + 8 * g4 + 4 * h];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int r = 4 * g4 + e;
+          const float s = (float)(shi[r] * 128 + slo[r]);
+          if constexpr (F::MIN)
+            acc[rt][r] += (ydv[e] * dai) * s - (ydv[e] * dmi) * mins[r];
+          else
+            acc[rt][r] += (ydv[e] * dai) * s;
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  const int64_t i = i0 + 32 * wi + lr;
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int64_t j = j0 + 64 * wj + 32 * rt + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (i < p.M && j < p.N) Cz[j * p.ldc + i] = acc[rt][r];
+    }
+}
+
+template <int T>
+hipError_t launch_kq(const GemvArgs& p, hipStream_t s) {
+  const dim3 grid((unsigned)((p.M + KQ_TI - 1) / KQ_TI), (unsigned)((p.N + KQ_TJ - 1) / KQ_TJ),
+                  (unsigned)(p.ne12 * p.ne13));
+  constexpr size_t lds = sizeof(KQSmem<T>);
+  static_assert(lds <= 160 * 1024, "LDS");
+  (void)hipFuncSetAttribute((const void*)gemm_kq_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(gemm_kq_kernel<T>, grid, dim3(KQ_T), lds, s, p);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+bool gemm_kq_supported(int type) { return type == kQ4_K || type == kQ5_K || type == kQ6_K; }
+
+hipError_t launch_gemm_kq(int type, const GemvArgs& p, hipStream_t s) {
+  if (p.M == 0 || p.N == 0) return hipSuccess;
+  if ((p.ldb & 3) || ((uintptr_t)p.B & 3) || (p.sb2 & 3) || (p.sb3 & 3)) return hipErrorInvalidValue;
+  switch (type) {
+    case kQ4_K: return launch_kq<kQ4_K>(p, s);
+    case kQ5_K: return launch_kq<kQ5_K>(p, s);
+    case kQ6_K: return launch_kq<kQ6_K>(p, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace lamm

@@ -191,6 +191,9 @@ int matmul_impl(const lamm_matrix* A, const lamm_matrix* B, const lamm_matrix* C
     e = launch_gemv(A->type, p, s);
   } else if (gemm_dense_supported(A->type) && !getenv_flag0("LAMM_DENSE_GEMM")) {
     e = launch_gemm_dense(A->type, p, s);
+  } else if (gemm_kq_supported(A->type) && !getenv_flag0("LAMM_KQ_GEMM") && (ldb & 3) == 0 &&
+             ((uintptr_t)B->data & 3) == 0 && (bt.nbb2 & 3) == 0 && (bt.nbb3 & 3) == 0) {
+    e = launch_gemm_kq(A->type, p, s);
   } else if (gemm_fp6_supported(A->type) && gemm_path(p, W && W->packed) == 0) {
     const void* prepA = W ? W->packed : nullptr;
     const size_t wsb = gemm_fp6_workspace_bytes(A->type, p, prepA != nullptr);

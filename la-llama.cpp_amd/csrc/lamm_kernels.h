@@ -23,6 +23,9 @@ struct GemvArgs {
 hipError_t launch_gemv(int type, const GemvArgs& p, hipStream_t s);
 size_t gemv_lds_bytes(int type, int nc);
 hipError_t launch_gemv_dense(int type, const GemvArgs& p, hipStream_t s);   // F32 / F16 rows
+// q4_K / q5_K / q6_K prefill GEMM (lamm_gemm_kq.hip); B rows (q8_K) 4-byte aligned
+hipError_t launch_gemm_kq(int type, const GemvArgs& p, hipStream_t s);
+bool gemm_kq_supported(int type);
 // F32 / F16 prefill GEMM on the matrix cores (lamm_gemm_dense.hip)
 hipError_t launch_gemm_dense(int type, const GemvArgs& p, hipStream_t s);
 bool gemm_dense_supported(int type);

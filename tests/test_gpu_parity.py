@@ -142,6 +142,66 @@ def test_kquants_random_bytes_vs_oracle(t, shape):
     assert err < TOL, err
 
 
+KQG_SHAPES = [(130, 129, 2048), (64, 300, 256), (257, 40, 1024), (9, 9, 512)]
+
+
+@pytest.mark.parametrize("t", ol.KQ_TYPES, ids=[ol.NAMES[t] for t in ol.KQ_TYPES])
+@pytest.mark.parametrize("shape", KQG_SHAPES, ids=[f"{m}x{n}x{k}" for m, n, k in KQG_SHAPES])
+def test_kquant_gemm_vs_oracle(t, shape, monkeypatch):
+    """The k-quant prefill GEMM (lamm_gemm_kq.hip: integer sub-block scales folded into the
+    weight operand, split exactly into two int8 planes): ragged M / N against its 64 x 128
+    tile, several super-blocks, row pitch padding; the grouped GEMV (LAMM_KQ_GEMM=0) must
+    agree within the same tolerance."""
+    M, N, K = shape
+    rng = np.random.default_rng(M * 13 + N * 5 + K + t)
+    A_q = ol.random_kq_blocks(t, M, K, rng)
+    B_q = ORACLE.quantize(ol.Q8_K, rng.standard_normal((N, K), dtype=np.float32))
+    ref = ORACLE.mul_mat(t, M, N, K, A_q, B_q)
+    den = absdot(t, A_q, B_q, M, N, K)
+    kb = K // 256
+    c, raw = gpu_mul_mat(t, A_q, B_q, M, N, K, lda=pitch_blocks(t, kb + 1), ldc=M + 5)
+    assert rel_err(c, ref, den).max() < TOL
+    assert np.isnan(np.concatenate([raw[j * (M + 5) + M:(j + 1) * (M + 5)] for j in range(N)])).all()
+    monkeypatch.setenv("LAMM_KQ_GEMM", "0")
+    c2, _ = gpu_mul_mat(t, A_q, B_q, M, N, K)
+    assert rel_err(c2, ref, den).max() < TOL
+
+
+@pytest.mark.parametrize("t", ol.KQ_TYPES, ids=[ol.NAMES[t] for t in ol.KQ_TYPES])
+def test_kquant_gemm_extremes_and_broadcast(t):
+    """Extreme operands: every weight byte 0xFF / 0x00 patterns with the largest scales
+    (q6_K: sc = -128, q - 32 = -32 -> A' = 4096, the top of the hi/lo split) against q8_K
+    quants of +-127, and a ggml broadcast (2 weight slices over 4 activation slices)."""
+    M, N, K = 70, 33, 512
+    bpb = {ol.Q4_K: 144, ol.Q5_K: 176, ol.Q6_K: 210}[t]
+    rng = np.random.default_rng(t)
+    As = []
+    for s in range(2):
+        blk = np.full((M * K // 256, bpb), 0xFF if s == 0 else 0x00, np.uint8)
+        if t == ol.Q6_K:
+            blk[:, 192:208] = 0x80                       # int8 scale -128
+        for off in ol.FP16_FIELDS[t]:
+            blk[:, off:off + 2] = np.array([0.01], np.float16).view(np.uint8)
+        As.append(blk.reshape(-1))
+    x = np.where(rng.random((4 * N, K)) < 0.5, -1.0, 1.0).astype(np.float32)
+    Bs = [ORACLE.quantize(ol.Q8_K, x[s * N:(s + 1) * N]) for s in range(4)]
+    kb = K // 256
+    lda = pitch_blocks(t, kb)
+    abytes = M * lda * bpb
+    A = dev_bytes(np.concatenate([pitched_A(t, a, M, kb, lda)[:abytes] for a in As] + [np.zeros(64, np.uint8)]))
+    bbytes = N * kb * 292
+    B = dev_bytes(np.concatenate(Bs))
+    C = torch.full((4 * N * M,), float("nan"), dtype=torch.float32, device="cuda")
+    bt = la.Batch(2, 1, 4, 1, abytes, 2 * abytes, bbytes, 4 * bbytes, 4 * M * N, 4 * M * N * 4)
+    la.mul_mat_torch(t, A, B, C, M, N, K, lda=lda, batch=bt)
+    torch.cuda.synchronize()
+    c = C.cpu().numpy().reshape(4, N, M)
+    for z in range(4):
+        a = As[z // 2]
+        ref = ORACLE.mul_mat(t, M, N, K, a, Bs[z])
+        assert rel_err(c[z], ref, absdot(t, a, Bs[z], M, N, K)).max() < TOL, z
+
+
 FP6_TYPES = [ol.Q4_0, ol.Q4_1, ol.Q5_0]
 GEMM_SHAPES = [(33, 17, 1024), (130, 9, 8192 + 512), (257, 129, 4096 + 64), (300, 40, 96)]
 

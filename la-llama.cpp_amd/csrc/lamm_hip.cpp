@@ -193,7 +193,11 @@ int matmul_impl(const lamm_matrix* A, const lamm_matrix* B, const lamm_matrix* C
     e = launch_gemm_dense(A->type, p, s);
   } else if (gemm_kq_supported(A->type) && !getenv_flag0("LAMM_KQ_GEMM") && (ldb & 3) == 0 &&
              ((uintptr_t)B->data & 3) == 0 && (bt.nbb2 & 3) == 0 && (bt.nbb3 & 3) == 0) {
-    e = launch_gemm_kq(A->type, p, s);
+    const void* prepA = W ? W->packed : nullptr;
+    const size_t wsb = gemm_kq_workspace_bytes(A->type, p, prepA != nullptr);
+    void* ws = workspace(wsb, s);
+    if (!ws) return fail(LAMM_ERR_HIP, "workspace allocation of %zu bytes failed", wsb);
+    e = launch_gemm_kq(A->type, p, prepA, ws, s);
   } else if (gemm_fp6_supported(A->type) && gemm_path(p, W && W->packed) == 0) {
     const void* prepA = W ? W->packed : nullptr;
     const size_t wsb = gemm_fp6_workspace_bytes(A->type, p, prepA != nullptr);
@@ -238,14 +242,17 @@ extern "C" int lamm_hip_weights_create(const lamm_matrix* A, int64_t ne02, int64
     return fail(LAMM_ERR_ALIGN, "A must be 16-byte aligned with 16-byte row/slice pitches");
   if (probe().count == 0) return fail(LAMM_ERR_NODEV, "no gfx950 device");
   auto* W = new lamm_weights{*A, ne02, ne03, nba2, nba3};
-  if (gemm_fp6_supported(A->type) && A->row > 0 && A->col > 0) {
+  const bool fp6 = gemm_fp6_supported(A->type), kq = gemm_kq_supported(A->type);
+  if ((fp6 || kq) && A->row > 0 && A->col > 0) {
     const GemvArgs p = weight_args(A, ne02, ne03, nba2, nba3);
-    W->packed_bytes = gemm_fp6_weight_bytes(A->type, p);
+    W->packed_bytes = fp6 ? gemm_fp6_weight_bytes(A->type, p) : gemm_kq_weight_bytes(A->type, p);
     if (hipMalloc(&W->packed, W->packed_bytes) != hipSuccess) {
+      const size_t nb = W->packed_bytes;
       delete W;
-      return fail(LAMM_ERR_HIP, "hipMalloc of %zu packed weight bytes failed", W->packed_bytes);
+      return fail(LAMM_ERR_HIP, "hipMalloc of %zu packed weight bytes failed", nb);
     }
-    const hipError_t e = prepare_fp6_weights(A->type, p, W->packed, static_cast<hipStream_t>(hip_stream));
+    const hipError_t e = fp6 ? prepare_fp6_weights(A->type, p, W->packed, static_cast<hipStream_t>(hip_stream))
+                             : prepare_kq_weights(A->type, p, W->packed, static_cast<hipStream_t>(hip_stream));
     if (e != hipSuccess) {
       (void)hipFree(W->packed);
       delete W;
@@ -595,7 +602,8 @@ extern "C" void lamm_mul_mat(const struct ggml_compute_params* vparams, struct g
   pa.ne13 = (int)ne13;
   pa.r2 = (int)(ne12 / ne02);
   pa.r3 = (int)(ne13 / ne03);
-  const bool stationary = N > 8 && gemm_fp6_supported(t0) && gemm_path(pa, true) == 0;
+  const bool stationary = N > 8 && ((gemm_fp6_supported(t0) && gemm_path(pa, true) == 0) ||
+                                    (gemm_kq_supported(t0) && !getenv_flag0("LAMM_KQ_GEMM")));
   const int rc = stationary ? lamm_hip_matmul_weights(rt.prepared(w, A, ne02, ne03), &B, &C, &bt, s)
                             : lamm_hip_matmul_batched(&A, &B, &C, &bt, s);
   if (rc != LAMM_OK) {

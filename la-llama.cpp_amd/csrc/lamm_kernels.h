@@ -24,8 +24,11 @@ hipError_t launch_gemv(int type, const GemvArgs& p, hipStream_t s);
 size_t gemv_lds_bytes(int type, int nc);
 hipError_t launch_gemv_dense(int type, const GemvArgs& p, hipStream_t s);   // F32 / F16 rows
 // q4_K / q5_K / q6_K prefill GEMM (lamm_gemm_kq.hip); B rows (q8_K) 4-byte aligned
-hipError_t launch_gemm_kq(int type, const GemvArgs& p, hipStream_t s);
+hipError_t launch_gemm_kq(int type, const GemvArgs& p, const void* prepA, void* workspace, hipStream_t s);
 bool gemm_kq_supported(int type);
+size_t gemm_kq_workspace_bytes(int type, const GemvArgs& p, bool prepared);
+size_t gemm_kq_weight_bytes(int type, const GemvArgs& p);
+hipError_t prepare_kq_weights(int type, const GemvArgs& p, void* wsA, hipStream_t s);
 // F32 / F16 prefill GEMM on the matrix cores (lamm_gemm_dense.hip)
 hipError_t launch_gemm_dense(int type, const GemvArgs& p, hipStream_t s);
 bool gemm_dense_supported(int type);

@@ -23,14 +23,14 @@ BY_NAME = {v: k for k, v in NAMES.items()}
 A_TYPES = [F32, Q4_0, Q4_1, Q5_0, Q5_1, Q8_0, Q2_K, F16]   # quantizers restated (F16: §8f)
 KQ_TYPES = [Q4_K, Q5_K, Q6_K]                        # vec_dot only, no quantizer
 # byte offsets of the fp16 scale fields of a block (random-byte test inputs keep them finite)
-FP16_FIELDS = {Q4_K: [0, 2], Q5_K: [0, 2], Q6_K: [208]}
+FP16_FIELDS = {Q4_K: [0, 2], Q5_K: [0, 2], Q6_K: [208], Q2_K: [80, 82]}
 
 
 def random_kq_blocks(t, rows, k, rng):
     """Random bytes for `rows` x `k` elements of k-quant type t, with finite positive fp16
     scales (vec_dot is defined for every byte pattern; this is how the GPU tests feed the
     formats the oracle has no quantizer for)."""
-    bpb = {Q4_K: 144, Q5_K: 176, Q6_K: 210}[t]
+    bpb = {Q4_K: 144, Q5_K: 176, Q6_K: 210, Q2_K: 84}[t]
     nb = rows * (k // 256)
     blk = rng.integers(0, 256, size=(nb, bpb), dtype=np.uint8)
     for off in FP16_FIELDS[t]:

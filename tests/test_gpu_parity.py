@@ -143,9 +143,10 @@ def test_kquants_random_bytes_vs_oracle(t, shape):
 
 
 KQG_SHAPES = [(130, 129, 2048), (64, 300, 256), (257, 40, 1024), (9, 9, 512)]
+KQG_TYPES = ol.KQ_TYPES + [ol.Q2_K]   # q2_K shares the super-block GEMM engine
 
 
-@pytest.mark.parametrize("t", ol.KQ_TYPES, ids=[ol.NAMES[t] for t in ol.KQ_TYPES])
+@pytest.mark.parametrize("t", KQG_TYPES, ids=[ol.NAMES[t] for t in KQG_TYPES])
 @pytest.mark.parametrize("shape", KQG_SHAPES, ids=[f"{m}x{n}x{k}" for m, n, k in KQG_SHAPES])
 def test_kquant_gemm_vs_oracle(t, shape, monkeypatch):
     """The k-quant prefill GEMM (lamm_gemm_kq.hip: integer sub-block scales folded into the
@@ -167,13 +168,41 @@ def test_kquant_gemm_vs_oracle(t, shape, monkeypatch):
     assert rel_err(c2, ref, den).max() < TOL
 
 
-@pytest.mark.parametrize("t", ol.KQ_TYPES, ids=[ol.NAMES[t] for t in ol.KQ_TYPES])
+@pytest.mark.parametrize("variant", ["0", "1"], ids=["dma", "simple"])
+@pytest.mark.parametrize("t", KQG_TYPES, ids=[ol.NAMES[t] for t in KQG_TYPES])
+def test_kquant_gemm_variants_and_stationary(t, variant, monkeypatch):
+    """Both k-quant GEMM kernels (LAMM_KQ_VARIANT) and the weight-stationary handle (packed
+    planes made once) against the oracle; the handle's bytes equal the per-call path's."""
+    monkeypatch.setenv("LAMM_KQ_VARIANT", variant)
+    M, N, K = 200, 150, 1536
+    rng = np.random.default_rng(t * 3 + int(variant))
+    A_q = ol.random_kq_blocks(t, M, K, rng)
+    B_q = ORACLE.quantize(ol.Q8_K, rng.standard_normal((N, K), dtype=np.float32))
+    ref = ORACLE.mul_mat(t, M, N, K, A_q, B_q)
+    c, _ = gpu_mul_mat(t, A_q, B_q, M, N, K)
+    assert rel_err(c, ref, absdot(t, A_q, B_q, M, N, K)).max() < TOL
+    kb = K // 256
+    lda = pitch_blocks(t, kb)
+    A = dev_bytes(np.concatenate([pitched_A(t, A_q, M, kb, lda), np.zeros(64, np.uint8)]))
+    B = dev_bytes(B_q)
+    W = la.Weights(t, A, M, K, lda=lda)
+    assert W.packed_bytes > 0
+    C0 = torch.full((N * M,), float("nan"), dtype=torch.float32, device="cuda")
+    C1 = torch.full_like(C0, float("nan"))
+    la.mul_mat_torch(t, A, B, C0, M, N, K, lda=lda)
+    W.matmul_torch(B, C1, N)
+    torch.cuda.synchronize()
+    assert torch.equal(C0, C1)
+    W.close()
+
+
+@pytest.mark.parametrize("t", KQG_TYPES, ids=[ol.NAMES[t] for t in KQG_TYPES])
 def test_kquant_gemm_extremes_and_broadcast(t):
     """Extreme operands: every weight byte 0xFF / 0x00 patterns with the largest scales
     (q6_K: sc = -128, q - 32 = -32 -> A' = 4096, the top of the hi/lo split) against q8_K
     quants of +-127, and a ggml broadcast (2 weight slices over 4 activation slices)."""
     M, N, K = 70, 33, 512
-    bpb = {ol.Q4_K: 144, ol.Q5_K: 176, ol.Q6_K: 210}[t]
+    bpb = {ol.Q4_K: 144, ol.Q5_K: 176, ol.Q6_K: 210, ol.Q2_K: 84}[t]
     rng = np.random.default_rng(t)
     As = []
     for s in range(2):

@@ -272,7 +272,9 @@ def main():
                      "traffic": traffic.get("bytes_per_launch") if traffic and traffic.get(
                          "algorithmic_bytes_per_launch") == launch_bytes else None,
                      "traffic_source": "profiles/traffic_%s_gemv.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE)" % args.fmt,
-                     "kernel": "lamm::gemv_stream_kernel (csrc/lamm_gemv.hip)", "per_launch_us": round(kern * 1e6, 3),
+                     "kernel": ("lamm::gemv_stream_dma_kernel" if args.fmt in ("q4_0", "q4_k") else
+                                "lamm::gemv_stream_kernel") + " (csrc/lamm_gemv.hip)",
+                     "per_launch_us": round(kern * 1e6, 3),
                      "algorithmic_bytes_per_launch": launch_bytes},
     }
     if not args.no_gemm:

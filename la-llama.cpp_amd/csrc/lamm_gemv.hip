@@ -607,6 +607,154 @@ __global__ __launch_bounds__(64 * WAVES) void gemv_stream_kernel(GemvArgs p) {
   }
 }
 
+// ---- LDS-DMA variant of the streaming kernel (A/B: LAMM_GEMV_VARIANT=8 / 9) ----------------
+// Group bytes go HBM -> LDS directly (buffer_load ... lds, non-temporal), NS slots per wave, NS-1
+// groups in flight; no VGPR landing zone and no ds_write pass.  A wave reads only the slots its
+// own DMAs filled, so its counted vmcnt is the only ordering needed (no barrier in the loop).
+template <int T, int NC, int WAVES, int NS>
+struct SmemStreamD {
+  using GG = Geo<T>;
+  uint32_t a[WAVES][NS][WGeo<T>::SLOT / 4];
+  uint32_t bq[NC][GG::BQ_WORDS];
+  float bd[NC][(T == kF32 || T == kF16) ? 1 : GG::VBLK];
+  float bx[NC][(T == kF32 || T == kF16) ? 1 : GG::VBLK];
+  int bs[NC][Fmt<T>::VQK == 256 ? GG::VBLK * 16 : 1];
+};
+
+template <int N_>
+__device__ __forceinline__ void gv_wait_vm() {   // s_waitcnt vmcnt(N) (lgkmcnt untouched)
+  static_assert(N_ >= 0 && N_ < 64, "vmcnt");
+  __builtin_amdgcn_s_waitcnt((N_ & 0xF) | ((N_ >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+  asm volatile("" ::: "memory");
+}
+
+template <int T, int NC, int WAVES, int NS>
+__global__ __launch_bounds__(64 * WAVES) void gemv_stream_dma_kernel(GemvArgs p) {
+  using GG = Geo<T>;
+  using WG = WGeo<T>;
+  using F = Fmt<T>;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  SmemStreamD<T, NC, WAVES, NS>& sm = *reinterpret_cast<SmemStreamD<T, NC, WAVES, NS>*>(smem_raw);
+  static_assert(WG::NPW * (NS - 1) < 64, "vmcnt range");
+
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int row = lane / kSC, ch = lane % kSC;
+  const int z = blockIdx.y, i12 = z % p.ne12, i13 = z / p.ne12;
+  const unsigned char* Az = p.A + (int64_t)(i12 / p.r2) * p.sa2 + (int64_t)(i13 / p.r3) * p.sa3;
+  const unsigned char* Bz = p.B + (int64_t)i12 * p.sb2 + (int64_t)i13 * p.sb3;
+  float* Cz = p.C + (int64_t)i12 * p.sc2 + (int64_t)i13 * p.sc3;
+  const int ngroups = (p.M + kWRows - 1) / kWRows;
+  const int row_bytes = p.nblk * F::BPB;
+  const int ncols = p.N < NC ? p.N : NC;
+  const int stride = gridDim.x * WAVES;
+
+  auto issue = [&](int q, int slot) {
+    const int64_t r0 = (int64_t)q * kWRows;
+    const int rows = (int)min((int64_t)kWRows, (int64_t)p.M - r0);
+    const int64_t avail = (int64_t)(rows - 1) * p.lda + row_bytes;
+    const auto ra = make_rsrc(Az + r0 * p.lda, (uint32_t)min((avail + 3) & ~int64_t(3), (int64_t)0x7fffffff));
+#pragma unroll
+    for (int k = 0; k < WG::NPW; ++k) {
+      const int pc = lane + 64 * k;
+      const int rr = pc / (GG::ROW_BYTES / 16), oo = pc % (GG::ROW_BYTES / 16);
+      const uint32_t off = (pc * 16 < WG::BYTES && rr < rows) ? (uint32_t)(rr * p.lda + 16 * oo) : 0x7ffffff0u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          ra, (__attribute__((address_space(3))) void*)&sm.a[w][slot][4 * 64 * k], 16, off, 0, 0, 2);
+    }
+  };
+
+  const int q0 = blockIdx.x * WAVES + w;
+#pragma unroll
+  for (int k = 0; k < NS - 1; ++k)
+    if (q0 + k * stride < ngroups) issue(q0 + k * stride, k);
+  stage_b<T, NC>(sm, p, Bz, 0);
+  __syncthreads();   // B visible to every wave
+
+  int it = 0;
+  for (int q = q0; q < ngroups; q += stride, ++it) {
+    const int slot = it % NS;
+    {   // refill the slot consumed one iteration ago (its LDS reads retired: lgkmcnt(0))
+      const int qn = q + (NS - 1) * stride;
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      if (qn < ngroups) issue(qn, (it + NS - 1) % NS);
+    }
+    // groups issued after q that are still allowed in flight
+    const int after = min(NS - 1, (ngroups - 1 - q) / stride);
+    if constexpr (NS >= 4) {
+      if (after >= 3) gv_wait_vm<3 * WG::NPW>();
+      else if (after == 2) gv_wait_vm<2 * WG::NPW>();
+      else if (after == 1) gv_wait_vm<WG::NPW>();
+      else gv_wait_vm<0>();
+    } else if constexpr (NS == 3) {
+      if (after >= 2) gv_wait_vm<2 * WG::NPW>();
+      else if (after == 1) gv_wait_vm<WG::NPW>();
+      else gv_wait_vm<0>();
+    } else {
+      if (after >= 1) gv_wait_vm<WG::NPW>();
+      else gv_wait_vm<0>();
+    }
+
+    const int64_t r0 = (int64_t)q * kWRows;
+    const int rows = (int)min((int64_t)kWRows, (int64_t)p.M - r0);
+    float acc[NC];
+#pragma unroll
+    for (int j = 0; j < NC; ++j) acc[j] = 0.f;
+    const int cb0 = ch * F::G;
+    if (row < rows && cb0 < p.nblk) {
+      uint32_t wv[GG::CH_WORDS + 1];
+      const int cbyte = row * GG::ROW_BYTES + ch * GG::CH_BYTES;
+      const uint32_t* src = &sm.a[w][slot][cbyte / 4];
+      if constexpr (GG::CH_BYTES % 4 != 0) {
+        const int sh = (cbyte & 3) * 8;
+#pragma unroll
+        for (int c = 0; c < GG::CH_WORDS; ++c) wv[c] = __builtin_amdgcn_alignbit(src[c + 1], src[c], sh);
+      } else if constexpr (GG::CH_BYTES % 16 == 0) {
+#pragma unroll
+        for (int c = 0; c < GG::CH_WORDS / 4; ++c) {
+          const u32x4 x = *(const u32x4*)&src[4 * c];
+          wv[4 * c] = x[0]; wv[4 * c + 1] = x[1]; wv[4 * c + 2] = x[2]; wv[4 * c + 3] = x[3];
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < GG::CH_WORDS; ++c) wv[c] = src[c];
+      }
+      wv[GG::CH_WORDS] = 0;
+      chunk_dot<T, NC, 0>(wv, sm, ch, min(F::G, p.nblk - cb0), ncols, acc);
+    }
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      float x = acc[j];
+      x += __shfl_xor(x, 8);
+      x += __shfl_xor(x, 4);
+      x += __shfl_xor(x, 2);
+      x += __shfl_xor(x, 1);
+      acc[j] = x;
+    }
+    if (ch == 0 && row < rows) {
+#pragma unroll
+      for (int j = 0; j < NC; ++j)
+        if (j < ncols) Cz[(int64_t)j * p.ldc + r0 + row] = acc[j];
+    }
+  }
+}
+
+template <int T, int NC, int WAVES, int NS>
+hipError_t launch_stream_dma(const GemvArgs& p, hipStream_t s) {
+  constexpr size_t lds = sizeof(SmemStreamD<T, NC, WAVES, NS>);
+  static_assert(lds <= 160 * 1024, "LDS");
+  const int ngroups = (p.M + kWRows - 1) / kWRows;
+  const int slices = p.ne12 * p.ne13;
+  const int per_cu = (int)((160 * 1024) / lds) < 1 ? 1 : (int)((160 * 1024) / lds);
+  int gx = (256 * per_cu) / slices;
+  const int gmax = (ngroups + WAVES - 1) / WAVES;
+  gx = gx < 1 ? 1 : (gx > gmax ? gmax : gx);
+  (void)hipFuncSetAttribute((const void*)gemv_stream_dma_kernel<T, NC, WAVES, NS>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL((gemv_stream_dma_kernel<T, NC, WAVES, NS>), dim3(gx, slices), dim3(64 * WAVES), lds, s, p);
+  return hipGetLastError();
+}
+
 template <int T, int NC, int WAVES>
 constexpr bool stream_fits() { return sizeof(SmemStream<T, NC, WAVES>) <= 160 * 1024; }
 
@@ -670,10 +818,18 @@ hipError_t launch_t(const GemvArgs& p, hipStream_t s) {
   // the 256-element super-block formats decode a whole super-block per lane: with more than
   // one activation column their stream kernel outgrows 256 VGPRs (spills), so only NC == 1
   // (the decode GEMV) streams; wider N takes the LDS-staged segment kernel
+  // single-column decode with a group small enough for 8 waves x 2 LDS slots (q4_0, q4_K):
+  // the LDS-DMA streaming kernel (+2 %, profiles/r01/ab_gemv.txt); q2_K's decode is heavier
+  // per byte and keeps the 16-wave VGPR-landing kernel (DMA -12 %).  LAMM_GEMV_VARIANT=10
+  // forces the VGPR-landing stream kernel for A/B
+  if constexpr (NC == 1 && T != kQ2_K && sizeof(SmemStreamD<T, NC, 8, 2>) <= 160 * 1024) {
+    if (p.nblk <= Geo<T>::SEG_BLK && v == 0) return launch_stream_dma<T, NC, 8, 2>(p, s);
+  }
   if constexpr (stream_fits<T, NC, 4>() && (Fmt<T>::VQK != 256 || NC == 1)) {
-    if (p.nblk <= Geo<T>::SEG_BLK && v == 0) return launch_stream<T, NC>(p, s);
+    if (p.nblk <= Geo<T>::SEG_BLK && (v == 0 || v == 10)) return launch_stream<T, NC>(p, s);
   }
   if constexpr (T == kQ4_0 && NC == 1) {
+    if (v == 8) return launch_stream_dma<T, NC, 4, 4>(p, s);   // A/B: LDS-DMA streaming, 4 waves x 4 slots
     switch (v) {
       case 1: return launch_v<T, NC, 1>(p, s);
       case 2: return launch_v<T, NC, 2>(p, s);

@@ -1,8 +1,7 @@
 #!/usr/bin/env python3
-"""Interleaved A/B timing of GEMV staging variants in ONE process (guide §5.4 rule 24).
-
-Each variant (LAMM_GEMV_VARIANT) runs the batched q4_0 GEMV (R slices > MALL) `iters`
-times per round; rounds interleave the variants.  Outputs must be bit-identical."""
+"""Interleaved A/B timing of GEMV kernel variants (LAMM_GEMV_VARIANT) on BASELINE config 2
+(q4_0 4096x4096, N=1, 33 slices per launch > MALL) in ONE process; checks every variant's C
+against variant 0 bit for bit.  Prints one JSON line (TB/s of algorithmic bytes)."""
 import json
 import os
 import sys
@@ -17,30 +16,29 @@ import bench  # noqa: E402
 
 
 def main():
-    variants = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "0,1,2,3").split(",")]
-    fmt, M, K, N = os.environ.get("FMT", "q4_0"), 4096, 4096, int(os.environ.get("NCOL", "1"))
+    variants = (sys.argv[1] if len(sys.argv) > 1 else "0,8,9").split(",")
+    fmt = os.environ.get("FMT", "q4_0")
+    M = K = 4096
     t = la.BY_NAME[fmt]
     vt = la.vec_dot_type(t)
-    unit = bench.gemv_bytes(la, fmt, M, K, N)
-    slices = max(8, -(-int(1.15 * bench.MALL_BYTES) // unit))
+    u = bench.gemv_bytes(la, fmt, M, K)
+    sl = max(8, -(-int(1.15 * bench.MALL_BYTES) // u))
     gen = torch.Generator(device="cuda")
-    gen.manual_seed(7)
-    A, arow = bench.make_weights(torch, la, fmt, slices, M, K, gen)
-    B = bench.make_activations(torch, la, fmt, slices * N, K, gen)
+    gen.manual_seed(3)
+    A, arow = bench.make_weights(torch, la, fmt, sl, M, K, gen)
+    B = bench.make_activations(torch, la, fmt, sl, K, gen)
     kb = K // la.blck_size(t)
     brow = la.row_bytes(vt, K)
-    outs = {}
-    res = {v: [] for v in variants}
+    C = torch.zeros(sl * M, dtype=torch.float32, device="cuda")
+    Am, Bm, Cm = la.Matrix(A.data_ptr(), t, M, kb, kb), la.Matrix(B.data_ptr(), vt, kb, 1, kb), \
+        la.Matrix(C.data_ptr(), la.F32, M, 1, M)
+    bt = la.Batch(sl, 1, sl, 1, M * arow, sl * M * arow, brow, sl * brow, 4 * M, 4 * M * sl)
     stream = torch.cuda.current_stream()
-    for rnd in range(6):
+    res = {v: [] for v in variants}
+    outs = {}
+    for rnd in range(7):
         for v in variants:
-            os.environ["LAMM_GEMV_VARIANT"] = str(v)
-            C = torch.zeros(slices * N * M, dtype=torch.float32, device="cuda")
-            Am = la.Matrix(A.data_ptr(), t, M, kb, kb)
-            Bm = la.Matrix(B.data_ptr(), vt, kb, N, kb)
-            Cm = la.Matrix(C.data_ptr(), la.F32, M, N, M)
-            bt = la.Batch(slices, 1, slices, 1, M * arow, slices * M * arow, N * brow, slices * N * brow,
-                          4 * M * N, 4 * M * N * slices)
+            os.environ["LAMM_GEMV_VARIANT"] = v
             for _ in range(3):
                 la.matmul_batched(Am, Bm, Cm, bt, stream.cuda_stream)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -49,18 +47,16 @@ def main():
                 la.matmul_batched(Am, Bm, Cm, bt, stream.cuda_stream)
             e1.record(stream)
             torch.cuda.synchronize()
-            us = e0.elapsed_time(e1) * 1e3 / 20
-            res[v].append(us)
+            res[v].append(e0.elapsed_time(e1) * 1e3 / 20)
             if rnd == 0:
-                outs[v] = C.cpu()
-    base = outs[variants[0]]
+                outs[v] = C.clone()
+    os.environ["LAMM_GEMV_VARIANT"] = "0"
     summary = {}
     for v in variants:
         med = sorted(res[v])[len(res[v]) // 2]
-        summary[v] = {"median_us": round(med, 2), "min_us": round(min(res[v]), 2),
-                      "GBs": round(slices * unit / (med * 1e-6) / 1e9, 1),
-                      "identical": bool(torch.equal(outs[v], base))}
-    print(json.dumps({"fmt": fmt, "N": N, "slices": slices, "variants": summary}))
+        summary[v] = {"median_us": round(med, 2), "TBs": round(sl * u / (med * 1e-6) / 1e12, 3),
+                      "equal_to_v0": bool(torch.equal(outs[v], outs[variants[0]]))}
+    print(json.dumps({"fmt": fmt, "slices": sl, "variants": summary}), flush=True)
 
 
 if __name__ == "__main__":

@@ -17,6 +17,8 @@
 // step's MFMAs) -> ds_write_b128, double-buffered LDS, one barrier per step.
 // Ragged M / N are zero-filled by the loads, ragged K masked per element (row padding may be
 // NaN), so every lane runs the same MFMA stream.
+#include <cstdlib>
+
 #include "lamm_device.h"
 #include "lamm_kernels.h"
 
@@ -51,7 +53,7 @@ __device__ __forceinline__ u32x4 mask_piece(u32x4 v, int nv) {
 
 // BAL: B rows 16-byte aligned (b128 loads); else dword (f32) / halfword (f16) loads
 template <int T, bool BAL>
-__global__ __launch_bounds__(DG_NT) void gemm_dense_kernel(GemvArgs p) {
+__global__ __launch_bounds__(DG_NT) void gemm_dense_kernel(GemvArgs p, int nsplit, float* part) {
   constexpr int EB = DenseG<T>::EB, KS = 128 / EB, EPP = 16 / EB;   // elems per step / piece
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
@@ -62,11 +64,13 @@ __global__ __launch_bounds__(DG_NT) void gemm_dense_kernel(GemvArgs p) {
   const int nit = (p.M + DG_T - 1) / DG_T, njt = (p.N + DG_T - 1) / DG_T;
   // XCD-aware order: the 8 workgroups dealt to the 8 XCDs in one round take 8 different
   // column groups, and consecutive ids on one XCD walk neighbouring tiles (shared L2 lines)
-  int it, jt, z;
+  int it, jt, z, sp;
   {
-    const int nwg = nit * njt * p.ne12 * p.ne13;
+    const int ntile = nit * njt * p.ne12 * p.ne13, nwg = ntile * nsplit;
     const int id = blockIdx.x, x = id & 7, k = id >> 3, q = nwg >> 3, rmd = nwg & 7;
-    const int wv = x < rmd ? x * (q + 1) + k : rmd * (q + 1) + (x - rmd) * q + k;
+    int wv = x < rmd ? x * (q + 1) + k : rmd * (q + 1) + (x - rmd) * q + k;
+    sp = wv / ntile;   // split-major (K-splits of a tile run on different XCDs' rounds)
+    wv %= ntile;
     z = wv / (nit * njt);
     const int r = wv % (nit * njt);
     jt = r / nit;
@@ -77,6 +81,7 @@ __global__ __launch_bounds__(DG_NT) void gemm_dense_kernel(GemvArgs p) {
   const unsigned char* Bz = p.B + (int64_t)i12 * p.sb2 + (int64_t)i13 * p.sb3;
   float* Cz = p.C + (int64_t)i12 * p.sc2 + (int64_t)i13 * p.sc3;
   const int K = p.K, nsteps = (K + KS - 1) / KS;
+  const int k0 = (int)((int64_t)sp * nsteps / nsplit), k1 = (int)((int64_t)(sp + 1) * nsteps / nsplit);
   const int i0 = it * DG_T, j0 = jt * DG_T;
   const int mrows = min(DG_T, p.M - i0), ncols = min(DG_T, p.N - j0);
   const int64_t abytes = (int64_t)(mrows - 1) * p.lda + (int64_t)K * EB;
@@ -141,11 +146,11 @@ __global__ __launch_bounds__(DG_NT) void gemm_dense_kernel(GemvArgs p) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[x][y][e] = 0.f;
 
-  gload(0);
-  swrite(0);
+  gload(k0);
+  swrite(k0 & 1);
   __syncthreads();
-  for (int ks = 0; ks < nsteps; ++ks) {
-    if (ks + 1 < nsteps) gload(ks + 1);   // in flight during this step's MFMAs
+  for (int ks = k0; ks < k1; ++ks) {
+    if (ks + 1 < k1) gload(ks + 1);   // in flight during this step's MFMAs
     const unsigned char* sA = smem + (ks & 1) * DG_STAGE;
     const unsigned char* sB = sA + DG_OP;
 #pragma unroll
@@ -175,12 +180,18 @@ __global__ __launch_bounds__(DG_NT) void gemm_dense_kernel(GemvArgs p) {
             }
       }
     }
-    if (ks + 1 < nsteps) swrite((ks + 1) & 1);   // the buffer everyone finished reading at step ks-1
+    if (ks + 1 < k1) swrite((ks + 1) & 1);   // the buffer everyone finished reading at step ks-1
     __syncthreads();
   }
 
   // D layout (srcA = activation rows j, srcB = weight rows i): lane -> i = lr, element e ->
   // j = (e & 3) + 8 (e >> 2) + 4 h.  For each e the 32 lanes of a half store 128 contiguous bytes.
+  float* Co = Cz;
+  int64_t ldo = p.ldc;
+  if (nsplit > 1) {   // partial tile of split sp -> part[sp][z][j][i]
+    Co = part + ((int64_t)sp * p.ne12 * p.ne13 + z) * p.N * p.M;
+    ldo = p.M;
+  }
 #pragma unroll
   for (int x = 0; x < 2; ++x)
 #pragma unroll
@@ -189,15 +200,33 @@ __global__ __launch_bounds__(DG_NT) void gemm_dense_kernel(GemvArgs p) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int j = j0 + 64 * wj + 32 * x + (e & 3) + 8 * (e >> 2) + 4 * h;
-        if (i < p.M && j < p.N) Cz[(int64_t)j * p.ldc + i] = acc[x][y][e];
+        if (i < p.M && j < p.N) Co[(int64_t)j * ldo + i] = acc[x][y][e];
       }
     }
 }
 
-template <int T, bool BAL>
-hipError_t launch_dg(const GemvArgs& p, hipStream_t s) {
+// K-splits: double until the grid covers 256 CUs, keeping >= 4 K-steps per split
+// (LAMM_DENSE_SPLIT=n forces n)
+int dg_nsplit(const GemvArgs& p, int eb) {
   const int nit = (p.M + DG_T - 1) / DG_T, njt = (p.N + DG_T - 1) / DG_T;
-  const int64_t nwg = (int64_t)nit * njt * p.ne12 * p.ne13;
+  const int tiles = nit * njt * p.ne12 * p.ne13;
+  const int nsteps = (p.K + 128 / eb - 1) / (128 / eb);
+  const char* e = getenv("LAMM_DENSE_SPLIT");
+  int n = 1;
+  if (e && atoi(e) > 0) {
+    n = atoi(e);
+  } else {
+    while (tiles * n < 256 && n < 8 && nsteps / (2 * n) >= 4) n *= 2;
+  }
+  return n < 1 ? 1 : (n > nsteps ? (nsteps < 1 ? 1 : nsteps) : n);
+}
+
+template <int T, bool BAL>
+hipError_t launch_dg(const GemvArgs& p, void* ws, hipStream_t s) {
+  const int nit = (p.M + DG_T - 1) / DG_T, njt = (p.N + DG_T - 1) / DG_T;
+  const int nsplit = dg_nsplit(p, DenseG<T>::EB);
+  const int64_t nwg = (int64_t)nit * njt * p.ne12 * p.ne13 * nsplit;
+  float* part = static_cast<float*>(ws);
   if (nwg > 0x7fffffff) return hipErrorInvalidValue;
   constexpr size_t lds = 2 * DG_STAGE;
   static bool attr_set = false;
@@ -206,7 +235,8 @@ hipError_t launch_dg(const GemvArgs& p, hipStream_t s) {
                               (int)lds);
     attr_set = true;
   }
-  hipLaunchKernelGGL((gemm_dense_kernel<T, BAL>), dim3((unsigned)nwg), dim3(DG_NT), lds, s, p);
+  hipLaunchKernelGGL((gemm_dense_kernel<T, BAL>), dim3((unsigned)nwg), dim3(DG_NT), lds, s, p, nsplit, part);
+  if (nsplit > 1) launch_splitk_reduce(p, nsplit, part, s);
   return hipGetLastError();
 }
 
@@ -214,12 +244,17 @@ hipError_t launch_dg(const GemvArgs& p, hipStream_t s) {
 
 bool gemm_dense_supported(int type) { return type == kF32 || type == kF16; }
 
-hipError_t launch_gemm_dense(int type, const GemvArgs& p, hipStream_t s) {
+size_t gemm_dense_workspace_bytes(int type, const GemvArgs& p) {
+  const int n = dg_nsplit(p, type == kF32 ? 4 : 2);
+  return n > 1 ? (size_t)n * p.ne12 * p.ne13 * (size_t)p.N * p.M * sizeof(float) + 256 : 0;
+}
+
+hipError_t launch_gemm_dense(int type, const GemvArgs& p, void* ws, hipStream_t s) {
   if (p.M == 0 || p.N == 0) return hipSuccess;
   const bool bal = ((uintptr_t)p.B & 15) == 0 && (p.ldb & 15) == 0 && (p.sb2 & 15) == 0 && (p.sb3 & 15) == 0;
   switch (type) {
-    case kF32: return bal ? launch_dg<kF32, true>(p, s) : launch_dg<kF32, false>(p, s);
-    case kF16: return bal ? launch_dg<kF16, true>(p, s) : launch_dg<kF16, false>(p, s);
+    case kF32: return bal ? launch_dg<kF32, true>(p, ws, s) : launch_dg<kF32, false>(p, ws, s);
+    case kF16: return bal ? launch_dg<kF16, true>(p, ws, s) : launch_dg<kF16, false>(p, ws, s);
     default: return hipErrorInvalidValue;
   }
 }

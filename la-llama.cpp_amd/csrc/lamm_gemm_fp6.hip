@@ -526,6 +526,19 @@ __global__ __launch_bounds__(256) void f6_reduce(GemvArgs p, int nsplit, const f
   }
 }
 
+}  // namespace
+
+void launch_splitk_reduce(const GemvArgs& p, int nsplit, const float* part, hipStream_t s) {
+  const int64_t n = (int64_t)p.N * p.M * p.ne12 * p.ne13;
+  const bool v4 = p.M % 4 == 0 && p.ldc % 4 == 0 && p.sc2 % 4 == 0 && p.sc3 % 4 == 0 && ((uintptr_t)p.C & 15) == 0;
+  if (v4)
+    hipLaunchKernelGGL(f6_reduce<true>, dim3((unsigned)((n / 4 + 255) / 256)), dim3(256), 0, s, p, nsplit, part);
+  else
+    hipLaunchKernelGGL(f6_reduce<false>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, p, nsplit, part);
+}
+
+namespace {
+
 // K-splits for a grid of `tiles` workgroups: double until 256 CUs have one each, keeping
 // >= 8 K-steps per split.  LAMM_FP6_SPLIT=n forces n (A/B).
 int f6_nsplit(const GemvArgs& p, const F6Layout& L) {
@@ -592,15 +605,7 @@ hipError_t launch_fp6_t(const GemvArgs& p, const void* prepA, void* ws, hipStrea
     default: go(gemm_fp6_kernel<T, 0, 2>, NT2);
   }
   if (nsplit > 1) {
-    const int64_t n = (int64_t)p.N * p.M * p.ne12 * p.ne13;
-    const bool v4 = p.M % 4 == 0 && p.ldc % 4 == 0 && p.sc2 % 4 == 0 && p.sc3 % 4 == 0 &&
-                    ((uintptr_t)p.C & 15) == 0;
-    if (v4)
-      hipLaunchKernelGGL(f6_reduce<true>, dim3((unsigned)((n / 4 + 255) / 256)), dim3(256), 0, s, p, nsplit,
-                         static_cast<const float*>(part));
-    else
-      hipLaunchKernelGGL(f6_reduce<false>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, p, nsplit,
-                         static_cast<const float*>(part));
+    launch_splitk_reduce(p, nsplit, part, s);
   }
   return hipGetLastError();
 }

@@ -190,7 +190,10 @@ int matmul_impl(const lamm_matrix* A, const lamm_matrix* B, const lamm_matrix* C
   if (N <= 8) {
     e = launch_gemv(A->type, p, s);
   } else if (gemm_dense_supported(A->type) && !getenv_flag0("LAMM_DENSE_GEMM")) {
-    e = launch_gemm_dense(A->type, p, s);
+    const size_t wsb = gemm_dense_workspace_bytes(A->type, p);
+    void* ws = nullptr;
+    if (wsb && !(ws = workspace(wsb, s))) return fail(LAMM_ERR_HIP, "workspace allocation of %zu bytes failed", wsb);
+    e = launch_gemm_dense(A->type, p, ws, s);
   } else if (gemm_kq_supported(A->type) && !getenv_flag0("LAMM_KQ_GEMM") && (ldb & 3) == 0 &&
              ((uintptr_t)B->data & 3) == 0 && (bt.nbb2 & 3) == 0 && (bt.nbb3 & 3) == 0) {
     const void* prepA = W ? W->packed : nullptr;

@@ -29,9 +29,14 @@ bool gemm_kq_supported(int type);
 size_t gemm_kq_workspace_bytes(int type, const GemvArgs& p, bool prepared);
 size_t gemm_kq_weight_bytes(int type, const GemvArgs& p);
 hipError_t prepare_kq_weights(int type, const GemvArgs& p, void* wsA, hipStream_t s);
-// F32 / F16 prefill GEMM on the matrix cores (lamm_gemm_dense.hip)
-hipError_t launch_gemm_dense(int type, const GemvArgs& p, hipStream_t s);
+// F32 / F16 prefill GEMM on the matrix cores (lamm_gemm_dense.hip); split-K partials in the
+// workspace for grids under 256 tiles
+hipError_t launch_gemm_dense(int type, const GemvArgs& p, void* workspace, hipStream_t s);
+size_t gemm_dense_workspace_bytes(int type, const GemvArgs& p);
 bool gemm_dense_supported(int type);
+
+// C (slice z, row j, col i) = sum_{s < nsplit} part[s][z][j][i] in split order (deterministic)
+void launch_splitk_reduce(const GemvArgs& p, int nsplit, const float* part, hipStream_t s);
 
 hipError_t launch_gemm(int type, const GemvArgs& p, void* workspace, hipStream_t s);
 size_t gemm_workspace_bytes(int type, const GemvArgs& p);   // device scratch launch_gemm needs

@@ -478,3 +478,23 @@ def test_weights_stationary_matches_per_call(t, monkeypatch):
     with pytest.raises(la.LammError):
         W.matmul_torch(B, C1, N, batch=bad)
     W.close()
+
+
+@pytest.mark.parametrize("split", ["1", "3", "8"])
+@pytest.mark.parametrize("t", [ol.F32, ol.F16], ids=["f32", "f16"])
+def test_dense_gemm_split_k(t, split, monkeypatch):
+    """Dense GEMM with K split over workgroups (LAMM_DENSE_SPLIT; auto under 256 tiles):
+    uneven splits, ragged K tail in the last split, partials summed in split order."""
+    monkeypatch.setenv("LAMM_DENSE_SPLIT", split)
+    M, N, K = 200, 130, 2000 + 3
+    A_q, B_q, Ap, Bp, lda, ldb = _dense_case(t, M, N, K, int(split) * 7 + t, (-K) % (16 // la.type_size(t)))
+    A = dev_bytes(np.concatenate([Ap.reshape(-1), np.zeros(64, np.uint8)]))
+    B = dev_bytes(np.concatenate([Bp.reshape(-1), np.zeros(64, np.uint8)]))
+    C = torch.full((N * (M + 2) + 16,), float("nan"), dtype=torch.float32, device="cuda")
+    la.mul_mat_torch(t, A, B, C, M, N, K, lda=lda, ldb=ldb, ldc=M + 2)
+    torch.cuda.synchronize()
+    c = C.cpu().numpy()
+    got = np.stack([c[j * (M + 2):j * (M + 2) + M] for j in range(N)])
+    ref = ORACLE.mul_mat(t, M, N, K, A_q, B_q)
+    assert rel_err(got, ref, absdot(t, A_q, B_q, M, N, K)).max() < TOL
+    assert np.isnan(np.concatenate([c[j * (M + 2) + M:(j + 1) * (M + 2)] for j in range(N)])).all()

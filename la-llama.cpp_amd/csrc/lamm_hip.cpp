@@ -66,29 +66,40 @@ const DeviceProbe& probe() {
   return p;
 }
 
-// Device scratch for the GEMM's decoded activations: grow-only, one per process and
-// device.  Growing synchronises `s` before the old buffer is released.
+// Device scratch of the GEMM engines (packed activations, split-K partials): grow-only, one
+// per (device, stream), so calls on different streams never share one (work on ONE stream is
+// ordered by the stream itself).  Growing synchronises that stream before the old buffer is
+// released.
+struct WsKey {
+  int dev;
+  hipStream_t stream;
+  bool operator==(const WsKey& o) const { return dev == o.dev && stream == o.stream; }
+};
+struct WsKeyHash {
+  size_t operator()(const WsKey& k) const { return std::hash<const void*>()(k.stream) ^ (size_t)k.dev * 0x9e3779b9u; }
+};
+struct WsBuf {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+};
 std::mutex g_ws_mu;
-void* g_ws = nullptr;
-size_t g_ws_bytes = 0;
-int g_ws_dev = -1;
+std::unordered_map<WsKey, WsBuf, WsKeyHash> g_ws;
 
 void* workspace(size_t bytes, hipStream_t s) {
-  std::lock_guard<std::mutex> lock(g_ws_mu);
   int dev = 0;
   (void)hipGetDevice(&dev);
-  if (g_ws && g_ws_bytes >= bytes && g_ws_dev == dev) return g_ws;
-  if (g_ws) {
+  std::lock_guard<std::mutex> lock(g_ws_mu);
+  WsBuf& b = g_ws[WsKey{dev, s}];
+  if (b.ptr && b.bytes >= bytes) return b.ptr;
+  if (b.ptr) {
     (void)hipStreamSynchronize(s);
-    (void)hipDeviceSynchronize();
-    (void)hipFree(g_ws);
-    g_ws = nullptr;
+    (void)hipFree(b.ptr);
+    b = WsBuf{};
   }
   const size_t want = bytes + bytes / 4;
-  if (hipMalloc(&g_ws, want) != hipSuccess) { g_ws = nullptr; g_ws_bytes = 0; return nullptr; }
-  g_ws_bytes = want;
-  g_ws_dev = dev;
-  return g_ws;
+  if (hipMalloc(&b.ptr, want) != hipSuccess) { b = WsBuf{}; return nullptr; }
+  b.bytes = want;
+  return b.ptr;
 }
 
 // env var set to "0" (A/B switches that turn a default path off)

@@ -498,3 +498,28 @@ def test_dense_gemm_split_k(t, split, monkeypatch):
     ref = ORACLE.mul_mat(t, M, N, K, A_q, B_q)
     assert rel_err(got, ref, absdot(t, A_q, B_q, M, N, K)).max() < TOL
     assert np.isnan(np.concatenate([c[j * (M + 2) + M:(j + 1) * (M + 2)] for j in range(N)])).all()
+
+
+def test_concurrent_streams_have_private_workspaces(monkeypatch):
+    """Two GEMMs that need workspaces, issued back to back on two streams without
+    synchronising in between: each (device, stream) has its own workspace, so neither
+    overwrites the other's packed operands."""
+    monkeypatch.setenv("LAMM_GEMM_PATH", "fp6")
+    t, M, N, K = ol.Q4_0, 300, 100, 2048
+    cases = [random_case(t, M, N, K, seed=90 + s) for s in range(2)]
+    kb = K // 32
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    outs = []
+    for (A_q, B_q), st in zip(cases, streams):
+        A = dev_bytes(pitched_A(t, A_q, M, kb, kb))
+        B = dev_bytes(B_q)
+        C = torch.full((N * M,), float("nan"), dtype=torch.float32, device="cuda")
+        torch.cuda.synchronize()
+        with torch.cuda.stream(st):
+            for _ in range(3):
+                la.mul_mat_torch(t, A, B, C, M, N, K, stream=st.cuda_stream)
+        outs.append((A, B, C))
+    torch.cuda.synchronize()
+    for (A_q, B_q), (_, _, C) in zip(cases, outs):
+        ref = ORACLE.mul_mat(t, M, N, K, A_q, B_q)
+        assert rel_err(C.cpu().numpy().reshape(N, M), ref, absdot(t, A_q, B_q, M, N, K)).max() < TOL

@@ -322,10 +322,7 @@ def main():
             if not args.no_gemm:
                 gN = args.gemm_N
                 _, _, gk = run_case(torch, la, dist, f, M, gN, K, 1, max(3, args.steps // 4), 2, world)
-                t = la.BY_NAME[f]
-                engine = ("dense-mfma" if t in (la.F32, la.F16) else
-                          la.gemm_engine(f, M, gN, K, 1, stationary=True) if t in (la.Q4_0, la.Q4_1, la.Q5_0) else
-                          "i8" if t in (la.Q5_1, la.Q8_0) else "kq-i8")
+                engine = la.gemm_engine(f, M, gN, K, 1, stationary=True)
                 sw[f].update({"gemm_GFLOPS": round(2.0 * M * gN * K / gk / 1e9, 1), "gemm_us": round(gk * 1e6, 2),
                               "gemm_engine": engine})
         out["sweep"] = sw

@@ -241,8 +241,12 @@ def gemm_engine(fmt, M, N, K, slices=1, stationary=False):
     t = BY_NAME[fmt] if isinstance(fmt, str) else fmt
     if N <= 8:
         return "gemv"
+    if t in (F32, F16):
+        return "dense"          # lamm_gemm_dense.hip (LAMM_DENSE_GEMM=0: grouped GEMV)
+    if t in (Q2_K, Q4_K, Q5_K, Q6_K):
+        return "superblock"     # lamm_gemm_kq.hip (LAMM_KQ_GEMM=0: q2_K i8 / grouped GEMV)
     if t not in (Q4_0, Q4_1, Q5_0):
-        return "i8" if t != F32 else "gemv"
+        return "i8"
     env = os.environ.get("LAMM_GEMM_PATH")
     if env in ("i8", "1"):
         return "i8"

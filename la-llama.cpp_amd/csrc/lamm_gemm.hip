@@ -134,11 +134,12 @@ __global__ __launch_bounds__(256) void prep_act_kernel(GemvArgs p, unsigned char
   const int64_t nb_pad = (int64_t)L.nsteps * KBLK;
   if (it >= (int64_t)p.N * nb_pad) return;
   const int j = (int)(it / nb_pad), b = (int)(it % nb_pad);
-  const int64_t bbytes = (int64_t)(p.N - 1) * p.ldb + (int64_t)p.nblk * VBPB;
-  const auto rs = make_rsrc(Bz, (uint32_t)min((bbytes + 3) & ~int64_t(3), (int64_t)0x7fffffff));
+  // resource based at row j (offsets < 2^31 for any slice size)
+  const auto rs = make_rsrc(Bz + (int64_t)j * p.ldb,
+                            (uint32_t)min(((int64_t)p.nblk * VBPB + 3) & ~int64_t(3), (int64_t)0x7fffffff));
   constexpr int VQS = VBPB == 36 ? 4 : 2;
   const bool ok = b < p.nblk;
-  const uint32_t off = ok ? (uint32_t)(j * p.ldb + (int64_t)b * VBPB) : 0xfffffff0u;
+  const uint32_t off = ok ? (uint32_t)((int64_t)b * VBPB) : 0xfffffff0u;
   const uint32_t base = off & ~3u;
   const int sh = (int)(off & 3u);
   uint32_t w[10], m[10];

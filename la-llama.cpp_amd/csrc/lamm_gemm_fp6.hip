@@ -143,8 +143,10 @@ __global__ __launch_bounds__(PW_NT) void prep_w_fp6(GemvArgs p, unsigned char* w
   const int64_t i0 = (int64_t)(blockIdx.x / nkg) * PW_ROWS;
   const int kb0 = (blockIdx.x % nkg) * PW_NB;
   const int a = blockIdx.y, ne02 = p.ne12 / p.r2, i02 = a % ne02, i03 = a / ne02;
-  const unsigned char* Az = p.A + (int64_t)i02 * p.sa2 + (int64_t)i03 * p.sa3;
-  const int64_t abytes = (int64_t)(p.M - 1) * p.lda + (int64_t)p.nblk * F::ABPB;
+  // resource based at this workgroup's first row: offsets stay < 2^31 for any slice size
+  const unsigned char* Az = p.A + (int64_t)i02 * p.sa2 + (int64_t)i03 * p.sa3 + min(i0, (int64_t)p.M) * p.lda;
+  const int64_t nrow = min((int64_t)PW_ROWS, (int64_t)p.M - i0);
+  const int64_t abytes = nrow > 0 ? (nrow - 1) * p.lda + (int64_t)p.nblk * F::ABPB : 0;
   const auto rs = make_rsrc(Az, (uint32_t)min((abytes + 15) & ~int64_t(15), (int64_t)0x7fffffff));
   const int t = threadIdx.x;
   constexpr int PIECES = PW_ROWS * SEG / 16;
@@ -154,7 +156,7 @@ __global__ __launch_bounds__(PW_NT) void prep_w_fp6(GemvArgs p, unsigned char* w
     if (pc < PIECES) {
       const int r = pc / (SEG / 16), o = pc % (SEG / 16);
       const int64_t i = i0 + r;
-      const uint32_t off = i < p.M ? (uint32_t)(i * p.lda + (int64_t)kb0 * F::ABPB + 16 * o) : 0x7ffffff0u;
+      const uint32_t off = i < p.M ? (uint32_t)((int64_t)r * p.lda + (int64_t)kb0 * F::ABPB + 16 * o) : 0x7ffffff0u;
       const u32x4 v = bload16(rs, off);
 #pragma unroll
       for (int q = 0; q < 4; ++q) raw[r * SEGW + 4 * o + q] = v[q];
@@ -224,15 +226,15 @@ __global__ __launch_bounds__(PREP_NT) void prep_b_fp6(GemvArgs p, unsigned char*
   if (j >= (int64_t)L.njt * F6_TJ) return;
   const int jt = (int)(j / F6_TJ), r = (int)(j % F6_TJ);
   unsigned char* wsb = ws + (int64_t)z * L.b_slice + (int64_t)jt * L.nsteps * F6_B_BYTES;
-  const unsigned char* Bz = p.B + (int64_t)i12 * p.sb2 + (int64_t)i13 * p.sb3;
-  const int64_t bbytes = (int64_t)(p.N - 1) * p.ldb + (int64_t)p.nblk * VBPB;
-  const auto rs = make_rsrc(Bz, (uint32_t)min((bbytes + 3) & ~int64_t(3), (int64_t)0x7fffffff));
+  // resource based at this thread's row (offsets < 2^31 for any slice size)
+  const unsigned char* Bz = p.B + (int64_t)i12 * p.sb2 + (int64_t)i13 * p.sb3 + min(j, (int64_t)p.N - 1) * p.ldb;
+  const auto rs = make_rsrc(Bz, (uint32_t)min(((int64_t)p.nblk * VBPB + 3) & ~int64_t(3), (int64_t)0x7fffffff));
   for (int kb = kb0; kb < kb0 + PREP_NB && kb < L.nsteps * F6_KB; ++kb) {
     uint32_t chi[32], clo[32];
     uint32_t d = 0, sv = 0;
     if (j < p.N && kb < p.nblk) {
       uint32_t m[9];
-      load_block<9>(rs, (uint32_t)(j * p.ldb + (int64_t)kb * VBPB), m);
+      load_block<9>(rs, (uint32_t)((int64_t)kb * VBPB), m);
       d = m[0] & 0xffffu;
       if constexpr (VBPB == 36) sv = m[0] >> 16;
 #pragma unroll

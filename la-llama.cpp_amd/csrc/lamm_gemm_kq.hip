@@ -317,9 +317,10 @@ __global__ __launch_bounds__(256) void prep_w_kq(GemvArgs p, unsigned char* wsA)
   uint32_t raw[NW];
   int sh = 0;
   {
-    const int64_t avail = (int64_t)(p.M - 1) * p.lda + (int64_t)p.nblk * ABPB;
-    const auto ra = make_rsrc(Az, (uint32_t)min((avail + 3) & ~int64_t(3), (int64_t)0x7fffffff));
-    const int64_t off = ok ? i * p.lda + (int64_t)sb * ABPB : 0x7fffff00;
+    // resource based at row i (offsets < 2^31 for any slice size)
+    const auto ra = make_rsrc(Az + min(i, (int64_t)p.M - 1) * p.lda,
+                              (uint32_t)min(((int64_t)p.nblk * ABPB + 3) & ~int64_t(3), (int64_t)0x7fffffff));
+    const int64_t off = ok ? (int64_t)sb * ABPB : 0x7fffff00;
     sh = (int)(off & 3);
 #pragma unroll
     for (int k = 0; k < NW; ++k) raw[k] = bload4(ra, (uint32_t)((off & ~int64_t(3)) + 4 * k));
@@ -412,9 +413,10 @@ __global__ __launch_bounds__(256) void prep_b_kq(GemvArgs p, unsigned char* wsB)
   unsigned char* ch = wsB + (int64_t)z * L.b_slice + ((j / KQ_TJ) * L.nsb + sb) * KQC_B;
   const int r = (int)(j % KQ_TJ);
   const bool ok = j < p.N;
-  const int64_t bbytes = (int64_t)(p.N - 1) * p.ldb + (int64_t)p.nblk * 292;
-  const auto rb = make_rsrc(Bz, (uint32_t)min((bbytes + 3) & ~int64_t(3), (int64_t)0x7fffffff));
-  const uint32_t off = ok ? (uint32_t)(j * p.ldb + (int64_t)sb * 292) : 0x7ffffe00u;
+  // resource based at row j (offsets < 2^31 for any slice size)
+  const auto rb = make_rsrc(Bz + min(j, (int64_t)p.N - 1) * p.ldb,
+                            (uint32_t)min(((int64_t)p.nblk * 292 + 3) & ~int64_t(3), (int64_t)0x7fffffff));
+  const uint32_t off = ok ? (uint32_t)((int64_t)sb * 292) : 0x7ffffe00u;
   uint32_t w[73];
 #pragma unroll
   for (int k = 0; k < 73; ++k) w[k] = bload4(rb, off + 4 * k);

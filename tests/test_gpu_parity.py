@@ -523,3 +523,39 @@ def test_concurrent_streams_have_private_workspaces(monkeypatch):
     for (A_q, B_q), (_, _, C) in zip(cases, outs):
         ref = ORACLE.mul_mat(t, M, N, K, A_q, B_q)
         assert rel_err(C.cpu().numpy().reshape(N, M), ref, absdot(t, A_q, B_q, M, N, K)).max() < TOL
+
+
+@pytest.mark.parametrize("engine", ["fp6", "i8", "kq"])
+def test_weight_slice_beyond_2gib(engine, monkeypatch):
+    """One weight slice of ~2.3 GB (1M rows): the prep passes address rows through buffer
+    resources based at the rows they read, so rows past 2 GiB are not clipped to zeros.
+    Checks the first and last 64 rows of C against the oracle."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    t = ol.Q4_K if engine == "kq" else ol.Q4_0
+    if engine != "kq":
+        monkeypatch.setenv("LAMM_GEMM_PATH", engine)
+    M, N, K = 1_000_000, 16, 4096
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(5)
+    fmt = ol.NAMES[t]
+    A, arow = bench.make_weights(torch, la, fmt, 1, M, K, gen)
+    assert M * arow > 2 ** 31
+    rng = np.random.default_rng(1)
+    vt = la.vec_dot_type(t)
+    B_q = ORACLE.quantize(vt, rng.standard_normal((N, K), dtype=np.float32),
+                          ol.QUANT_AVX if vt == ol.Q8_0 else ol.QUANT_REF)
+    B = dev_bytes(B_q)
+    C = torch.full((N * M,), float("nan"), dtype=torch.float32, device="cuda")
+    la.mul_mat_torch(t, A, B, C, M, N, K)
+    torch.cuda.synchronize()
+    c = C.view(N, M)
+    for r0 in (0, M - 64):
+        a_rows = A[r0 * arow:(r0 + 64) * arow].cpu().numpy()
+        ref = ORACLE.mul_mat(t, 64, N, K, a_rows, B_q)
+        got = c[:, r0:r0 + 64].cpu().numpy()
+        assert rel_err(got, ref, absdot(t, a_rows, B_q, 64, N, K)).max() < TOL, r0
+    del A, C
+    torch.cuda.empty_cache()

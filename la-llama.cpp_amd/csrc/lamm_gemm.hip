@@ -134,12 +134,15 @@ __global__ __launch_bounds__(256) void prep_act_kernel(GemvArgs p, unsigned char
   const int64_t nb_pad = (int64_t)L.nsteps * KBLK;
   if (it >= (int64_t)p.N * nb_pad) return;
   const int j = (int)(it / nb_pad), b = (int)(it % nb_pad);
-  // resource based at row j (offsets < 2^31 for any slice size)
-  const auto rs = make_rsrc(Bz + (int64_t)j * p.ldb,
-                            (uint32_t)min(((int64_t)p.nblk * VBPB + 3) & ~int64_t(3), (int64_t)0x7fffffff));
+  // resource based at the workgroup's first row: wave-uniform (a per-lane base would turn
+  // every buffer load into a waterfall loop) and offsets < 2^31 for any slice size
+  const int64_t jw = ((int64_t)blockIdx.x * 256) / nb_pad;
+  const int64_t jl = min((int64_t)p.N - 1, ((int64_t)blockIdx.x * 256 + 255) / nb_pad);
+  const int64_t bbytes = (jl - jw) * p.ldb + (int64_t)p.nblk * VBPB;
+  const auto rs = make_rsrc(Bz + jw * p.ldb, (uint32_t)min((bbytes + 3) & ~int64_t(3), (int64_t)0x7fffffff));
   constexpr int VQS = VBPB == 36 ? 4 : 2;
   const bool ok = b < p.nblk;
-  const uint32_t off = ok ? (uint32_t)((int64_t)b * VBPB) : 0xfffffff0u;
+  const uint32_t off = ok ? (uint32_t)((j - jw) * p.ldb + (int64_t)b * VBPB) : 0xfffffff0u;
   const uint32_t base = off & ~3u;
   const int sh = (int)(off & 3u);
   uint32_t w[10], m[10];

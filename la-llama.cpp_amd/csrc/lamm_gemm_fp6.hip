@@ -41,11 +41,17 @@ namespace {
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 half4 __attribute__((ext_vector_type(4)));
 
-constexpr int F6_KB = 2;        // 32-element blocks per K-step
+#ifndef F6_KB_CFG
+#define F6_KB_CFG 2
+#endif
+#ifndef F6_NBUF_CFG
+#define F6_NBUF_CFG 4
+#endif
+constexpr int F6_KB = F6_KB_CFG;   // 32-element blocks per K-step (4 with 2 stages: A/B builds)
 constexpr int F6_TI = 256;      // weight rows per tile
 constexpr int F6_TJ = 128;      // activation rows per tile
 constexpr int F6_PIECE = 1024;  // bytes one wave moves per LDS-DMA instruction (64 lanes x 16 B)
-constexpr int F6_NBUF = 4;      // LDS stages (3 K-steps of DMA in flight)
+constexpr int F6_NBUF = F6_NBUF_CFG;   // LDS stages (3 K-steps of DMA in flight)
 constexpr int SCALE_W = 130, SCALE_HI = 134, SCALE_LO = 130;   // E8M0: 2^(s-127)
 #ifndef F6_PD
 #define F6_PD 1   // MFMA pipeline depth: unit n+PD's MFMAs are issued before unit n's FMAs (2: no gain, +20 VGPRs)
@@ -214,27 +220,33 @@ __global__ __launch_bounds__(PW_NT) void prep_w_fp6(GemvArgs p, unsigned char* w
 
 // ---------------------------------------------------------------- activation prep
 // grid: x = row group of PREP_NT rows * kgroups + kgroup, y = B slice z
-template <int T>
+// NB blocks per thread: PREP_NB on batched calls, 1 when a single slice would leave the grid
+// at a few dozen workgroups (one 4096x512 slice: 64 -> 256)
+template <int T, int NB>
 __global__ __launch_bounds__(PREP_NT) void prep_b_fp6(GemvArgs p, unsigned char* ws) {
   using F = F6<T>;
   constexpr int VBPB = F::VBPB, VQS = VBPB == 36 ? 4 : 2;
   const F6Layout L = F6Layout::of(p);
-  const int nkg = (F6Layout::of(p).nsteps * F6_KB + PREP_NB - 1) / PREP_NB;
+  const int nkg = (F6Layout::of(p).nsteps * F6_KB + NB - 1) / NB;
   const int64_t j = (int64_t)(blockIdx.x / nkg) * PREP_NT + threadIdx.x;
-  const int kb0 = (blockIdx.x % nkg) * PREP_NB;
+  const int kb0 = (blockIdx.x % nkg) * NB;
   const int z = blockIdx.y, i12 = z % p.ne12, i13 = z / p.ne12;
   if (j >= (int64_t)L.njt * F6_TJ) return;
   const int jt = (int)(j / F6_TJ), r = (int)(j % F6_TJ);
   unsigned char* wsb = ws + (int64_t)z * L.b_slice + (int64_t)jt * L.nsteps * F6_B_BYTES;
-  // resource based at this thread's row (offsets < 2^31 for any slice size)
-  const unsigned char* Bz = p.B + (int64_t)i12 * p.sb2 + (int64_t)i13 * p.sb3 + min(j, (int64_t)p.N - 1) * p.ldb;
-  const auto rs = make_rsrc(Bz, (uint32_t)min(((int64_t)p.nblk * VBPB + 3) & ~int64_t(3), (int64_t)0x7fffffff));
-  for (int kb = kb0; kb < kb0 + PREP_NB && kb < L.nsteps * F6_KB; ++kb) {
+  // resource based at the workgroup's first row: wave-uniform (a per-lane base would turn
+  // every buffer load into a waterfall loop) and offsets < 2^31 for any slice size
+  const int64_t jw = (int64_t)(blockIdx.x / nkg) * PREP_NT;
+  const int64_t nrow = min((int64_t)PREP_NT, (int64_t)p.N - jw);
+  const unsigned char* Bz = p.B + (int64_t)i12 * p.sb2 + (int64_t)i13 * p.sb3 + min(jw, (int64_t)p.N) * p.ldb;
+  const int64_t bbytes = nrow > 0 ? (nrow - 1) * p.ldb + (int64_t)p.nblk * VBPB : 0;
+  const auto rs = make_rsrc(Bz, (uint32_t)min((bbytes + 3) & ~int64_t(3), (int64_t)0x7fffffff));
+  for (int kb = kb0; kb < kb0 + NB && kb < L.nsteps * F6_KB; ++kb) {
     uint32_t chi[32], clo[32];
     uint32_t d = 0, sv = 0;
     if (j < p.N && kb < p.nblk) {
       uint32_t m[9];
-      load_block<9>(rs, (uint32_t)((int64_t)kb * VBPB), m);
+      load_block<9>(rs, (uint32_t)((j - jw) * p.ldb + (int64_t)kb * VBPB), m);
       d = m[0] & 0xffffu;
       if constexpr (VBPB == 36) sv = m[0] >> 16;
 #pragma unroll
@@ -570,15 +582,19 @@ hipError_t launch_fp6_t(const GemvArgs& p, const void* prepA, void* ws, hipStrea
   auto* w = static_cast<unsigned char*>(ws);
   unsigned char* wsA = prepA ? nullptr : w;
   unsigned char* wsB = w + (prepA ? 0 : L.a_bytes);
-  const int nkg = (L.nsteps * F6_KB + PREP_NB - 1) / PREP_NB;
   // LAMM_GEMM_SKIP_PREP=1 (measurement only, bench.py): re-run the main kernel on the
   // workspace the previous identical call prepared, so its own duration can be event-timed
   const char* sp = getenv("LAMM_GEMM_SKIP_PREP");
   if (!(sp && sp[0] == '1')) {
     if (!prepA) launch_prep_w<T>(p, wsA, s);
-    hipLaunchKernelGGL(prep_b_fp6<T>,
-                       dim3((unsigned)(((L.njt * F6_TJ + PREP_NT - 1) / PREP_NT) * nkg), (unsigned)(p.ne12 * p.ne13)),
-                       dim3(PREP_NT), 0, s, p, wsB);
+    const int rgroups = (L.njt * F6_TJ + PREP_NT - 1) / PREP_NT, nb_all = L.nsteps * F6_KB;
+    if ((int64_t)rgroups * ((nb_all + PREP_NB - 1) / PREP_NB) * p.ne12 * p.ne13 >= 256)
+      hipLaunchKernelGGL((prep_b_fp6<T, PREP_NB>),
+                         dim3((unsigned)(rgroups * ((nb_all + PREP_NB - 1) / PREP_NB)), (unsigned)(p.ne12 * p.ne13)),
+                         dim3(PREP_NT), 0, s, p, wsB);
+    else
+      hipLaunchKernelGGL((prep_b_fp6<T, 1>), dim3((unsigned)(rgroups * nb_all), (unsigned)(p.ne12 * p.ne13)),
+                         dim3(PREP_NT), 0, s, p, wsB);
   }
   const size_t lds = (size_t)F6_NBUF * F6_STAGE;
   const int nsplit = f6_nsplit(p, L);

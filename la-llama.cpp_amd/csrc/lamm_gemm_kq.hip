@@ -317,10 +317,13 @@ __global__ __launch_bounds__(256) void prep_w_kq(GemvArgs p, unsigned char* wsA)
   uint32_t raw[NW];
   int sh = 0;
   {
-    // resource based at row i (offsets < 2^31 for any slice size)
-    const auto ra = make_rsrc(Az + min(i, (int64_t)p.M - 1) * p.lda,
-                              (uint32_t)min(((int64_t)p.nblk * ABPB + 3) & ~int64_t(3), (int64_t)0x7fffffff));
-    const int64_t off = ok ? (int64_t)sb * ABPB : 0x7fffff00;
+    // resource based at the workgroup's first row: wave-uniform (a per-lane base would turn
+    // every buffer load into a waterfall loop) and offsets < 2^31 for any slice size
+    const int64_t iw = min(((int64_t)blockIdx.x * 256) / L.nsb, (int64_t)p.M - 1);
+    const int64_t il = min((int64_t)p.M - 1, ((int64_t)blockIdx.x * 256 + 255) / L.nsb);
+    const int64_t abytes = (il - iw) * p.lda + (int64_t)p.nblk * ABPB;
+    const auto ra = make_rsrc(Az + iw * p.lda, (uint32_t)min((abytes + 3) & ~int64_t(3), (int64_t)0x7fffffff));
+    const int64_t off = ok ? (i - iw) * p.lda + (int64_t)sb * ABPB : 0x7fffff00;
     sh = (int)(off & 3);
 #pragma unroll
     for (int k = 0; k < NW; ++k) raw[k] = bload4(ra, (uint32_t)((off & ~int64_t(3)) + 4 * k));
@@ -401,38 +404,46 @@ __global__ __launch_bounds__(256) void prep_w_kq(GemvArgs p, unsigned char* wsA)
   *(float*)(ch + 33024 + 4 * r) = dm;
 }
 
-// one thread per (activation row, super-block)
+// 18 threads per (activation row, super-block): 16 copy a 16-quant piece each, one the f32
+// d_b, one the 16 bsums (as exact fp16); consecutive threads read consecutive 16-byte pieces
 __global__ __launch_bounds__(256) void prep_b_kq(GemvArgs p, unsigned char* wsB) {
   const KQLayout L = KQLayout::of(p);
   const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (g >= (int64_t)L.njt * KQ_TJ * L.nsb) return;
-  const int sb = (int)(g % L.nsb);
-  const int64_t j = g / L.nsb;
+  if (g >= (int64_t)L.njt * KQ_TJ * L.nsb * 18) return;
+  const int q = (int)(g % 18);
+  const int64_t rest = g / 18;
+  const int sb = (int)(rest % L.nsb);
+  const int64_t j = rest / L.nsb;
   const int z = blockIdx.y, i12 = z % p.ne12, i13 = z / p.ne12;
   const unsigned char* Bz = p.B + (int64_t)i12 * p.sb2 + (int64_t)i13 * p.sb3;
   unsigned char* ch = wsB + (int64_t)z * L.b_slice + ((j / KQ_TJ) * L.nsb + sb) * KQC_B;
   const int r = (int)(j % KQ_TJ);
   const bool ok = j < p.N;
-  // resource based at row j (offsets < 2^31 for any slice size)
-  const auto rb = make_rsrc(Bz + min(j, (int64_t)p.N - 1) * p.ldb,
-                            (uint32_t)min(((int64_t)p.nblk * 292 + 3) & ~int64_t(3), (int64_t)0x7fffffff));
-  const uint32_t off = ok ? (uint32_t)((int64_t)sb * 292) : 0x7ffffe00u;
-  uint32_t w[73];
+  // resource based at the workgroup's first row: wave-uniform (a per-lane base would turn
+  // every buffer load into a waterfall loop) and offsets < 2^31 for any slice size
+  const int64_t jw = min(((int64_t)blockIdx.x * 256 / 18) / L.nsb, (int64_t)p.N - 1);
+  const int64_t jl = min((int64_t)p.N - 1, (((int64_t)blockIdx.x * 256 + 255) / 18) / L.nsb);
+  const int64_t bbytes = (jl - jw) * p.ldb + (int64_t)p.nblk * 292;
+  const auto rb = make_rsrc(Bz + jw * p.ldb, (uint32_t)min((bbytes + 3) & ~int64_t(3), (int64_t)0x7fffffff));
+  const uint32_t off = ok ? (uint32_t)((j - jw) * p.ldb + (int64_t)sb * 292) : 0x7ffffe00u;
+  if (q < 16) {   // quants 16q .. 16q+15 (dwords 1 + 4q ..)
+    u32x4 v;
 #pragma unroll
-  for (int k = 0; k < 73; ++k) w[k] = bload4(rb, off + 4 * k);
+    for (int k = 0; k < 4; ++k) v[k] = bload4(rb, off + 4 * (1 + 4 * q + k));
+    *(u32x4*)(ch + kq_swz(r, q)) = v;
+  } else if (q == 16) {
+    *(float*)(ch + 32768 + 4 * r) = __uint_as_float(bload4(rb, off));
+  } else {
+    uint32_t hb[8];
 #pragma unroll
-  for (int q16 = 0; q16 < 16; ++q16)
-    *(u32x4*)(ch + kq_swz(r, q16)) = u32x4{w[1 + 4 * q16], w[2 + 4 * q16], w[3 + 4 * q16], w[4 + 4 * q16]};
-  *(float*)(ch + 32768 + 4 * r) = __uint_as_float(w[0]);
-  uint32_t hb[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const uint32_t v = w[65 + k];
-    const _Float16 lo = (_Float16)(float)(int16_t)(v & 0xffff), hi = (_Float16)(float)(int16_t)(v >> 16);
-    hb[k] = (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
+    for (int k = 0; k < 8; ++k) {
+      const uint32_t v = bload4(rb, off + 4 * (65 + k));
+      const _Float16 lo = (_Float16)(float)(int16_t)(v & 0xffff), hi = (_Float16)(float)(int16_t)(v >> 16);
+      hb[k] = (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
+    }
+    *(u32x4*)(ch + 33280 + 32 * r) = u32x4{hb[0], hb[1], hb[2], hb[3]};
+    *(u32x4*)(ch + 33280 + 32 * r + 16) = u32x4{hb[4], hb[5], hb[6], hb[7]};
   }
-  *(u32x4*)(ch + 33280 + 32 * r) = u32x4{hb[0], hb[1], hb[2], hb[3]};
-  *(u32x4*)(ch + 33280 + 32 * r + 16) = u32x4{hb[4], hb[5], hb[6], hb[7]};
 }
 
 template <int N_>
@@ -569,7 +580,7 @@ hipError_t launch_kq(const GemvArgs& p, const void* prepA, void* ws, hipStream_t
   unsigned char* wsA = prepA ? nullptr : w;
   unsigned char* wsB = w + (prepA ? 0 : L.a_bytes);
   if (!prepA) launch_prep_w_kq<T>(p, wsA, s);
-  const int64_t nb = (int64_t)L.njt * KQ_TJ * L.nsb;
+  const int64_t nb = (int64_t)L.njt * KQ_TJ * L.nsb * 18;
   hipLaunchKernelGGL(prep_b_kq, dim3((unsigned)((nb + 255) / 256), (unsigned)(p.ne12 * p.ne13)), dim3(256), 0, s, p,
                      wsB);
   constexpr size_t lds = 2 * (KQC_A + KQC_B);

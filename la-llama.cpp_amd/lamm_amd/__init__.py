@@ -17,7 +17,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "liblamm_hip.so")
+# LAMM_HIP_LIB: load another build of the library (A/B of compile-time kernel variants)
+LIB_PATH = os.environ.get("LAMM_HIP_LIB") or os.path.join(os.path.dirname(_HERE), "liblamm_hip.so")
 
 F32, Q4_0, Q4_1, Q5_0, Q5_1, Q8_0, Q8_1, Q2_K, Q8_K = 0, 2, 3, 6, 7, 8, 9, 10, 15
 Q4_K, Q5_K, Q6_K = 12, 13, 14   # SURVEY §8f "next" formats (beyond the reference's lamm set)

@@ -93,8 +93,8 @@ def run_case(torch, la, dist, fmt, M, N, K, slices, steps, warmup, world, warm_f
     B = make_activations(torch, la, fmt, slices * N, K, gen)
     C = torch.zeros(slices * N * M, dtype=torch.float32, device="cuda")
     # rows of A shard across ranks (weak scaling: each rank owns an M-row slab of every
-    # slice); the slabs of C meet in one RCCL all-gather + one interleaving copy
-    gather = RowGather(dist, slices * N, M, world, torch.float32, "cuda") if world > 1 else None
+    # slice); the slabs of C meet in RCCL all-gathers + interleaving copies (step() below)
+    gather = None
     kb = K // la.blck_size(t)
     brow = la.row_bytes(vt, K)
     Am = la.Matrix(A.data_ptr(), t, M, kb, kb)
@@ -111,10 +111,39 @@ def run_case(torch, la, dist, fmt, M, N, K, slices, steps, warmup, world, warm_f
         else:
             la.matmul_batched(Am, Bm, Cm, bt, stream.cuda_stream)
 
+    # N > 1 ranks: the launch is split into up to 4 groups of slices; group g's all-gather runs
+    # on a second stream while group g+1 computes (the collective overlaps the next compute)
+    chunks = []
+    if world > 1:
+        nch = min(4, slices)
+        for c in range(nch):
+            s0, s1 = c * slices // nch, (c + 1) * slices // nch
+            ns = s1 - s0
+            a_c = A[s0 * M * arow:s1 * M * arow]
+            b_c = B[s0 * N * brow:]
+            c_c = C[s0 * N * M:s1 * N * M]
+            bt_c = la.Batch(ns, 1, ns, 1, M * arow, ns * M * arow, N * brow, ns * N * brow, 4 * M * N, 4 * M * N * ns)
+            w_c = la.Weights(t, a_c, M, K, ne02=ns, ne03=1, nba2=M * arow, nba3=ns * M * arow) if stationary else None
+            m_c = (la.Matrix(a_c.data_ptr(), t, M, kb, kb), la.Matrix(b_c.data_ptr(), vt, kb, N, kb),
+                   la.Matrix(c_c.data_ptr(), la.F32, M, N, M))
+            chunks.append((w_c, m_c, bt_c, b_c, c_c, RowGather(dist, ns * N, M, world, torch.float32, "cuda")))
+    comm = torch.cuda.Stream() if world > 1 else None
+
     def step():
-        call()
-        if world > 1:  # row shards -> every rank holds all of C (RCCL over xGMI)
-            gather(C)
+        if world == 1:
+            call()
+            return
+        for w_c, m_c, bt_c, b_c, c_c, g_c in chunks:   # row shards -> every rank holds all of C
+            if w_c is not None:
+                w_c.matmul_torch(b_c, c_c, N, batch=bt_c, stream=stream.cuda_stream)
+            else:
+                la.matmul_batched(*m_c, bt_c, stream.cuda_stream)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            comm.wait_event(ev)
+            with torch.cuda.stream(comm):
+                g_c(c_c)                                  # RCCL all-gather over xGMI + interleave
+        stream.wait_stream(comm)
 
     if warm_first:
         skip = os.environ.pop("LAMM_GEMM_SKIP_PREP", None)
@@ -157,7 +186,10 @@ def run_case(torch, la, dist, fmt, M, N, K, slices, steps, warmup, world, warm_f
     kern = e2.elapsed_time(e3) / 1e3 / steps
     if W is not None:
         W.close()
-    del A, B, C, gather, W
+    for ch in chunks:
+        if ch[0] is not None:
+            ch[0].close()
+    del A, B, C, gather, W, chunks
     torch.cuda.empty_cache()
     return per[0].item(), per[1].item(), kern
 

@@ -621,6 +621,15 @@ struct SmemStreamD {
   int bs[NC][Fmt<T>::VQK == 256 ? GG::VBLK * 16 : 1];
 };
 
+template <int T, int NC>
+struct alignas(16) BPart {   // 16-byte aligned: a part at index > 0 is read with ds_read_b128
+  using GG = Geo<T>;
+  uint32_t bq[NC][GG::BQ_WORDS];
+  float bd[NC][(T == kF32 || T == kF16) ? 1 : GG::VBLK];
+  float bx[NC][(T == kF32 || T == kF16) ? 1 : GG::VBLK];
+  int bs[NC][Fmt<T>::VQK == 256 ? GG::VBLK * 16 : 1];
+};
+
 template <int N_>
 __device__ __forceinline__ void gv_wait_vm() {   // s_waitcnt vmcnt(N) (lgkmcnt untouched)
   static_assert(N_ >= 0 && N_ < 64, "vmcnt");
@@ -755,20 +764,152 @@ hipError_t launch_stream_dma(const GemvArgs& p, hipStream_t s) {
   return hipGetLastError();
 }
 
+// ---- multi-segment LDS-DMA streaming kernel (K up to NSEG x 4096: e.g. ffn_down's 11008) ---
+// Work items are (4-row group, K-segment) pairs in group-major order per wave; the activation
+// of every segment is staged once (one 16-byte aligned part per segment), partial sums carry
+// across a group's segments, C is written after its last one.  Pieces past the row's last
+// byte (ragged last segment) are pointed out of range, so they land as zeros.
+template <int T, int NC, int WAVES, int NS, int NSEG>
+struct SmemSegD {
+  uint32_t a[WAVES][NS][WGeo<T>::SLOT / 4];
+  BPart<T, NC> b[NSEG];
+};
+
+template <int T, int NC, int WAVES, int NS, int NSEG>
+__global__ __launch_bounds__(64 * WAVES) void gemv_seg_dma_kernel(GemvArgs p) {
+  using GG = Geo<T>;
+  using WG = WGeo<T>;
+  using F = Fmt<T>;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  SmemSegD<T, NC, WAVES, NS, NSEG>& sm = *reinterpret_cast<SmemSegD<T, NC, WAVES, NS, NSEG>*>(smem_raw);
+  static_assert(WG::NPW * (NS - 1) < 64, "vmcnt range");
+
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int row = lane / kSC, ch = lane % kSC;
+  const int z = blockIdx.y, i12 = z % p.ne12, i13 = z / p.ne12;
+  const unsigned char* Az = p.A + (int64_t)(i12 / p.r2) * p.sa2 + (int64_t)(i13 / p.r3) * p.sa3;
+  const unsigned char* Bz = p.B + (int64_t)i12 * p.sb2 + (int64_t)i13 * p.sb3;
+  float* Cz = p.C + (int64_t)i12 * p.sc2 + (int64_t)i13 * p.sc3;
+  const int ngroups = (p.M + kWRows - 1) / kWRows;
+  const int row_bytes = p.nblk * F::BPB;
+  const int nseg = (p.nblk + GG::SEG_BLK - 1) / GG::SEG_BLK;   // <= NSEG (launcher)
+  const int ncols = p.N < NC ? p.N : NC;
+  const int stride = gridDim.x * WAVES;
+  const int q0 = blockIdx.x * WAVES + w;
+  // this wave's items: k -> (group q0 + (k / nseg) * stride, segment k % nseg)
+  const int ngw = q0 < ngroups ? (ngroups - 1 - q0) / stride + 1 : 0;
+  const int nitems = ngw * nseg;
+
+  auto issue = [&](int k, int slot) {
+    const int q = q0 + (k / nseg) * stride, sg = k % nseg;
+    const int64_t r0 = (int64_t)q * kWRows;
+    const int rows = (int)min((int64_t)kWRows, (int64_t)p.M - r0);
+    const int64_t avail = (int64_t)(rows - 1) * p.lda + row_bytes;
+    const auto ra = make_rsrc(Az + r0 * p.lda, (uint32_t)min((avail + 3) & ~int64_t(3), (int64_t)0x7fffffff));
+#pragma unroll
+    for (int kk = 0; kk < WG::NPW; ++kk) {
+      const int pc = lane + 64 * kk;
+      const int rr = pc / (GG::ROW_BYTES / 16), oo = pc % (GG::ROW_BYTES / 16);
+      const int cbyte = sg * GG::ROW_BYTES + 16 * oo;   // byte within the row
+      const uint32_t off =
+          (pc * 16 < WG::BYTES && rr < rows && cbyte < row_bytes) ? (uint32_t)(rr * p.lda + cbyte) : 0x7ffffff0u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          ra, (__attribute__((address_space(3))) void*)&sm.a[w][slot][4 * 64 * kk], 16, off, 0, 0, 2);
+    }
+  };
+
+#pragma unroll
+  for (int k = 0; k < NS - 1; ++k)
+    if (k < nitems) issue(k, k);
+  for (int sg = 0; sg < nseg; ++sg) stage_b<T, NC>(sm.b[sg], p, Bz, sg);
+  __syncthreads();   // B visible to every wave
+
+  float acc[NC];
+  for (int k = 0; k < nitems; ++k) {
+    const int slot = k % NS;
+    {
+      const int kn = k + NS - 1;
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      if (kn < nitems) issue(kn, kn % NS);
+    }
+    const int after = min(NS - 1, nitems - 1 - k);
+    if constexpr (NS >= 3) {
+      if (after >= 2) gv_wait_vm<2 * WG::NPW>();
+      else if (after == 1) gv_wait_vm<WG::NPW>();
+      else gv_wait_vm<0>();
+    } else {
+      if (after >= 1) gv_wait_vm<WG::NPW>();
+      else gv_wait_vm<0>();
+    }
+    const int q = q0 + (k / nseg) * stride, sg = k % nseg;
+    if (sg == 0) {
+#pragma unroll
+      for (int j = 0; j < NC; ++j) acc[j] = 0.f;
+    }
+    const int64_t r0 = (int64_t)q * kWRows;
+    const int rows = (int)min((int64_t)kWRows, (int64_t)p.M - r0);
+    const int cb0 = sg * GG::SEG_BLK + ch * F::G;
+    if (row < rows && cb0 < p.nblk) {
+      uint32_t wv[GG::CH_WORDS + 1];
+      const int cbyte = row * GG::ROW_BYTES + ch * GG::CH_BYTES;
+      const uint32_t* src = &sm.a[w][slot][cbyte / 4];
+      if constexpr (GG::CH_BYTES % 4 != 0) {
+        const int sh = (cbyte & 3) * 8;
+#pragma unroll
+        for (int c = 0; c < GG::CH_WORDS; ++c) wv[c] = __builtin_amdgcn_alignbit(src[c + 1], src[c], sh);
+      } else if constexpr (GG::CH_BYTES % 16 == 0) {
+#pragma unroll
+        for (int c = 0; c < GG::CH_WORDS / 4; ++c) {
+          const u32x4 x = *(const u32x4*)&src[4 * c];
+          wv[4 * c] = x[0]; wv[4 * c + 1] = x[1]; wv[4 * c + 2] = x[2]; wv[4 * c + 3] = x[3];
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < GG::CH_WORDS; ++c) wv[c] = src[c];
+      }
+      wv[GG::CH_WORDS] = 0;
+      chunk_dot<T, NC, 0>(wv, sm.b[sg], ch, min(F::G, p.nblk - cb0), ncols, acc);
+    }
+    if (sg == nseg - 1) {
+      float o[NC];
+#pragma unroll
+      for (int j = 0; j < NC; ++j) {
+        float x = acc[j];
+        x += __shfl_xor(x, 8);
+        x += __shfl_xor(x, 4);
+        x += __shfl_xor(x, 2);
+        x += __shfl_xor(x, 1);
+        o[j] = x;
+      }
+      if (ch == 0 && row < rows) {
+#pragma unroll
+        for (int j = 0; j < NC; ++j)
+          if (j < ncols) Cz[(int64_t)j * p.ldc + r0 + row] = o[j];
+      }
+    }
+  }
+}
+
+template <int T, int NC, int WAVES, int NS, int NSEG>
+hipError_t launch_seg_dma(const GemvArgs& p, hipStream_t s) {
+  const size_t lds = sizeof(SmemSegD<T, NC, WAVES, NS, NSEG>);
+  const int ngroups = (p.M + kWRows - 1) / kWRows;
+  const int slices = p.ne12 * p.ne13;
+  int gx = 256 / slices;
+  const int gmax = (ngroups + WAVES - 1) / WAVES;
+  gx = gx < 1 ? 1 : (gx > gmax ? gmax : gx);
+  (void)hipFuncSetAttribute((const void*)gemv_seg_dma_kernel<T, NC, WAVES, NS, NSEG>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL((gemv_seg_dma_kernel<T, NC, WAVES, NS, NSEG>), dim3(gx, slices), dim3(64 * WAVES), lds, s, p);
+  return hipGetLastError();
+}
+
 // ---- flattened LDS-DMA streaming kernel: one workgroup per CU over ALL slices -----------
 // With one 149 KiB workgroup per CU, a (groups-per-slice x slices) grid cannot match 256 CUs
 // (33 slices -> 7 workgroups each = 231 busy CUs).  Here the (slice, group) list is flattened
 // and cut into exactly one contiguous range per workgroup; a range spans at most two slices
 // (the launcher guarantees it), whose activation rows are both staged in LDS.
-template <int T, int NC>
-struct alignas(16) BPart {   // 16-byte aligned: b[1]'s bq is read with ds_read_b128
-  using GG = Geo<T>;
-  uint32_t bq[NC][GG::BQ_WORDS];
-  float bd[NC][(T == kF32 || T == kF16) ? 1 : GG::VBLK];
-  float bx[NC][(T == kF32 || T == kF16) ? 1 : GG::VBLK];
-  int bs[NC][Fmt<T>::VQK == 256 ? GG::VBLK * 16 : 1];
-};
-
 template <int T, int NC, int WAVES, int NS>
 struct SmemFlat {
   uint32_t a[WAVES][NS][WGeo<T>::SLOT / 4];
@@ -988,6 +1129,13 @@ hipError_t launch_t(const GemvArgs& p, hipStream_t s) {
       if (v == 12 && launch_flat_dma<T, NC, 8, 2>(p, s, &e)) return e;
       return launch_stream_dma<T, NC, 8, 2>(p, s);
     }
+  }
+  // single-column decode with 2-3 K-segments (e.g. ffn_down K = 11008): the multi-segment
+  // DMA streaming kernel (8 waves x 2 slots + 3 staged activation segments <= 160 KiB);
+  // LAMM_GEMV_VARIANT=13 forces the LDS-staged segment kernel for A/B
+  if constexpr (NC == 1 && T != kQ2_K && sizeof(SmemSegD<T, NC, 8, 2, 3>) <= 160 * 1024) {
+    const int nseg = (p.nblk + Geo<T>::SEG_BLK - 1) / Geo<T>::SEG_BLK;
+    if (nseg > 1 && nseg <= 3 && v == 0) return launch_seg_dma<T, NC, 8, 2, 3>(p, s);
   }
   if constexpr (stream_fits<T, NC, 4>() && (Fmt<T>::VQK != 256 || NC == 1)) {
     if (p.nblk <= Geo<T>::SEG_BLK && (v == 0 || v == 10)) return launch_stream<T, NC>(p, s);

@@ -333,6 +333,29 @@ def test_full_size_gemv_4096(t):
     assert rel_err(c, ref, absdot(t, A_q, B_q, M, N, K)).max() < TOL
 
 
+SEG_KS = [4096 + 256, 11008, 12288, 12288 + 256]   # 2, 3 (ragged), 3 and 4 K-segments
+
+
+@pytest.mark.parametrize("variant", ["0", "13"], ids=["segdma", "staged"])
+@pytest.mark.parametrize("K", SEG_KS)
+@pytest.mark.parametrize("t", ol.A_TYPES + ol.KQ_TYPES, ids=[ol.NAMES[t] for t in ol.A_TYPES + ol.KQ_TYPES])
+def test_decode_multi_segment_k(t, K, variant, monkeypatch):
+    """Single-column decode with K beyond one 4096-element segment (ffn_down's K = 11008):
+    the multi-segment LDS-DMA kernel (default, 2-3 segments) and the LDS-staged segment
+    kernel (LAMM_GEMV_VARIANT=13) against the oracle; ragged M (133 = 33 groups of 4 + 1)."""
+    monkeypatch.setenv("LAMM_GEMV_VARIANT", variant)
+    M, N = 133, 1
+    if t in ol.KQ_TYPES:
+        rng = np.random.default_rng(K + t)
+        A_q = ol.random_kq_blocks(t, M, K, rng)
+        B_q = ORACLE.quantize(ol.Q8_K, rng.standard_normal((N, K), dtype=np.float32))
+    else:
+        A_q, B_q = random_case(t, M, N, K, seed=K + t)
+    c, _ = gpu_mul_mat(t, A_q, B_q, M, N, K)
+    ref = ORACLE.mul_mat(t, M, N, K, A_q, B_q)
+    assert rel_err(c, ref, absdot(t, A_q, B_q, M, N, K)).max() < TOL
+
+
 def test_extreme_quants():
     """All-max / all-min quants (int8 -128/127 in B, nibble 0/15 in A): the exact
     int32 block dots must not saturate (v_dot4 without clamp)."""

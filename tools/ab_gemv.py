@@ -18,7 +18,8 @@ import bench  # noqa: E402
 def main():
     variants = (sys.argv[1] if len(sys.argv) > 1 else "0,8,9").split(",")
     fmt = os.environ.get("FMT", "q4_0")
-    M = K = 4096
+    M = int(os.environ.get("MM", "4096"))
+    K = int(os.environ.get("KK", "4096"))
     t = la.BY_NAME[fmt]
     vt = la.vec_dot_type(t)
     u = bench.gemv_bytes(la, fmt, M, K)
@@ -56,7 +57,7 @@ def main():
         med = sorted(res[v])[len(res[v]) // 2]
         summary[v] = {"median_us": round(med, 2), "TBs": round(sl * u / (med * 1e-6) / 1e12, 3),
                       "equal_to_v0": bool(torch.equal(outs[v], outs[variants[0]]))}
-    print(json.dumps({"fmt": fmt, "slices": sl, "variants": summary}), flush=True)
+    print(json.dumps({"fmt": fmt, "M": M, "K": K, "slices": sl, "variants": summary}), flush=True)
 
 
 if __name__ == "__main__":

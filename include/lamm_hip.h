@@ -107,7 +107,10 @@ int lamm_hip_matmul_batched(const lamm_matrix *A, const lamm_matrix *B, const la
  * the GPU): x[N][K] f32 (row j at x + j*ldx floats) -> y, N rows of `vec_type`
  * blocks (row j at y + j*ldy blocks).  flavour 0 = *_reference rounding
  * (roundf), 1 = the AVX2 from_float rounding (nearest-even, id = 127/amax).
- * vec_type: q8_0, q8_1, q8_K, or f16 (ggml_fp32_to_fp16_row, nearest-even). */
+ * vec_type: q8_0, q8_1, q8_K, or f16 (ggml_fp32_to_fp16_row, nearest-even).
+ * Weight types (src0 side, ggml_quantize_chunk LC/ggml.c:20413 with no importance
+ * matrix): q4_0, q4_1, q5_0, q5_1, q2_K, q4_K, q5_K, q6_K reproduce the bytes of the
+ * *_reference row quantizers (flavour ignored); q8_0 weights = q8_0 with flavour 0. */
 int lamm_hip_quantize(int vec_type, int flavour, const float *x, int64_t ldx, void *y,
                       int64_t ldy, int K, int N, void *hip_stream);
 

@@ -209,7 +209,7 @@ struct Smem3 {
 // NBUF = 2: the next K-step's DMA is in flight during this one's unpack + MFMA.
 // V: ablations (1 no MFMA phase, 2 no unpack, 3 no DMA) for tools/ab_gemm.py.
 template <int T, int NBUF, int V>
-__device__ __forceinline__ void gemm3_body(const GemvArgs& p, const unsigned char* ws) {
+__device__ __forceinline__ void gemm3_body(const GemvArgs& p, const unsigned char* ws, int nsplit, float* part) {
   using C = G3<T>;
   using S = Smem3<T, NBUF>;
   constexpr int ABPB = C::ABPB;
@@ -224,10 +224,15 @@ __device__ __forceinline__ void gemm3_body(const GemvArgs& p, const unsigned cha
   const int wj = w >> 1, wi = w & 1;
   const int jb = 32 * wj, ib = 32 * wi;
   const int64_t i0 = (int64_t)blockIdx.x * TI, j0 = (int64_t)blockIdx.y * TJ;
-  const int z = blockIdx.z, i12 = z % p.ne12, i13 = z / p.ne12;
+  // blockIdx.z = split * slices + slice: split sp runs K-steps [k0, k1) and writes its partial
+  // tile to part[sp][z] (summed in split order by launch_splitk_reduce); nsplit 1 writes C
+  const int nz = p.ne12 * p.ne13, z = (int)blockIdx.z % nz, sp = (int)blockIdx.z / nz;
+  const int i12 = z % p.ne12, i13 = z / p.ne12;
   const unsigned char* Az = p.A + (int64_t)(i12 / p.r2) * p.sa2 + (int64_t)(i13 / p.r3) * p.sa3 + i0 * p.lda;
   const unsigned char* wsz = ws + (int64_t)z * L.slice_bytes;
-  float* Cz = p.C + (int64_t)i12 * p.sc2 + (int64_t)i13 * p.sc3;
+  float* Cz = nsplit == 1 ? p.C + (int64_t)i12 * p.sc2 + (int64_t)i13 * p.sc3
+                          : part + ((int64_t)sp * nz + z) * p.N * p.M;
+  const int64_t ldc = nsplit == 1 ? p.ldc : p.M;
   const int rowsA = (int)min((int64_t)TI, (int64_t)p.M - i0);
   const int rowsB = (int)min((int64_t)TJ, (int64_t)p.N - j0);
 
@@ -281,12 +286,12 @@ __device__ __forceinline__ void gemm3_body(const GemvArgs& p, const unsigned cha
 #pragma unroll
   for (int e = 0; e < 16; ++e) { acc[e] = 0.f; macc[e] = 0.f; }
 
-  const int nsteps = L.nsteps;
-  if (V != 3) issue(0, 0);
-  if (NBUF == 2 && V != 3 && nsteps > 1) issue(1, 1);
-  for (int ks = 0; ks < nsteps; ++ks) {
-    const int buf = NBUF == 2 ? (ks & 1) : 0;
-    wait_step(ks + 1 < nsteps);
+  const int k0 = (int)((int64_t)sp * L.nsteps / nsplit), k1 = (int)((int64_t)(sp + 1) * L.nsteps / nsplit);
+  if (V != 3) issue(k0, 0);
+  if (NBUF == 2 && V != 3 && k1 - k0 > 1) issue(k0 + 1, 1);
+  for (int ks = k0; ks < k1; ++ks) {
+    const int buf = NBUF == 2 ? ((ks - k0) & 1) : 0;
+    wait_step(ks + 1 < k1);
     raw_barrier();                                   // step ks's DMA visible to all waves
     // ---- unpack the weight tile (one (row, block) item per thread) ----
     if (V != 2) {
@@ -353,20 +358,20 @@ __device__ __forceinline__ void gemm3_body(const GemvArgs& p, const unsigned cha
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);              // this wave's LDS reads are done
     raw_barrier();                                   // nobody reads buf / wt any more
-    if (V != 3 && ks + NBUF < nsteps) issue(ks + NBUF, buf);
+    if (V != 3 && ks + NBUF < k1) issue(ks + NBUF, buf);
   }
 
   const int64_t i = i0 + ib + lr;
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
     const int64_t j = j0 + jb + (e & 3) + 8 * (e >> 2) + 4 * h;
-    if (i < p.M && j < p.N) Cz[j * p.ldc + i] = 0.5f * acc[e] + (AFF ? macc[e] : 0.f);
+    if (i < p.M && j < p.N) Cz[j * ldc + i] = 0.5f * acc[e] + (AFF ? macc[e] : 0.f);
   }
 }
 
 template <int T, int NBUF, int V = 0>
-__global__ __launch_bounds__(GT8) void gemm3_kernel(GemvArgs p, const unsigned char* ws) {
-  gemm3_body<T, NBUF, V>(p, ws);
+__global__ __launch_bounds__(GT8) void gemm3_kernel(GemvArgs p, const unsigned char* ws, int nsplit, float* part) {
+  gemm3_body<T, NBUF, V>(p, ws, nsplit, part);
 }
 
 // ------------------------------------------------------------------ q2_K x q8_K
@@ -523,6 +528,27 @@ int gemm_variant() {   // A/B and ablation switch for tools/ab_gemm.py; 0 in pro
   return e ? atoi(e) : 0;
 }
 
+// K-splits of the i8 GEMM: its 64x128 tiles have no other way to fill 256 CUs on a small grid
+// (one 4096 x 128 GEMM = 64 tiles); double until 256 workgroups, >= 4 K-steps (32 blocks) per
+// split, at most 16.  LAMM_I8_SPLIT=n forces n (A/B).
+int i8_nsplit(const GemvArgs& p) {
+  const PrepLayout L = PrepLayout::of(p);
+  const int tiles = ((p.M + TI - 1) / TI) * ((p.N + TJ - 1) / TJ) * p.ne12 * p.ne13;
+  const char* e = getenv("LAMM_I8_SPLIT");
+  int n = 1;
+  if (e && atoi(e) > 0) {
+    n = atoi(e);
+  } else {
+    while (tiles * n < 256 && n < 16 && L.nsteps / (2 * n) >= 4) n *= 2;
+  }
+  return n < 1 ? 1 : (n > L.nsteps ? L.nsteps : n);
+}
+
+size_t i8_part_offset(const GemvArgs& p) {
+  const PrepLayout L = PrepLayout::of(p);
+  return ((size_t)(p.ne12 * p.ne13) * (size_t)L.slice_bytes + 255) & ~(size_t)255;
+}
+
 template <int T>
 hipError_t launch_v3(const GemvArgs& p, void* ws, hipStream_t s) {
   constexpr int VBPB = GF<T>::VBPB;
@@ -533,12 +559,15 @@ hipError_t launch_v3(const GemvArgs& p, void* ws, hipStream_t s) {
     hipLaunchKernelGGL((prep_act_kernel<VBPB>), dim3((unsigned)((items + 255) / 256), p.ne12 * p.ne13), dim3(256), 0,
                        s, p, static_cast<unsigned char*>(ws));
   constexpr int NB = 2;
-  const dim3 grid((unsigned)((p.M + TI - 1) / TI), (unsigned)((p.N + TJ - 1) / TJ), (unsigned)(p.ne12 * p.ne13));
+  const int nsplit = i8_nsplit(p);
+  float* part = reinterpret_cast<float*>(static_cast<unsigned char*>(ws) + i8_part_offset(p));
+  const dim3 grid((unsigned)((p.M + TI - 1) / TI), (unsigned)((p.N + TJ - 1) / TJ),
+                  (unsigned)(p.ne12 * p.ne13 * nsplit));
   const auto* wsc = static_cast<const unsigned char*>(ws);
   auto go = [&](auto kern, size_t lds_bytes = 0) {
     const size_t lds = lds_bytes ? lds_bytes : sizeof(Smem3<T, NB>);
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(kern, grid, dim3(GT8), lds, s, p, wsc);
+    hipLaunchKernelGGL(kern, grid, dim3(GT8), lds, s, p, wsc, nsplit, part);
   };
   switch (gemm_variant()) {
     case 1: go(gemm3_kernel<T, NB, 1>); break;
@@ -548,6 +577,7 @@ hipError_t launch_v3(const GemvArgs& p, void* ws, hipStream_t s) {
     case 5: go(gemm3_kernel<T, 1, 0>, sizeof(Smem3<T, 1>)); break;   // single-buffered
     default: go(gemm3_kernel<T, NB, 0>);
   }
+  if (nsplit > 1 && gemm_variant() != 4) launch_splitk_reduce(p, nsplit, part, s);
   return hipGetLastError();
 }
 
@@ -566,8 +596,9 @@ bool gemm_args_ok(int type, const GemvArgs& p) {
 
 size_t gemm_workspace_bytes(int type, const GemvArgs& p) {
   if (type == kQ2_K) return 0;
-  const PrepLayout L = PrepLayout::of(p);
-  return (size_t)(p.ne12 * p.ne13) * (size_t)L.slice_bytes + 256;
+  const int nsplit = i8_nsplit(p);
+  const size_t part = nsplit > 1 ? (size_t)nsplit * p.ne12 * p.ne13 * (size_t)p.N * p.M * sizeof(float) : 0;
+  return i8_part_offset(p) + part + 256;
 }
 
 hipError_t launch_gemm(int type, const GemvArgs& p, void* ws, hipStream_t s) {

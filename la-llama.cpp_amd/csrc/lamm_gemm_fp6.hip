@@ -554,7 +554,8 @@ void launch_splitk_reduce(const GemvArgs& p, int nsplit, const float* part, hipS
 namespace {
 
 // K-splits for a grid of `tiles` workgroups: double until 256 CUs have one each, keeping
-// >= 8 K-steps per split.  LAMM_FP6_SPLIT=n forces n (A/B).
+// >= 8 K-steps per split, at most 16 (K=11008, 16 tiles: 8 splits 247, 16 splits 288, 21
+// splits 230 TFLOP/s, profiles/r01/ab_driver_split.txt).  LAMM_FP6_SPLIT=n forces n (A/B).
 int f6_nsplit(const GemvArgs& p, const F6Layout& L) {
   const char* e = getenv("LAMM_FP6_SPLIT");
   const int tiles = L.nit * L.njt * p.ne12 * p.ne13;
@@ -562,7 +563,7 @@ int f6_nsplit(const GemvArgs& p, const F6Layout& L) {
   if (e && atoi(e) > 0) {
     n = atoi(e);
   } else {
-    while (tiles * n < 256 && n < 8 && L.nsteps / (2 * n) >= 8) n *= 2;
+    while (tiles * n < 256 && n < 16 && L.nsteps / (2 * n) >= 8) n *= 2;
   }
   return n < 1 ? 1 : (n > L.nsteps ? L.nsteps : n);
 }

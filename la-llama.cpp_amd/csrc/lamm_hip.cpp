@@ -115,7 +115,10 @@ bool getenv_flag0(const char* name) {
 // resident) the fp6 kernel's K-split fills the chip from 64 tiles up and wins there too
 // (profiles/r01/ab_stationary.txt: one 4096x512x4096 slice 44.4 us at 4 splits vs 48.2 us
 // on i8; two slices 65.1 vs 88.1); per call, re-packing the weights costs it that margin on
-// a single slice (53.8 vs 47.9).  LAMM_GEMM_PATH=fp6 / i8 forces one (A/B measurements).
+// a single slice (53.8 vs 47.9).  Both engines split K on small grids: la-benchmark-matmult's
+// own shape K=11008, M=4096, N=128 (64 i8 tiles, 16 fp6 tiles) measures 231 TFLOP/s on i8 at 4
+// splits (93 unsplit), 199 on fp6 re-packing per call at 16 splits, 286 with the packed weights
+// resident (profiles/r01/ab_driver_split.txt).  LAMM_GEMM_PATH=fp6 / i8 forces one (A/B).
 int gemm_path(const GemvArgs& p, bool stationary) {
   const char* e = getenv("LAMM_GEMM_PATH");
   if (e && (!strcmp(e, "i8") || !strcmp(e, "1"))) return 1;
@@ -307,13 +310,15 @@ extern "C" int lamm_hip_matmul(const lamm_matrix* A, const lamm_matrix* B, const
 
 extern "C" int lamm_hip_quantize(int vec_type, int flavour, const float* x, int64_t ldx, void* y,
                                  int64_t ldy, int K, int N, void* hip_stream) {
-  if (vec_type != kQ8_0 && vec_type != kQ8_1 && vec_type != kQ8_K && vec_type != kF16)
+  const bool wq = quantize_weights_supported(vec_type);
+  if (!wq && vec_type != kQ8_0 && vec_type != kQ8_1 && vec_type != kQ8_K && vec_type != kF16)
     return fail(LAMM_ERR_TYPE, "quantize: unsupported type %d", vec_type);
   if (K % block_elems(vec_type)) return fail(LAMM_ERR_SHAPE, "quantize: K %% block != 0");
   if (((uintptr_t)x & 15) || (ldx & 3)) return fail(LAMM_ERR_ALIGN, "quantize: x must be 16B aligned, ldx %% 4 == 0");
   if (probe().count == 0) return fail(LAMM_ERR_NODEV, "no gfx950 device");
-  hipError_t e = launch_quantize(vec_type, flavour, x, ldx, y, ldy * (int64_t)block_bytes(vec_type), K, N,
-                                 static_cast<hipStream_t>(hip_stream));
+  const int64_t ldyb = ldy * (int64_t)block_bytes(vec_type);
+  hipError_t e = wq ? launch_quantize_weights(vec_type, x, ldx, y, ldyb, K, N, static_cast<hipStream_t>(hip_stream))
+                    : launch_quantize(vec_type, flavour, x, ldx, y, ldyb, K, N, static_cast<hipStream_t>(hip_stream));
   if (e != hipSuccess) return fail(LAMM_ERR_HIP, "quantize launch: %s", hipGetErrorString(e));
   return LAMM_OK;
 }

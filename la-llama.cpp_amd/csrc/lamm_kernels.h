@@ -38,6 +38,11 @@ bool gemm_dense_supported(int type);
 // C (slice z, row j, col i) = sum_{s < nsplit} part[s][z][j][i] in split order (deterministic)
 void launch_splitk_reduce(const GemvArgs& p, int nsplit, const float* part, hipStream_t s);
 
+// weight quantizers (lamm_quantize_w.hip): ggml_quantize_chunk's *_reference row quantizers
+bool quantize_weights_supported(int type);
+hipError_t launch_quantize_weights(int type, const float* x, int64_t ldx, void* y, int64_t ldy_bytes, int K, int M,
+                                   hipStream_t s);
+
 hipError_t launch_gemm(int type, const GemvArgs& p, void* workspace, hipStream_t s);
 size_t gemm_workspace_bytes(int type, const GemvArgs& p);   // device scratch launch_gemm needs
 bool gemm_supported(int type);

@@ -238,7 +238,8 @@ def quantize_torch(vtype, x, y, flavour=1, stream=None):
 def gemm_engine(fmt, M, N, K, slices=1, stationary=False):
     """Which prefill engine lamm_hip_matmul* picks for N > 8 (mirrors gemm_path() in
     csrc/lamm_hip.cpp): "fp6" (q4_0/q4_1/q5_0 when its 256x128 tiles fill >= 256 CUs -- or,
-    for stationary weights (la.Weights), its tiles x K-splits do), "i8" otherwise; LAMM_GEMM_PATH overrides."""
+    for stationary weights (la.Weights), its tiles x K-splits do), "i8" (K-split on small grids)
+    otherwise; LAMM_GEMM_PATH overrides."""
     t = BY_NAME[fmt] if isinstance(fmt, str) else fmt
     if N <= 8:
         return "gemv"
@@ -254,15 +255,14 @@ def gemm_engine(fmt, M, N, K, slices=1, stationary=False):
     if env in ("fp6", "0"):
         return "fp6"
     tiles = -(-M // 256) * -(-N // 128) * slices
-    if stationary:   # f6_nsplit(): double until 256 workgroups, >= 8 K-steps per split
-        nsteps = -(-(K // 32) // 2)
-        split = int(os.environ.get("LAMM_FP6_SPLIT", "0") or 0)
-        if split <= 0:
-            split = 1
-            while tiles * split < 256 and split < 8 and nsteps // (2 * split) >= 8:
-                split *= 2
-        tiles *= max(1, min(split, nsteps))
-    return "fp6" if tiles >= 256 else "i8"
+    nsteps = -(-(K // 32) // 2)
+    split = int(os.environ.get("LAMM_FP6_SPLIT", "0") or 0)
+    if split <= 0:   # f6_nsplit(): double until 256 workgroups, >= 8 K-steps per split, <= 16
+        split = 1
+        while tiles * split < 256 and split < 16 and nsteps // (2 * split) >= 8:
+            split *= 2
+    grid = tiles * max(1, min(split, nsteps))
+    return "fp6" if (grid if stationary else tiles) >= 256 else "i8"
 
 
 def can_mul_mat(params, dst):

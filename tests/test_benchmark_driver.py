@@ -1,0 +1,52 @@
+"""la-benchmark-matmult (la-llama.cpp_amd/driver/la_benchmark_matmult.cpp): the reference's
+benchmark CLI and output contract, run on the GPU through liblamm_hip.so.
+
+Mirrors the reference's own harness: test/test_correctness.py:10-34 (every dtype under the
+LAMM_DEBUG shape, pass = exit code 0, the binary aborts when the sum of C is off by > 1e-2)
+and test/test_matmult_performance.py:28-55 (the `Average <gflops>` line, regex :42)."""
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "la-llama.cpp_amd", "la-benchmark-matmult")
+DTYPES = ["f32", "f16", "q2_k", "q4_0", "q4_1", "q4_k", "q5_0", "q5_1", "q5_k", "q6_k", "q8_0"]
+AVERAGE = re.compile(r"\nAverage\s*(\d+\.\d+)\n")   # test/test_matmult_performance.py:42
+
+
+def run(*args, timeout=180):
+    return subprocess.run([BIN, *args], capture_output=True, text=True, timeout=timeout)
+
+
+def test_driver_cli_without_gpu():
+    """-h prints the usage and exits 1; an unknown dtype is rejected like the reference (:74-83)."""
+    assert os.path.exists(BIN), "run `make -C la-llama.cpp_amd` (or __graft_entry__.build())"
+    r = run("-h")
+    assert r.returncode == 1 and "--dtype" in r.stderr and "--iter" in r.stderr
+    r = run("-d", "q3_k")
+    assert r.returncode == 1 and "Unknonw type name: q3_k" in r.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", DTYPES)
+def test_driver_debug_shape_correct(dtype):
+    """test_correctness.py: --debug (K=4096, M=33, N=18, srand(0) inputs), exit code 0."""
+    r = run("--debug", "-d", dtype, "-t", "1", "-i", "2")
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "ABORT" not in r.stdout
+    assert AVERAGE.search(r.stdout), r.stdout[-1000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("extra", [[], ["-s"]], ids=["plain", "stationary"])
+def test_driver_default_shape_average(extra):
+    """test_matmult_performance.py: the default shape (K=11008, M=4096, N=128), the
+    per-iteration table and a positive Average GFLOPS."""
+    r = run("-d", "q4_0", "-t", "4", "-i", "3", *extra)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    m = AVERAGE.search(r.stdout)
+    assert m and float(m.group(1)) > 0
+    rows = [ln for ln in r.stdout.splitlines() if re.match(r"\s+\d+;\s+4;", ln)]
+    assert len(rows) == 3 and all("; 11008;  4096;   128;" in ln for ln in rows), rows

@@ -461,7 +461,7 @@ __device__ __forceinline__ void kq_barrier() {
 
 template <int T>
 __global__ __launch_bounds__(KQ_T) void gemm_kq_kernel(GemvArgs p, const unsigned char* wsA,
-                                                       const unsigned char* wsB) {
+                                                       const unsigned char* wsB, int nsplit, float* part) {
   constexpr bool MIN = KQ<T>::MIN;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const KQLayout L = KQLayout::of(p);
@@ -469,7 +469,10 @@ __global__ __launch_bounds__(KQ_T) void gemm_kq_kernel(GemvArgs p, const unsigne
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int lr = lane & 31, h = lane >> 5;
   const int wj = w >> 1, wi = w & 1;
-  const int it = blockIdx.x, jt = blockIdx.y, z = blockIdx.z;
+  // blockIdx.z = split * slices + slice: split sp runs super-blocks [k0, k1) and writes a
+  // partial tile (summed in split order by launch_splitk_reduce); nsplit 1 writes C
+  const int nz = p.ne12 * p.ne13, z = (int)blockIdx.z % nz, sp = (int)blockIdx.z / nz;
+  const int it = blockIdx.x, jt = blockIdx.y;
   const int i12 = z % p.ne12, i13 = z / p.ne12;
   const int ne02 = p.ne12 / p.r2, a = (i12 / p.r2) + (i13 / p.r3) * ne02;
   const unsigned char* ga = wsA + ((int64_t)a * L.nit + it) * L.nsb * KQC_A;
@@ -498,11 +501,12 @@ __global__ __launch_bounds__(KQ_T) void gemm_kq_kernel(GemvArgs p, const unsigne
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[r][e] = 0.f;
 
-  issue(0);
-  if (nsb > 1) issue(1);
+  const int k0 = (int)((int64_t)sp * nsb / nsplit), k1 = (int)((int64_t)(sp + 1) * nsb / nsplit);
+  issue(k0);
+  if (k1 - k0 > 1) issue(k0 + 1);
   const int ia = 32 * wi + lr;
-  for (int sb = 0; sb < nsb; ++sb) {
-    if (sb + 1 < nsb) kq_wait_vm<KQ_PPW>(); else kq_wait_vm<0>();
+  for (int sb = k0; sb < k1; ++sb) {
+    if (sb + 1 < k1) kq_wait_vm<KQ_PPW>(); else kq_wait_vm<0>();
     kq_barrier();   // step sb's chunks visible to every wave
     const unsigned char* sA = smem + (sb & 1) * (KQC_A + KQC_B);
     const unsigned char* sB = sA + KQC_A;
@@ -552,18 +556,40 @@ __global__ __launch_bounds__(KQ_T) void gemm_kq_kernel(GemvArgs p, const unsigne
       }
     }
     kq_barrier();   // every wave is done with buffer sb & 1
-    if (sb + 2 < nsb) issue(sb + 2);
+    if (sb + 2 < k1) issue(sb + 2);
   }
 
-  float* Cz = p.C + (int64_t)i12 * p.sc2 + (int64_t)i13 * p.sc3;
+  float* Cz = nsplit == 1 ? p.C + (int64_t)i12 * p.sc2 + (int64_t)i13 * p.sc3
+                          : part + ((int64_t)sp * nz + z) * p.N * p.M;
+  const int64_t ldc = nsplit == 1 ? p.ldc : p.M;
   const int64_t i = (int64_t)it * KQ_TI + ia;
 #pragma unroll
   for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int64_t j = (int64_t)jt * KQ_TJ + 64 * wj + 32 * rt + (r & 3) + 8 * (r >> 2) + 4 * h;
-      if (i < p.M && j < p.N) Cz[j * p.ldc + i] = acc[rt][r];
+      if (i < p.M && j < p.N) Cz[j * ldc + i] = acc[rt][r];
     }
+}
+
+// K-splits (in super-blocks) for small grids, e.g. one 4096 x 128 GEMM = 64 tiles: double until
+// 256 workgroups, >= 4 super-blocks per split, at most 16.  LAMM_KQ_SPLIT=n forces n (A/B).
+int kq_nsplit(const GemvArgs& p) {
+  const KQLayout L = KQLayout::of(p);
+  const int tiles = L.nit * L.njt * p.ne12 * p.ne13;
+  const char* e = getenv("LAMM_KQ_SPLIT");
+  int n = 1;
+  if (e && atoi(e) > 0) {
+    n = atoi(e);
+  } else {
+    while (tiles * n < 256 && n < 16 && L.nsb / (2 * n) >= 4) n *= 2;
+  }
+  return n < 1 ? 1 : (n > L.nsb ? L.nsb : n);
+}
+
+size_t kq_part_offset(const GemvArgs& p, bool prepared) {
+  const KQLayout L = KQLayout::of(p);
+  return ((prepared ? 0 : (size_t)L.a_bytes) + (size_t)(p.ne12 * p.ne13) * (size_t)L.b_slice + 255) & ~(size_t)255;
 }
 
 template <int T>
@@ -586,9 +612,12 @@ hipError_t launch_kq(const GemvArgs& p, const void* prepA, void* ws, hipStream_t
   constexpr size_t lds = 2 * (KQC_A + KQC_B);
   static_assert(lds <= 160 * 1024, "LDS");
   (void)hipFuncSetAttribute((const void*)gemm_kq_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(gemm_kq_kernel<T>, dim3((unsigned)L.nit, (unsigned)L.njt, (unsigned)(p.ne12 * p.ne13)),
+  const int nsplit = kq_nsplit(p);
+  float* part = reinterpret_cast<float*>(w + kq_part_offset(p, prepA != nullptr));
+  hipLaunchKernelGGL(gemm_kq_kernel<T>, dim3((unsigned)L.nit, (unsigned)L.njt, (unsigned)(p.ne12 * p.ne13 * nsplit)),
                      dim3(KQ_T), lds, s, p, prepA ? static_cast<const unsigned char*>(prepA) : wsA,
-                     static_cast<const unsigned char*>(wsB));
+                     static_cast<const unsigned char*>(wsB), nsplit, part);
+  if (nsplit > 1) launch_splitk_reduce(p, nsplit, part, s);
   return hipGetLastError();
 }
 
@@ -603,8 +632,9 @@ size_t gemm_kq_weight_bytes(int type, const GemvArgs& p) {
 
 size_t gemm_kq_workspace_bytes(int type, const GemvArgs& p, bool prepared) {
   (void)type;
-  const KQLayout L = KQLayout::of(p);
-  return (prepared ? 0 : (size_t)L.a_bytes) + (size_t)(p.ne12 * p.ne13) * (size_t)L.b_slice + 256;
+  const int nsplit = kq_nsplit(p);
+  const size_t part = nsplit > 1 ? (size_t)nsplit * p.ne12 * p.ne13 * (size_t)p.N * p.M * sizeof(float) : 0;
+  return kq_part_offset(p, prepared) + part + 256;
 }
 
 hipError_t prepare_kq_weights(int type, const GemvArgs& p, void* wsA, hipStream_t s) {

@@ -582,3 +582,32 @@ def test_weight_slice_beyond_2gib(engine, monkeypatch):
         assert rel_err(got, ref, absdot(t, a_rows, B_q, 64, N, K)).max() < TOL, r0
     del A, C
     torch.cuda.empty_cache()
+
+
+SPLIT_TYPES = [ol.Q4_0, ol.Q5_1, ol.Q8_0, ol.Q4_K, ol.Q6_K, ol.Q2_K]
+
+
+@pytest.mark.parametrize("split", ["0", "1", "3", "16"])
+@pytest.mark.parametrize("t", SPLIT_TYPES, ids=[ol.NAMES[t] for t in SPLIT_TYPES])
+def test_gemm_split_k_i8_and_superblock(t, split, monkeypatch):
+    """K-split of the MFMA-i8 (LAMM_I8_SPLIT) and super-block (LAMM_KQ_SPLIT) GEMMs, on a
+    la-benchmark-matmult-like shape (K = 11008, the reference's default; one 64-row tile
+    column so the auto policy splits): uneven splits, partials summed in split order, padded
+    C pitch left untouched."""
+    monkeypatch.setenv("LAMM_GEMM_PATH", "i8")
+    monkeypatch.setenv("LAMM_I8_SPLIT", split)
+    monkeypatch.setenv("LAMM_KQ_SPLIT", split)
+    M, N, K = 200, 130, 11008
+    rng = np.random.default_rng(int(split) * 31 + t)
+    if t in ol.KQ_TYPES:
+        A_q = ol.random_kq_blocks(t, M, K, rng)
+    else:
+        A_q = ORACLE.quantize(t, rng.standard_normal((M, K), dtype=np.float32))
+    vt = ORACLE.vec_dot_type(t)
+    B_q = ORACLE.quantize(vt, rng.standard_normal((N, K), dtype=np.float32),
+                          ol.QUANT_AVX if vt in (ol.Q8_0, ol.Q8_1) else 0)
+    kb = K // la.blck_size(t)
+    c, raw = gpu_mul_mat(t, A_q, B_q, M, N, K, lda=pitch_blocks(t, kb), ldc=M + 3)
+    ref = ORACLE.mul_mat(t, M, N, K, A_q, B_q)
+    assert rel_err(c, ref, absdot(t, A_q, B_q, M, N, K)).max() < TOL
+    assert np.isnan(np.concatenate([raw[j * (M + 3) + M:(j + 1) * (M + 3)] for j in range(N)])).all()

@@ -80,7 +80,10 @@ enum lamm_status {
  * A: weights (f32/q4_0/q4_1/q5_0/q5_1/q8_0/q2_K, + f16/q4_K/q5_K/q6_K), A.col = K/blck,
  *    A.ld >= A.col.
  * B: activations of type vec_dot_type(A.type) (f32/q8_0/q8_1/q8_K/f16), column j at
- *    B.data + j*B.ld blocks, B.row = A.col.
+ *    B.data + j*B.ld blocks, B.row = A.col.  For A in q4_0/q4_1/q5_0/q5_1/q8_0 and
+ *    B.col <= 8, B may instead be the F32 rows (B.row = K elements, B.ld in floats): the
+ *    decode GEMV quantizes them while staging (ggml's INIT with the AVX2 from_float
+ *    rounding), giving exactly the C of lamm_hip_quantize(.., flavour 1, ..) + matmul.
  * C: f32, C.ld >= C.row.   Returns a lamm_status.  Asynchronous on hip_stream.
  * Loads are range-checked per dword: A and B must be readable up to the next
  * 4-byte boundary past their last byte (always true for hipMalloc / torch memory). */

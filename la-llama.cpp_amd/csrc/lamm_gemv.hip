@@ -77,11 +77,67 @@ struct Smem {
 };
 
 // ---- stage the activation segment (decoded) into LDS --------------------------
+// ggml's INIT quantization of F32 activations (AVX2 from_float flavour: d = amax/127,
+// id = 127/amax, round-half-even; q8_1 also s = fp16(d * sum q)), done per 32-block while
+// staging B, so a decode GEMV needs no separate quantize launch.  Produces exactly the bytes
+// quant_q8_32<.., flavour 1> writes (lamm_quantize.hip), then the same LDS image stage_b
+// builds from them: quads, fp32(fp16 d), and sum q (q8_0) or fp32(fp16 s) (q8_1).
+template <int T, int NC, class SM>
+__device__ __forceinline__ void stage_b_f32(SM& sm, const GemvArgs& p, const unsigned char* Bz, int seg) {
+  using GG = Geo<T>;
+  using F = Fmt<T>;
+  const int64_t bbytes = (int64_t)(p.N - 1) * p.ldb + (int64_t)p.K * 4;
+  const auto rs = make_rsrc(Bz, (uint32_t)min(bbytes, (int64_t)0x7fffffff));
+  for (int it = threadIdx.x; it < NC * GG::VBLK; it += kThreads) {
+    const int j = it / GG::VBLK, bi = it % GG::VBLK;
+    const int gb = seg * GG::VBLK + bi;
+    const bool ok = j < p.N && gb * 32 < p.K;
+    const uint32_t off = ok ? (uint32_t)(j * p.ldb + (int64_t)gb * 128) : 0x7ffffff0u;
+    float x[32];
+#pragma unroll
+    for (int k = 0; k < 32; ++k) x[k] = __builtin_bit_cast(float, bload4(rs, off + 4 * k));
+    float amax = 0.f;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) amax = fmaxf(amax, fabsf(x[k]));
+    const float d = amax / 127.f;
+    const float id = amax != 0.0f ? 127.f / amax : 0.0f;
+    int sum = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      uint32_t qw = 0;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        int r = (int)__builtin_rintf(x[4 * k + e] * id);
+        r = r > 127 ? 127 : (r < -128 ? -128 : r);
+        sum += r;
+        qw |= (uint32_t)(r & 0xff) << (8 * e);
+      }
+      sm.bq[j][swz(bi * 8 + k)] = qw;
+    }
+    float dh = d;
+    asm volatile("" : "+v"(dh));   // keep the fp16 round trip a separate conversion
+    sm.bd[j][bi] = (float)(_Float16)dh;
+    if constexpr (F::VBPB == 36) {
+      float sd = (float)sum * d;
+      asm volatile("" : "+v"(sd));
+      sm.bx[j][bi] = (float)(_Float16)sd;
+    } else {
+      sm.bx[j][bi] = (float)sum;
+    }
+  }
+}
+
 template <int T, int NC, class SM>
 __device__ __forceinline__ void stage_b(SM& sm, const GemvArgs& p, const unsigned char* Bz, int seg) {
   using GG = Geo<T>;
   using F = Fmt<T>;
   const int t = threadIdx.x;
+  if constexpr (T != kF32 && T != kF16 && F::VQK == 32) {
+    if (p.b_f32) {   // F32 rows quantized here: quant_q8_32 flavour 1 (lamm_quantize.hip)
+      stage_b_f32<T, NC>(sm, p, Bz, seg);
+      return;
+    }
+  }
   const int64_t bbytes = (int64_t)(p.N - 1) * p.ldb + (int64_t)(p.K / F::VQK) * F::VBPB;
   // range-checked per dword: round up so a dword straddling the logical end is read
   // (allocations are readable to the next 4-byte boundary: include/lamm_hip.h)

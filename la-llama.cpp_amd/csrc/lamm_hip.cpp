@@ -160,14 +160,20 @@ int matmul_impl(const lamm_matrix* A, const lamm_matrix* B, const lamm_matrix* C
                 void* hip_stream, const lamm_weights* W) {
   if (!A || !B || !C) return fail(LAMM_ERR_SHAPE, "null matrix");
   if (!is_weight_type(A->type)) return fail(LAMM_ERR_TYPE, "unsupported A type %d", A->type);
-  if (B->type != vec_dot_type(A->type))
-    return fail(LAMM_ERR_TYPE, "B type %d is not vec_dot_type(%d)=%d", B->type, A->type, vec_dot_type(A->type));
+  // F32 activations for a q8_0 / q8_1 weight type (N <= 8): ggml's INIT quantization runs
+  // inside the GEMV launch (stage_b_f32, AVX2 flavour), bit-exact with lamm_hip_quantize + matmul
+  const int vdt = vec_dot_type(A->type);
+  const bool b_f32 = B->type == kF32 && (vdt == kQ8_0 || vdt == kQ8_1);
+  if (B->type != vdt && !(b_f32 && B->col <= 8))
+    return fail(LAMM_ERR_TYPE, "B type %d is not vec_dot_type(%d)=%d%s", B->type, A->type, vdt,
+                b_f32 ? " (F32 activations only for N <= 8)" : "");
   if (C->type != kF32) return fail(LAMM_ERR_TYPE, "C must be f32");
   const int M = A->row, N = B->col, Kb = A->col;
-  if (M < 0 || N < 0 || Kb < 0 || B->row != Kb || C->row != M || C->col != N)
+  const int brows = b_f32 ? Kb * block_elems(A->type) : Kb;   // B.row: K in blocks of B's own type
+  if (M < 0 || N < 0 || Kb < 0 || B->row != brows || C->row != M || C->col != N)
     return fail(LAMM_ERR_SHAPE, "shape mismatch A(%d,%d) B(%d,%d) C(%d,%d)", A->row, A->col, B->row, B->col,
                 C->row, C->col);
-  if (A->ld < Kb || (N > 1 && B->ld < Kb) || (N > 1 && C->ld < M))
+  if (A->ld < Kb || (N > 1 && B->ld < brows) || (N > 1 && C->ld < M))
     return fail(LAMM_ERR_SHAPE, "leading dimension too small");
   lamm_batch bt{1, 1, 1, 1, 0, 0, 0, 0, 0, 0};
   if (batch) bt = *batch;
@@ -200,6 +206,7 @@ int matmul_impl(const lamm_matrix* A, const lamm_matrix* B, const lamm_matrix* C
   p.sb3 = (int64_t)bt.nbb3;
   p.sc2 = (int64_t)(bt.nbc2 / 4);
   p.sc3 = (int64_t)(bt.nbc3 / 4);
+  p.b_f32 = b_f32 ? 1 : 0;
   hipError_t e;
   if (N <= 8) {
     e = launch_gemv(A->type, p, s);

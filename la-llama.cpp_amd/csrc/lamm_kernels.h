@@ -18,6 +18,9 @@ struct GemvArgs {
   int ne12 = 1, ne13 = 1, r2 = 1, r3 = 1;
   int64_t sa2 = 0, sa3 = 0, sb2 = 0, sb3 = 0;   // bytes
   int64_t sc2 = 0, sc3 = 0;                     // floats
+  // GEMV only, q8_0 / q8_1 activations: B holds F32 rows (ldb in bytes) that the kernel
+  // quantizes while staging them (ggml's INIT fused into the launch, AVX2 flavour, bit-exact)
+  int b_f32 = 0;
 };
 
 hipError_t launch_gemv(int type, const GemvArgs& p, hipStream_t s);

@@ -1,0 +1,289 @@
+// llama-matmul-bench: the weight-matmul workload of one Llama-7B step (BASELINE config 5's
+// model) through liblamm_hip.so, on one GPU.
+//
+// What llama.cpp-b2430 sends to the lamm hook per token step (build_llama
+// LC/llama.cpp:5708-5830): per layer wq, wk, wv, wo (4096 x 4096), ffn_gate, ffn_up
+// (11008 x 4096), ffn_down (4096 x 11008), each preceded by the INIT quantization of its F32
+// activations (LC/ggml.c:10865-10887; wq/wk/wv share one, as do gate/up), and per step the
+// Q6_K output.weight (32000 x 4096: llama.cpp's quant policy for Q4_0 models,
+// LC/llama.cpp:11731-11742).  This tool runs exactly that sequence of lamm_hip_quantize +
+// lamm_hip_matmul calls over 32 layers of distinct synthetic weights (quantized on the GPU
+// from random F32 values), captured once into a hipGraph and replayed.  It is NOT the whole
+// model: attention (F16 KV-cache matmuls, softmax), RMSNorm, RoPE, SiLU and the residual adds
+// are left out, so the result is an upper bound on tok/s set by the weight matmuls (which
+// the reference's profiling puts at > 90 % of CPU inference time, README.md:150).
+// Each matmul's input is the previous matmul's output (re-quantized), as in the model.
+//
+// usage: llama-matmul-bench [-d q4_0] [-n tokens per step] [-i replays] [-l layers]
+//                           [--no-graph] [-s] [--output-type q6_k] [--unfused]
+// Single-token decode steps (N = 1) hand the F32 activations of q8_0/q8_1-typed weights straight to the
+// GEMV, which quantizes them while staging (bit-exact with the separate quantizer);
+// --unfused runs the separate lamm_hip_quantize launches instead.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <strings.h>
+#include <vector>
+
+#include "lamm_hip.h"
+
+namespace {
+
+void hip_ok(hipError_t e, const char* what) {
+  if (e != hipSuccess) {
+    fprintf(stderr, "llama-matmul-bench: %s: %s\n", what, hipGetErrorString(e));
+    exit(1);
+  }
+}
+void lamm_ok(int rc, const char* what) {
+  if (rc != LAMM_OK) {
+    fprintf(stderr, "llama-matmul-bench: %s failed (%d): %s\n", what, rc, lamm_hip_last_error());
+    exit(1);
+  }
+}
+
+struct DType { const char* name; int type; };
+const DType kTypes[] = {{"f16", 1},  {"q2_k", 10}, {"q4_0", 2},  {"q4_1", 3}, {"q4_k", 12},
+                        {"q5_0", 6}, {"q5_1", 7},  {"q5_k", 13}, {"q6_k", 14}, {"q8_0", 8}};
+const char* type_name(int t) {
+  for (const DType& d : kTypes)
+    if (d.type == t) return d.name;
+  return "?";
+}
+int parse_type(const char* s) {
+  for (const DType& d : kTypes)
+    if (strcasecmp(s, d.name) == 0) return d.type;
+  fprintf(stderr, "llama-matmul-bench: unknown type %s\n", s);
+  exit(1);
+}
+
+// one weight tensor on the device (rows of `type` blocks, 16-byte aligned pitch)
+struct Tensor {
+  int type = 0, M = 0, K = 0, kb = 0;
+  int64_t ld = 0;
+  void* data = nullptr;
+  lamm_weights* handle = nullptr;
+  size_t bytes() const { return (size_t)ld * lamm_type_size(type) * M; }
+};
+
+// random F32 values (fixed LCG) quantized on the GPU into `copies` distinct tensors
+std::vector<Tensor> make_weights(int type, int M, int K, int copies, bool stationary, hipStream_t s) {
+  std::vector<float> h((size_t)M * K);
+  uint32_t st = 0x9e3779b9u ^ (uint32_t)(M * 131 + K);
+  for (float& v : h) {
+    st = st * 1664525u + 1013904223u;
+    v = ((int)(st >> 9) - (1 << 22)) * (1.0f / (1 << 22));   // uniform in [-1, 1)
+  }
+  const float amp = std::sqrt(3.0f / K);   // unit gain per matmul: activations stay O(1) over 32 layers
+  for (float& v : h) v *= amp;
+  float* dx = nullptr;
+  hip_ok(hipMalloc(&dx, h.size() * 4), "hipMalloc");
+  hip_ok(hipMemcpy(dx, h.data(), h.size() * 4, hipMemcpyHostToDevice), "upload");
+  std::vector<Tensor> out;
+  for (int c = 0; c < copies; ++c) {
+    Tensor t;
+    t.type = type;
+    t.M = M;
+    t.K = K;
+    t.kb = K / lamm_blck_size(type);
+    t.ld = t.kb;
+    while ((t.ld * lamm_type_size(type)) % 16) ++t.ld;
+    hip_ok(hipMalloc(&t.data, t.bytes() + 256), "hipMalloc(weights)");
+    lamm_ok(lamm_hip_quantize(type, 0, dx, K, t.data, t.ld, K, M, s), "lamm_hip_quantize(weights)");
+    if (stationary) {
+      lamm_matrix A{t.data, type, M, t.kb, t.ld};
+      lamm_ok(lamm_hip_weights_create(&A, 1, 1, 0, 0, s, &t.handle), "lamm_hip_weights_create");
+    }
+    out.push_back(t);
+  }
+  hip_ok(hipStreamSynchronize(s), "quantize weights");
+  hip_ok(hipFree(dx), "hipFree");
+  return out;
+}
+
+struct Act {   // F32 activations [N][K] and their vec_dot-typed copy
+  float* x = nullptr;
+  void* q = nullptr;
+  int K = 0;
+};
+
+struct Model {
+  int N = 1;
+  std::vector<Tensor> wq, wk, wv, wo, w1, w3, w2, out;
+  Act a4096, b4096, c4096, a11008;
+  float *q, *k, *v, *o, *g, *u, *d, *logits;
+};
+
+bool g_fused = true;   // decode (N <= 8): F32 activations straight into the GEMV (INIT fused)
+
+bool fused(int wtype, int N) {
+  const int vt = lamm_vec_dot_type(wtype);
+  // one column only: with 8 columns every workgroup re-quantizes 8 rows before its first
+  // dot and the step gets slower (3.87 -> 4.66 ms at N = 8; N = 1: 2.05 -> 1.89 ms)
+  return g_fused && N == 1 && (vt == 8 || vt == 9);
+}
+
+void quantize(int wtype, Act& a, int N, hipStream_t s) {
+  const int vt = lamm_vec_dot_type(wtype);
+  if (vt == 0 || fused(wtype, N)) return;
+  lamm_ok(lamm_hip_quantize(vt, 1, a.x, a.K, a.q, a.K / lamm_blck_size(vt), a.K, N, s), "lamm_hip_quantize(act)");
+}
+
+void matmul(const Tensor& w, const Act& a, float* C, int N, hipStream_t s) {
+  const int vt = lamm_vec_dot_type(w.type);
+  lamm_matrix B{vt == 0 ? (void*)a.x : a.q, vt, w.kb, N, (int64_t)(a.K / lamm_blck_size(vt))};
+  if (fused(w.type, N)) B = lamm_matrix{a.x, 0, a.K, N, (int64_t)a.K};
+  lamm_matrix Cm{C, 0, w.M, N, w.M};
+  if (w.handle) {
+    lamm_ok(lamm_hip_matmul_weights(w.handle, &B, &Cm, nullptr, s), "lamm_hip_matmul_weights");
+  } else {
+    lamm_matrix A{w.data, w.type, w.M, w.kb, w.ld};
+    lamm_ok(lamm_hip_matmul(&A, &B, &Cm, s), "lamm_hip_matmul");
+  }
+}
+
+// one token step: the mul_mat nodes of build_llama in graph order
+void step(Model& m, int layers, hipStream_t s) {
+  const int N = m.N;
+  for (int l = 0; l < layers; ++l) {
+    quantize(m.wq[l].type, m.a4096, N, s);           // attn_norm output -> wq / wk / wv
+    matmul(m.wq[l], m.a4096, m.q, N, s);
+    matmul(m.wk[l], m.a4096, m.k, N, s);
+    matmul(m.wv[l], m.a4096, m.v, N, s);
+    quantize(m.wo[l].type, m.b4096, N, s);           // kqv_out (here: the q projection) -> wo
+    matmul(m.wo[l], m.b4096, m.o, N, s);
+    quantize(m.w1[l].type, m.c4096, N, s);           // ffn_norm output (here: wo's) -> gate / up
+    matmul(m.w1[l], m.c4096, m.g, N, s);
+    matmul(m.w3[l], m.c4096, m.u, N, s);
+    quantize(m.w2[l].type, m.a11008, N, s);          // silu(gate) * up (here: up) -> ffn_down
+    matmul(m.w2[l], m.a11008, m.d, N, s);
+  }
+  quantize(m.out[0].type, m.a4096, N, s);            // result_norm -> output.weight
+  matmul(m.out[0], m.a4096, m.logits, N, s);
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  int type = 2, N = 1, iters = 20, layers = 32, out_type = 14;
+  bool graph = true, stationary = false;
+  for (int i = 1; i < argc; ++i) {
+    const std::string a = argv[i];
+    auto next = [&]() -> const char* {
+      if (++i >= argc) { fprintf(stderr, "missing value for %s\n", a.c_str()); exit(1); }
+      return argv[i];
+    };
+    if (a == "-d") type = parse_type(next());
+    else if (a == "-n") N = atoi(next());
+    else if (a == "-i") iters = atoi(next());
+    else if (a == "-l") layers = atoi(next());
+    else if (a == "--output-type") out_type = parse_type(next());
+    else if (a == "--no-graph") graph = false;
+    else if (a == "-s") stationary = true;
+    else if (a == "--unfused") g_fused = false;
+    else {
+      fprintf(stderr, "usage: %s [-d q4_0] [-n tokens] [-i replays] [-l layers] [--no-graph] [-s] [--output-type q6_k] [--unfused]\n",
+              argv[0]);
+      return 1;
+    }
+  }
+  if (lamm_hip_device_count() <= 0) {
+    fprintf(stderr, "llama-matmul-bench: no gfx950 device (%s)\n", lamm_hip_last_error());
+    return 1;
+  }
+  constexpr int H = 4096, F = 11008, V = 32000;
+  hipStream_t s;
+  hip_ok(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
+  Model m;
+  m.N = N;
+  m.wq = make_weights(type, H, H, layers, stationary, s);
+  m.wk = make_weights(type, H, H, layers, stationary, s);
+  m.wv = make_weights(type, H, H, layers, stationary, s);
+  m.wo = make_weights(type, H, H, layers, stationary, s);
+  m.w1 = make_weights(type, F, H, layers, stationary, s);
+  m.w3 = make_weights(type, F, H, layers, stationary, s);
+  m.w2 = make_weights(type, H, F, layers, stationary, s);
+  m.out = make_weights(out_type, V, H, 1, stationary, s);
+  size_t wbytes = 0;
+  double params = 0;
+  for (auto* v : {&m.wq, &m.wk, &m.wv, &m.wo, &m.w1, &m.w3, &m.w2, &m.out})
+    for (const Tensor& t : *v) {
+      wbytes += (size_t)t.kb * lamm_type_size(t.type) * t.M;
+      params += (double)t.M * t.K;
+    }
+
+  // activations: F32 rows + a vec_dot-typed buffer large enough for any of the formats
+  auto mk_act = [&](Act& a, int K, float* alias) {
+    a.K = K;
+    a.x = alias;
+    hip_ok(hipMalloc(&a.q, (size_t)N * K * 2 + 4096), "hipMalloc(q act)");
+  };
+  auto mk_out = [&](float*& p, int M) {
+    hip_ok(hipMalloc(&p, (size_t)N * M * 4 + 256), "hipMalloc(out)");
+    hip_ok(hipMemset(p, 0, (size_t)N * M * 4 + 256), "hipMemset");
+  };
+  mk_out(m.q, H); mk_out(m.k, H); mk_out(m.v, H); mk_out(m.o, H);
+  mk_out(m.g, F); mk_out(m.u, F); mk_out(m.d, H); mk_out(m.logits, V);
+  {   // the first layer's input: random values in the ffn_down output buffer
+    std::vector<float> h((size_t)N * H);
+    for (size_t i = 0; i < h.size(); ++i) h[i] = std::sin(0.37f * (float)i);
+    hip_ok(hipMemcpy(m.d, h.data(), h.size() * 4, hipMemcpyHostToDevice), "upload x");
+  }
+  mk_act(m.a4096, H, m.d);    // layer input = previous layer's ffn_down output
+  mk_act(m.b4096, H, m.q);
+  mk_act(m.c4096, H, m.o);
+  mk_act(m.a11008, F, m.u);
+
+  printf("llama-matmul-bench: Llama-7B weight matmuls, %d layers, weights %s, output.weight %s, "
+         "%.2f GB of weight blocks, %d token(s) per step, %s%s\n",
+         layers, type_name(type), type_name(out_type), wbytes / 1e9, N, graph ? "hipGraph" : "stream",
+         stationary ? ", weight-stationary handles" : "");
+
+  // warm-up (workspaces reach their final size before capture), then capture one step
+  for (int w = 0; w < 2; ++w) step(m, layers, s);
+  hip_ok(hipStreamSynchronize(s), "warm-up");
+  hipGraphExec_t exec = nullptr;
+  if (graph) {
+    hipGraph_t g;
+    hip_ok(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed), "hipStreamBeginCapture");
+    step(m, layers, s);
+    hip_ok(hipStreamEndCapture(s, &g), "hipStreamEndCapture");
+    hip_ok(hipGraphInstantiate(&exec, g, nullptr, nullptr, 0), "hipGraphInstantiate");
+    hip_ok(hipGraphDestroy(g), "hipGraphDestroy");
+    hip_ok(hipGraphLaunch(exec, s), "hipGraphLaunch");
+    hip_ok(hipStreamSynchronize(s), "graph warm-up");
+  }
+  hipEvent_t e0, e1;
+  hip_ok(hipEventCreate(&e0), "hipEventCreate");
+  hip_ok(hipEventCreate(&e1), "hipEventCreate");
+  hip_ok(hipEventRecord(e0, s), "hipEventRecord");
+  for (int it = 0; it < iters; ++it) {
+    if (graph) hip_ok(hipGraphLaunch(exec, s), "hipGraphLaunch");
+    else step(m, layers, s);
+  }
+  hip_ok(hipEventRecord(e1, s), "hipEventRecord");
+  hip_ok(hipEventSynchronize(e1), "hipEventSynchronize");
+  float ms = 0;
+  hip_ok(hipEventElapsedTime(&ms, e0, e1), "hipEventElapsedTime");
+  const double t = ms * 1e-3 / iters;
+  std::vector<float> lg((size_t)N * V);
+  hip_ok(hipMemcpy(lg.data(), m.logits, lg.size() * 4, hipMemcpyDeviceToHost), "download logits");
+  double cs = 0;
+  for (float v : lg) cs += std::fabs(v);
+  if (!std::isfinite(cs)) {
+    fprintf(stderr, "llama-matmul-bench: non-finite logits\n");
+    return 1;
+  }
+  printf("step %.3f ms  |  %.1f tok/s  |  weight stream %.1f GB/s  |  %.1f TFLOP/s  |  %d matmuls + %d quantizations per step  |  logits |sum| %.4g\n",
+         t * 1e3, N / t, wbytes / t / 1e9, 2.0 * params * N / t / 1e12, 7 * layers + 1,
+         fused(type, N) ? 1 : 4 * layers + 1, cs);
+  printf("{\"tool\": \"llama-matmul-bench\", \"layers\": %d, \"tokens_per_step\": %d, \"ms_per_step\": %.4f, \"tok_per_s\": %.2f, "
+         "\"weight_GBps\": %.1f, \"TFLOPs\": %.2f, \"graph\": %s, \"stationary\": %s, \"type\": \"%s\"}\n",
+         layers, N, t * 1e3, N / t, wbytes / t / 1e9, 2.0 * params * N / t / 1e12, graph ? "true" : "false",
+         stationary ? "true" : "false", type_name(type));
+  return 0;
+}

@@ -611,3 +611,56 @@ def test_gemm_split_k_i8_and_superblock(t, split, monkeypatch):
     ref = ORACLE.mul_mat(t, M, N, K, A_q, B_q)
     assert rel_err(c, ref, absdot(t, A_q, B_q, M, N, K)).max() < TOL
     assert np.isnan(np.concatenate([raw[j * (M + 3) + M:(j + 1) * (M + 3)] for j in range(N)])).all()
+
+
+FUSED_TYPES = [ol.Q4_0, ol.Q4_1, ol.Q5_0, ol.Q5_1, ol.Q8_0]
+FUSED_SHAPES = [(64, 1, 4096), (200, 3, 11008), (37, 8, 96), (130, 5, 4160), (64, 2, 8192 + 512)]
+
+
+@pytest.mark.parametrize("t", FUSED_TYPES, ids=[ol.NAMES[t] for t in FUSED_TYPES])
+@pytest.mark.parametrize("shape", FUSED_SHAPES, ids=[f"{m}x{n}x{k}" for m, n, k in FUSED_SHAPES])
+def test_decode_gemv_f32_activations_fused(t, shape):
+    """F32 activations straight into the decode GEMV (ggml's INIT quantization fused into the
+    launch): C must be BIT-identical to lamm_hip_quantize(flavour 1) + matmul on the same
+    rows -- every GEMV kernel (stream, LDS-DMA, multi-segment, segmented) -- and match the
+    oracle on the reference's quantized bytes."""
+    M, N, K = shape
+    rng = np.random.default_rng(M + 7 * N + K + t)
+    A_q = ORACLE.quantize(t, rng.standard_normal((M, K), dtype=np.float32))
+    x = rng.standard_normal((N, K), dtype=np.float32)
+    x[0, :32] = 0.0                                   # an all-zero block (d = 0)
+    ldx = K + 4                                        # padded F32 rows (NaN padding)
+    xp = np.full((N, ldx), np.nan, np.float32)
+    xp[:, :K] = x
+    kb = K // 32
+    lda = pitch_blocks(t, kb)
+    dA = dev_bytes(pitched_A(t, A_q, M, kb, lda))
+    dx = torch.from_numpy(xp.reshape(-1)).cuda()
+    s = torch.cuda.current_stream().cuda_stream
+    c1 = torch.full((N * M,), np.nan, dtype=torch.float32, device="cuda")
+    la.matmul(la.Matrix(dA.data_ptr(), t, M, kb, lda), la.Matrix(dx.data_ptr(), la.F32, K, N, ldx),
+              la.Matrix(c1.data_ptr(), la.F32, M, N, M), s)
+    vt = ORACLE.vec_dot_type(t)
+    dq = torch.zeros(N * la.row_bytes(vt, K) + 64, dtype=torch.uint8, device="cuda")
+    la.quantize_torch(vt, dx.view(N, ldx)[:, :K], dq, flavour=1)
+    c2 = torch.full((N * M,), np.nan, dtype=torch.float32, device="cuda")
+    la.matmul(la.Matrix(dA.data_ptr(), t, M, kb, lda), la.Matrix(dq.data_ptr(), vt, kb, N, kb),
+              la.Matrix(c2.data_ptr(), la.F32, M, N, M), s)
+    torch.cuda.synchronize()
+    a, b = c1.cpu().numpy(), c2.cpu().numpy()
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    B_q = ORACLE.quantize(vt, x, ol.QUANT_AVX)
+    assert np.array_equal(dq.cpu().numpy()[:B_q.size], B_q)
+    ref = ORACLE.mul_mat(t, M, N, K, A_q, B_q)
+    assert rel_err(a.reshape(N, M), ref, absdot(t, A_q, B_q, M, N, K)).max() < TOL
+
+
+def test_f32_activations_rejected_beyond_decode():
+    """F32 B is a decode (N <= 8) form only; wider calls must pass quantized rows."""
+    t, M, K, N = ol.Q4_0, 64, 256, 9
+    dA = torch.zeros(M * (K // 32) * 18 + 64, dtype=torch.uint8, device="cuda")
+    dx = torch.zeros(N * K, dtype=torch.float32, device="cuda")
+    c = torch.zeros(N * M, dtype=torch.float32, device="cuda")
+    with pytest.raises(la.LammError):
+        la.matmul(la.Matrix(dA.data_ptr(), t, M, K // 32, K // 32), la.Matrix(dx.data_ptr(), la.F32, K, N, K),
+                  la.Matrix(c.data_ptr(), la.F32, M, N, M), 0)

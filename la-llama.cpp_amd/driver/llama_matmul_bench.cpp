@@ -15,7 +15,10 @@
 // Each matmul's input is the previous matmul's output (re-quantized), as in the model.
 //
 // usage: llama-matmul-bench [-d q4_0] [-n tokens per step] [-i replays] [-l layers]
-//                           [--no-graph] [-s] [--output-type q6_k] [--unfused]
+//                           [--no-graph] [-s] [--output-type q6_k] [--unfused] [--batch-proj]
+// --batch-proj stores wq|wk|wv and ffn_gate|ffn_up as slices of one tensor each and runs each
+// group as ONE lamm_hip_matmul_batched launch against the shared input (B slice stride 0):
+// 4 launches per layer instead of 7 (a GPU-native layout; llama.cpp-b2430 issues 7 mul_mats).
 // Single-token decode steps (N = 1) hand the F32 activations of q8_0/q8_1-typed weights straight to the
 // GEMV, which quantizes them while staging (bit-exact with the separate quantizer);
 // --unfused runs the separate lamm_hip_quantize launches instead.
@@ -63,15 +66,16 @@ int parse_type(const char* s) {
 
 // one weight tensor on the device (rows of `type` blocks, 16-byte aligned pitch)
 struct Tensor {
-  int type = 0, M = 0, K = 0, kb = 0;
+  int type = 0, M = 0, K = 0, kb = 0, slices = 1;   // slices: projections sharing one input
   int64_t ld = 0;
   void* data = nullptr;
   lamm_weights* handle = nullptr;
-  size_t bytes() const { return (size_t)ld * lamm_type_size(type) * M; }
+  size_t bytes() const { return (size_t)ld * lamm_type_size(type) * M; }   // one slice
 };
 
 // random F32 values (fixed LCG) quantized on the GPU into `copies` distinct tensors
-std::vector<Tensor> make_weights(int type, int M, int K, int copies, bool stationary, hipStream_t s) {
+std::vector<Tensor> make_weights(int type, int M, int K, int copies, bool stationary, hipStream_t s,
+                                 int slices = 1) {
   std::vector<float> h((size_t)M * K);
   uint32_t st = 0x9e3779b9u ^ (uint32_t)(M * 131 + K);
   for (float& v : h) {
@@ -89,14 +93,17 @@ std::vector<Tensor> make_weights(int type, int M, int K, int copies, bool statio
     t.type = type;
     t.M = M;
     t.K = K;
+    t.slices = slices;
     t.kb = K / lamm_blck_size(type);
     t.ld = t.kb;
     while ((t.ld * lamm_type_size(type)) % 16) ++t.ld;
-    hip_ok(hipMalloc(&t.data, t.bytes() + 256), "hipMalloc(weights)");
-    lamm_ok(lamm_hip_quantize(type, 0, dx, K, t.data, t.ld, K, M, s), "lamm_hip_quantize(weights)");
+    hip_ok(hipMalloc(&t.data, t.bytes() * slices + 256), "hipMalloc(weights)");
+    for (int z = 0; z < slices; ++z)
+      lamm_ok(lamm_hip_quantize(type, 0, dx, K, (char*)t.data + z * t.bytes(), t.ld, K, M, s),
+              "lamm_hip_quantize(weights)");
     if (stationary) {
       lamm_matrix A{t.data, type, M, t.kb, t.ld};
-      lamm_ok(lamm_hip_weights_create(&A, 1, 1, 0, 0, s, &t.handle), "lamm_hip_weights_create");
+      lamm_ok(lamm_hip_weights_create(&A, slices, 1, t.bytes(), 0, s, &t.handle), "lamm_hip_weights_create");
     }
     out.push_back(t);
   }
@@ -138,11 +145,13 @@ void matmul(const Tensor& w, const Act& a, float* C, int N, hipStream_t s) {
   lamm_matrix B{vt == 0 ? (void*)a.x : a.q, vt, w.kb, N, (int64_t)(a.K / lamm_blck_size(vt))};
   if (fused(w.type, N)) B = lamm_matrix{a.x, 0, a.K, N, (int64_t)a.K};
   lamm_matrix Cm{C, 0, w.M, N, w.M};
+  // slices > 1: one batched launch, every weight slice against the same B (B slice stride 0)
+  const lamm_batch bt{w.slices, 1, w.slices, 1, w.bytes(), 0, 0, 0, (size_t)N * w.M * 4, 0};
   if (w.handle) {
-    lamm_ok(lamm_hip_matmul_weights(w.handle, &B, &Cm, nullptr, s), "lamm_hip_matmul_weights");
+    lamm_ok(lamm_hip_matmul_weights(w.handle, &B, &Cm, &bt, s), "lamm_hip_matmul_weights");
   } else {
     lamm_matrix A{w.data, w.type, w.M, w.kb, w.ld};
-    lamm_ok(lamm_hip_matmul(&A, &B, &Cm, s), "lamm_hip_matmul");
+    lamm_ok(lamm_hip_matmul_batched(&A, &B, &Cm, &bt, s), "lamm_hip_matmul_batched");
   }
 }
 
@@ -151,14 +160,16 @@ void step(Model& m, int layers, hipStream_t s) {
   const int N = m.N;
   for (int l = 0; l < layers; ++l) {
     quantize(m.wq[l].type, m.a4096, N, s);           // attn_norm output -> wq / wk / wv
-    matmul(m.wq[l], m.a4096, m.q, N, s);
-    matmul(m.wk[l], m.a4096, m.k, N, s);
-    matmul(m.wv[l], m.a4096, m.v, N, s);
+    matmul(m.wq[l], m.a4096, m.q, N, s);             // --batch-proj: wq holds wq | wk | wv
+    if (m.wq[l].slices == 1) {
+      matmul(m.wk[l], m.a4096, m.k, N, s);
+      matmul(m.wv[l], m.a4096, m.v, N, s);
+    }
     quantize(m.wo[l].type, m.b4096, N, s);           // kqv_out (here: the q projection) -> wo
     matmul(m.wo[l], m.b4096, m.o, N, s);
     quantize(m.w1[l].type, m.c4096, N, s);           // ffn_norm output (here: wo's) -> gate / up
-    matmul(m.w1[l], m.c4096, m.g, N, s);
-    matmul(m.w3[l], m.c4096, m.u, N, s);
+    matmul(m.w1[l], m.c4096, m.g, N, s);             // --batch-proj: w1 holds gate | up
+    if (m.w1[l].slices == 1) matmul(m.w3[l], m.c4096, m.u, N, s);
     quantize(m.w2[l].type, m.a11008, N, s);          // silu(gate) * up (here: up) -> ffn_down
     matmul(m.w2[l], m.a11008, m.d, N, s);
   }
@@ -170,7 +181,7 @@ void step(Model& m, int layers, hipStream_t s) {
 
 int main(int argc, char** argv) {
   int type = 2, N = 1, iters = 20, layers = 32, out_type = 14;
-  bool graph = true, stationary = false;
+  bool graph = true, stationary = false, batch_proj = false;
   for (int i = 1; i < argc; ++i) {
     const std::string a = argv[i];
     auto next = [&]() -> const char* {
@@ -185,8 +196,9 @@ int main(int argc, char** argv) {
     else if (a == "--no-graph") graph = false;
     else if (a == "-s") stationary = true;
     else if (a == "--unfused") g_fused = false;
+    else if (a == "--batch-proj") batch_proj = true;
     else {
-      fprintf(stderr, "usage: %s [-d q4_0] [-n tokens] [-i replays] [-l layers] [--no-graph] [-s] [--output-type q6_k] [--unfused]\n",
+      fprintf(stderr, "usage: %s [-d q4_0] [-n tokens] [-i replays] [-l layers] [--no-graph] [-s] [--output-type q6_k] [--unfused] [--batch-proj]\n",
               argv[0]);
       return 1;
     }
@@ -200,20 +212,25 @@ int main(int argc, char** argv) {
   hip_ok(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
   Model m;
   m.N = N;
-  m.wq = make_weights(type, H, H, layers, stationary, s);
-  m.wk = make_weights(type, H, H, layers, stationary, s);
-  m.wv = make_weights(type, H, H, layers, stationary, s);
+  if (batch_proj) {   // q|k|v and gate|up as slices of one tensor each: 4 launches per layer
+    m.wq = make_weights(type, H, H, layers, stationary, s, 3);
+    m.w1 = make_weights(type, F, H, layers, stationary, s, 2);
+  } else {
+    m.wq = make_weights(type, H, H, layers, stationary, s);
+    m.wk = make_weights(type, H, H, layers, stationary, s);
+    m.wv = make_weights(type, H, H, layers, stationary, s);
+    m.w1 = make_weights(type, F, H, layers, stationary, s);
+    m.w3 = make_weights(type, F, H, layers, stationary, s);
+  }
   m.wo = make_weights(type, H, H, layers, stationary, s);
-  m.w1 = make_weights(type, F, H, layers, stationary, s);
-  m.w3 = make_weights(type, F, H, layers, stationary, s);
   m.w2 = make_weights(type, H, F, layers, stationary, s);
   m.out = make_weights(out_type, V, H, 1, stationary, s);
   size_t wbytes = 0;
   double params = 0;
   for (auto* v : {&m.wq, &m.wk, &m.wv, &m.wo, &m.w1, &m.w3, &m.w2, &m.out})
     for (const Tensor& t : *v) {
-      wbytes += (size_t)t.kb * lamm_type_size(t.type) * t.M;
-      params += (double)t.M * t.K;
+      wbytes += (size_t)t.kb * lamm_type_size(t.type) * t.M * t.slices;
+      params += (double)t.M * t.K * t.slices;
     }
 
   // activations: F32 rows + a vec_dot-typed buffer large enough for any of the formats
@@ -226,8 +243,8 @@ int main(int argc, char** argv) {
     hip_ok(hipMalloc(&p, (size_t)N * M * 4 + 256), "hipMalloc(out)");
     hip_ok(hipMemset(p, 0, (size_t)N * M * 4 + 256), "hipMemset");
   };
-  mk_out(m.q, H); mk_out(m.k, H); mk_out(m.v, H); mk_out(m.o, H);
-  mk_out(m.g, F); mk_out(m.u, F); mk_out(m.d, H); mk_out(m.logits, V);
+  mk_out(m.q, 3 * H); mk_out(m.k, H); mk_out(m.v, H); mk_out(m.o, H);
+  mk_out(m.g, 2 * F); mk_out(m.u, F); mk_out(m.d, H); mk_out(m.logits, V);
   {   // the first layer's input: random values in the ffn_down output buffer
     std::vector<float> h((size_t)N * H);
     for (size_t i = 0; i < h.size(); ++i) h[i] = std::sin(0.37f * (float)i);
@@ -236,7 +253,7 @@ int main(int argc, char** argv) {
   mk_act(m.a4096, H, m.d);    // layer input = previous layer's ffn_down output
   mk_act(m.b4096, H, m.q);
   mk_act(m.c4096, H, m.o);
-  mk_act(m.a11008, F, m.u);
+  mk_act(m.a11008, F, batch_proj ? m.g + (size_t)N * F : m.u);   // the up projection's output
 
   printf("llama-matmul-bench: Llama-7B weight matmuls, %d layers, weights %s, output.weight %s, "
          "%.2f GB of weight blocks, %d token(s) per step, %s%s\n",
@@ -278,8 +295,8 @@ int main(int argc, char** argv) {
     fprintf(stderr, "llama-matmul-bench: non-finite logits\n");
     return 1;
   }
-  printf("step %.3f ms  |  %.1f tok/s  |  weight stream %.1f GB/s  |  %.1f TFLOP/s  |  %d matmuls + %d quantizations per step  |  logits |sum| %.4g\n",
-         t * 1e3, N / t, wbytes / t / 1e9, 2.0 * params * N / t / 1e12, 7 * layers + 1,
+  printf("step %.3f ms  |  %.1f tok/s  |  weight stream %.1f GB/s  |  %.1f TFLOP/s  |  %d matmul launches + %d quantizations per step  |  logits |sum| %.4g\n",
+         t * 1e3, N / t, wbytes / t / 1e9, 2.0 * params * N / t / 1e12, (batch_proj ? 4 : 7) * layers + 1,
          fused(type, N) ? 1 : 4 * layers + 1, cs);
   printf("{\"tool\": \"llama-matmul-bench\", \"layers\": %d, \"tokens_per_step\": %d, \"ms_per_step\": %.4f, \"tok_per_s\": %.2f, "
          "\"weight_GBps\": %.1f, \"TFLOPs\": %.2f, \"graph\": %s, \"stationary\": %s, \"type\": \"%s\"}\n",

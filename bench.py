@@ -237,6 +237,26 @@ def cpu_baseline(fmt, M, N, K, budget_s, gemv_unit_bytes):
             "median_us": med * 1e6, "sample": f"{len(ts)} x scalar oracle mul_mat M={M} N={N} K={K}"}
 
 
+def llama_step(fmt):
+    """BASELINE config 5's model on one GPU: the weight matmuls of a Llama-7B step (32 layers x
+    7 projections + the Q6_K output.weight, llama.cpp-b2430's mul_mat sequence) replayed as a
+    hipGraph by la-llama.cpp_amd/llama-matmul-bench, a child process.  Attention, norms and
+    activations are not part of it: tok/s is the bound the weight matmuls set."""
+    exe = os.path.join(ROOT, "la-llama.cpp_amd", "llama-matmul-bench")
+    res = {"note": "weight matmuls only (no attention/norms), synthetic weights, hipGraph replay; "
+                   "decode = 1 token/step (F32 activations fused into the GEMV), prefill = 512 tokens/step "
+                   "with weight-stationary handles; reference: Llama-2-7B Q4_0 on 3A6000 t=4, text-gen "
+                   "4.69 tok/s, prompt 8.27 tok/s (README.md:684,710), whole model"}
+    for name, argv in (("decode_n1", ["-n", "1", "-i", "50"]), ("prefill_n512", ["-n", "512", "-i", "5", "-s"])):
+        try:
+            r = subprocess.run([exe, "-d", fmt] + argv, capture_output=True, text=True, timeout=180)
+            line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+            res[name] = json.loads(line[-1]) if r.returncode == 0 and line else {"error": r.stderr[-300:]}
+        except Exception as e:  # noqa: BLE001 -- reported, never fatal for the main bench line
+            res[name] = {"error": str(e)[:300]}
+    return res
+
+
 def read_traffic(tag):
     p = os.path.join(ROOT, "profiles", f"traffic_{tag}.json")
     if os.path.exists(p):
@@ -258,6 +278,7 @@ def main():
     ap.add_argument("--gemm-N", type=int, default=512)
     ap.add_argument("--no-gemm", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-llama", action="store_true", help="skip the Llama-7B weight-matmul step (config 5 model)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--sweep", action="store_true", help="also time every weight format (config 4)")
     args = ap.parse_args()
@@ -358,6 +379,8 @@ def main():
                 sw[f].update({"gemm_GFLOPS": round(2.0 * M * gN * K / gk / 1e9, 1), "gemm_us": round(gk * 1e6, 2),
                               "gemm_engine": engine})
         out["sweep"] = sw
+    if rank == 0 and world == 1 and not args.no_llama:
+        out["llama7b_matmul_step"] = llama_step(args.fmt)
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.fmt, M, 1, K, args.cpu_budget, unit)
     if world > 1:

@@ -111,7 +111,9 @@ Weights make_weights(const std::vector<float>& host, int type, int M, int K, int
   hip_ok(hipMemcpy(dx, host.data(), host.size() * sizeof(float), hipMemcpyHostToDevice), "upload weights");
   void* first = nullptr;
   hip_ok(hipMalloc(&first, w.bytes + 256), "hipMalloc(weights)");
-  hip_ok(hipMemset(first, 0, w.bytes + 256), "hipMemset");
+  // on s, like the copy / quantizer that fill it: a null-stream hipMemset is not ordered with a
+  // non-blocking stream and could land after them (it once zeroed part of the F32 weights)
+  hip_ok(hipMemsetAsync(first, 0, w.bytes + 256, s), "hipMemsetAsync");
   if (type == 0) {
     hip_ok(hipMemcpy2DAsync(first, w.ld * 4, dx, (size_t)K * 4, (size_t)K * 4, M, hipMemcpyDeviceToDevice, s), "copy f32");
   } else {

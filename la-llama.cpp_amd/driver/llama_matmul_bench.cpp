@@ -241,13 +241,14 @@ int main(int argc, char** argv) {
   };
   auto mk_out = [&](float*& p, int M) {
     hip_ok(hipMalloc(&p, (size_t)N * M * 4 + 256), "hipMalloc(out)");
-    hip_ok(hipMemset(p, 0, (size_t)N * M * 4 + 256), "hipMemset");
+    hip_ok(hipMemsetAsync(p, 0, (size_t)N * M * 4 + 256, s), "hipMemsetAsync");   // ordered on s
   };
   mk_out(m.q, 3 * H); mk_out(m.k, H); mk_out(m.v, H); mk_out(m.o, H);
   mk_out(m.g, 2 * F); mk_out(m.u, F); mk_out(m.d, H); mk_out(m.logits, V);
   {   // the first layer's input: random values in the ffn_down output buffer
     std::vector<float> h((size_t)N * H);
     for (size_t i = 0; i < h.size(); ++i) h[i] = std::sin(0.37f * (float)i);
+    hip_ok(hipStreamSynchronize(s), "memsets");
     hip_ok(hipMemcpy(m.d, h.data(), h.size() * 4, hipMemcpyHostToDevice), "upload x");
   }
   mk_act(m.a4096, H, m.d);    // layer input = previous layer's ffn_down output

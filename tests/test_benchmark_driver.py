@@ -50,3 +50,27 @@ def test_driver_default_shape_average(extra):
     assert m and float(m.group(1)) > 0
     rows = [ln for ln in r.stdout.splitlines() if re.match(r"\s+\d+;\s+4;", ln)]
     assert len(rows) == 3 and all("; 11008;  4096;   128;" in ln for ln in rows), rows
+
+
+LLAMA = os.path.join(ROOT, "la-llama.cpp_amd", "llama-matmul-bench")
+
+
+def test_llama_bench_cli_without_gpu():
+    assert os.path.exists(LLAMA), "run `make -C la-llama.cpp_amd`"
+    r = subprocess.run([LLAMA, "--bogus"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1 and "usage" in r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("args", [["-n", "1"], ["-n", "1", "--unfused"], ["-n", "3", "--batch-proj"],
+                                  ["-n", "20", "-s"], ["-n", "1", "--no-graph", "-d", "q4_k"]],
+                         ids=["decode", "decode-unfused", "n3-batched", "prefill-stationary", "q4k-stream"])
+def test_llama_bench_runs(args):
+    """llama-matmul-bench (2 layers): the hipGraph capture of a whole step works on every path
+    (fused / unfused activation quantization, batched projections, stationary weights, k-quants),
+    and the logits stay finite through the chain of matmuls."""
+    import json
+    r = subprocess.run([LLAMA, "-l", "2", "-i", "3", *args], capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stdout[-1500:] + r.stderr[-1500:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert d["tok_per_s"] > 0 and d["layers"] == 2

@@ -156,6 +156,24 @@ GemvArgs weight_args(const lamm_matrix* A, int64_t ne02, int64_t ne03, size_t nb
   return p;
 }
 
+// Widest activation count the GEMV kernels take; wider calls go to the prefill GEMM engines.
+// The super-block formats' GEMV decodes a whole super-block per lane, and F16 rows carry no
+// block scale to amortise, so their per-column cost grows faster than the matrix cores':
+// measured crossovers (us per 4096 x 4096 slice, stationary weights, > MALL per launch,
+// profiles/r01/gemv_vs_gemm_n.txt): q2_K GEMM from N = 6 (9.69 vs 8.83), q4_K from 7
+// (11.56 vs 10.51), q5_K / q6_K / f16 from 5 (16.67 / 18.56 / 9.63 vs 10.72 / 10.19 / 7.59);
+// the 32-block formats stay on the GEMV up to 8 (q4_0 N = 8: 4.74 vs 6.50).
+// LAMM_GEMV_MAX_N=n overrides (A/B).
+int gemv_max_n(int type) {
+  const char* e = getenv("LAMM_GEMV_MAX_N");
+  int n = 8;
+  if (e) n = atoi(e);
+  else if (type == kQ2_K) n = 5;
+  else if (type == kQ4_K) n = 6;
+  else if (type == kQ5_K || type == kQ6_K || type == kF16) n = 4;
+  return n < 1 ? 1 : (n > 8 ? 8 : n);
+}
+
 int matmul_impl(const lamm_matrix* A, const lamm_matrix* B, const lamm_matrix* C, const lamm_batch* batch,
                 void* hip_stream, const lamm_weights* W) {
   if (!A || !B || !C) return fail(LAMM_ERR_SHAPE, "null matrix");
@@ -208,7 +226,7 @@ int matmul_impl(const lamm_matrix* A, const lamm_matrix* B, const lamm_matrix* C
   p.sc3 = (int64_t)(bt.nbc3 / 4);
   p.b_f32 = b_f32 ? 1 : 0;
   hipError_t e;
-  if (N <= 8) {
+  if (N <= gemv_max_n(A->type) || (b_f32 && N <= 8)) {
     e = launch_gemv(A->type, p, s);
   } else if (gemm_dense_supported(A->type) && !getenv_flag0("LAMM_DENSE_GEMM")) {
     const size_t wsb = gemm_dense_workspace_bytes(A->type, p);
@@ -628,7 +646,7 @@ extern "C" void lamm_mul_mat(const struct ggml_compute_params* vparams, struct g
   pa.ne13 = (int)ne13;
   pa.r2 = (int)(ne12 / ne02);
   pa.r3 = (int)(ne13 / ne03);
-  const bool stationary = N > 8 && ((gemm_fp6_supported(t0) && gemm_path(pa, true) == 0) ||
+  const bool stationary = N > gemv_max_n(t0) && ((gemm_fp6_supported(t0) && gemm_path(pa, true) == 0) ||
                                     (gemm_kq_supported(t0) && !getenv_flag0("LAMM_KQ_GEMM")));
   const int rc = stationary ? lamm_hip_matmul_weights(rt.prepared(w, A, ne02, ne03), &B, &C, &bt, s)
                             : lamm_hip_matmul_batched(&A, &B, &C, &bt, s);

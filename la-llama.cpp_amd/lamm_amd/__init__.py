@@ -241,7 +241,9 @@ def gemm_engine(fmt, M, N, K, slices=1, stationary=False):
     for stationary weights (la.Weights), its tiles x K-splits do), "i8" (K-split on small grids)
     otherwise; LAMM_GEMM_PATH overrides."""
     t = BY_NAME[fmt] if isinstance(fmt, str) else fmt
-    if N <= 8:
+    env_n = os.environ.get("LAMM_GEMV_MAX_N")   # gemv_max_n() in csrc/lamm_hip.cpp
+    max_n = int(env_n) if env_n else {Q2_K: 5, Q4_K: 6, Q5_K: 4, Q6_K: 4, F16: 4}.get(t, 8)
+    if N <= max(1, min(8, max_n)):
         return "gemv"
     if t in (F32, F16):
         return "dense"          # lamm_gemm_dense.hip (LAMM_DENSE_GEMM=0: grouped GEMV)

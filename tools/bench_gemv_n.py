@@ -20,7 +20,7 @@ def main():
     out = {}
     for f in fmts:
         out[f] = {}
-        for N in (1, 2, 4, 8):
+        for N in [int(n) for n in os.environ.get("NS", "1,2,4,8").split(",")]:
             u = bench.gemv_bytes(la, f, M, K, N)
             sl = max(4, -(-int(1.15 * bench.MALL_BYTES) // u))
             _, _, kk = bench.run_case(torch, la, None, f, M, N, K, sl, 10, 2, 1)

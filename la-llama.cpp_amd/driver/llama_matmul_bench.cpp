@@ -19,6 +19,10 @@
 // --batch-proj stores wq|wk|wv and ffn_gate|ffn_up as slices of one tensor each and runs each
 // group as ONE lamm_hip_matmul_batched launch against the shared input (B slice stride 0):
 // 4 launches per layer instead of 7 (a GPU-native layout; llama.cpp-b2430 issues 7 mul_mats).
+// --concurrent keeps llama.cpp's 7 separate tensors but forks wk / wv and ffn_up onto side
+// streams (parallel branches of the captured graph) -- measured SLOWER (decode 1.88 -> 2.14
+// ms): each GEMV grid wants every CU (one 149 KiB-LDS workgroup per CU), so concurrent
+// branches only contend; batching (--batch-proj) is the way to share the launch cost.
 // Single-token decode steps (N = 1) hand the F32 activations of q8_0/q8_1-typed weights straight to the
 // GEMV, which quantizes them while staging (bit-exact with the separate quantizer);
 // --unfused runs the separate lamm_hip_quantize launches instead.
@@ -120,6 +124,9 @@ struct Act {   // F32 activations [N][K] and their vec_dot-typed copy
 
 struct Model {
   int N = 1;
+  // --concurrent: projections that share an input run on forked streams (graph branches)
+  hipStream_t side[2] = {nullptr, nullptr};
+  hipEvent_t fork = nullptr, join[2] = {nullptr, nullptr};
   std::vector<Tensor> wq, wk, wv, wo, w1, w3, w2, out;
   Act a4096, b4096, c4096, a11008;
   float *q, *k, *v, *o, *g, *u, *d, *logits;
@@ -160,16 +167,37 @@ void step(Model& m, int layers, hipStream_t s) {
   const int N = m.N;
   for (int l = 0; l < layers; ++l) {
     quantize(m.wq[l].type, m.a4096, N, s);           // attn_norm output -> wq / wk / wv
-    matmul(m.wq[l], m.a4096, m.q, N, s);             // --batch-proj: wq holds wq | wk | wv
-    if (m.wq[l].slices == 1) {
-      matmul(m.wk[l], m.a4096, m.k, N, s);
-      matmul(m.wv[l], m.a4096, m.v, N, s);
+    if (m.side[0] && m.wq[l].slices == 1) {          // wk / wv on forked streams, joined before wo
+      hip_ok(hipEventRecord(m.fork, s), "hipEventRecord");
+      for (int b = 0; b < 2; ++b) hip_ok(hipStreamWaitEvent(m.side[b], m.fork, 0), "hipStreamWaitEvent");
+      matmul(m.wk[l], m.a4096, m.k, N, m.side[0]);
+      matmul(m.wv[l], m.a4096, m.v, N, m.side[1]);
+      matmul(m.wq[l], m.a4096, m.q, N, s);
+      for (int b = 0; b < 2; ++b) {
+        hip_ok(hipEventRecord(m.join[b], m.side[b]), "hipEventRecord");
+        hip_ok(hipStreamWaitEvent(s, m.join[b], 0), "hipStreamWaitEvent");
+      }
+    } else {
+      matmul(m.wq[l], m.a4096, m.q, N, s);           // --batch-proj: wq holds wq | wk | wv
+      if (m.wq[l].slices == 1) {
+        matmul(m.wk[l], m.a4096, m.k, N, s);
+        matmul(m.wv[l], m.a4096, m.v, N, s);
+      }
     }
     quantize(m.wo[l].type, m.b4096, N, s);           // kqv_out (here: the q projection) -> wo
     matmul(m.wo[l], m.b4096, m.o, N, s);
     quantize(m.w1[l].type, m.c4096, N, s);           // ffn_norm output (here: wo's) -> gate / up
-    matmul(m.w1[l], m.c4096, m.g, N, s);             // --batch-proj: w1 holds gate | up
-    if (m.w1[l].slices == 1) matmul(m.w3[l], m.c4096, m.u, N, s);
+    if (m.side[0] && m.w1[l].slices == 1) {          // ffn_up on a forked stream
+      hip_ok(hipEventRecord(m.fork, s), "hipEventRecord");
+      hip_ok(hipStreamWaitEvent(m.side[0], m.fork, 0), "hipStreamWaitEvent");
+      matmul(m.w3[l], m.c4096, m.u, N, m.side[0]);
+      matmul(m.w1[l], m.c4096, m.g, N, s);
+      hip_ok(hipEventRecord(m.join[0], m.side[0]), "hipEventRecord");
+      hip_ok(hipStreamWaitEvent(s, m.join[0], 0), "hipStreamWaitEvent");
+    } else {
+      matmul(m.w1[l], m.c4096, m.g, N, s);           // --batch-proj: w1 holds gate | up
+      if (m.w1[l].slices == 1) matmul(m.w3[l], m.c4096, m.u, N, s);
+    }
     quantize(m.w2[l].type, m.a11008, N, s);          // silu(gate) * up (here: up) -> ffn_down
     matmul(m.w2[l], m.a11008, m.d, N, s);
   }
@@ -181,7 +209,7 @@ void step(Model& m, int layers, hipStream_t s) {
 
 int main(int argc, char** argv) {
   int type = 2, N = 1, iters = 20, layers = 32, out_type = 14;
-  bool graph = true, stationary = false, batch_proj = false;
+  bool graph = true, stationary = false, batch_proj = false, concurrent = false;
   for (int i = 1; i < argc; ++i) {
     const std::string a = argv[i];
     auto next = [&]() -> const char* {
@@ -197,8 +225,9 @@ int main(int argc, char** argv) {
     else if (a == "-s") stationary = true;
     else if (a == "--unfused") g_fused = false;
     else if (a == "--batch-proj") batch_proj = true;
+    else if (a == "--concurrent") concurrent = true;
     else {
-      fprintf(stderr, "usage: %s [-d q4_0] [-n tokens] [-i replays] [-l layers] [--no-graph] [-s] [--output-type q6_k] [--unfused] [--batch-proj]\n",
+      fprintf(stderr, "usage: %s [-d q4_0] [-n tokens] [-i replays] [-l layers] [--no-graph] [-s] [--output-type q6_k] [--unfused] [--batch-proj] [--concurrent]\n",
               argv[0]);
       return 1;
     }
@@ -212,6 +241,13 @@ int main(int argc, char** argv) {
   hip_ok(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
   Model m;
   m.N = N;
+  if (concurrent) {
+    for (int b = 0; b < 2; ++b) {
+      hip_ok(hipStreamCreateWithFlags(&m.side[b], hipStreamNonBlocking), "hipStreamCreate");
+      hip_ok(hipEventCreateWithFlags(&m.join[b], hipEventDisableTiming), "hipEventCreate");
+    }
+    hip_ok(hipEventCreateWithFlags(&m.fork, hipEventDisableTiming), "hipEventCreate");
+  }
   if (batch_proj) {   // q|k|v and gate|up as slices of one tensor each: 4 launches per layer
     m.wq = make_weights(type, H, H, layers, stationary, s, 3);
     m.w1 = make_weights(type, F, H, layers, stationary, s, 2);

@@ -383,6 +383,12 @@ def main():
         out["llama7b_matmul_step"] = llama_step(args.fmt)
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.fmt, M, 1, K, args.cpu_budget, unit)
+        if not args.no_gemm and "gemm" in out:   # the same reference path at BASELINE config 3
+            cb = cpu_baseline(args.fmt, M, args.gemm_N, K, args.cpu_budget, 0)
+            us = cb["median_us"]
+            out["gemm"]["cpu_baseline"] = {
+                "value": round(2.0 * M * args.gemm_N * K / (us * 1e-6) / 1e9, 2), "unit": "GFLOPS",
+                "cores": cb["cores"], "kind": cb["kind"], "median_us": round(us, 1), "sample": cb["sample"]}
     if world > 1:
         dist.destroy_process_group()
     if rank == 0:

@@ -479,6 +479,17 @@ class Runtime {
     return buf_[which];
   }
 
+  // pinned host staging (grow-only): decode-sized B uploads / C downloads as one DMA each
+  // instead of HIP's pageable-copy path; LAMM_HIP_PINNED=0 turns it off (A/B)
+  unsigned char* pinned(int which, size_t bytes) {
+    if (hcap_[which] < bytes) {
+      if (hbuf_[which]) HIPCHK(hipHostFree(hbuf_[which]));
+      HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&hbuf_[which]), bytes + 256, hipHostMallocDefault));
+      hcap_[which] = bytes;
+    }
+    return hbuf_[which];
+  }
+
   void clear() {
     while (!lru_.empty()) evict(cache_.find(lru_.back()));
   }
@@ -505,7 +516,21 @@ class Runtime {
   std::list<WeightKey> lru_;
   void* buf_[3] = {nullptr, nullptr, nullptr};
   size_t cap_[3] = {0, 0, 0};
+  unsigned char* hbuf_[2] = {nullptr, nullptr};
+  size_t hcap_[2] = {0, 0};
 };
+
+bool use_pinned(size_t bytes) {
+  static const bool on = [] {
+    const char* e = getenv("LAMM_HIP_PINNED");
+    return !(e && e[0] == '0');
+  }();
+  // decode-sized transfers only: through the unchanged ggml (tools/ab_pinned.sh,
+  // profiles/r01/ab_pinned.txt) Q4_0 4096x1x4096 27.7 -> 23.3 us, but N = 8 (128 KiB of C)
+  // 41.8 -> 46 us and N = 512 (8 MiB) 367 -> 691 us: the host-side strided copy out of the
+  // pinned buffer costs more than HIP's own pageable path saves
+  return on && bytes <= ((size_t)32 << 10);
+}
 
 int opt_level() {
   static int lvl = [] {
@@ -626,7 +651,14 @@ extern "C" void lamm_mul_mat(const struct ggml_compute_params* vparams, struct g
       std::abort();
     }
   } else if (use_wdata) {
-    HIPCHK(hipMemcpyAsync(dB, params->wdata, b_row * (size_t)(N * nslices), hipMemcpyHostToDevice, s));
+    const size_t nb = b_row * (size_t)(N * nslices);
+    if (use_pinned(nb)) {
+      unsigned char* hB = rt.pinned(0, nb);
+      memcpy(hB, params->wdata, nb);
+      HIPCHK(hipMemcpyAsync(dB, hB, nb, hipMemcpyHostToDevice, s));
+    } else {
+      HIPCHK(hipMemcpyAsync(dB, params->wdata, nb, hipMemcpyHostToDevice, s));
+    }
   } else {
     HIPCHK(hipMemcpy2DAsync(dB, b_row, src1->data, src1->nb[1], b_row, (size_t)(N * nslices),
                             hipMemcpyHostToDevice, s));
@@ -653,6 +685,18 @@ extern "C" void lamm_mul_mat(const struct ggml_compute_params* vparams, struct g
   if (rc != LAMM_OK) {
     fprintf(stderr, "lamm_hip: lamm_hip_matmul_batched failed (%d): %s\n", rc, g_err.c_str());
     std::abort();
+  }
+  if (use_pinned(c_slice * (size_t)nslices)) {   // one DMA into pinned memory, then strided host copies
+    unsigned char* hC = rt.pinned(1, c_slice * (size_t)nslices);
+    HIPCHK(hipMemcpyAsync(hC, dC, c_slice * (size_t)nslices, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    for (int64_t i13 = 0; i13 < ne13; ++i13)
+      for (int64_t i12 = 0; i12 < ne12; ++i12) {
+        unsigned char* c_host = static_cast<unsigned char*>(dst->data) + i12 * dst->nb[2] + i13 * dst->nb[3];
+        const unsigned char* src = hC + (size_t)(i13 * ne12 + i12) * c_slice;
+        for (int64_t j = 0; j < N; ++j) memcpy(c_host + j * dst->nb[1], src + (size_t)j * M * sizeof(float), M * sizeof(float));
+      }
+    return;
   }
   for (int64_t i13 = 0; i13 < ne13; ++i13)
     for (int64_t i12 = 0; i12 < ne12; ++i12) {

@@ -136,6 +136,8 @@ void lamm_hip_weights_destroy(lamm_weights *W);
 
 const char *lamm_hip_last_error(void);
 int lamm_hip_device_count(void);
+/* Provenance: hash (sha256, 16 hex digits) of the sources this library was built from. */
+const char *lamm_hip_build_id(void);
 
 /* ggml type traits for the supported types (LC/ggml.c:477-775). */
 int lamm_blck_size(int type);

@@ -134,6 +134,10 @@ extern "C" size_t lamm_type_size(int type) { return block_bytes(type); }
 extern "C" int lamm_vec_dot_type(int type) { return vec_dot_type(type); }
 extern "C" const char* lamm_hip_last_error(void) { return g_err.c_str(); }
 extern "C" int lamm_hip_device_count(void) { return probe().count; }
+#ifndef LAMM_BUILD_ID
+#define LAMM_BUILD_ID "unknown"
+#endif
+extern "C" const char* lamm_hip_build_id(void) { return LAMM_BUILD_ID; }
 
 // ======================================================== operator API
 struct lamm_weights {
@@ -366,15 +370,17 @@ struct WeightKey {
   const void* host;
   int type;
   int64_t rows, kb;
-  size_t host_pitch;
+  size_t host_pitch, host_s2, host_s3;   // nb[1], nb[2], nb[3]
   bool operator==(const WeightKey& o) const {
-    return host == o.host && type == o.type && rows == o.rows && kb == o.kb && host_pitch == o.host_pitch;
+    return host == o.host && type == o.type && rows == o.rows && kb == o.kb && host_pitch == o.host_pitch &&
+           host_s2 == o.host_s2 && host_s3 == o.host_s3;
   }
 };
 struct WeightKeyHash {
   size_t operator()(const WeightKey& k) const {
     size_t h = std::hash<const void*>()(k.host);
     h ^= std::hash<int64_t>()(k.rows * 1315423911ll + k.kb * 2654435761ll + k.type) + 0x9e3779b9 + (h << 6);
+    h ^= std::hash<size_t>()(k.host_s2 * 40503u + k.host_s3) + 0x9e3779b9 + (h << 6);
     return h;
   }
 };
@@ -470,6 +476,49 @@ class Runtime {
     return e.prepared;
   }
 
+  // A src0 that is not a weight -- a view of the KV cache or an intermediate -- is uploaded on
+  // EVERY call and never cached: b2430's K/V views keep one data pointer while single token
+  // rows change inside them (llama.cpp:5322-5372 views, :8887 kv_self.n padded to 32), which no
+  // sampled fingerprint can see.  Device layout (pitch, slice strides in bytes):
+  //   rows stacked (nb2 = nb1*ne1, nb3 = nb2*ne2; the transposed V view): one 2D copy;
+  //   dense interleaved slices (the K view: the heads of a token side by side in one cache
+  //     row, nb1 = n_embd_k_gqa*2, nb2 = 256): one linear copy of the byte span, host strides;
+  //   anything else: a 2D copy per slice.
+  struct Transient {
+    void* dev;
+    int64_t pitch;
+    size_t s2, s3;
+  };
+  Transient transient(const ggml::tensor* src0, size_t row_bytes) {
+    const int64_t ne1 = src0->ne[1], ne2 = src0->ne[2], ne3 = src0->ne[3];
+    const size_t nb1 = src0->nb[1], nb2 = src0->nb[2], nb3 = src0->nb[3];
+    const auto* host = static_cast<const unsigned char*>(src0->data);
+    const size_t bpb = block_bytes(src0->type);
+    const size_t span = (size_t)(ne1 - 1) * nb1 + (size_t)(ne2 - 1) * nb2 + (size_t)(ne3 - 1) * nb3 + row_bytes;
+    const size_t payload = row_bytes * (size_t)(ne1 * ne2 * ne3);
+    const bool stacked = nb2 == nb1 * (size_t)ne1 && nb3 == nb2 * (size_t)ne2;
+    if (!stacked && nb1 % 16 == 0 && nb2 % 16 == 0 && nb3 % 16 == 0 && nb1 % bpb == 0 && nb1 >= row_bytes &&
+        span <= 2 * payload) {
+      void* dev = scratch(3, span + 64);
+      HIPCHK(hipMemcpyAsync(dev, host, span, hipMemcpyHostToDevice, stream_));
+      return Transient{dev, (int64_t)nb1, nb2, nb3};
+    }
+    size_t pb = row_bytes / bpb;
+    while ((pb * bpb) % 16) ++pb;
+    const int64_t pitch = (int64_t)(pb * bpb);
+    void* dev = scratch(3, (size_t)pitch * (size_t)(ne1 * ne2 * ne3) + 64);
+    auto* d = static_cast<unsigned char*>(dev);
+    if (stacked) {
+      HIPCHK(hipMemcpy2DAsync(d, pitch, host, nb1, row_bytes, (size_t)(ne1 * ne2 * ne3), hipMemcpyHostToDevice, stream_));
+    } else {
+      for (int64_t i3 = 0; i3 < ne3; ++i3)
+        for (int64_t i2 = 0; i2 < ne2; ++i2)
+          HIPCHK(hipMemcpy2DAsync(d + (i3 * ne2 + i2) * ne1 * pitch, pitch, host + i2 * nb2 + i3 * nb3, nb1, row_bytes,
+                                  (size_t)ne1, hipMemcpyHostToDevice, stream_));
+    }
+    return Transient{dev, pitch, (size_t)pitch * ne1, (size_t)pitch * ne1 * ne2};
+  }
+
   void* scratch(int which, size_t bytes) {
     if (cap_[which] < bytes) {
       if (buf_[which]) HIPCHK(hipFree(buf_[which]));
@@ -514,8 +563,8 @@ class Runtime {
   size_t budget_ = 0, cached_bytes_ = 0;
   std::unordered_map<WeightKey, WeightEntry, WeightKeyHash> cache_;
   std::list<WeightKey> lru_;
-  void* buf_[3] = {nullptr, nullptr, nullptr};
-  size_t cap_[3] = {0, 0, 0};
+  void* buf_[4] = {nullptr, nullptr, nullptr, nullptr};   // B, C, F32 src1, transient src0
+  size_t cap_[4] = {0, 0, 0, 0};
   unsigned char* hbuf_[2] = {nullptr, nullptr};
   size_t hcap_[2] = {0, 0};
 };
@@ -545,6 +594,23 @@ bool is_contiguous(const ggml::tensor* t) {
   const int be = block_elems(t->type);
   return t->nb[0] == ts && t->nb[1] == t->nb[0] * (size_t)(t->ne[0] / be) && t->nb[2] == t->nb[1] * (size_t)t->ne[1] &&
          t->nb[3] == t->nb[2] * (size_t)t->ne[2];
+}
+
+// A real weight: a leaf tensor that owns its bytes (GGML_OP_NONE = 0, not a view).  Only those
+// are kept device-resident across calls; KV-cache views and intermediates are re-uploaded.
+bool is_weight(const ggml::tensor* t) { return t->view_src == nullptr && t->op == 0; }
+
+// Non-weight src0 (the F16 KV-cache attention matmuls KQ / KQV, llama.cpp:5329,5372) costs a
+// host->device copy of the viewed cache on every call.  LAMM_HIP_VIEWS=0 leaves them to ggml's
+// CPU loop (the reference's routing for F16), =1 always takes them; unset: taken from
+// kViewMinRows activation rows (prefill), left to the CPU for decode.
+constexpr int64_t kViewMinRows = 8;
+bool views_accepted(const ggml::tensor* src0, const ggml::tensor* src1) {
+  if (is_weight(src0)) return true;
+  const char* e = getenv("LAMM_HIP_VIEWS");
+  if (e && e[0] == '0') return false;
+  if (e && e[0] == '1') return true;
+  return src1->ne[1] >= kViewMinRows;
 }
 
 bool extra_types_enabled() {
@@ -604,6 +670,7 @@ extern "C" bool lamm_can_mul_mat(const struct ggml_compute_params* vparams, cons
   if (src0->ne[0] % block_elems(src0->type)) return false;
   if (src0->nb[0] != block_bytes(src0->type)) return false;
   if (dst->nb[0] != sizeof(float)) return false;
+  if (!views_accepted(src0, src1)) return false;
   return probe().count > 0;                                  // no GPU: ggml's CPU loop
 }
 
@@ -630,8 +697,27 @@ extern "C" void lamm_mul_mat(const struct ggml_compute_params* vparams, struct g
   rt.ensure_init();
   hipStream_t s = rt.stream();
 
-  // weights: every (i02, i03) slice, device resident, rows re-pitched to 16 B
-  WeightEntry& w = rt.weights(WeightKey{src0->data, t0, M * ne02 * ne03, kb, src0->nb[1]}, a_row, src0);
+  // weights: every (i02, i03) slice, device resident, rows re-pitched to 16 B; any other src0
+  // (KV-cache views, intermediates) uploaded afresh
+  const bool weight = is_weight(src0);
+  WeightEntry* w = nullptr;
+  void* a_dev;
+  int64_t a_pitch;
+  size_t a_s2, a_s3;
+  if (weight) {
+    w = &rt.weights(WeightKey{src0->data, t0, M * ne02 * ne03, kb, src0->nb[1], src0->nb[2], src0->nb[3]}, a_row,
+                    src0);
+    a_dev = w->dev;
+    a_pitch = w->dev_pitch;
+    a_s2 = (size_t)a_pitch * M;
+    a_s3 = a_s2 * ne02;
+  } else {
+    const Runtime::Transient tr = rt.transient(src0, a_row);
+    a_dev = tr.dev;
+    a_pitch = tr.pitch;
+    a_s2 = tr.s2;
+    a_s3 = tr.s3;
+  }
   // activations: INIT-phase wdata (contiguous rows) or a contiguous vec_dot-typed src1
   void* dB = rt.scratch(0, b_row * (size_t)(N * nslices) + 64);
   if (use_wdata && gpu_quantizes(src0, src1)) {
@@ -666,10 +752,10 @@ extern "C" void lamm_mul_mat(const struct ggml_compute_params* vparams, struct g
   const size_t c_slice = (size_t)M * N * sizeof(float);
   float* dC = static_cast<float*>(rt.scratch(1, c_slice * (size_t)nslices + 64));
 
-  lamm_matrix A{w.dev, t0, (int)M, (int)kb, w.dev_pitch / (int64_t)block_bytes(t0)};
+  lamm_matrix A{a_dev, t0, (int)M, (int)kb, a_pitch / (int64_t)block_bytes(t0)};
   lamm_matrix B{dB, vdt, (int)kb, (int)N, (int64_t)kb};
   lamm_matrix C{dC, kF32, (int)M, (int)N, M};
-  lamm_batch bt{ne02, ne03, ne12, ne13, (size_t)(w.dev_pitch * M), (size_t)(w.dev_pitch * M * ne02),
+  lamm_batch bt{ne02, ne03, ne12, ne13, a_s2, a_s3,
                 b_row * (size_t)N, b_row * (size_t)(N * ne12), c_slice, c_slice * (size_t)ne12};
   // prefill calls on the fp6 engine reuse the weights' packed form (weight-stationary)
   GemvArgs pa = weight_args(&A, ne02, ne03, bt.nba2, bt.nba3);
@@ -678,9 +764,9 @@ extern "C" void lamm_mul_mat(const struct ggml_compute_params* vparams, struct g
   pa.ne13 = (int)ne13;
   pa.r2 = (int)(ne12 / ne02);
   pa.r3 = (int)(ne13 / ne03);
-  const bool stationary = N > gemv_max_n(t0) && ((gemm_fp6_supported(t0) && gemm_path(pa, true) == 0) ||
+  const bool stationary = weight && N > gemv_max_n(t0) && ((gemm_fp6_supported(t0) && gemm_path(pa, true) == 0) ||
                                     (gemm_kq_supported(t0) && !getenv_flag0("LAMM_KQ_GEMM")));
-  const int rc = stationary ? lamm_hip_matmul_weights(rt.prepared(w, A, ne02, ne03), &B, &C, &bt, s)
+  const int rc = stationary ? lamm_hip_matmul_weights(rt.prepared(*w, A, ne02, ne03), &B, &C, &bt, s)
                             : lamm_hip_matmul_batched(&A, &B, &C, &bt, s);
   if (rc != LAMM_OK) {
     fprintf(stderr, "lamm_hip: lamm_hip_matmul_batched failed (%d): %s\n", rc, g_err.c_str());

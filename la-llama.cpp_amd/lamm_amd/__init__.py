@@ -114,6 +114,7 @@ lib.lamm_hip_device_count.restype = ctypes.c_int
 lib.lamm_blck_size.restype = ctypes.c_int
 lib.lamm_type_size.restype = ctypes.c_size_t
 lib.lamm_vec_dot_type.restype = ctypes.c_int
+lib.lamm_hip_build_id.restype = ctypes.c_char_p
 lib.lamm_hip_cache_clear.restype = None
 lib.lamm_hip_cache_bytes.restype = ctypes.c_size_t
 
@@ -140,6 +141,27 @@ def last_error():
 
 def device_count():
     return lib.lamm_hip_device_count()
+
+
+def build_id():
+    """Hash of the sources the loaded liblamm_hip.so was built from (Makefile BUILD_ID)."""
+    return lib.lamm_hip_build_id().decode()
+
+
+def source_build_id():
+    """The same hash recomputed from this tree: sha256 over the Makefile's ID_FILES (SRCS +
+    csrc/*.h + ../include/lamm_hip.h, sorted by path as make's $(sort) sorts them)."""
+    import glob
+    import hashlib
+    pkg = os.path.dirname(_HERE)
+    mk = open(os.path.join(pkg, "Makefile")).read()
+    srcs = next(ln for ln in mk.splitlines() if ln.startswith("SRCS")).split(":=", 1)[1].split()
+    hdrs = [os.path.relpath(p, pkg) for p in glob.glob(os.path.join(pkg, "csrc", "*.h"))] + ["../include/lamm_hip.h"]
+    h = hashlib.sha256()
+    for rel in sorted(set(srcs + hdrs)):
+        with open(os.path.join(pkg, rel), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
 
 
 def _check(rc, what):

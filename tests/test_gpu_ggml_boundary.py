@@ -1,5 +1,7 @@
 """The drop-in boundary on the GPU: lamm_can_mul_mat / lamm_mul_mat driven exactly as
 ggml_compute_forward_mul_mat drives the reference plug-in (tests/ggml_emu.py)."""
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -121,5 +123,114 @@ def test_non_compute_phases_and_unsupported(monkeypatch):
     assert la.can_mul_mat(p, dstb.t)
     p.type = la.TASK_COMPUTE
     assert la.can_mul_mat(p, dst.t)
-    src0.t.type = 1  # F16 src0 (KV cache matmuls): not on the lamm path
+
+
+def test_f16_policy(monkeypatch):
+    """F16 src0 (the KV-cache attention matmuls) is on the GPU path by
+    default and declined under LAMM_HIP_EXTRA_TYPES=0, the reference's exact 7-pair set
+    (src/loongarch_matmul.cpp:37-52)."""
+    M, N, K = 16, 2, 256
+    src0, src1, _, _ = make_node(ol.F16, M, N, K)
+    assert src0.t.nb[0] == 2
+    dst = ggml_emu.mul_mat_node(src0, src1)
+    p = la.GgmlComputeParams()
+    p.ith, p.nth, p.type = 0, 1, la.TASK_COMPUTE
+    assert la.can_mul_mat(p, dst.t)
+    monkeypatch.setenv("LAMM_HIP_EXTRA_TYPES", "0")
     assert not la.can_mul_mat(p, dst.t)
+    monkeypatch.delenv("LAMM_HIP_EXTRA_TYPES")
+    # a view of a KV cache (view_src set) in decode (N < 8) is left to ggml's CPU loop unless
+    # LAMM_HIP_VIEWS=1; prefill-sized calls take it
+    cache = ggml_emu.Tensor(ol.F16, [K, M])
+    src0.t.view_src = ctypes.pointer(cache.t)
+    assert not la.can_mul_mat(p, dst.t)
+    monkeypatch.setenv("LAMM_HIP_VIEWS", "1")
+    assert la.can_mul_mat(p, dst.t)
+    monkeypatch.setenv("LAMM_HIP_VIEWS", "0")
+    src0b, src1b, _, _ = make_node(ol.F16, M, 16, K)
+    src0b.t.view_src = ctypes.pointer(cache.t)
+    dstb = ggml_emu.mul_mat_node(src0b, src1b)
+    assert not la.can_mul_mat(p, dstb.t)
+    monkeypatch.delenv("LAMM_HIP_VIEWS")
+    assert la.can_mul_mat(p, dstb.t)
+
+
+GGML_OP_VIEW = 31   # LC/ggml.h enum ggml_op (b2430)
+
+
+@pytest.mark.parametrize("n_tokens,n_head", [(1, 4), (9, 8)], ids=["decode", "prefill_gqa"])
+def test_kv_cache_views_fresh_every_token(n_tokens, n_head, monkeypatch):
+    """b2430's attention matmuls on a live F16 KV cache (llm_build_kqv, llama.cpp:5322-5372):
+    K view ne=[128, n_kv, n_head_kv], nb1 = n_embd_k_gqa*2, nb2 = 256; transposed V view
+    ne=[n_kv, 128, n_head_kv], nb1 = 2*n_ctx, nb2 = 2*n_ctx*128; both keep the cache's data
+    pointer while new token rows land inside a 32-padded window (kv_self.n, llama.cpp:8887).
+    After every token KQ and KQV must match the oracle -- the boundary may not serve a
+    device copy of an older cache."""
+    monkeypatch.setenv("LAMM_HIP_VIEWS", "1")
+    rng = np.random.default_rng(42)
+    hd, n_head_kv, n_ctx = 128, 4, 96
+    r2 = n_head // n_head_kv
+    n_embd_gqa = hd * n_head_kv
+    kcache = ggml_emu.Tensor(ol.F16, [n_ctx * n_embd_gqa])
+    vcache = ggml_emu.Tensor(ol.F16, [n_ctx * n_embd_gqa])
+    kc = kcache.buf.view(np.float16).reshape(n_ctx, n_embd_gqa)     # [token][head*128 + d]
+    vc = vcache.buf.view(np.float16).reshape(n_embd_gqa, n_ctx)     # [head*128 + d][token]
+    pos = 0
+    for step in range(5):
+        # append n_tokens new rows (the ggml_cpy into the cache views, llama.cpp:5254-5277)
+        for _ in range(n_tokens):
+            kc[pos] = rng.standard_normal(n_embd_gqa).astype(np.float16)
+            vc[:, pos] = rng.standard_normal(n_embd_gqa).astype(np.float16)
+            pos += 1
+        n_kv = min(n_ctx, max(32, -(-pos // 32) * 32))
+        # ---- KQ = mul_mat(k_view, q)
+        k = ggml_emu.Tensor(ol.F16, [hd, n_kv, n_head_kv], data=kcache.buf, nb=[2, 2 * n_embd_gqa, 2 * hd, 2 * hd * n_head_kv])
+        k.t.view_src = ctypes.pointer(kcache.t)
+        k.t.op = GGML_OP_VIEW
+        q = rng.standard_normal((n_head * n_tokens, hd), dtype=np.float32)
+        qt = ggml_emu.Tensor(ol.F32, [hd, n_tokens, n_head], data=q)
+        kq = ggml_emu.mul_mat_node(k, qt)
+        assert ggml_emu.compute(kq, nth=2)
+        got = kq.buf.view(np.float32).reshape(n_head, n_tokens, n_kv)
+        qq = ORACLE.quantize(ol.F16, q).view(np.uint16).reshape(n_head, n_tokens, hd)
+        for h in range(n_head):
+            A = np.ascontiguousarray(kc[:n_kv, (h // r2) * hd:(h // r2 + 1) * hd]).view(np.uint8).reshape(-1)
+            want = ORACLE.mul_mat(ol.F16, n_kv, n_tokens, hd, A, qq[h].view(np.uint8).reshape(-1))
+            absdot = np.abs(q[h * n_tokens:(h + 1) * n_tokens]) @ np.abs(kc[:n_kv, (h // r2) * hd:(h // r2 + 1) * hd].astype(np.float32)).T
+            assert rel_err(got[h], want, absdot).max() < 1e-3, (step, h)
+        # ---- KQV = mul_mat(v_view, kq_softmax)
+        v = ggml_emu.Tensor(ol.F16, [n_kv, hd, n_head_kv], data=vcache.buf, nb=[2, 2 * n_ctx, 2 * n_ctx * hd, 2 * n_ctx * hd * n_head_kv])
+        v.t.view_src = ctypes.pointer(vcache.t)
+        v.t.op = GGML_OP_VIEW
+        p = rng.random((n_head * n_tokens, n_kv), dtype=np.float32)
+        pt = ggml_emu.Tensor(ol.F32, [n_kv, n_tokens, n_head], data=p)
+        kqv = ggml_emu.mul_mat_node(v, pt)
+        assert ggml_emu.compute(kqv, nth=2)
+        got = kqv.buf.view(np.float32).reshape(n_head, n_tokens, hd)
+        pq = ORACLE.quantize(ol.F16, p).view(np.uint16).reshape(n_head, n_tokens, n_kv)
+        for h in range(n_head):
+            Vh = np.ascontiguousarray(vc[(h // r2) * hd:(h // r2 + 1) * hd, :n_kv])
+            want = ORACLE.mul_mat(ol.F16, hd, n_tokens, n_kv, Vh.view(np.uint8).reshape(-1),
+                                  pq[h].view(np.uint8).reshape(-1))
+            absdot = np.abs(p[h * n_tokens:(h + 1) * n_tokens]) @ np.abs(Vh.astype(np.float32)).T
+            assert rel_err(got[h], want, absdot).max() < 1e-3, (step, h)
+
+
+def test_views_bypass_weight_cache(monkeypatch):
+    """A view src0 is uploaded per call and never held in the weight cache."""
+    monkeypatch.setenv("LAMM_HIP_VIEWS", "1")
+    la.cache_clear()
+    M, N, K = 64, 2, 256
+    cache = ggml_emu.Tensor(ol.F16, [K * M])
+    cache.buf.view(np.float16)[:] = np.random.default_rng(3).standard_normal(K * M).astype(np.float16)
+    v = ggml_emu.Tensor(ol.F16, [K, M], data=cache.buf)
+    v.t.view_src = ctypes.pointer(cache.t)
+    b = np.random.default_rng(4).standard_normal((N, K), dtype=np.float32)
+    dst = ggml_emu.mul_mat_node(v, ggml_emu.Tensor(ol.F32, [K, N], data=b))
+    assert ggml_emu.compute(dst)
+    assert la.cache_bytes() == 0
+    cache.buf.view(np.float16)[5 * K + 7] = np.float16(100.0)    # one element of one row
+    assert ggml_emu.compute(dst)
+    want = ORACLE.mul_mat(ol.F16, M, N, K, cache.buf, ORACLE.quantize(ol.F16, b))
+    got = dst.buf.view(np.float32).reshape(N, M)
+    np.testing.assert_allclose(got[:, 5], want[:, 5], rtol=1e-5)

@@ -664,3 +664,78 @@ def test_f32_activations_rejected_beyond_decode():
     with pytest.raises(la.LammError):
         la.matmul(la.Matrix(dA.data_ptr(), t, M, K // 32, K // 32), la.Matrix(dx.data_ptr(), la.F32, K, N, K),
                   la.Matrix(c.data_ptr(), la.F32, M, N, M), 0)
+
+
+# ---------------------------------------------------------------- BASELINE config 3, full size
+def _config3_operands(seed, slices):
+    """Q4_0 A (4096 x 4096, `slices` distinct slices) quantized from N(0,1) by the oracle's
+    reference quantizer, B = 512 q8_0 rows (AVX2 flavour, ggml's INIT on x86)."""
+    M, N, K = 4096, 512, 4096
+    rng = np.random.default_rng(seed)
+    As = [ORACLE.quantize(ol.Q4_0, rng.standard_normal((M, K), dtype=np.float32)) for _ in range(slices)]
+    Bs = [ORACLE.quantize(ol.Q8_0, rng.standard_normal((N, K), dtype=np.float32), ol.QUANT_AVX)
+          for _ in range(slices)]
+    return As, Bs
+
+
+def _config3_check(c, A_q, B_q, rows):
+    """c: [N][M] GPU result; compare the sampled rows (all 512 columns) with the oracle."""
+    M, N, K = 4096, 512, 4096
+    arow = la.row_bytes(ol.Q4_0, K)
+    a = np.concatenate([A_q[r * arow:(r + 1) * arow] for r in rows])
+    ref = ORACLE.mul_mat(ol.Q4_0, len(rows), N, K, a, B_q)
+    err = rel_err(c[:, rows], ref, absdot(ol.Q4_0, a, B_q, len(rows), N, K)).max()
+    assert np.isfinite(c).all()
+    return err
+
+
+CONFIG3_ROWS = np.unique(np.concatenate([np.arange(0, 4096, 16), [1, 127, 128, 255, 256, 2047, 2048, 4095]]))
+
+
+@pytest.mark.parametrize("path", ["stationary_fp6_auto_split", "per_call_default", "per_call_fp6", "per_call_i8"])
+def test_config3_full_size_gemm(path, monkeypatch):
+    """BASELINE config 3 at its real size: Q4_0 x Q8_0 M=4096 N=512 K=4096, one slice.
+    Paths: the weight-stationary handle (the ggml boundary's and bench.py's; fp6 engine with its
+    automatic K-split over 64 tiles), the per-call API's default engine (i8, split-K), and both
+    engines forced per call.  >= 256 sampled rows x all 512 columns vs the oracle."""
+    M, N, K = 4096, 512, 4096
+    (A_q,), (B_q,) = _config3_operands(2024, 1)
+    if path in ("per_call_fp6", "per_call_i8"):
+        monkeypatch.setenv("LAMM_GEMM_PATH", path.rsplit("_", 1)[1])
+    A = dev_bytes(np.concatenate([A_q, np.zeros(64, np.uint8)]))
+    B = dev_bytes(B_q)
+    C = torch.full((N * M,), float("nan"), dtype=torch.float32, device="cuda")
+    if path.startswith("stationary"):
+        assert la.gemm_engine("q4_0", M, N, K, 1, stationary=True) == "fp6"
+        W = la.Weights(ol.Q4_0, A, M, K)
+        W.matmul_torch(B, C, N)
+        torch.cuda.synchronize()
+        W.close()
+    else:
+        la.mul_mat_torch(ol.Q4_0, A, B, C, M, N, K)
+        torch.cuda.synchronize()
+    err = _config3_check(C.cpu().numpy().reshape(N, M), A_q, B_q, CONFIG3_ROWS)
+    print(f"config 3 {path}: max rel err {err:.2e} over {len(CONFIG3_ROWS)} rows x {N}")
+    assert err < TOL
+
+
+def test_config3_four_slice_batched_launch():
+    """The 4-slice batched launch bench.py times (ne02 = ne12 = 4, stationary weights, fp6
+    engine with 256 tiles): every slice's sampled rows x all columns vs the oracle."""
+    M, N, K = 4096, 512, 4096
+    As, Bs = _config3_operands(77, 4)
+    arow, brow = la.row_bytes(ol.Q4_0, K), la.row_bytes(ol.Q8_0, K)
+    A = dev_bytes(np.concatenate(As + [np.zeros(64, np.uint8)]))
+    B = dev_bytes(np.concatenate(Bs))
+    C = torch.full((4 * N * M,), float("nan"), dtype=torch.float32, device="cuda")
+    bt = la.Batch(4, 1, 4, 1, M * arow, 4 * M * arow, N * brow, 4 * N * brow, 4 * M * N, 16 * M * N)
+    assert la.gemm_engine("q4_0", M, N, K, 4, stationary=True) == "fp6"
+    W = la.Weights(ol.Q4_0, A, M, K, ne02=4, ne03=1, nba2=M * arow, nba3=4 * M * arow)
+    W.matmul_torch(B, C, N, batch=bt)
+    torch.cuda.synchronize()
+    W.close()
+    c = C.cpu().numpy().reshape(4, N, M)
+    rows = CONFIG3_ROWS[::4]
+    for z in range(4):
+        err = _config3_check(c[z], As[z], Bs[z], rows)
+        assert err < TOL, (z, err)

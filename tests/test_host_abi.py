@@ -81,7 +81,12 @@ def test_validation_errors():
     B.type = la.Q8_1
     assert _rc(A, B, C) == la.LAMM_ERR_TYPE
     A, B, C = _mats()
-    A.type = 1  # F16 unsupported
+    A.type = la.F16            # F16 weights are supported, but only against F16 activations
+    assert _rc(A, B, C) == la.LAMM_ERR_TYPE      # B is still q8_0: not vec_dot_type(F16)
+    B.type = la.F16
+    assert _rc(A, B, C) in (la.LAMM_OK, la.LAMM_ERR_NODEV, la.LAMM_ERR_SHAPE)
+    A, B, C = _mats()
+    A.type = 11                # Q3_K: no kernel
     assert _rc(A, B, C) == la.LAMM_ERR_TYPE
     A, B, C = _mats()
     B.row = 64
@@ -103,3 +108,10 @@ def test_no_gpu_behaviour():
     dst = ggml_emu.mul_mat_node(src0, src1)
     # no GPU: the hook declines and ggml keeps its CPU loop
     assert ggml_emu.compute(dst, nth=2) is False
+
+
+def test_build_id_matches_tree():
+    """Provenance: the loaded liblamm_hip.so was built from exactly this tree's sources
+    (Makefile BUILD_ID vs lamm_amd.source_build_id()); a stale prebuilt library fails here."""
+    assert la.build_id() == la.source_build_id(), (
+        f"liblamm_hip.so build id {la.build_id()} != sources {la.source_build_id()}: rebuild with make -C la-llama.cpp_amd")

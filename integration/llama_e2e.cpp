@@ -1,0 +1,381 @@
+// llama_e2e.cpp -- BASELINE config 5 through the UNCHANGED caller: llama.cpp-b2430's own
+// model code (build_llama, llama.cpp:5708-5830; attention llm_build_kqv, :5295-5372) and ggml
+// runtime, compiled from the reference's sources where they lie, with ggml's LA_LLAMA hook
+// (ggml.c:10858-10863) resolved to liblamm_hip.so (integration/Makefile) -- or, built by
+// oracle/Makefile against the reference's own lamm plug-in, the CPU reference the GPU build is
+// checked and timed against.  This file is only the driver around llama.h; nothing in it
+// computes a matmul.
+//
+//   llama_e2e [-m model.gguf] [--layers L] [--regen] [-t threads] [-p n_prompt] [-n n_gen]
+//             [-r reps] [--logits out.bin] [--write-only] [--seed S]
+//
+// The model is a Llama-2-7B-shaped GGUF (n_embd 4096, n_ff 11008, 32 heads, n_vocab 32000,
+// `--layers` blocks, default 32) with synthetic weights, written by write_model() below when
+// the file is missing: Q4_0 projections and token embedding, Q6_K output.weight (the
+// quantization llama.cpp picks for a Q4_0 model, llama.cpp:11731-11742), F32 norms, no
+// vocabulary ("no_vocab", llama.cpp:3657-3668; the driver feeds token ids).
+//
+// The timed run mirrors llama-bench's pp/tg tests: one llama_decode of n_prompt tokens
+// (prompt processing), then n_gen single-token decodes with greedy argmax sampling (text
+// generation), the KV cache cleared between repetitions; a warm-up pass first (it also
+// uploads the weights to the device cache of the GPU build).  Output: one JSON line.
+#include "llama.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace {
+
+// ------------------------------------------------------------------ GGUF v3 writer
+enum : uint32_t { GGUF_U32 = 4, GGUF_F32 = 6, GGUF_STR = 8 };
+constexpr int kTypeF32 = 0, kTypeQ4_0 = 2, kTypeQ6_K = 14;   // ggml_type ids (ggml.h)
+
+struct Kv {
+  std::string key;
+  uint32_t type;
+  uint32_t u32;
+  float f32;
+  std::string str;
+};
+
+struct TensorSpec {
+  std::string name;
+  int type;
+  int64_t ne0, ne1;   // ne1 = 1 for vectors
+  uint64_t offset = 0, bytes = 0;
+};
+
+uint64_t row_bytes(int type, int64_t ne0) {
+  switch (type) {
+    case kTypeF32: return 4 * (uint64_t)ne0;
+    case kTypeQ4_0: return 18 * (uint64_t)(ne0 / 32);
+    case kTypeQ6_K: return 210 * (uint64_t)(ne0 / 256);
+  }
+  return 0;
+}
+
+void put_str(FILE* f, const std::string& s) {
+  const uint64_t n = s.size();
+  fwrite(&n, 8, 1, f);
+  fwrite(s.data(), 1, n, f);
+}
+
+uint16_t f32_to_f16(float x) {   // positive normal range only (the scales below)
+  uint32_t b;
+  memcpy(&b, &x, 4);
+  const int e = (int)((b >> 23) & 0xff) - 127 + 15;
+  const uint32_t m = (b >> 13) & 0x3ff;
+  return (uint16_t)((e << 10) | m);
+}
+
+inline uint64_t splitmix(uint64_t& s) {
+  uint64_t z = (s += 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// Synthetic tensor bytes, deterministic per (tensor, seed): random quants with scales chosen
+// so every weight has an RMS near 0.02 (a trained Llama's order of magnitude) and the
+// residual stream stays O(1) through 32 blocks.
+void fill(const TensorSpec& t, uint64_t seed, std::vector<uint8_t>& buf) {
+  buf.resize(t.bytes);
+  const size_t nthreads = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  const uint64_t rb = row_bytes(t.type, t.ne0);
+  std::vector<std::thread> pool;
+  for (size_t w = 0; w < nthreads; ++w)
+    pool.emplace_back([&, w] {
+      for (int64_t r = (int64_t)w; r < t.ne1; r += (int64_t)nthreads) {
+        uint8_t* row = buf.data() + (uint64_t)r * rb;
+        uint64_t s = seed * 0x100000001B3ull ^ (uint64_t)r * 0x9E3779B97F4A7C15ull;
+        if (t.type == kTypeF32) {
+          for (int64_t i = 0; i < t.ne0; ++i) reinterpret_cast<float*>(row)[i] = 1.0f;   // norm weights
+        } else if (t.type == kTypeQ4_0) {
+          for (uint64_t b = 0; b < rb / 18; ++b) {
+            uint8_t* blk = row + b * 18;
+            const uint64_t z0 = splitmix(s);
+            const float d = 0.0035f + 0.0015f * (float)(z0 & 0xffff) / 65536.0f;   // RMS(q-8) ~ 4.3
+            const uint16_t h = f32_to_f16(d);
+            memcpy(blk, &h, 2);
+            // nibbles uniform in 1..15: q-8 symmetric in [-7, 7] (a uniform 0..15 nibble has mean
+            // -0.5 after the -8 offset, a common-mode bias that swamps the signal within 2 blocks)
+            for (int i = 0; i < 16; i += 2) {
+              const uint64_t z = splitmix(s);
+              for (int j = 0; j < 2; ++j) {
+                const uint32_t w = (uint32_t)(z >> (32 * j));
+                blk[2 + i + j] = (uint8_t)((1 + (w & 0xffff) % 15) | ((1 + (w >> 16) % 15) << 4));
+              }
+            }
+          }
+        } else {   // Q6_K: ql[128] qh[64] scales[16] d
+          for (uint64_t b = 0; b < rb / 210; ++b) {
+            uint8_t* blk = row + b * 210;
+            for (int i = 0; i < 208; i += 8) {
+              const uint64_t z = splitmix(s);
+              memcpy(blk + i, &z, 8);
+            }
+            for (int i = 192; i < 208; ++i) blk[i] = (uint8_t)(int8_t)(8 + (blk[i] & 15));   // scales 8..23
+            const uint16_t h = f32_to_f16(0.00012f);
+            memcpy(blk + 208, &h, 2);
+          }
+        }
+      }
+    });
+  for (auto& th : pool) th.join();
+}
+
+bool write_model(const std::string& path, int n_layer, uint64_t seed) {
+  const int64_t n_embd = 4096, n_ff = 11008, n_vocab = 32000;
+  std::vector<Kv> kv = {
+      {"general.architecture", GGUF_STR, 0, 0, "llama"},
+      {"general.name", GGUF_STR, 0, 0, "synthetic-llama-7b-q4_0"},
+      {"general.file_type", GGUF_U32, 2, 0, ""},   // LLAMA_FTYPE_MOSTLY_Q4_0
+      {"llama.vocab_size", GGUF_U32, (uint32_t)n_vocab, 0, ""},
+      {"llama.context_length", GGUF_U32, 4096, 0, ""},
+      {"llama.embedding_length", GGUF_U32, (uint32_t)n_embd, 0, ""},
+      {"llama.feed_forward_length", GGUF_U32, (uint32_t)n_ff, 0, ""},
+      {"llama.attention.head_count", GGUF_U32, 32, 0, ""},
+      {"llama.attention.head_count_kv", GGUF_U32, 32, 0, ""},
+      {"llama.block_count", GGUF_U32, (uint32_t)n_layer, 0, ""},
+      {"llama.rope.dimension_count", GGUF_U32, 128, 0, ""},
+      {"llama.attention.layer_norm_rms_epsilon", GGUF_F32, 0, 1e-5f, ""},
+      {"tokenizer.ggml.model", GGUF_STR, 0, 0, "no_vocab"},
+  };
+  std::vector<TensorSpec> ts;
+  ts.push_back({"token_embd.weight", kTypeQ4_0, n_embd, n_vocab});
+  for (int l = 0; l < n_layer; ++l) {
+    const std::string p = "blk." + std::to_string(l) + ".";
+    ts.push_back({p + "attn_norm.weight", kTypeF32, n_embd, 1});
+    ts.push_back({p + "attn_q.weight", kTypeQ4_0, n_embd, n_embd});
+    ts.push_back({p + "attn_k.weight", kTypeQ4_0, n_embd, n_embd});
+    ts.push_back({p + "attn_v.weight", kTypeQ4_0, n_embd, n_embd});
+    ts.push_back({p + "attn_output.weight", kTypeQ4_0, n_embd, n_embd});
+    ts.push_back({p + "ffn_norm.weight", kTypeF32, n_embd, 1});
+    ts.push_back({p + "ffn_gate.weight", kTypeQ4_0, n_embd, n_ff});
+    ts.push_back({p + "ffn_down.weight", kTypeQ4_0, n_ff, n_embd});
+    ts.push_back({p + "ffn_up.weight", kTypeQ4_0, n_embd, n_ff});
+  }
+  ts.push_back({"output_norm.weight", kTypeF32, n_embd, 1});
+  ts.push_back({"output.weight", kTypeQ6_K, n_embd, n_vocab});
+  uint64_t off = 0;
+  for (auto& t : ts) {
+    t.bytes = row_bytes(t.type, t.ne0) * (uint64_t)t.ne1;
+    t.offset = off;
+    off = (off + t.bytes + 31) / 32 * 32;   // GGUF_DEFAULT_ALIGNMENT (ggml.h:250)
+  }
+  const std::string tmp = path + ".part";
+  FILE* f = fopen(tmp.c_str(), "wb");
+  if (!f) { perror(tmp.c_str()); return false; }
+  const uint32_t magic = 0x46554747u, version = 3;   // "GGUF", GGUF_VERSION (ggml.h:248)
+  const uint64_t n_tensors = ts.size(), n_kv = kv.size();
+  fwrite(&magic, 4, 1, f);
+  fwrite(&version, 4, 1, f);
+  fwrite(&n_tensors, 8, 1, f);
+  fwrite(&n_kv, 8, 1, f);
+  for (const auto& k : kv) {
+    put_str(f, k.key);
+    fwrite(&k.type, 4, 1, f);
+    if (k.type == GGUF_U32) fwrite(&k.u32, 4, 1, f);
+    else if (k.type == GGUF_F32) fwrite(&k.f32, 4, 1, f);
+    else put_str(f, k.str);
+  }
+  for (const auto& t : ts) {
+    put_str(f, t.name);
+    const uint32_t nd = t.ne1 == 1 ? 1 : 2;
+    fwrite(&nd, 4, 1, f);
+    const uint64_t ne[2] = {(uint64_t)t.ne0, (uint64_t)t.ne1};
+    fwrite(ne, 8, nd, f);
+    const uint32_t ty = (uint32_t)t.type;
+    fwrite(&ty, 4, 1, f);
+    fwrite(&t.offset, 8, 1, f);
+  }
+  long pos = ftell(f);
+  static const uint8_t zeros[32] = {0};
+  fwrite(zeros, 1, (32 - pos % 32) % 32, f);
+  std::vector<uint8_t> buf;
+  uint64_t written = 0;
+  for (size_t i = 0; i < ts.size(); ++i) {
+    fill(ts[i], seed * 1000003ull + i, buf);
+    fwrite(zeros, 1, ts[i].offset - written, f);
+    fwrite(buf.data(), 1, buf.size(), f);
+    written = ts[i].offset + ts[i].bytes;
+  }
+  if (fclose(f) != 0) { perror("fclose"); return false; }
+  return rename(tmp.c_str(), path.c_str()) == 0;
+}
+
+double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+int argmax(const float* x, int n) {
+  int b = 0;
+  for (int i = 1; i < n; ++i)
+    if (x[i] > x[b]) b = i;
+  return b;
+}
+
+// --dump DIR: every F32 node of the first prefill, one file per node (debugging parity
+// differences node by node through ggml's scheduler eval callback)
+std::string g_dump_dir;
+bool g_dump_on = false;
+int g_dump_idx = 0;
+
+bool dump_cb(struct ggml_tensor* t, bool ask, void*) {
+  if (ask) return g_dump_on;
+  if (!g_dump_on || t->type != GGML_TYPE_F32 || !ggml_is_contiguous(t)) return true;
+  char path[1024];
+  snprintf(path, sizeof path, "%s/%04d_%s_%lldx%lldx%lld.bin", g_dump_dir.c_str(), g_dump_idx++, t->name,
+           (long long)t->ne[0], (long long)t->ne[1], (long long)t->ne[2]);
+  for (char* c = path + g_dump_dir.size() + 1; *c; ++c)
+    if (*c == ' ' || *c == '/') *c = '_';
+  FILE* f = fopen(path, "wb");
+  if (f) {
+    fwrite(t->data, 1, ggml_nbytes(t), f);
+    fclose(f);
+  }
+  return true;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  std::string model = "/tmp/lamm_synth_llama7b_q4_0.gguf", logits_path;
+  int n_layer = 32, threads = 16, n_prompt = 512, n_gen = 128, reps = 1;
+  uint64_t seed = 1;
+  bool regen = false, write_only = false;
+  for (int i = 1; i < argc; ++i) {
+    const std::string a = argv[i];
+    auto next = [&]() -> const char* {
+      if (i + 1 >= argc) { fprintf(stderr, "missing value for %s\n", a.c_str()); exit(2); }
+      return argv[++i];
+    };
+    if (a == "-m") model = next();
+    else if (a == "--layers") n_layer = atoi(next());
+    else if (a == "-t") threads = atoi(next());
+    else if (a == "-p") n_prompt = atoi(next());
+    else if (a == "-n") n_gen = atoi(next());
+    else if (a == "-r") reps = atoi(next());
+    else if (a == "--seed") seed = strtoull(next(), nullptr, 10);
+    else if (a == "--logits") logits_path = next();
+    else if (a == "--regen") regen = true;
+    else if (a == "--write-only") write_only = true;
+    else if (a == "--dump") g_dump_dir = next();
+    else { fprintf(stderr, "unknown argument %s\n", a.c_str()); return 2; }
+  }
+  double t_write = 0;
+  if (regen || !fopen(model.c_str(), "rb")) {
+    const double t0 = now_ms();
+    if (!write_model(model, n_layer, seed)) return 1;
+    t_write = now_ms() - t0;
+    fprintf(stderr, "llama_e2e: wrote %s (%d layers) in %.0f ms\n", model.c_str(), n_layer, t_write);
+  }
+  if (write_only) return 0;
+
+  llama_backend_init();
+  llama_model_params mp = llama_model_default_params();
+  const double t_load0 = now_ms();
+  llama_model* m = llama_load_model_from_file(model.c_str(), mp);
+  if (!m) { fprintf(stderr, "llama_e2e: cannot load %s\n", model.c_str()); return 1; }
+  const double t_load = now_ms() - t_load0;
+  llama_context_params cp = llama_context_default_params();
+  cp.n_ctx = (uint32_t)((n_prompt + n_gen + 255) / 256 * 256);
+  cp.n_batch = cp.n_ubatch = (uint32_t)std::max(n_prompt, 1);
+  cp.n_threads = cp.n_threads_batch = (uint32_t)threads;
+  cp.seed = 1234;
+  if (!g_dump_dir.empty()) {
+    cp.cb_eval = dump_cb;
+    g_dump_on = true;
+  }
+  llama_context* ctx = llama_new_context_with_model(m, cp);
+  if (!ctx) { fprintf(stderr, "llama_e2e: cannot create context\n"); return 1; }
+  const int n_vocab = llama_n_vocab(m);
+  {
+    char buf[32] = {0};
+    if (llama_model_meta_val_str(m, "llama.block_count", buf, sizeof buf) > 0) n_layer = atoi(buf);
+  }
+
+  std::vector<llama_token> prompt(n_prompt);
+  uint64_t s = seed * 7919;
+  for (auto& tok : prompt) tok = (llama_token)(1 + splitmix(s) % (uint64_t)(n_vocab - 1));
+
+  std::vector<float> logits_out;
+  std::vector<int> gen_tokens;
+  auto run = [&](bool record, double* pp_ms, double* tg_ms) -> bool {
+    llama_kv_cache_clear(ctx);
+    llama_batch b = llama_batch_init(n_prompt, 0, 1);
+    for (int i = 0; i < n_prompt; ++i) {
+      b.token[i] = prompt[i];
+      b.pos[i] = i;
+      b.n_seq_id[i] = 1;
+      b.seq_id[i][0] = 0;
+      b.logits[i] = i == n_prompt - 1;
+    }
+    b.n_tokens = n_prompt;
+    const double t0 = now_ms();
+    if (llama_decode(ctx, b) != 0) { fprintf(stderr, "llama_decode (prompt) failed\n"); return false; }
+    const double t1 = now_ms();
+    g_dump_on = false;
+    llama_batch_free(b);
+    const float* lg = llama_get_logits_ith(ctx, n_prompt - 1);
+    if (record) logits_out.insert(logits_out.end(), lg, lg + n_vocab);
+    llama_token tok = argmax(lg, n_vocab);
+    llama_batch g = llama_batch_init(1, 0, 1);
+    for (int k = 0; k < n_gen; ++k) {
+      if (record) gen_tokens.push_back(tok);
+      g.token[0] = tok;
+      g.pos[0] = n_prompt + k;
+      g.n_seq_id[0] = 1;
+      g.seq_id[0][0] = 0;
+      g.logits[0] = 1;
+      g.n_tokens = 1;
+      if (llama_decode(ctx, g) != 0) { fprintf(stderr, "llama_decode (gen) failed\n"); return false; }
+      const float* l2 = llama_get_logits_ith(ctx, 0);
+      if (record) logits_out.insert(logits_out.end(), l2, l2 + n_vocab);
+      tok = argmax(l2, n_vocab);
+    }
+    const double t2 = now_ms();
+    llama_batch_free(g);
+    *pp_ms = t1 - t0;
+    *tg_ms = t2 - t1;
+    return true;
+  };
+
+  double pp, tg;
+  if (!run(false, &pp, &tg)) return 1;   // warm-up (weights reach the device cache)
+  std::vector<double> pps, tgs;
+  for (int r = 0; r < reps; ++r) {
+    if (!run(r == 0, &pp, &tg)) return 1;
+    pps.push_back(pp);
+    tgs.push_back(tg);
+  }
+  std::sort(pps.begin(), pps.end());
+  std::sort(tgs.begin(), tgs.end());
+  const double pp_med = pps[pps.size() / 2], tg_med = tgs[tgs.size() / 2];
+  if (!logits_path.empty()) {
+    FILE* f = fopen(logits_path.c_str(), "wb");
+    if (!f) { perror(logits_path.c_str()); return 1; }
+    fwrite(logits_out.data(), sizeof(float), logits_out.size(), f);
+    fclose(f);
+  }
+  printf("{\"model\": \"llama-7b-shaped q4_0 (output q6_K), synthetic\", \"n_layer\": %d, \"threads\": %d, "
+         "\"n_prompt\": %d, \"n_gen\": %d, \"reps\": %d, \"pp_ms\": %.3f, \"tg_ms\": %.3f, "
+         "\"pp_tok_s\": %.2f, \"tg_tok_s\": %.2f, \"t_load_ms\": %.1f, \"t_write_ms\": %.1f, \"tokens\": [",
+         n_layer, threads, n_prompt, n_gen, reps, pp_med, tg_med, n_prompt / (pp_med * 1e-3),
+         n_gen > 0 ? n_gen / (tg_med * 1e-3) : 0.0, t_load, t_write);
+  for (size_t i = 0; i < gen_tokens.size(); ++i) printf("%s%d", i ? ", " : "", gen_tokens[i]);
+  printf("]}\n");
+  fflush(stdout);
+  llama_free(ctx);
+  llama_free_model(m);
+  llama_backend_free();
+  return 0;
+}

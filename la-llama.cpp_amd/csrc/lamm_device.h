@@ -64,6 +64,26 @@ __device__ __forceinline__ int dot4(uint32_t a, uint32_t b, int c) {
   return __builtin_amdgcn_sdot4((int)a, (int)b, c, false);
 }
 
+// Sum over the 64 lanes of a wave in a fixed order (deterministic), returned in every lane:
+// DPP within each row of 16 (pairs, quads, 8s via row_half_mirror, 16s via row_mirror), then
+// the four row sums read back with v_readlane -- no LDS round trips (__shfl_xor compiles to
+// ds_bpermute, ~100+ cycles each, 6 in a row).
+template <int CTRL>
+__device__ __forceinline__ float dpp_get(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float wave_sum(float x) {
+  x += dpp_get<0xB1>(x);    // quad_perm [1,0,3,2]
+  x += dpp_get<0x4E>(x);    // quad_perm [2,3,0,1]
+  x += dpp_get<0x141>(x);   // row_half_mirror
+  x += dpp_get<0x140>(x);   // row_mirror
+  const float r0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 0));
+  const float r1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 16));
+  const float r2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 32));
+  const float r3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 48));
+  return (r0 + r1) + (r2 + r3);
+}
+
 // bit i (i<4) of x -> bit 4 of byte i  (the 5th quant bit of q5_0/q5_1)
 __device__ __forceinline__ uint32_t spread4_hi(uint32_t x4) {
   return ((x4 * 0x00204081u) & 0x01010101u) << 4;

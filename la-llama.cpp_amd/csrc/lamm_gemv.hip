@@ -1234,7 +1234,27 @@ size_t gemv_lds_bytes(int type, int nc) {
 #undef LDS_CASE
 }
 
+// Row-per-wave kernel (lamm_gemv_rpw.hip) for the 32-element formats at N <= 2 on launches of
+// up to 32768 rows (one decode projection; a 4-slice batch of them): the wave-group kernels
+// below leave half the chip idle on one 4096-row slice (1024 four-row groups) and only pay off
+// once several slices share a launch.  hipGraph-replayed single calls, q4_0 (tools/
+// ab_gemv_single.py, profiles/r02/ab_gemv_single.json): 4096x4096 6.03 -> 4.67 us, 11008x4096
+// 8.81 -> 7.78, 4096x11008 11.34 -> 8.25; 33 stacked slices stay on the wave-group kernel
+// (52 vs 75 us).  Workgroup size: 4 waves (K <= 4096) / 8 (larger K), 16 for F32 activations
+// (each workgroup quantizes the activation row once).  LAMM_GEMV_RPW=0 off, =4/8/16 forces.
+int rpw_waves(const GemvArgs& p) {
+  const char* e = getenv("LAMM_GEMV_RPW");
+  if (e) return atoi(e);
+  if ((int64_t)p.M * p.ne12 * p.ne13 > 32768) return 0;
+  if (p.nblk > 128) return 8;
+  return p.b_f32 ? 16 : 4;
+}
+
 hipError_t launch_gemv(int type, const GemvArgs& p, hipStream_t s) {
+  if (gemv_rpw_supported(type, p)) {
+    const int w = rpw_waves(p);
+    if (w > 0) return launch_gemv_rpw(type, p, s, w);
+  }
   switch (type) {
     case kQ4_0: return launch_nc<kQ4_0>(p, s);
     case kQ4_1: return launch_nc<kQ4_1>(p, s);

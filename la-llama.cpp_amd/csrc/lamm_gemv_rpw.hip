@@ -1,0 +1,331 @@
+// lamm_gemv_rpw.hip -- row-per-wave decode GEMV for the 32-element block formats
+// (q4_0, q4_1, q5_0, q5_1, q8_0 against q8_0 / q8_1 or F32 activations), N <= 2.
+//
+// The per-block arithmetic of lamm_gemv.hip's block_dot (the reference's lamm_kernel_q*.hpp:
+// exact int32 block dots, d_a*d_b*S [+ m_a*s_b] in fp32), laid out for ONE call that is too
+// small to fill the chip with the wave-group kernel: a 4096 x 4096 q4_0 GEMV (BASELINE config
+// 2) is 1024 four-row groups there -- 128 workgroups of 8 waves, half the CUs.  Here:
+//   * a wave owns a whole row at a time; lane l takes blocks l, l+64, l+128, ... (each block
+//     whole in one lane: no cross-lane unpacking), all of the row's loads in flight at once,
+//     and the wave's NEXT row (rows strided over the grid) is issued before the current one
+//     is computed;
+//   * the activation row(s) are decoded once per workgroup into LDS (quads, d, s or sum b);
+//     those loads are issued before the row stream so waiting for them does not wait for HBM;
+//   * the q4_0 / q5_0 offset is applied in the integer domain (sum (q-c) b = sum q b - c sum b);
+//   * the 64 lane partials reduce through DPP + readlane in a fixed order (deterministic).
+// Bytes per call are the algorithmic A + B + C (A streamed once, non-temporal).
+#include "lamm_device.h"
+#include "lamm_kernels.h"
+
+#include <cstdlib>
+
+namespace lamm {
+namespace {
+
+template <int T> struct RFmt;
+template <> struct RFmt<kQ4_0> { static constexpr int BPB = 18, VBPB = 34; };
+template <> struct RFmt<kQ4_1> { static constexpr int BPB = 20, VBPB = 36; };
+template <> struct RFmt<kQ5_0> { static constexpr int BPB = 22, VBPB = 34; };
+template <> struct RFmt<kQ5_1> { static constexpr int BPB = 24, VBPB = 36; };
+template <> struct RFmt<kQ8_0> { static constexpr int BPB = 34, VBPB = 34; };
+
+// NW consecutive dwords at byte offset `off` (dword aligned) of a buffer resource, as wide
+// buffer loads (b128 / b64 / b32); out-of-range dwords read as 0.
+template <int NW, int AUX>
+__device__ __forceinline__ void load_words(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t (&w)[NW]) {
+  unroll<NW / 4>([&](auto I) {
+    constexpr int i = I;
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off + 16 * i, 0, AUX);
+    w[4 * i] = v[0]; w[4 * i + 1] = v[1]; w[4 * i + 2] = v[2]; w[4 * i + 3] = v[3];
+  });
+  constexpr int b = NW / 4 * 4;
+  if constexpr (NW - b >= 2) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, off + 4 * b, 0, AUX);
+    w[b] = (uint32_t)v[0];
+    w[b + 1] = (uint32_t)v[1];
+    if constexpr (NW - b == 3) w[b + 2] = __builtin_amdgcn_raw_buffer_load_b32(r, off + 4 * b + 8, 0, AUX);
+  } else if constexpr (NW - b == 1) {
+    w[b] = __builtin_amdgcn_raw_buffer_load_b32(r, off + 4 * b, 0, AUX);
+  }
+}
+
+// bytes [sh, sh + 4*(NW-1)) of w as NW-1 dwords (sh in {0, 1, 2, 3} bytes)
+template <int NW>
+__device__ __forceinline__ void realign(const uint32_t (&w)[NW], uint32_t (&m)[NW - 1], int sh) {
+  unroll<NW - 1>([&](auto K) {
+    constexpr int k = K;
+    m[k] = __builtin_amdgcn_alignbit(w[k + 1], w[k], sh * 8);
+  });
+}
+
+// A 32-element block as the dot needs it: 8 int8 quads (the 4-bit / 5-bit formats unpacked to
+// unsigned bytes) + d (+ m for q4_1 / q5_1)
+template <int T, int NW>
+__device__ __forceinline__ void unpack_a(const uint32_t (&m)[NW], uint32_t (&q)[8], float& da, float& ma) {
+  ma = 0.f;
+  if constexpr (T == kQ8_0) {
+    da = h2f(get16<0>(m));
+    unroll<8>([&](auto K) { q[K] = get32<2 + 4 * K>(m); });
+  } else {
+    constexpr bool AFF = (T == kQ4_1 || T == kQ5_1);
+    constexpr bool FIVE = (T == kQ5_0 || T == kQ5_1);
+    constexpr int QS = (AFF ? 4 : 2) + (FIVE ? 4 : 0);
+    da = h2f(get16<0>(m));
+    if constexpr (AFF) ma = h2f(get16<2>(m));
+    uint32_t qh = 0;
+    if constexpr (FIVE) qh = get32<AFF ? 4 : 2>(m);
+    unroll<4>([&](auto K) {
+      constexpr int k = K;
+      const uint32_t x = get32<QS + 4 * k>(m);
+      q[k] = x & 0x0f0f0f0fu;
+      q[4 + k] = (x >> 4) & 0x0f0f0f0fu;
+      if constexpr (FIVE) {
+        q[k] |= spread4_hi((qh >> (4 * k)) & 0xf);
+        q[4 + k] |= spread4_hi((qh >> (16 + 4 * k)) & 0xf);
+      }
+      // q4_0 / q5_0 quants stay unsigned: their offset is applied to the dot in the integer
+      // domain, sum (q - c) b = sum q b - c sum b, with sum b precomputed per activation block
+    });
+  }
+}
+
+// The activation rows, decoded once per workgroup: per column j and block b, the 8 int8 quads
+// as two 16-byte halves (lanes read consecutive 16-byte slots: conflict-free ds_read_b128),
+// fp32(fp16 d) and, for q8_1, fp32(fp16 s).  F32 rows are quantized here (ggml's AVX2
+// from_float, bit for bit as stage_b_f32 in lamm_gemv.hip).  Split in two so a thread's
+// activation loads can be issued BEFORE its wave's A loads: waiting for them then does not wait
+// for the HBM stream (vmcnt retires in order).
+template <int T, bool BF32>
+struct ActStage {
+  using F = RFmt<T>;
+  static constexpr int NWB = (F::VBPB + 3) / 4 + 1;
+  static constexpr int NW = BF32 ? 32 : NWB;
+  uint32_t w[NW];
+  uint32_t off = 0;
+
+  template <int NC>
+  __device__ __forceinline__ void load(const GemvArgs& p, __amdgpu_buffer_rsrc_t rb, int it) {
+    const int ncols = p.N < NC ? p.N : NC;
+    const int j = it / p.nblk, b = it % p.nblk;
+    const bool ok = j < ncols && it < NC * p.nblk;
+    if constexpr (BF32) {
+      off = ok ? (uint32_t)(j * p.ldb + (int64_t)b * 128) : 0x7ffffff0u;
+      load_words<32, 0>(rb, off, w);
+    } else {
+      off = ok ? (uint32_t)(j * p.ldb + (int64_t)b * F::VBPB) : 0x7ffffff0u;
+      load_words<NWB, 0>(rb, off & ~3u, w);
+    }
+  }
+
+  __device__ __forceinline__ void store(int it, u32x4* q0, u32x4* q1, float* bd, float* bs) const {
+    uint32_t q[8];
+    float d = 0.f, sx = 0.f;
+    if constexpr (BF32) {
+      float amax = 0.f;
+#pragma unroll
+      for (int k = 0; k < 32; ++k) amax = fmaxf(amax, fabsf(__builtin_bit_cast(float, w[k])));
+      const float dd = amax / 127.f;
+      const float id = amax != 0.0f ? 127.f / amax : 0.0f;
+      int sum = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        uint32_t qw = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          int v = (int)__builtin_rintf(__builtin_bit_cast(float, w[4 * k + e]) * id);
+          v = v > 127 ? 127 : (v < -128 ? -128 : v);
+          sum += v;
+          qw |= (uint32_t)(v & 0xff) << (8 * e);
+        }
+        q[k] = qw;
+      }
+      float dh = dd;
+      asm volatile("" : "+v"(dh));
+      d = (float)(_Float16)dh;
+      if constexpr (F::VBPB == 36) {
+        float sd = (float)sum * dd;
+        asm volatile("" : "+v"(sd));
+        sx = (float)(_Float16)sd;
+      }
+    } else {
+      uint32_t m[NWB - 1];
+      realign(w, m, (int)(off & 3u));
+      constexpr int VQS = F::VBPB == 36 ? 4 : 2;
+      unroll<8>([&](auto K) { q[K] = get32<VQS + 4 * K>(m); });
+      d = h2f(m[0] & 0xffff);
+      if constexpr (VQS == 4) sx = h2f(m[0] >> 16);
+    }
+    if constexpr (T == kQ4_0 || T == kQ5_0) {   // sum b (exact int) for the offset term
+      int sb = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) sb = dot4(q[k], 0x01010101u, sb);
+      sx = __builtin_bit_cast(float, sb);
+    }
+    q0[it] = u32x4{q[0], q[1], q[2], q[3]};
+    q1[it] = u32x4{q[4], q[5], q[6], q[7]};
+    bd[it] = d;
+    bs[it] = sx;
+  }
+};
+
+template <int T, int NC, bool BF32>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t act_rsrc(const GemvArgs& p, const unsigned char* Bz) {
+  using F = RFmt<T>;
+  const int ncols = p.N < NC ? p.N : NC;
+  const int64_t bbytes = BF32 ? (int64_t)(ncols - 1) * p.ldb + (int64_t)p.K * 4
+                              : (int64_t)(ncols - 1) * p.ldb + (int64_t)p.nblk * F::VBPB;
+  return make_rsrc(Bz, (uint32_t)min((bbytes + 3) & ~int64_t(3), (int64_t)0x7fffffff));
+}
+
+// One wave per row: the row's loads for ITER blocks per lane (K <= ITER * 2048) go out at once;
+// each wave also issues its NEXT row's loads before computing the current one (rows strided by
+// the grid), so a persistent grid keeps HBM busy across rows.
+template <int T, int NC, int WAVES, bool BF32, int ITER>
+__global__ __launch_bounds__(64 * WAVES) void gemv_rpw_kernel(GemvArgs p) {
+  using F = RFmt<T>;
+  constexpr int NWA = (F::BPB + 3) / 4 + 1;     // A dwords per block incl. realignment slack
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  const int nb = p.nblk;
+  u32x4* sq0 = reinterpret_cast<u32x4*>(smem_raw);
+  u32x4* sq1 = sq0 + NC * nb;
+  float* sbd = reinterpret_cast<float*>(sq1 + NC * nb);
+  float* sbs = sbd + NC * nb;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int z = blockIdx.y, i12 = z % p.ne12, i13 = z / p.ne12;
+  const unsigned char* Az = p.A + (int64_t)(i12 / p.r2) * p.sa2 + (int64_t)(i13 / p.r3) * p.sa3;
+  const unsigned char* Bz = p.B + (int64_t)i12 * p.sb2 + (int64_t)i13 * p.sb3;
+  float* Cz = p.C + (int64_t)i12 * p.sc2 + (int64_t)i13 * p.sc3;
+  const int ncols = p.N < NC ? p.N : NC;
+  const uint32_t row_bytes = (uint32_t)((nb * F::BPB + 3) & ~3);
+  const int stride = gridDim.x * WAVES;
+
+  auto issue = [&](int64_t row, uint32_t (&wa)[ITER][NWA]) {
+    const auto ra = make_rsrc(Az + row * p.lda, row_bytes);
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+      const int b = lane + 64 * it;
+      const uint32_t off = b < nb ? (uint32_t)(b * F::BPB) & ~3u : 0x7ffffff0u;
+      load_words<NWA, 2>(ra, off, wa[it]);   // non-temporal: A is read once
+    }
+  };
+  auto compute = [&](int64_t row, const uint32_t (&wa)[ITER][NWA]) {
+    float acc[NC];
+#pragma unroll
+    for (int j = 0; j < NC; ++j) acc[j] = 0.f;
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+      const int b = lane + 64 * it;
+      if (b < nb) {
+        uint32_t m[NWA - 1];
+        realign(wa[it], m, (int)((uint32_t)(b * F::BPB) & 3u));
+        uint32_t q[8];
+        float da, ma;
+        unpack_a<T>(m, q, da, ma);
+#pragma unroll
+        for (int j = 0; j < NC; ++j) {
+          const u32x4 b0 = sq0[j * nb + b], b1 = sq1[j * nb + b];
+          int s = 0;
+          s = dot4(q[0], b0[0], s); s = dot4(q[1], b0[1], s); s = dot4(q[2], b0[2], s); s = dot4(q[3], b0[3], s);
+          s = dot4(q[4], b1[0], s); s = dot4(q[5], b1[1], s); s = dot4(q[6], b1[2], s); s = dot4(q[7], b1[3], s);
+          const float db = sbd[j * nb + b];
+          if constexpr (T == kQ4_0) s -= 8 * __builtin_bit_cast(int, sbs[j * nb + b]);
+          if constexpr (T == kQ5_0) s -= 16 * __builtin_bit_cast(int, sbs[j * nb + b]);
+          if constexpr (T == kQ4_1 || T == kQ5_1)
+            acc[j] = __builtin_fmaf(da * db, (float)s, __builtin_fmaf(ma, sbs[j * nb + b], acc[j]));
+          else
+            acc[j] = __builtin_fmaf(da * db, (float)s, acc[j]);
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NC; ++j) acc[j] = wave_sum(acc[j]);   // 64-lane reduction, fixed order
+    if (lane == 0) {
+#pragma unroll
+      for (int j = 0; j < NC; ++j)
+        if (j < ncols) Cz[(int64_t)j * p.ldc + row] = acc[j];
+    }
+  };
+
+  int64_t row = (int64_t)blockIdx.x * WAVES + wave;
+  uint32_t wa0[ITER][NWA], wa1[ITER][NWA];
+  const auto rb = act_rsrc<T, NC, BF32>(p, Bz);
+  const int nact = NC * nb;
+  ActStage<T, BF32> st;
+  const int t0 = threadIdx.x;
+  // straight-line (no branch between them), so the activation loads stay ahead of the row's
+  // HBM stream and waiting for them does not wait for A; out-of-range loads read zeros
+  st.template load<NC>(p, rb, t0);
+  __builtin_amdgcn_sched_barrier(0);   // keep the activation loads first in the vmcnt order
+  issue(row < p.M ? row : 0, wa0);
+  __builtin_amdgcn_sched_barrier(0);
+  if (t0 < nact) st.store(t0, sq0, sq1, sbd, sbs);
+  for (int it = t0 + blockDim.x; it < nact; it += blockDim.x) {
+    st.template load<NC>(p, rb, it);
+    st.store(it, sq0, sq1, sbd, sbs);
+  }
+  __syncthreads();
+  while (row < p.M) {
+    int64_t next = row + stride;
+    if (next < p.M) issue(next, wa1);
+    compute(row, wa0);
+    row = next;
+    if (row >= p.M) break;
+    next = row + stride;
+    if (next < p.M) issue(next, wa0);
+    compute(row, wa1);
+    row = next;
+  }
+}
+
+template <int T, int NC, int WAVES, bool BF32, int ITER>
+hipError_t launch_rpw_k(const GemvArgs& p, hipStream_t s) {
+  const size_t lds = (size_t)NC * p.nblk * 40;
+  const int slices = p.ne12 * p.ne13;
+  const int gmax = (p.M + WAVES - 1) / WAVES;
+  // one round of workgroups over the chip: ~2 per CU in total across the slices
+  int gx = (512 + slices - 1) / slices;
+  gx = gx < 1 ? 1 : (gx > gmax ? gmax : gx);
+  if (lds > 64 * 1024) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((gemv_rpw_kernel<T, NC, WAVES, BF32, ITER>), dim3(gx, slices), dim3(64 * WAVES), lds, s, p);
+  return hipGetLastError();
+}
+
+template <int T, int NC>
+hipError_t launch_rpw_nc(const GemvArgs& p, hipStream_t s, int waves) {
+  const bool bf = p.b_f32 != 0;
+  if (p.nblk <= 128) {
+    if (waves >= 16) return bf ? launch_rpw_k<T, NC, 16, true, 2>(p, s) : launch_rpw_k<T, NC, 16, false, 2>(p, s);
+    if (waves >= 8) return bf ? launch_rpw_k<T, NC, 8, true, 2>(p, s) : launch_rpw_k<T, NC, 8, false, 2>(p, s);
+    return bf ? launch_rpw_k<T, NC, 4, true, 2>(p, s) : launch_rpw_k<T, NC, 4, false, 2>(p, s);
+  }
+  if (waves >= 8) return bf ? launch_rpw_k<T, NC, 8, true, 6>(p, s) : launch_rpw_k<T, NC, 8, false, 6>(p, s);
+  return bf ? launch_rpw_k<T, NC, 4, true, 6>(p, s) : launch_rpw_k<T, NC, 4, false, 6>(p, s);
+}
+
+template <int T>
+hipError_t launch_rpw_t(const GemvArgs& p, hipStream_t s, int waves) {
+  if (p.N <= 1) return launch_rpw_nc<T, 1>(p, s, waves);
+  return launch_rpw_nc<T, 2>(p, s, waves);
+}
+
+}  // namespace
+
+bool gemv_rpw_supported(int type, const GemvArgs& p) {
+  return p.N <= 2 && p.nblk <= 6 * 64 &&
+         (type == kQ4_0 || type == kQ4_1 || type == kQ5_0 || type == kQ5_1 || type == kQ8_0);
+}
+
+hipError_t launch_gemv_rpw(int type, const GemvArgs& p, hipStream_t s, int waves) {
+  switch (type) {
+    case kQ4_0: return launch_rpw_t<kQ4_0>(p, s, waves);
+    case kQ4_1: return launch_rpw_t<kQ4_1>(p, s, waves);
+    case kQ5_0: return launch_rpw_t<kQ5_0>(p, s, waves);
+    case kQ5_1: return launch_rpw_t<kQ5_1>(p, s, waves);
+    case kQ8_0: return launch_rpw_t<kQ8_0>(p, s, waves);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace lamm

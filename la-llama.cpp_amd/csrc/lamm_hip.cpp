@@ -7,6 +7,7 @@
 //                        device-resident weight cache and strided B/C transfers.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -407,6 +408,41 @@ uint64_t fingerprint(const unsigned char* p, size_t pitch, size_t row_bytes, int
   return h;
 }
 
+// LAMM_HIP_STATS=1: per-category count and wall time of lamm_mul_mat (thread 0, entry to
+// return: transfers, kernels, synchronisation), printed to stderr at exit -- how much of a
+// llama.cpp token the boundary accounts for.
+struct CallStats {
+  const char* name;
+  uint64_t calls = 0;
+  double us = 0;
+};
+CallStats g_stats[4] = {{"weights N<=8"}, {"weights N>8"}, {"views N<=8"}, {"views N>8"}};
+bool stats_on() {
+  static const bool on = [] {
+    const char* e = getenv("LAMM_HIP_STATS");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+void print_stats() {
+  for (const auto& c : g_stats)
+    if (c.calls)
+      fprintf(stderr, "lamm_hip stats: %-13s %8llu calls %12.1f us total %8.2f us/call\n", c.name,
+              (unsigned long long)c.calls, c.us, c.us / (double)c.calls);
+}
+struct StatScope {
+  CallStats* c;
+  std::chrono::steady_clock::time_point t0;
+  explicit StatScope(CallStats* cs) : c(cs), t0(std::chrono::steady_clock::now()) {}
+  ~StatScope() {
+    if (c) {
+      c->calls++;
+      c->us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    }
+  }
+};
+
+
 class Runtime {
  public:
   static Runtime& get() {
@@ -422,6 +458,7 @@ class Runtime {
     HIPCHK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     const char* b = getenv("LAMM_HIP_CACHE_GB");
     budget_ = (size_t)((b ? atof(b) : 64.0) * (1ull << 30));
+    if (stats_on()) atexit(print_stats);
   }
 
   // k.rows = ne01*ne02*ne03 device rows; host slices may be strided (nb[2], nb[3])
@@ -696,10 +733,11 @@ extern "C" void lamm_mul_mat(const struct ggml_compute_params* vparams, struct g
   std::lock_guard<std::mutex> lock(rt.mu);
   rt.ensure_init();
   hipStream_t s = rt.stream();
+  const bool weight = is_weight(src0);
+  StatScope stat(stats_on() ? &g_stats[(weight ? 0 : 2) + (N > 8 ? 1 : 0)] : nullptr);
 
   // weights: every (i02, i03) slice, device resident, rows re-pitched to 16 B; any other src0
   // (KV-cache views, intermediates) uploaded afresh
-  const bool weight = is_weight(src0);
   WeightEntry* w = nullptr;
   void* a_dev;
   int64_t a_pitch;

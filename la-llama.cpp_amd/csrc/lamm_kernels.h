@@ -24,6 +24,10 @@ struct GemvArgs {
 };
 
 hipError_t launch_gemv(int type, const GemvArgs& p, hipStream_t s);
+// row-per-wave decode GEMV (lamm_gemv_rpw.hip): 32-element block formats, N <= 2, K <= 12288;
+// `waves` per workgroup (4 / 8 / 16; 8 at most for K > 4096)
+bool gemv_rpw_supported(int type, const GemvArgs& p);
+hipError_t launch_gemv_rpw(int type, const GemvArgs& p, hipStream_t s, int waves);
 size_t gemv_lds_bytes(int type, int nc);
 hipError_t launch_gemv_dense(int type, const GemvArgs& p, hipStream_t s);   // F32 / F16 rows
 // q4_K / q5_K / q6_K prefill GEMM (lamm_gemm_kq.hip); B rows (q8_K) 4-byte aligned

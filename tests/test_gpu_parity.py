@@ -739,3 +739,59 @@ def test_config3_four_slice_batched_launch():
     for z in range(4):
         err = _config3_check(c[z], As[z], Bs[z], rows)
         assert err < TOL, (z, err)
+
+
+# ---------------------------------------------------------------- row-per-wave decode GEMV
+RPW_TYPES = [ol.Q4_0, ol.Q4_1, ol.Q5_0, ol.Q5_1, ol.Q8_0]
+RPW_SHAPES = [(1, 1, 32), (5, 1, 96), (67, 2, 512), (130, 1, 4096), (33, 2, 4096 + 256), (9, 1, 11008),
+              (257, 1, 8192 + 32)]
+
+
+@pytest.mark.parametrize("rows", ["4", "8", "16"])
+@pytest.mark.parametrize("t", RPW_TYPES, ids=[ol.NAMES[t] for t in RPW_TYPES])
+@pytest.mark.parametrize("shape", RPW_SHAPES, ids=[f"{m}x{n}x{k}" for m, n, k in RPW_SHAPES])
+def test_gemv_row_per_wave(t, shape, rows, monkeypatch):
+    """lamm_gemv_rpw.hip (LAMM_GEMV_RPW = waves per workgroup, 8 at most past K = 4096): ragged
+    M / K, one and two columns,
+    q8 activations and F32 activations (INIT fused, must equal quantize + matmul)."""
+    monkeypatch.setenv("LAMM_GEMV_RPW", rows)
+    M, N, K = shape
+    A_q, B_q = random_case(t, M, N, K, seed=M * 7 + K + int(rows))
+    got, _ = gpu_mul_mat(t, A_q, B_q, M, N, K)
+    ref = ORACLE.mul_mat(t, M, N, K, A_q, B_q)
+    assert rel_err(got, ref, absdot(t, A_q, B_q, M, N, K)).max() < TOL
+    # F32 activations: the kernel quantizes them (AVX2 flavour) -> same C as the q8 path
+    rng = np.random.default_rng(M + K)
+    x = rng.standard_normal((N, K), dtype=np.float32)
+    vt = la.vec_dot_type(t)
+    Bx = ORACLE.quantize(vt, x, ol.QUANT_AVX)
+    kb = K // 32
+    lda = pitch_blocks(t, kb)
+    A = dev_bytes(pitched_A(t, A_q, M, kb, lda))
+    X = torch.from_numpy(x).cuda()
+    C = torch.full((N * M,), float("nan"), dtype=torch.float32, device="cuda")
+    la.matmul(la.Matrix(A.data_ptr(), t, M, kb, lda), la.Matrix(X.data_ptr(), la.F32, K, N, K),
+              la.Matrix(C.data_ptr(), la.F32, M, N, M), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    want, _ = gpu_mul_mat(t, A_q, Bx, M, N, K)
+    np.testing.assert_array_equal(C.cpu().numpy().reshape(N, M), want)
+
+
+def test_gemv_row_per_wave_batched_broadcast(monkeypatch):
+    """Batch slices (ne02 = 2 broadcast over ne12 = 4) through the row-per-wave kernel."""
+    monkeypatch.setenv("LAMM_GEMV_RPW", "16")
+    t, M, N, K = ol.Q4_0, 100, 1, 1024
+    kb = K // 32
+    As = [random_case(t, M, N, K, seed=200 + s)[0] for s in range(2)]
+    Bs = [random_case(t, M, N, K, seed=210 + s)[1] for s in range(4)]
+    abytes, bbytes = M * kb * 18, N * kb * 34
+    A = dev_bytes(np.concatenate(As + [np.zeros(64, np.uint8)]))
+    B = dev_bytes(np.concatenate(Bs))
+    C = torch.full((4 * N * M,), float("nan"), dtype=torch.float32, device="cuda")
+    bt = la.Batch(2, 1, 4, 1, abytes, 2 * abytes, bbytes, 4 * bbytes, 4 * M * N, 16 * M * N)
+    la.mul_mat_torch(t, A, B, C, M, N, K, batch=bt)
+    torch.cuda.synchronize()
+    c = C.cpu().numpy().reshape(4, N, M)
+    for z in range(4):
+        ref = ORACLE.mul_mat(t, M, N, K, As[z // 2], Bs[z])
+        assert rel_err(c[z], ref, absdot(t, As[z // 2], Bs[z], M, N, K)).max() < TOL, z

@@ -144,6 +144,37 @@ int lamm_blck_size(int type);
 size_t lamm_type_size(int type);
 int lamm_vec_dot_type(int type);
 
+/* ---- 3. multi-GPU row sharding (the reference's row split over threads,
+ *         src/lamm_impl.hpp:38-43 / :107-112, mapped onto GPUs) -------------------------
+ * Every rank of a communicator owns a contiguous slab of A's rows, computes its slab of C with
+ * the calls above (A.data / C.data offset to its rows), and lamm_hip_allgather_rows gives every
+ * rank the whole C through one RCCL all-gather over xGMI.  RCCL is loaded at the first
+ * communicator (dlopen); all calls return a lamm_status (lamm_hip_comm_last_error explains). */
+typedef struct lamm_comm lamm_comm;
+#define LAMM_COMM_ID_BYTES 128
+/* Rows [*r0, *r0 + *rows) of rank `rank` of `world`: whole `align`-row tiles, the tile remainder
+ * spread over the first ranks -- every row exactly once, for any M (the reference's M / nth
+ * split drops M % nth rows: SURVEY §8a defect 1). */
+void lamm_hip_shard_rows(int64_t M, int world, int rank, int align, int64_t *r0, int64_t *rows);
+/* One process per GPU: rank 0 makes the id (LAMM_COMM_ID_BYTES) and shares it (e.g. over
+ * torch.distributed); every rank then joins with its own device. */
+int lamm_hip_comm_unique_id(void *id);
+int lamm_hip_comm_init_rank(lamm_comm **out, int world, int rank, const void *id, int device);
+/* One process driving `ndev` devices (ncclCommInitAll).  Ranks that share a device (a rehearsal
+ * on a one-GPU box; RCCL refuses duplicates) exchange slabs with device copies instead. */
+int lamm_hip_comm_init_all(lamm_comm **out, int ndev, const int *devices);
+int lamm_hip_comm_size(const lamm_comm *c);
+int lamm_hip_comm_local_ranks(const lamm_comm *c);      /* ranks driven by this process */
+int lamm_hip_comm_rank(const lamm_comm *c, int local);   /* global rank of local rank `local` */
+void lamm_hip_comm_destroy(lamm_comm *c);
+const char *lamm_hip_comm_last_error(void);
+/* For each local rank i (arrays of lamm_hip_comm_local_ranks entries): slabs[i] holds its C slab
+ * (N columns of its rows, column stride ld_slab[i] floats, on its device); C[i] receives the
+ * whole C (C[j*ldc + row], ldc >= M) on that device.  Enqueued on streams[i]; the slab may
+ * alias C[i] + r0. */
+int lamm_hip_allgather_rows(lamm_comm *c, const float *const *slabs, const int64_t *ld_slab, float *const *C,
+                            int64_t ldc, int64_t M, int N, int align, void *const *streams);
+
 /* Device weight residency used by the ggml boundary (keyed by src0->data/type/
  * shape/strides plus a sampled fingerprint of the bytes). */
 void lamm_hip_cache_clear(void);

@@ -115,6 +115,22 @@ lib.lamm_blck_size.restype = ctypes.c_int
 lib.lamm_type_size.restype = ctypes.c_size_t
 lib.lamm_vec_dot_type.restype = ctypes.c_int
 lib.lamm_hip_build_id.restype = ctypes.c_char_p
+lib.lamm_hip_shard_rows.restype = None
+lib.lamm_hip_shard_rows.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                    ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]
+lib.lamm_hip_comm_unique_id.argtypes = [ctypes.c_void_p]
+lib.lamm_hip_comm_init_rank.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                        ctypes.c_int]
+lib.lamm_hip_comm_init_all.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+lib.lamm_hip_comm_size.argtypes = [ctypes.c_void_p]
+lib.lamm_hip_comm_local_ranks.argtypes = [ctypes.c_void_p]
+lib.lamm_hip_comm_rank.argtypes = [ctypes.c_void_p, ctypes.c_int]
+lib.lamm_hip_comm_destroy.argtypes = [ctypes.c_void_p]
+lib.lamm_hip_comm_destroy.restype = None
+lib.lamm_hip_comm_last_error.restype = ctypes.c_char_p
+lib.lamm_hip_allgather_rows.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_int64),
+                                        ctypes.POINTER(ctypes.c_void_p), ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
+                                        ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
 lib.lamm_hip_cache_clear.restype = None
 lib.lamm_hip_cache_bytes.restype = ctypes.c_size_t
 
@@ -287,6 +303,79 @@ def gemm_engine(fmt, M, N, K, slices=1, stationary=False):
             split *= 2
     grid = tiles * max(1, min(split, nsteps))
     return "fp6" if (grid if stationary else tiles) >= 256 else "i8"
+
+
+COMM_ID_BYTES = 128
+
+
+def shard_rows(M, world, rank, align=1):
+    """(r0, rows) of `rank`'s contiguous slab of M rows (lamm_hip_shard_rows)."""
+    r0, rows = ctypes.c_int64(), ctypes.c_int64()
+    lib.lamm_hip_shard_rows(M, world, rank, align, ctypes.byref(r0), ctypes.byref(rows))
+    return r0.value, rows.value
+
+
+def comm_unique_id():
+    buf = ctypes.create_string_buffer(COMM_ID_BYTES)
+    _check_comm(lib.lamm_hip_comm_unique_id(buf), "lamm_hip_comm_unique_id")
+    return buf.raw
+
+
+def _check_comm(rc, what):
+    if rc != LAMM_OK:
+        raise LammError(f"{what} failed ({rc}): {lib.lamm_hip_comm_last_error().decode()}")
+
+
+class Comm:
+    """lamm_comm: row-sharded multi-GPU communicator.  Comm.rank(world, rank, id,
+    device) joins a one-process-per-GPU communicator; Comm.all(devices) drives several devices
+    from this process (duplicate devices = loopback exchange, for one-GPU rehearsals)."""
+
+    def __init__(self, handle):
+        self.h = handle
+
+    @classmethod
+    def rank(cls, world, rank, uid, device):
+        h = ctypes.c_void_p()
+        _check_comm(lib.lamm_hip_comm_init_rank(ctypes.byref(h), world, rank, uid, device), "lamm_hip_comm_init_rank")
+        return cls(h)
+
+    @classmethod
+    def all(cls, devices):
+        h = ctypes.c_void_p()
+        arr = (ctypes.c_int * len(devices))(*devices)
+        _check_comm(lib.lamm_hip_comm_init_all(ctypes.byref(h), len(devices), arr), "lamm_hip_comm_init_all")
+        return cls(h)
+
+    @property
+    def size(self):
+        return lib.lamm_hip_comm_size(self.h)
+
+    @property
+    def local_ranks(self):
+        return lib.lamm_hip_comm_local_ranks(self.h)
+
+    def global_rank(self, local=0):
+        return lib.lamm_hip_comm_rank(self.h, local)
+
+    def allgather_rows(self, slabs, ld_slabs, Cs, ldc, M, N, align, streams):
+        """Per local rank i: slabs[i] (device pointer, column stride ld_slabs[i] floats) -> Cs[i]
+        (whole C, C[j*ldc + row]); enqueued on streams[i]."""
+        n = len(slabs)
+        P = ctypes.c_void_p * n
+        _check_comm(lib.lamm_hip_allgather_rows(self.h, P(*slabs), (ctypes.c_int64 * n)(*ld_slabs), P(*Cs), ldc, M, N,
+                                                align, P(*streams)), "lamm_hip_allgather_rows")
+
+    def close(self):
+        if self.h:
+            lib.lamm_hip_comm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def can_mul_mat(params, dst):

@@ -115,3 +115,23 @@ def test_build_id_matches_tree():
     (Makefile BUILD_ID vs lamm_amd.source_build_id()); a stale prebuilt library fails here."""
     assert la.build_id() == la.source_build_id(), (
         f"liblamm_hip.so build id {la.build_id()} != sources {la.source_build_id()}: rebuild with make -C la-llama.cpp_amd")
+
+
+@pytest.mark.parametrize("align", [1, 4, 16, 128, 256])
+def test_shard_rows_cover_every_row_once(align):
+    """lamm_hip_shard_rows (the multi-GPU row split): contiguous slabs in rank order
+    covering [0, M) exactly once, boundaries on `align`-row tiles, slab sizes differing by at most
+    one tile -- unlike the reference's M / nth split (src/lamm_impl.hpp:38-43), which drops the
+    M % nth tail rows (SURVEY §8a defect 1)."""
+    for M in [0, 1, 5, 63, 64, 65, 4095, 4096, 4097, 11008, 32000]:
+        for world in [1, 2, 3, 4, 7, 8]:
+            slabs = [la.shard_rows(M, world, r, align) for r in range(world)]
+            pos = 0
+            for r0, rows in slabs:
+                assert r0 == pos and rows >= 0
+                pos += rows
+                if rows and r0 + rows < M:
+                    assert (r0 + rows) % align == 0
+            assert pos == M
+            tiles = [-(-rows // align) for _, rows in slabs]
+            assert max(tiles) - min(tiles) <= 1

@@ -179,6 +179,12 @@ int lamm_hip_allgather_rows(lamm_comm *c, const float *const *slabs, const int64
  * shape/strides plus a sampled fingerprint of the bytes). */
 void lamm_hip_cache_clear(void);
 size_t lamm_hip_cache_bytes(void);
+/* The boundary's devices: LAMM_HIP_DEVICES unset = one device (LAMM_HIP_DEVICE or the first
+ * gfx950); "all" = every gfx950 device; "0,1,2,3" = that list.  With several, each weight's rows
+ * are split over them (lamm_hip_shard_rows) and every device copies its rows of C straight into
+ * dst -- the host consumes C, no collective.  Read at the first call; reset drops
+ * every device's cache and stream so the next call reads the environment again. */
+void lamm_hip_boundary_reset(void);
 
 #ifdef __cplusplus
 }

@@ -16,6 +16,7 @@
 #include <mutex>
 #include <string>
 #include <unordered_map>
+#include <vector>
 
 #include "../../include/lamm_hip.h"
 #include "ggml_b2430_abi.h"
@@ -44,8 +45,9 @@ int fail(int code, const char* fmt, ...) {
 }
 
 struct DeviceProbe {
-  int count = 0;      // gfx950 devices visible
-  int device = 0;     // device used by the ggml boundary
+  int count = 0;          // gfx950 devices visible
+  int device = 0;         // device used by the ggml boundary
+  std::vector<int> ids;   // every gfx950 device
 };
 
 const DeviceProbe& probe() {
@@ -58,6 +60,7 @@ const DeviceProbe& probe() {
       if (hipGetDeviceProperties(&prop, i) == hipSuccess && strncmp(prop.gcnArchName, "gfx950", 6) == 0) {
         if (d.count == 0) d.device = i;
         ++d.count;
+        d.ids.push_back(i);
       }
     }
     const char* env = getenv("LAMM_HIP_DEVICE");
@@ -443,6 +446,98 @@ struct StatScope {
 };
 
 
+// One device of the ggml boundary: its stream, its weight cache (LRU under the per-device budget)
+// and grow-only scratch.  With LAMM_HIP_DEVICES listing several devices, every weight's rows are
+// split over them (SURVEY §8e "host consumes C": each device computes its row slab of C and
+// copies it straight into dst's rows -- no collective); device ids may repeat (a rehearsal of the
+// multi-GPU path on one GPU).
+struct Dev {
+  int id = 0;
+  hipStream_t stream = nullptr;
+  std::unordered_map<WeightKey, WeightEntry, WeightKeyHash> cache;
+  std::list<WeightKey> lru;
+  size_t cached = 0;
+  void* buf[4] = {nullptr, nullptr, nullptr, nullptr};   // B, C, F32 src1, transient src0
+  size_t cap[4] = {0, 0, 0, 0};
+
+  void* scratch(int which, size_t bytes) {
+    if (cap[which] < bytes) {
+      if (buf[which]) HIPCHK(hipFree(buf[which]));
+      HIPCHK(hipMalloc(&buf[which], bytes + 256));
+      cap[which] = bytes;
+    }
+    return buf[which];
+  }
+  void evict(std::unordered_map<WeightKey, WeightEntry, WeightKeyHash>::iterator it) {
+    if (it == cache.end()) return;
+    (void)hipSetDevice(id);
+    (void)hipStreamSynchronize(stream);
+    (void)hipFree(it->second.dev);
+    if (it->second.prepared) {
+      cached -= lamm_hip_weights_bytes(it->second.prepared);
+      lamm_hip_weights_destroy(it->second.prepared);
+    }
+    cached -= it->second.bytes;
+    lru.erase(it->second.lru);
+    cache.erase(it);
+  }
+};
+
+// A src0 that is not a weight -- a view of the KV cache or an intermediate -- is uploaded on
+// EVERY call and never cached: b2430's K/V views keep one data pointer while single token
+// rows change inside them (llama.cpp:5322-5372 views, :8887 kv_self.n padded to 32), which no
+// sampled fingerprint can see.  Device layout (pitch, slice strides in bytes):
+//   rows stacked (nb2 = nb1*ne1, nb3 = nb2*ne2; the transposed V view): one 2D copy;
+//   dense interleaved slices (the K view: the heads of a token side by side in one cache
+//     row, nb1 = n_embd_k_gqa*2, nb2 = 256): one linear copy of the byte span, host strides;
+//   anything else: a 2D copy per slice.
+struct Transient {
+  void* dev;
+  int64_t pitch;
+  size_t s2, s3;
+};
+Transient upload_transient(Dev& d, const ggml::tensor* src0, size_t row_bytes) {
+  const int64_t ne1 = src0->ne[1], ne2 = src0->ne[2], ne3 = src0->ne[3];
+  const size_t nb1 = src0->nb[1], nb2 = src0->nb[2], nb3 = src0->nb[3];
+  const auto* host = static_cast<const unsigned char*>(src0->data);
+  const size_t bpb = block_bytes(src0->type);
+  const size_t span = (size_t)(ne1 - 1) * nb1 + (size_t)(ne2 - 1) * nb2 + (size_t)(ne3 - 1) * nb3 + row_bytes;
+  const size_t payload = row_bytes * (size_t)(ne1 * ne2 * ne3);
+  const bool stacked = nb2 == nb1 * (size_t)ne1 && nb3 == nb2 * (size_t)ne2;
+  if (!stacked && nb1 % 16 == 0 && nb2 % 16 == 0 && nb3 % 16 == 0 && nb1 % bpb == 0 && nb1 >= row_bytes &&
+      span <= 2 * payload) {
+    void* dev = d.scratch(3, span + 64);
+    HIPCHK(hipMemcpyAsync(dev, host, span, hipMemcpyHostToDevice, d.stream));
+    return Transient{dev, (int64_t)nb1, nb2, nb3};
+  }
+  size_t pb = row_bytes / bpb;
+  while ((pb * bpb) % 16) ++pb;
+  const int64_t pitch = (int64_t)(pb * bpb);
+  void* dev = d.scratch(3, (size_t)pitch * (size_t)(ne1 * ne2 * ne3) + 64);
+  auto* dp = static_cast<unsigned char*>(dev);
+  if (stacked) {
+    HIPCHK(hipMemcpy2DAsync(dp, pitch, host, nb1, row_bytes, (size_t)(ne1 * ne2 * ne3), hipMemcpyHostToDevice,
+                            d.stream));
+  } else {
+    for (int64_t i3 = 0; i3 < ne3; ++i3)
+      for (int64_t i2 = 0; i2 < ne2; ++i2)
+        HIPCHK(hipMemcpy2DAsync(dp + (i3 * ne2 + i2) * ne1 * pitch, pitch, host + i2 * nb2 + i3 * nb3, nb1, row_bytes,
+                                (size_t)ne1, hipMemcpyHostToDevice, d.stream));
+  }
+  return Transient{dev, pitch, (size_t)pitch * ne1, (size_t)pitch * ne1 * ne2};
+}
+
+// the fingerprint of every (i02, i03) slice of a weight (sampled bytes + shape), host side
+uint64_t weight_fingerprint(const ggml::tensor* src0, size_t row_bytes) {
+  uint64_t fp = 0;
+  for (int64_t i3 = 0; i3 < src0->ne[3]; ++i3)
+    for (int64_t i2 = 0; i2 < src0->ne[2]; ++i2)
+      fp = fp * 1099511628211ull ^ fingerprint(static_cast<const unsigned char*>(src0->data) + i2 * src0->nb[2] +
+                                                   i3 * src0->nb[3],
+                                               src0->nb[1], row_bytes, src0->ne[1]);
+  return fp;
+}
+
 class Runtime {
  public:
   static Runtime& get() {
@@ -451,118 +546,88 @@ class Runtime {
   }
 
   std::mutex mu;
+  std::vector<Dev> devs;
 
+  // LAMM_HIP_DEVICES: unset = the one boundary device (LAMM_HIP_DEVICE / the first gfx950);
+  // "all" = every gfx950 device; "0,1,2,3" = that list (repeats allowed: one-GPU rehearsal)
   void ensure_init() {
-    if (stream_) return;
-    HIPCHK(hipSetDevice(probe().device));
-    HIPCHK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    if (!devs.empty()) return;
+    std::vector<int> ids;
+    const char* e = getenv("LAMM_HIP_DEVICES");
+    int nvis = 0;
+    (void)hipGetDeviceCount(&nvis);
+    if (e && !strcmp(e, "all")) {
+      ids = probe().ids;
+    } else if (e && *e) {
+      for (const char* c = e; *c;) {
+        char* end = nullptr;
+        const long v = strtol(c, &end, 10);
+        if (end == c) break;
+        if (v < 0 || v >= nvis) {
+          fprintf(stderr, "lamm_hip: LAMM_HIP_DEVICES lists device %ld of %d\n", v, nvis);
+          std::abort();
+        }
+        ids.push_back((int)v);
+        c = *end == ',' ? end + 1 : end;
+      }
+    }
+    if (ids.empty()) ids.push_back(probe().device);
+    devs.resize(ids.size());
+    for (size_t i = 0; i < ids.size(); ++i) {
+      devs[i].id = ids[i];
+      HIPCHK(hipSetDevice(ids[i]));
+      HIPCHK(hipStreamCreateWithFlags(&devs[i].stream, hipStreamNonBlocking));
+    }
     const char* b = getenv("LAMM_HIP_CACHE_GB");
     budget_ = (size_t)((b ? atof(b) : 64.0) * (1ull << 30));
     if (stats_on()) atexit(print_stats);
   }
 
-  // k.rows = ne01*ne02*ne03 device rows; host slices may be strided (nb[2], nb[3])
-  WeightEntry& weights(const WeightKey& k, size_t row_bytes, const ggml::tensor* src0) {
-    const int64_t ne01 = src0->ne[1], ne02 = src0->ne[2], ne03 = src0->ne[3];
-    uint64_t fp = 0;
-    for (int64_t i3 = 0; i3 < ne03; ++i3)
-      for (int64_t i2 = 0; i2 < ne02; ++i2)
-        fp = fp * 1099511628211ull ^ fingerprint(static_cast<const unsigned char*>(k.host) + i2 * src0->nb[2] +
-                                                     i3 * src0->nb[3],
-                                                 k.host_pitch, row_bytes, ne01);
-    auto it = cache_.find(k);
-    if (it != cache_.end()) {
+  // rows [r0, r0 + rows) of every (i02, i03) slice of a weight on device d, re-pitched to 16 B
+  WeightEntry& weights(Dev& d, const WeightKey& k, size_t row_bytes, const ggml::tensor* src0, int64_t r0,
+                       int64_t rows, uint64_t fp) {
+    const int64_t ne02 = src0->ne[2], ne03 = src0->ne[3];
+    auto it = d.cache.find(k);
+    if (it != d.cache.end()) {
       if (it->second.fingerprint == fp) {
-        lru_.splice(lru_.begin(), lru_, it->second.lru);
+        d.lru.splice(d.lru.begin(), d.lru, it->second.lru);
         return it->second;
       }
-      evict(it);
+      d.evict(it);
     }
     WeightEntry e;
-    // device row pitch: >= row_bytes, a whole number of blocks, a multiple of 16 B
     const size_t bpb = block_bytes(k.type);
     size_t pitch_blocks = (size_t)k.kb;
     while ((pitch_blocks * bpb) % 16) ++pitch_blocks;
     e.dev_pitch = (int64_t)(pitch_blocks * bpb);
-    e.bytes = (size_t)e.dev_pitch * k.rows + 64;
-    while (cached_bytes_ + e.bytes > budget_ && !lru_.empty()) evict(cache_.find(lru_.back()));
+    e.bytes = (size_t)e.dev_pitch * (size_t)(rows * ne02 * ne03) + 64;
+    while (d.cached + e.bytes > budget_ && !d.lru.empty()) d.evict(d.cache.find(d.lru.back()));
     HIPCHK(hipMalloc(&e.dev, e.bytes));
     for (int64_t i3 = 0; i3 < ne03; ++i3)
       for (int64_t i2 = 0; i2 < ne02; ++i2)
-        HIPCHK(hipMemcpy2DAsync(static_cast<unsigned char*>(e.dev) + (i3 * ne02 + i2) * ne01 * e.dev_pitch,
+        HIPCHK(hipMemcpy2DAsync(static_cast<unsigned char*>(e.dev) + (i3 * ne02 + i2) * rows * e.dev_pitch,
                                 e.dev_pitch,
-                                static_cast<const unsigned char*>(k.host) + i2 * src0->nb[2] + i3 * src0->nb[3],
-                                k.host_pitch, row_bytes, ne01, hipMemcpyHostToDevice, stream_));
+                                static_cast<const unsigned char*>(k.host) + i2 * src0->nb[2] + i3 * src0->nb[3] +
+                                    r0 * src0->nb[1],
+                                k.host_pitch, row_bytes, rows, hipMemcpyHostToDevice, d.stream));
     e.fingerprint = fp;
-    lru_.push_front(k);
-    e.lru = lru_.begin();
-    cached_bytes_ += e.bytes;
-    return cache_.emplace(k, e).first->second;
+    d.lru.push_front(k);
+    e.lru = d.lru.begin();
+    d.cached += e.bytes;
+    return d.cache.emplace(k, e).first->second;
   }
 
-  // the entry's weight-stationary handle (packed fp6 GEMM form), created on first use
-  lamm_weights* prepared(WeightEntry& e, const lamm_matrix& A, int64_t ne02, int64_t ne03) {
+  // the entry's weight-stationary handle (packed GEMM form), created on first use
+  lamm_weights* prepared(Dev& d, WeightEntry& e, const lamm_matrix& A, int64_t ne02, int64_t ne03) {
     if (!e.prepared) {
       const size_t pitch = (size_t)e.dev_pitch * A.row;
-      if (lamm_hip_weights_create(&A, ne02, ne03, pitch, pitch * ne02, stream_, &e.prepared) != LAMM_OK) {
+      if (lamm_hip_weights_create(&A, ne02, ne03, pitch, pitch * ne02, d.stream, &e.prepared) != LAMM_OK) {
         fprintf(stderr, "lamm_hip: lamm_hip_weights_create failed: %s\n", g_err.c_str());
         std::abort();
       }
-      cached_bytes_ += lamm_hip_weights_bytes(e.prepared);
+      d.cached += lamm_hip_weights_bytes(e.prepared);
     }
     return e.prepared;
-  }
-
-  // A src0 that is not a weight -- a view of the KV cache or an intermediate -- is uploaded on
-  // EVERY call and never cached: b2430's K/V views keep one data pointer while single token
-  // rows change inside them (llama.cpp:5322-5372 views, :8887 kv_self.n padded to 32), which no
-  // sampled fingerprint can see.  Device layout (pitch, slice strides in bytes):
-  //   rows stacked (nb2 = nb1*ne1, nb3 = nb2*ne2; the transposed V view): one 2D copy;
-  //   dense interleaved slices (the K view: the heads of a token side by side in one cache
-  //     row, nb1 = n_embd_k_gqa*2, nb2 = 256): one linear copy of the byte span, host strides;
-  //   anything else: a 2D copy per slice.
-  struct Transient {
-    void* dev;
-    int64_t pitch;
-    size_t s2, s3;
-  };
-  Transient transient(const ggml::tensor* src0, size_t row_bytes) {
-    const int64_t ne1 = src0->ne[1], ne2 = src0->ne[2], ne3 = src0->ne[3];
-    const size_t nb1 = src0->nb[1], nb2 = src0->nb[2], nb3 = src0->nb[3];
-    const auto* host = static_cast<const unsigned char*>(src0->data);
-    const size_t bpb = block_bytes(src0->type);
-    const size_t span = (size_t)(ne1 - 1) * nb1 + (size_t)(ne2 - 1) * nb2 + (size_t)(ne3 - 1) * nb3 + row_bytes;
-    const size_t payload = row_bytes * (size_t)(ne1 * ne2 * ne3);
-    const bool stacked = nb2 == nb1 * (size_t)ne1 && nb3 == nb2 * (size_t)ne2;
-    if (!stacked && nb1 % 16 == 0 && nb2 % 16 == 0 && nb3 % 16 == 0 && nb1 % bpb == 0 && nb1 >= row_bytes &&
-        span <= 2 * payload) {
-      void* dev = scratch(3, span + 64);
-      HIPCHK(hipMemcpyAsync(dev, host, span, hipMemcpyHostToDevice, stream_));
-      return Transient{dev, (int64_t)nb1, nb2, nb3};
-    }
-    size_t pb = row_bytes / bpb;
-    while ((pb * bpb) % 16) ++pb;
-    const int64_t pitch = (int64_t)(pb * bpb);
-    void* dev = scratch(3, (size_t)pitch * (size_t)(ne1 * ne2 * ne3) + 64);
-    auto* d = static_cast<unsigned char*>(dev);
-    if (stacked) {
-      HIPCHK(hipMemcpy2DAsync(d, pitch, host, nb1, row_bytes, (size_t)(ne1 * ne2 * ne3), hipMemcpyHostToDevice, stream_));
-    } else {
-      for (int64_t i3 = 0; i3 < ne3; ++i3)
-        for (int64_t i2 = 0; i2 < ne2; ++i2)
-          HIPCHK(hipMemcpy2DAsync(d + (i3 * ne2 + i2) * ne1 * pitch, pitch, host + i2 * nb2 + i3 * nb3, nb1, row_bytes,
-                                  (size_t)ne1, hipMemcpyHostToDevice, stream_));
-    }
-    return Transient{dev, pitch, (size_t)pitch * ne1, (size_t)pitch * ne1 * ne2};
-  }
-
-  void* scratch(int which, size_t bytes) {
-    if (cap_[which] < bytes) {
-      if (buf_[which]) HIPCHK(hipFree(buf_[which]));
-      HIPCHK(hipMalloc(&buf_[which], bytes + 256));
-      cap_[which] = bytes;
-    }
-    return buf_[which];
   }
 
   // pinned host staging (grow-only): decode-sized B uploads / C downloads as one DMA each
@@ -577,31 +642,29 @@ class Runtime {
   }
 
   void clear() {
-    while (!lru_.empty()) evict(cache_.find(lru_.back()));
+    for (Dev& d : devs)
+      while (!d.lru.empty()) d.evict(d.cache.find(d.lru.back()));
   }
-  size_t cached_bytes() const { return cached_bytes_; }
-  hipStream_t stream() const { return stream_; }
+  // drop every device's cache, scratch and stream; the next call re-reads the environment
+  void reset() {
+    clear();
+    for (Dev& d : devs) {
+      (void)hipSetDevice(d.id);
+      (void)hipStreamSynchronize(d.stream);
+      for (void* b : d.buf)
+        if (b) (void)hipFree(b);
+      (void)hipStreamDestroy(d.stream);
+    }
+    devs.clear();
+  }
+  size_t cached_bytes() const {
+    size_t n = 0;
+    for (const Dev& d : devs) n += d.cached;
+    return n;
+  }
 
  private:
-  void evict(std::unordered_map<WeightKey, WeightEntry, WeightKeyHash>::iterator it) {
-    if (it == cache_.end()) return;
-    (void)hipStreamSynchronize(stream_);
-    (void)hipFree(it->second.dev);
-    if (it->second.prepared) {
-      cached_bytes_ -= lamm_hip_weights_bytes(it->second.prepared);
-      lamm_hip_weights_destroy(it->second.prepared);
-    }
-    cached_bytes_ -= it->second.bytes;
-    lru_.erase(it->second.lru);
-    cache_.erase(it);
-  }
-
-  hipStream_t stream_ = nullptr;
-  size_t budget_ = 0, cached_bytes_ = 0;
-  std::unordered_map<WeightKey, WeightEntry, WeightKeyHash> cache_;
-  std::list<WeightKey> lru_;
-  void* buf_[4] = {nullptr, nullptr, nullptr, nullptr};   // B, C, F32 src1, transient src0
-  size_t cap_[4] = {0, 0, 0, 0};
+  size_t budget_ = 0;
   unsigned char* hbuf_[2] = {nullptr, nullptr};
   size_t hcap_[2] = {0, 0};
 };
@@ -727,114 +790,143 @@ extern "C" void lamm_mul_mat(const struct ggml_compute_params* vparams, struct g
   const size_t a_row = (size_t)kb * block_bytes(t0);
   const size_t b_row = (size_t)kb * block_bytes(vdt);           // ggml_row_size(vdt, ne10)
   const bool use_wdata = src1->type != vdt;
+  const bool gpu_quant = use_wdata && gpu_quantizes(src0, src1);
   const int64_t M = ne01, N = ne11, nslices = ne12 * ne13;
 
   Runtime& rt = Runtime::get();
   std::lock_guard<std::mutex> lock(rt.mu);
   rt.ensure_init();
-  hipStream_t s = rt.stream();
   const bool weight = is_weight(src0);
   StatScope stat(stats_on() ? &g_stats[(weight ? 0 : 2) + (N > 8 ? 1 : 0)] : nullptr);
-
-  // weights: every (i02, i03) slice, device resident, rows re-pitched to 16 B; any other src0
-  // (KV-cache views, intermediates) uploaded afresh
-  WeightEntry* w = nullptr;
-  void* a_dev;
-  int64_t a_pitch;
-  size_t a_s2, a_s3;
-  if (weight) {
-    w = &rt.weights(WeightKey{src0->data, t0, M * ne02 * ne03, kb, src0->nb[1], src0->nb[2], src0->nb[3]}, a_row,
-                    src0);
-    a_dev = w->dev;
-    a_pitch = w->dev_pitch;
-    a_s2 = (size_t)a_pitch * M;
-    a_s3 = a_s2 * ne02;
-  } else {
-    const Runtime::Transient tr = rt.transient(src0, a_row);
-    a_dev = tr.dev;
-    a_pitch = tr.pitch;
-    a_s2 = tr.s2;
-    a_s3 = tr.s3;
+  // weights: rows split over the boundary's devices (one device: all rows); other src0
+  // (KV-cache views, intermediates): uploaded afresh, on the first device
+  const int G = weight ? (int)rt.devs.size() : 1;
+  const uint64_t fp = weight ? weight_fingerprint(src0, a_row) : 0;
+  const size_t b_bytes = b_row * (size_t)(N * nslices);
+  const unsigned char* b_host = nullptr;   // the activation bytes every device uploads
+  if (use_wdata && !gpu_quant) {
+    b_host = static_cast<const unsigned char*>(params->wdata);
+    if (use_pinned(b_bytes)) {
+      unsigned char* hB = rt.pinned(0, b_bytes);
+      memcpy(hB, params->wdata, b_bytes);
+      b_host = hB;
+    }
   }
-  // activations: INIT-phase wdata (contiguous rows) or a contiguous vec_dot-typed src1
-  void* dB = rt.scratch(0, b_row * (size_t)(N * nslices) + 64);
-  if (use_wdata && gpu_quantizes(src0, src1)) {
-    // F32 rows -> device (contiguous [slice][N][K]) -> vec_dot_type blocks on the GPU
-    const int64_t ldx = (ne00 + 3) & ~int64_t(3);   // the quantizer reads rows as float4
-    const size_t xrow = (size_t)ne00 * sizeof(float);
-    float* dX = static_cast<float*>(rt.scratch(2, (size_t)ldx * sizeof(float) * (size_t)(N * nslices) + 64));
-    for (int64_t i13 = 0; i13 < ne13; ++i13)
-      for (int64_t i12 = 0; i12 < ne12; ++i12) {
-        const unsigned char* x = static_cast<const unsigned char*>(src1->data) + i12 * src1->nb[2] + i13 * src1->nb[3];
-        HIPCHK(hipMemcpy2DAsync(dX + (i13 * ne12 + i12) * N * ldx, (size_t)ldx * sizeof(float), x, src1->nb[1], xrow,
-                                (size_t)N, hipMemcpyHostToDevice, s));
+  const bool pinned_c = G == 1 && use_pinned((size_t)M * N * nslices * sizeof(float));
+
+  for (int g = 0; g < G; ++g) {
+    Dev& d = rt.devs[g];
+    HIPCHK(hipSetDevice(d.id));
+    hipStream_t s = d.stream;
+    int64_t r0 = 0, rows = M;
+    if (G > 1) lamm_hip_shard_rows(M, G, g, 16, &r0, &rows);
+    if (rows == 0) continue;
+    WeightEntry* w = nullptr;
+    void* a_dev;
+    int64_t a_pitch;
+    size_t a_s2, a_s3;
+    if (weight) {
+      w = &rt.weights(d, WeightKey{src0->data, t0, rows * ne02 * ne03, kb, src0->nb[1], src0->nb[2], src0->nb[3]}, a_row,
+                      src0, r0, rows, fp);
+      a_dev = w->dev;
+      a_pitch = w->dev_pitch;
+      a_s2 = (size_t)a_pitch * rows;
+      a_s3 = a_s2 * ne02;
+    } else {
+      const Transient tr = upload_transient(d, src0, a_row);
+      a_dev = tr.dev;
+      a_pitch = tr.pitch;
+      a_s2 = tr.s2;
+      a_s3 = tr.s3;
+    }
+    // activations: INIT-phase wdata (contiguous rows), a contiguous vec_dot-typed src1, or the
+    // F32 rows quantized here on the GPU
+    void* dB = d.scratch(0, b_bytes + 64);
+    if (gpu_quant) {
+      const int64_t ldx = (ne00 + 3) & ~int64_t(3);   // the quantizer reads rows as float4
+      const size_t xrow = (size_t)ne00 * sizeof(float);
+      float* dX = static_cast<float*>(d.scratch(2, (size_t)ldx * sizeof(float) * (size_t)(N * nslices) + 64));
+      for (int64_t i13 = 0; i13 < ne13; ++i13)
+        for (int64_t i12 = 0; i12 < ne12; ++i12) {
+          const unsigned char* x =
+              static_cast<const unsigned char*>(src1->data) + i12 * src1->nb[2] + i13 * src1->nb[3];
+          HIPCHK(hipMemcpy2DAsync(dX + (i13 * ne12 + i12) * N * ldx, (size_t)ldx * sizeof(float), x, src1->nb[1], xrow,
+                                  (size_t)N, hipMemcpyHostToDevice, s));
+        }
+      const int qrc = lamm_hip_quantize(vdt, /*AVX2 flavour*/ 1, dX, ldx, dB, kb, (int)ne00, (int)(N * nslices), s);
+      if (qrc != LAMM_OK) {
+        fprintf(stderr, "lamm_hip: lamm_hip_quantize failed (%d): %s\n", qrc, g_err.c_str());
+        std::abort();
       }
-    const int qrc = lamm_hip_quantize(vdt, /*AVX2 flavour*/ 1, dX, ldx, dB, kb, (int)ne00, (int)(N * nslices), s);
-    if (qrc != LAMM_OK) {
-      fprintf(stderr, "lamm_hip: lamm_hip_quantize failed (%d): %s\n", qrc, g_err.c_str());
+    } else if (use_wdata) {
+      HIPCHK(hipMemcpyAsync(dB, b_host, b_bytes, hipMemcpyHostToDevice, s));
+    } else {
+      HIPCHK(hipMemcpy2DAsync(dB, b_row, src1->data, src1->nb[1], b_row, (size_t)(N * nslices), hipMemcpyHostToDevice,
+                              s));
+    }
+    const size_t c_slice = (size_t)rows * N * sizeof(float);
+    float* dC = static_cast<float*>(d.scratch(1, c_slice * (size_t)nslices + 64));
+
+    lamm_matrix A{a_dev, t0, (int)rows, (int)kb, a_pitch / (int64_t)block_bytes(t0)};
+    lamm_matrix B{dB, vdt, (int)kb, (int)N, (int64_t)kb};
+    lamm_matrix C{dC, kF32, (int)rows, (int)N, rows};
+    lamm_batch bt{ne02, ne03, ne12, ne13, a_s2, a_s3,
+                  b_row * (size_t)N, b_row * (size_t)(N * ne12), c_slice, c_slice * (size_t)ne12};
+    // prefill calls on the fp6 / super-block engines reuse the weights' packed form
+    GemvArgs pa = weight_args(&A, ne02, ne03, bt.nba2, bt.nba3);
+    pa.N = (int)N;
+    pa.ne12 = (int)ne12;
+    pa.ne13 = (int)ne13;
+    pa.r2 = (int)(ne12 / ne02);
+    pa.r3 = (int)(ne13 / ne03);
+    const bool stationary = weight && N > gemv_max_n(t0) && ((gemm_fp6_supported(t0) && gemm_path(pa, true) == 0) ||
+                                      (gemm_kq_supported(t0) && !getenv_flag0("LAMM_KQ_GEMM")));
+    const int rc = stationary ? lamm_hip_matmul_weights(rt.prepared(d, *w, A, ne02, ne03), &B, &C, &bt, s)
+                              : lamm_hip_matmul_batched(&A, &B, &C, &bt, s);
+    if (rc != LAMM_OK) {
+      fprintf(stderr, "lamm_hip: lamm_hip_matmul_batched failed (%d): %s\n", rc, g_err.c_str());
       std::abort();
     }
-  } else if (use_wdata) {
-    const size_t nb = b_row * (size_t)(N * nslices);
-    if (use_pinned(nb)) {
-      unsigned char* hB = rt.pinned(0, nb);
-      memcpy(hB, params->wdata, nb);
-      HIPCHK(hipMemcpyAsync(dB, hB, nb, hipMemcpyHostToDevice, s));
-    } else {
-      HIPCHK(hipMemcpyAsync(dB, params->wdata, nb, hipMemcpyHostToDevice, s));
+    if (pinned_c) {   // one DMA into pinned memory; strided host copies after the sync below
+      HIPCHK(hipMemcpyAsync(rt.pinned(1, c_slice * (size_t)nslices), dC, c_slice * (size_t)nslices,
+                            hipMemcpyDeviceToHost, s));
+    } else {   // this device's rows straight into dst
+      for (int64_t i13 = 0; i13 < ne13; ++i13)
+        for (int64_t i12 = 0; i12 < ne12; ++i12) {
+          unsigned char* c_host =
+              static_cast<unsigned char*>(dst->data) + i12 * dst->nb[2] + i13 * dst->nb[3] + r0 * sizeof(float);
+          HIPCHK(hipMemcpy2DAsync(c_host, dst->nb[1], dC + (i13 * ne12 + i12) * rows * N, (size_t)rows * sizeof(float),
+                                  (size_t)rows * sizeof(float), N, hipMemcpyDeviceToHost, s));
+        }
     }
-  } else {
-    HIPCHK(hipMemcpy2DAsync(dB, b_row, src1->data, src1->nb[1], b_row, (size_t)(N * nslices),
-                            hipMemcpyHostToDevice, s));
   }
-  const size_t c_slice = (size_t)M * N * sizeof(float);
-  float* dC = static_cast<float*>(rt.scratch(1, c_slice * (size_t)nslices + 64));
-
-  lamm_matrix A{a_dev, t0, (int)M, (int)kb, a_pitch / (int64_t)block_bytes(t0)};
-  lamm_matrix B{dB, vdt, (int)kb, (int)N, (int64_t)kb};
-  lamm_matrix C{dC, kF32, (int)M, (int)N, M};
-  lamm_batch bt{ne02, ne03, ne12, ne13, a_s2, a_s3,
-                b_row * (size_t)N, b_row * (size_t)(N * ne12), c_slice, c_slice * (size_t)ne12};
-  // prefill calls on the fp6 engine reuse the weights' packed form (weight-stationary)
-  GemvArgs pa = weight_args(&A, ne02, ne03, bt.nba2, bt.nba3);
-  pa.N = (int)N;
-  pa.ne12 = (int)ne12;
-  pa.ne13 = (int)ne13;
-  pa.r2 = (int)(ne12 / ne02);
-  pa.r3 = (int)(ne13 / ne03);
-  const bool stationary = weight && N > gemv_max_n(t0) && ((gemm_fp6_supported(t0) && gemm_path(pa, true) == 0) ||
-                                    (gemm_kq_supported(t0) && !getenv_flag0("LAMM_KQ_GEMM")));
-  const int rc = stationary ? lamm_hip_matmul_weights(rt.prepared(*w, A, ne02, ne03), &B, &C, &bt, s)
-                            : lamm_hip_matmul_batched(&A, &B, &C, &bt, s);
-  if (rc != LAMM_OK) {
-    fprintf(stderr, "lamm_hip: lamm_hip_matmul_batched failed (%d): %s\n", rc, g_err.c_str());
-    std::abort();
+  for (int g = 0; g < G; ++g) {
+    HIPCHK(hipSetDevice(rt.devs[g].id));
+    HIPCHK(hipStreamSynchronize(rt.devs[g].stream));
   }
-  if (use_pinned(c_slice * (size_t)nslices)) {   // one DMA into pinned memory, then strided host copies
-    unsigned char* hC = rt.pinned(1, c_slice * (size_t)nslices);
-    HIPCHK(hipMemcpyAsync(hC, dC, c_slice * (size_t)nslices, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
+  if (pinned_c) {
+    const unsigned char* hC = rt.pinned(1, (size_t)M * N * nslices * sizeof(float));
+    const size_t c_slice = (size_t)M * N * sizeof(float);
     for (int64_t i13 = 0; i13 < ne13; ++i13)
       for (int64_t i12 = 0; i12 < ne12; ++i12) {
         unsigned char* c_host = static_cast<unsigned char*>(dst->data) + i12 * dst->nb[2] + i13 * dst->nb[3];
         const unsigned char* src = hC + (size_t)(i13 * ne12 + i12) * c_slice;
-        for (int64_t j = 0; j < N; ++j) memcpy(c_host + j * dst->nb[1], src + (size_t)j * M * sizeof(float), M * sizeof(float));
+        for (int64_t j = 0; j < N; ++j)
+          memcpy(c_host + j * dst->nb[1], src + (size_t)j * M * sizeof(float), M * sizeof(float));
       }
-    return;
   }
-  for (int64_t i13 = 0; i13 < ne13; ++i13)
-    for (int64_t i12 = 0; i12 < ne12; ++i12) {
-      unsigned char* c_host = static_cast<unsigned char*>(dst->data) + i12 * dst->nb[2] + i13 * dst->nb[3];
-      HIPCHK(hipMemcpy2DAsync(c_host, dst->nb[1], dC + (i13 * ne12 + i12) * M * N, (size_t)M * sizeof(float),
-                              (size_t)M * sizeof(float), N, hipMemcpyDeviceToHost, s));
-    }
-  HIPCHK(hipStreamSynchronize(s));
 }
 
 extern "C" void lamm_hip_cache_clear(void) {
   Runtime& rt = Runtime::get();
   std::lock_guard<std::mutex> lock(rt.mu);
   rt.clear();
+}
+
+extern "C" void lamm_hip_boundary_reset(void) {
+  Runtime& rt = Runtime::get();
+  std::lock_guard<std::mutex> lock(rt.mu);
+  rt.reset();
 }
 
 extern "C" size_t lamm_hip_cache_bytes(void) {

@@ -133,6 +133,7 @@ lib.lamm_hip_allgather_rows.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c
                                         ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
 lib.lamm_hip_cache_clear.restype = None
 lib.lamm_hip_cache_bytes.restype = ctypes.c_size_t
+lib.lamm_hip_boundary_reset.restype = None
 
 
 def blck_size(t):
@@ -396,3 +397,8 @@ def cache_clear():
 
 def cache_bytes():
     return lib.lamm_hip_cache_bytes()
+
+
+def boundary_reset():
+    """Drop the ggml boundary's devices (caches, streams); the next call re-reads LAMM_HIP_DEVICES."""
+    lib.lamm_hip_boundary_reset()

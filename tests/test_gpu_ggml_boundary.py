@@ -234,3 +234,41 @@ def test_views_bypass_weight_cache(monkeypatch):
     want = ORACLE.mul_mat(ol.F16, M, N, K, cache.buf, ORACLE.quantize(ol.F16, b))
     got = dst.buf.view(np.float32).reshape(N, M)
     np.testing.assert_allclose(got[:, 5], want[:, 5], rtol=1e-5)
+
+
+@pytest.mark.parametrize("devices", ["0,0", "0,0,0"])
+@pytest.mark.parametrize("t,M,N,K", [(ol.Q4_0, 4096, 1, 4096), (ol.Q4_0, 1000, 20, 512), (ol.Q8_0, 77, 3, 256),
+                                     (ol.Q2_K, 300, 9, 512)])
+def test_boundary_rows_split_over_devices(devices, t, M, N, K, monkeypatch):
+    """LAMM_HIP_DEVICES: the weight's rows split over the listed devices, each copying its rows
+    of C straight into dst (host consumes C).  Rehearsed with one device listed
+    several times (separate streams and caches, the same slab bookkeeping as real devices);
+    the result must be bit-identical to the same slabs computed one by one, and match the
+    oracle within the parity tolerance."""
+    monkeypatch.setenv("LAMM_HIP_GPU_QUANT", "0")
+    src0, src1, A_q, b = make_node(t, M, N, K, seed=M + N)
+    want = expected(t, A_q, b, M, N, K, (1, 1), (1, 1))[0, 0]
+    try:
+        monkeypatch.setenv("LAMM_HIP_DEVICES", devices)
+        la.boundary_reset()
+        dst = ggml_emu.mul_mat_node(src0, src1)
+        assert ggml_emu.compute(dst, nth=2)
+        got = dst.buf.view(np.float32).reshape(N, M).copy()
+        assert la.cache_bytes() > 0
+        ggml_emu.compute(dst, nth=2)                       # second call: served from the caches
+        np.testing.assert_array_equal(dst.buf.view(np.float32).reshape(N, M), got)
+    finally:
+        monkeypatch.delenv("LAMM_HIP_DEVICES")
+        la.boundary_reset()
+    assert rel_err(got, want, np.abs(want) + 1.0).max() < 1e-3
+    # every slab equals the same rows computed alone (one device)
+    G = len(devices.split(","))
+    arow = ORACLE.row_bytes(t, K)
+    for g in range(G):
+        r0, rows = la.shard_rows(M, G, g, 16)
+        if rows == 0:
+            continue
+        s0 = ggml_emu.Tensor(t, [K, rows], data=A_q[r0 * arow:(r0 + rows) * arow].copy())
+        d1 = ggml_emu.mul_mat_node(s0, ggml_emu.Tensor(ol.F32, [K, N], data=b))
+        assert ggml_emu.compute(d1, nth=2)
+        np.testing.assert_array_equal(d1.buf.view(np.float32).reshape(N, rows), got[:, r0:r0 + rows])

@@ -3,26 +3,36 @@
 
 metric: "Q4_0xQ8_0 GEMM effective GFLOPS @ K=4096; achieved HBM GB/s (GEMV)"
 
-Workload (BASELINE config 2, the decode GEMV): Q4_0 weights M=4096 x K=4096 against one
-Q8_0 activation row (N=1).  One *step* = one launch of the hot path over one batch of
-synthetic input: R distinct 4096x4096 weight slices (ggml batch dims ne02 = ne12 = R,
-src/loongarch_matmul.cpp:130-142) with one activation row each.  R is chosen so that the
-bytes streamed per launch (R x 9,457,920 B for q4_0) exceed the 256 MiB Infinity Cache:
-every byte comes from HBM and the launch is long enough (~60 us) that the event-timed
-per-launch duration is kernel time, not launch gaps.
+Headline (`value`): BASELINE config 2 as the survey states it -- ONE Q4_0 x Q8_0
+GEMV, M = 4096, N = 1, K = 4096, per step, the steps rotating over enough distinct weight copies
+that every byte comes from HBM (> the 256 MiB Infinity Cache).  With N GPUs the ONE weight's rows
+are split over the ranks (strong scaling, lamm_hip_shard_rows) and every step ends with the
+library's RCCL all-gather of C (lamm_hip_allgather_rows), so each rank holds the whole C.
+  value    = algorithmic bytes of one GEMV (A + B + C = 9,457,920 B) x steps / max-over-ranks time
+  roofline = the rank's GEMV kernel alone: its slab's algorithmic bytes / its per-launch time
+             (HIP events on the stream it runs on), vs 8 TB/s HBM3E
+The K steps are captured once as a hipGraph and replayed (per-launch host submission through
+Python/ctypes costs ~5 us, more than the kernel; bench measures the GPU).
 
-  value      = algorithmic GEMV bytes (A + B + C) of all ranks / max-over-ranks time  [GB/s]
-  roofline   = the GEMV kernel vs 8 TB/s HBM3E (MI355X_MICROARCH.md)
-  gemm       = BASELINE config 3 (M=4096, N=512, K=4096) effective GFLOPS (2MNK / t), vs the
-               dense MFMA-i8 peak (2x bf16 = 5.0 POP/s)
-  cpu_baseline = the reference itself (oracle/_ref/ref_driver_lamm3 = lamm opt-3 AVX2 build
-               of /root/reference, timed like la-benchmark-matmult) on this host's cores
+Beside it (same JSON line):
+  gemv_stacked  : 33 4096x4096 slices in ONE launch (steady-state streaming rate), N = 1
+  gemm          : BASELINE config 3 (M=4096 N=512 K=4096, stationary weights): one slice and
+                  a 4-slice batch; roofline = the WHOLE launch (activation prep + main loop +
+                  split-K reduce); `main_loop_only` separately labelled.  N > 1: the slice's
+                  rows split over the ranks + the RCCL all-gather of C (8 MiB)
+  llama7b_e2e   : BASELINE config 5 through the unchanged caller -- llama.cpp-b2430's own
+                  llama_decode (integration/_build/llama_e2e_hip: the reference's llama.cpp and
+                  ggml with the LA_LLAMA hook linked to liblamm_hip.so), synthetic Llama-7B Q4_0
+                  GGUF, pp512 / tg128; with N GPUs the boundary splits every weight's rows over
+                  all N (LAMM_HIP_DEVICES)
+  llama7b_matmul_step : the same model's weight matmuls through the device API (hipGraph) --
+                  the ceiling without the ggml boundary's host round trips
+  cpu_baseline  : the reference itself (oracle/_ref: la-llama.cpp lamm opt-3 AVX2 build) on this
+                  host's cores, rank 0, N = 1; the same leg checks a sample of the GPU outputs
+                  above against the oracle (`parity_sample`)
 
-Multi-GPU (torchrun, one process per GPU): rows of A shard across ranks (weak scaling:
-each rank owns a 4096-row shard of every slice), then C is all-gathered over RCCL.
-
-Synthetic data: A bytes random with valid fp16 scales; B = the GPU activation quantizer
-applied to N(0,1) floats.  Inputs are resident in HBM before the timed region.
+Synthetic data: A bytes random with valid fp16 scales; B = the GPU activation quantizer applied
+to N(0,1) floats.  Inputs are resident in HBM before the timed region.
 """
 import argparse
 import json
@@ -33,11 +43,12 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "la-llama.cpp_amd"))
-from lamm_amd.shard import RowGather  # noqa: E402  (pure Python; the HIP library loads in main())
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 I8_DENSE_PEAK_TOPS = 5000.0    # dense MFMA-i8 = 2x the 2.5 PF dense bf16 rate (MI355X_MICROARCH.md)
 MALL_BYTES = 256 << 20
+ALIGN = 16                     # row-slab granularity of the GEMV split (one wave-group row tile)
+GEMM_ALIGN = 256               # fp6 GEMM row tile
 
 FP16_FIELDS = {  # byte offsets of fp16 scale fields inside one block (lamm_formats.h)
     "q4_0": [0], "q4_1": [0, 2], "q5_0": [0], "q5_1": [0, 2], "q8_0": [0], "q2_k": [80, 82],
@@ -53,14 +64,11 @@ def make_weights(torch, la, fmt, slices, M, K, gen):
     rb = la.row_bytes(t, K)
     assert rb % 16 == 0
     if fmt == "f32":
-        w = torch.randn(slices * M * K, device="cuda", generator=gen).view(torch.uint8)
-        return w, rb
+        return torch.randn(slices * M * K, device="cuda", generator=gen).view(torch.uint8), rb
     if fmt == "f16":
-        w = torch.randn(slices * M * K, device="cuda", generator=gen).half().view(torch.uint8)
-        return w, rb
+        return torch.randn(slices * M * K, device="cuda", generator=gen).half().view(torch.uint8), rb
     w = torch.randint(0, 256, (slices * M * rb,), dtype=torch.uint8, device="cuda", generator=gen)
-    bpb = la.type_size(t)
-    blocks = w.view(-1, bpb)
+    blocks = w.view(-1, la.type_size(t))
     for off in FP16_FIELDS[fmt]:
         d = (torch.rand(blocks.shape[0], device="cuda", generator=gen) * 0.02 + 1e-3).half()
         blocks[:, off:off + 2].view(torch.float16)[:, 0] = d
@@ -78,130 +86,269 @@ def make_activations(torch, la, fmt, rows, K, gen):
     return y
 
 
-def run_case(torch, la, dist, fmt, M, N, K, slices, steps, warmup, world, warm_first=False, stationary=True):
-    """One batched launch per step; returns per-step seconds (max over ranks).
-    warm_first: one launch without LAMM_GEMM_SKIP_PREP first, so a prep-skipping
-    measurement reads a workspace prepared from these very inputs.
-    stationary: the weights are a lamm_hip_weights handle made before the timed region (as
-    the ggml boundary's weight cache holds them), so the fp6 GEMM's packed weight form is
-    resident; False re-packs A inside every call (the plain device API)."""
-    t = la.BY_NAME[fmt]
-    vt = la.vec_dot_type(t)
-    gen = torch.Generator(device="cuda")
-    gen.manual_seed(1234 + (dist.get_rank() if world > 1 else 0))
-    A, arow = make_weights(torch, la, fmt, slices, M, K, gen)
-    B = make_activations(torch, la, fmt, slices * N, K, gen)
-    C = torch.zeros(slices * N * M, dtype=torch.float32, device="cuda")
-    # rows of A shard across ranks (weak scaling: each rank owns an M-row slab of every
-    # slice); the slabs of C meet in RCCL all-gathers + interleaving copies (step() below)
-    gather = None
-    kb = K // la.blck_size(t)
-    brow = la.row_bytes(vt, K)
-    Am = la.Matrix(A.data_ptr(), t, M, kb, kb)
-    Bm = la.Matrix(B.data_ptr(), vt, kb, N, kb)
-    Cm = la.Matrix(C.data_ptr(), la.F32, M, N, M)
-    bt = la.Batch(slices, 1, slices, 1, M * arow, slices * M * arow, N * brow, slices * N * brow,
-                  4 * M * N, 4 * M * N * slices)
-    stream = torch.cuda.current_stream()
-    W = la.Weights(t, A, M, K, ne02=slices, ne03=1, nba2=M * arow, nba3=slices * M * arow) if stationary else None
-
-    def call():
-        if W is not None:
-            W.matmul_torch(B, C, N, batch=bt, stream=stream.cuda_stream)
-        else:
-            la.matmul_batched(Am, Bm, Cm, bt, stream.cuda_stream)
-
-    # N > 1 ranks: the launch is split into up to 4 groups of slices; group g's all-gather runs
-    # on a second stream while group g+1 computes (the collective overlaps the next compute)
-    chunks = []
-    if world > 1:
-        nch = min(4, slices)
-        for c in range(nch):
-            s0, s1 = c * slices // nch, (c + 1) * slices // nch
-            ns = s1 - s0
-            a_c = A[s0 * M * arow:s1 * M * arow]
-            b_c = B[s0 * N * brow:]
-            c_c = C[s0 * N * M:s1 * N * M]
-            bt_c = la.Batch(ns, 1, ns, 1, M * arow, ns * M * arow, N * brow, ns * N * brow, 4 * M * N, 4 * M * N * ns)
-            w_c = la.Weights(t, a_c, M, K, ne02=ns, ne03=1, nba2=M * arow, nba3=ns * M * arow) if stationary else None
-            m_c = (la.Matrix(a_c.data_ptr(), t, M, kb, kb), la.Matrix(b_c.data_ptr(), vt, kb, N, kb),
-                   la.Matrix(c_c.data_ptr(), la.F32, M, N, M))
-            chunks.append((w_c, m_c, bt_c, b_c, c_c, RowGather(dist, ns * N, M, world, torch.float32, "cuda")))
-    comm = torch.cuda.Stream() if world > 1 else None
-
-    def step():
-        if world == 1:
-            call()
-            return
-        for w_c, m_c, bt_c, b_c, c_c, g_c in chunks:   # row shards -> every rank holds all of C
-            if w_c is not None:
-                w_c.matmul_torch(b_c, c_c, N, batch=bt_c, stream=stream.cuda_stream)
-            else:
-                la.matmul_batched(*m_c, bt_c, stream.cuda_stream)
-            ev = torch.cuda.Event()
-            ev.record(stream)
-            comm.wait_event(ev)
-            with torch.cuda.stream(comm):
-                g_c(c_c)                                  # RCCL all-gather over xGMI + interleave
-        stream.wait_stream(comm)
-
-    if warm_first:
-        skip = os.environ.pop("LAMM_GEMM_SKIP_PREP", None)
-        call()
-        if skip is not None:
-            os.environ["LAMM_GEMM_SKIP_PREP"] = skip
-    for _ in range(warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    e0.record(stream)
-    for _ in range(steps):
-        step()
-    e1.record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
-    ev = e0.elapsed_time(e1) / 1e3
-    per = torch.tensor([ev / steps, wall / steps], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(per, op=dist.ReduceOp.MAX)
-    # sanity: finite outputs
-    assert torch.isfinite(C).all().item(), "non-finite GEMV/GEMM output"
-    # kernel-only per-launch time (no collective) for the roofline; a few launches are
-    # queued first so the timed ones run back to back (no host-submission gap)
-    e2, e3 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    for _ in range(3):
-        call()
-    e2.record(stream)
-    for _ in range(steps):
-        call()
-    e3.record(stream)
-    torch.cuda.synchronize()
-    kern = e2.elapsed_time(e3) / 1e3 / steps
-    if W is not None:
-        W.close()
-    for ch in chunks:
-        if ch[0] is not None:
-            ch[0].close()
-    del A, B, C, gather, W, chunks
-    torch.cuda.empty_cache()
-    return per[0].item(), per[1].item(), kern
-
-
 def gemv_bytes(la, fmt, M, K, N=1):
     t = la.BY_NAME[fmt]
     return M * la.row_bytes(t, K) + N * la.row_bytes(la.vec_dot_type(t), K) + 4 * M * N
 
 
-def cpu_baseline(fmt, M, N, K, budget_s, gemv_unit_bytes):
-    """The real reference (lamm opt=3, AVX2; Q8_0 uses opt=0 stock ggml because lamm's
-    AVX2 Q8_0 is numerically wrong) timed like la-benchmark-matmult."""
+class Ctx:
+    """Ranks, devices and the communicators: gloo for control (barriers, the RCCL id, the
+    max-over-ranks timing, on host tensors), the library's RCCL communicator for data."""
+
+    def __init__(self, torch, la):
+        import torch.distributed as dist
+        self.torch, self.la, self.dist = torch, la, dist
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        # LAMM_BENCH_REHEARSE=1: the N>1 code path on a one-GPU box (every rank on cuda:0, the
+        # all-gather through gloo on host copies -- RCCL refuses ranks sharing a device)
+        self.rehearse = self.world > 1 and os.environ.get("LAMM_BENCH_REHEARSE") == "1"
+        self.device = 0 if self.rehearse else local
+        torch.cuda.set_device(self.device)
+        self.comm = None
+        if self.world > 1:
+            dist.init_process_group("gloo")
+            if not self.rehearse:
+                uid = [la.comm_unique_id() if self.rank == 0 else None]
+                dist.broadcast_object_list(uid, src=0)
+                self.comm = la.Comm.rank(self.world, self.rank, uid[0], self.device)
+        elif os.environ.get("LAMM_BENCH_COMM1") == "1":
+            # the RCCL path on one GPU: a one-rank communicator, every step's all-gather through
+            # RCCL (in the captured hipGraph) -- exercises what the multi-GPU run uses
+            self.comm = la.Comm.rank(1, 0, la.comm_unique_id(), self.device)
+
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
+
+    def max(self, *vals):
+        v = self.torch.tensor(vals, dtype=self.torch.float64)
+        if self.world > 1:
+            self.dist.all_reduce(v, op=self.dist.ReduceOp.MAX)
+        return v.tolist()
+
+    def allgather_rows(self, C, M, N, align, stream):
+        """C (device tensor, [N][M]) holds this rank's rows at their place; gather the rest."""
+        if self.world == 1 and self.comm is None:
+            return
+        if self.comm is not None:
+            r0, rows = self.la.shard_rows(M, self.world, self.rank, align)
+            self.comm.allgather_rows([C.data_ptr() + 4 * r0], [M], [C.data_ptr()], M, M, N, align, [stream])
+        else:   # rehearsal: gloo on host copies
+            from lamm_amd.shard import gather_rows
+            r0, rows = self.la.shard_rows(M, self.world, self.rank, align)
+            slab = C.view(N, M)[:, r0:r0 + rows].contiguous().cpu()
+            C.copy_(gather_rows(self.dist, slab, M, N, self.world, self.rank, align).reshape(-1).to(C.device))
+
+    def close(self):
+        if self.comm is not None:
+            self.comm.close()
+        if self.world > 1:
+            self.dist.destroy_process_group()
+
+
+def time_steps(ctx, step, steps, warmup, graph=True):
+    """Warm-up, then EXACTLY `steps` steps bracketed by barrier + synchronize on both sides;
+    returns (wall seconds per step, event-timed seconds per step -- both max over ranks --,
+    graph used).  graph: the steps are captured once as a hipGraph and replayed in the timed
+    region.  Everything runs on one side stream, the warm-up included, so the library's
+    per-stream workspaces exist before the capture (nothing allocates while capturing)."""
+    torch = ctx.torch
+    st = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    with torch.cuda.stream(st):
+        for i in range(warmup):
+            step(i)
+    torch.cuda.synchronize()
+    g = None
+    if graph:
+        try:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=st):
+                for s in range(steps):
+                    step(warmup + s)
+            g.replay()                      # one untimed replay (first-replay setup)
+            torch.cuda.synchronize()
+        except Exception as e:  # noqa: BLE001 -- eager fallback, reported
+            log("graph capture failed, eager steps:", str(e)[:200])
+            g = None
+            torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ctx.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    with torch.cuda.stream(st):
+        e0.record(st)
+        if g is not None:
+            g.replay()
+        else:
+            for s in range(steps):
+                step(warmup + s)
+        e1.record(st)
+    torch.cuda.synchronize()
+    ctx.barrier()
+    wall = time.perf_counter() - t0
+    ev = e0.elapsed_time(e1) / 1e3
+    wmax, emax = ctx.max(wall / steps, ev / steps)
+    return wmax, emax, g is not None
+
+
+def config2_gemv(ctx, fmt, M, K, steps, warmup):
+    """BASELINE config 2, strong-scaled: rank r owns rows [r0, r0 + rows) of ONE M x K weight;
+    a step = its slab's GEMV on the next of R rotated weight copies + the RCCL all-gather of C."""
+    torch, la = ctx.torch, ctx.la
+    t = la.BY_NAME[fmt]
+    vt = la.vec_dot_type(t)
+    kb = K // la.blck_size(t)
+    arow = la.row_bytes(t, K)
+    r0, rows = la.shard_rows(M, ctx.world, ctx.rank, ALIGN)
+    slab_bytes = rows * arow
+    R = max(8, min(4096, -(-int(1.15 * MALL_BYTES) // max(slab_bytes, 1))))
+    # copy c = rows [r0, r0+rows) of the full weight made from seed c (every rank can rebuild
+    # any full copy, so rank 0 can check the gathered C against one GPU computing all rows)
+    A = torch.empty(R * slab_bytes + 64, dtype=torch.uint8, device="cuda")
+    for c in range(R):
+        gen = torch.Generator(device="cuda")
+        gen.manual_seed(1000 + c)
+        full, _ = make_weights(torch, la, fmt, 1, M, K, gen)
+        A[c * slab_bytes:(c + 1) * slab_bytes] = full[r0 * arow:(r0 + rows) * arow]
+        del full
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(7)
+    B = make_activations(torch, la, fmt, 1, K, gen)
+    C = torch.zeros(M, dtype=torch.float32, device="cuda")
+    mats = [la.Matrix(A.data_ptr() + c * slab_bytes, t, rows, kb, kb) for c in range(R)]
+    Bm = la.Matrix(B.data_ptr(), vt, kb, 1, kb)
+    Cm = la.Matrix(C.data_ptr() + 4 * r0, la.F32, rows, 1, rows)
+
+    def gemv(i):
+        la.matmul(mats[i % R], Bm, Cm, torch.cuda.current_stream().cuda_stream)
+
+    def step(i):
+        gemv(i)
+        ctx.allgather_rows(C, M, 1, ALIGN, torch.cuda.current_stream().cuda_stream)
+
+    per_step, ev_step, graphed = time_steps(ctx, step, steps, warmup, graph=not ctx.rehearse)
+    last = warmup + steps - 1
+    torch.cuda.synchronize()
+    gathered = C.clone()      # C after the last timed step (copy last % R)
+    check = None
+    if ctx.world > 1:
+        # rank 0: the gathered C of the last step vs one GPU computing all rows of that copy
+        if ctx.rank == 0:
+            g2 = torch.Generator(device="cuda")
+            g2.manual_seed(1000 + last % R)
+            full, _ = make_weights(torch, la, fmt, 1, M, K, g2)
+            Cf = torch.zeros(M, dtype=torch.float32, device="cuda")
+            la.matmul(la.Matrix(full.data_ptr(), t, M, kb, kb), Bm, la.Matrix(Cf.data_ptr(), la.F32, M, 1, M),
+                      torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            check = "bit-exact" if torch.equal(gathered, Cf) else \
+                f"MISMATCH max abs {float((gathered - Cf).abs().max()):.3e}"
+    sample = {"fmt": fmt, "M": M, "N": 1, "K": K, "rows": [0, 1, M // 2, M - 1]} if ctx.world == 1 else None
+    if sample is not None:   # the last step's copy: weight rows + C for the cpu_baseline leg's parity check
+        a = A[(last % R) * slab_bytes:(last % R + 1) * slab_bytes].view(M, arow)
+        sample.update(A=a[sample["rows"]].cpu().numpy(), B=B[:la.row_bytes(vt, K)].cpu().numpy(),
+                      C=gathered[sample["rows"]].cpu().numpy())
+    # the rank's kernel alone (no collective): roofline numerator
+    _, kern, _ = time_steps(ctx, gemv, max(steps, 50), 3)
+    res = dict(per_step=per_step, ev_step=ev_step, kern=kern, graphed=graphed, R=R, rows=rows,
+               slab_bytes=slab_bytes + la.row_bytes(vt, K) + 4 * rows, gather_check=check, sample=sample)
+    del A, B, C
+    torch.cuda.empty_cache()
+    return res
+
+
+def stacked_gemv(ctx, fmt, M, K, steps):
+    """33 distinct M x K slices in one launch (> MALL): the steady-state streaming rate."""
+    torch, la = ctx.torch, ctx.la
+    t = la.BY_NAME[fmt]
+    vt = la.vec_dot_type(t)
+    kb = K // la.blck_size(t)
+    u = gemv_bytes(la, fmt, M, K)
+    sl = max(8, -(-int(1.15 * MALL_BYTES) // u))
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(11)
+    A, arow = make_weights(torch, la, fmt, sl, M, K, gen)
+    B = make_activations(torch, la, fmt, sl, K, gen)
+    C = torch.zeros(sl * M, dtype=torch.float32, device="cuda")
+    brow = la.row_bytes(vt, K)
+    Am, Bm, Cm = la.Matrix(A.data_ptr(), t, M, kb, kb), la.Matrix(B.data_ptr(), vt, kb, 1, kb), \
+        la.Matrix(C.data_ptr(), la.F32, M, 1, M)
+    bt = la.Batch(sl, 1, sl, 1, M * arow, sl * M * arow, brow, sl * brow, 4 * M, 4 * M * sl)
+    _, kern, _ = time_steps(ctx, lambda i: la.matmul_batched(Am, Bm, Cm, bt, torch.cuda.current_stream().cuda_stream),
+                            steps, 3)
+    del A, B, C
+    torch.cuda.empty_cache()
+    return {"workload": f"{fmt.upper()}xQ8 GEMV M={M} N=1 K={K}, {sl} distinct slices in ONE launch "
+                        f"(ggml ne02=ne12={sl}, {sl * u / 1e6:.1f} MB > MALL): steady-state streaming",
+            "kernel": "lamm::gemv_stream_dma_kernel (csrc/lamm_gemv.hip)", "per_launch_us": round(kern * 1e6, 3),
+            "achieved_GBs": round(sl * u / kern / 1e9, 1), "frac": round(sl * u / kern / 1e9 / HBM_PEAK_GBS, 4)}
+
+
+def config3_gemm(ctx, fmt, M, N, K, slices, steps):
+    """BASELINE config 3 with stationary weights: `slices` independent M x K weight slices, each
+    against its own N activation rows, per launch.  N GPUs: each slice's rows split over the
+    ranks + the RCCL all-gather of C (only for slices == 1).  Returns whole-launch seconds."""
+    torch, la = ctx.torch, ctx.la
+    t = la.BY_NAME[fmt]
+    vt = la.vec_dot_type(t)
+    kb = K // la.blck_size(t)
+    arow, brow = la.row_bytes(t, K), la.row_bytes(vt, K)
+    world = ctx.world if slices == 1 else 1
+    rank = ctx.rank if slices == 1 else 0
+    r0, rows = la.shard_rows(M, world, rank, GEMM_ALIGN)
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(21)
+    full, _ = make_weights(torch, la, fmt, slices, M, K, gen)
+    if world > 1:
+        A = full[r0 * arow:(r0 + rows) * arow].clone()
+        del full
+    else:
+        A = full
+    B = make_activations(torch, la, fmt, slices * N, K, gen)
+    C = torch.zeros(slices * N * M, dtype=torch.float32, device="cuda")
+    slab = torch.zeros(max(rows, 1) * N, dtype=torch.float32, device="cuda") if world > 1 else C
+    ld = rows if world > 1 else M
+    bt = la.Batch(slices, 1, slices, 1, rows * arow, slices * rows * arow, N * brow, slices * N * brow, 4 * ld * N,
+                  4 * ld * N * slices)
+    W = la.Weights(t, A, rows, K, ne02=slices, ne03=1, nba2=rows * arow, nba3=slices * rows * arow)
+
+    def gemm(i):
+        W.matmul_torch(B, slab, N, ldc=ld, batch=bt, stream=torch.cuda.current_stream().cuda_stream)
+
+    def step(i):
+        gemm(i)
+        if world > 1 and ctx.comm is not None:   # (a rehearsal times the slab alone)
+            ctx.comm.allgather_rows([slab.data_ptr()], [rows], [C.data_ptr()], M, M, N, GEMM_ALIGN,
+                                    [torch.cuda.current_stream().cuda_stream])
+
+    per_step, _, _ = time_steps(ctx, step, steps, 2, graph=not ctx.rehearse)
+    _, kern, _ = time_steps(ctx, gemm, steps, 2)
+    # main loop alone: LAMM_GEMM_SKIP_PREP re-runs the main kernel on the prepared workspace
+    os.environ["LAMM_GEMM_SKIP_PREP"] = "1"
+    try:
+        _, main_only, _ = time_steps(ctx, gemm, steps, 1, graph=False)
+    finally:
+        del os.environ["LAMM_GEMM_SKIP_PREP"]
+    gemm(0)   # a correct result again (the skip-prep launches leave C undefined)
+    torch.cuda.synchronize()
+    sample = None
+    if world == 1 and slices == 1:
+        rws = [0, 255, 2048, M - 1]
+        sample = {"fmt": fmt, "M": M, "N": N, "K": K, "rows": rws,
+                  "A": A.view(M, arow)[rws].cpu().numpy(), "B": B[:N * brow].cpu().numpy(),
+                  "C": C.view(N, M)[:, rws].cpu().numpy()}
+    W.close()
+    del A, B, C, slab, W
+    torch.cuda.empty_cache()
+    return per_step, kern, main_only, rows, sample
+
+
+def cpu_baseline(fmt, M, N, K, budget_s, unit_bytes):
+    """The real reference (lamm opt=3, AVX2; Q8_0 uses opt=0 stock ggml because lamm's AVX2 Q8_0
+    is numerically wrong) timed like la-benchmark-matmult."""
     threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
     threads = max(1, min(threads, 16))
     variant = "lamm0" if fmt == "q8_0" else "lamm3"
@@ -212,7 +359,7 @@ def cpu_baseline(fmt, M, N, K, budget_s, gemv_unit_bytes):
         if out.returncode == 0:
             r = json.loads(out.stdout.strip().splitlines()[-1])
             us = r["median_us"]
-            return {"value": round(gemv_unit_bytes / (us * 1e-6) / 1e9, 3), "unit": "GB/s", "cores": threads,
+            return {"value": round(unit_bytes / (us * 1e-6) / 1e9, 3), "unit": "GB/s", "cores": threads,
                     "kind": "reference", "median_us": us, "gflops": r["gflops"],
                     "sample": f"{r['iters']} x {fmt} mul_mat M={M} N={N} K={K} via ggml_graph_compute "
                               f"(ref_driver_{variant}: la-llama.cpp lamm opt {3 if variant == 'lamm3' else 0} "
@@ -233,26 +380,68 @@ def cpu_baseline(fmt, M, N, K, budget_s, gemv_unit_bytes):
         o.mul_mat(t, M, N, K, A, B)
         ts.append(time.perf_counter() - t0)
     med = sorted(ts)[len(ts) // 2]
-    return {"value": round(gemv_unit_bytes / med / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
+    return {"value": round(unit_bytes / med / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
             "median_us": med * 1e6, "sample": f"{len(ts)} x scalar oracle mul_mat M={M} N={N} K={K}"}
 
 
+def parity_sample(samples):
+    """cpu_baseline leg: the GPU's outputs for sampled rows (last timed step) vs the oracle,
+    |c - ref| / max(|ref|, sum |a b|)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import numpy as np
+    import oracle_lib as ol
+    o = ol.Oracle()
+    out = {}
+    for name, s in samples.items():
+        if not s:
+            continue
+        t = ol.BY_NAME[s["fmt"]]
+        vt = o.vec_dot_type(t)
+        n, K, rows = s["N"], s["K"], s["rows"]
+        A = np.ascontiguousarray(s["A"]).reshape(-1)
+        ref = o.mul_mat(t, len(rows), n, K, A, s["B"])
+        Ad = o.dequantize(t, A, len(rows), K).astype(np.float64)
+        Bd = o.dequantize(vt, s["B"], n, K).astype(np.float64)
+        denom = np.maximum(np.abs(Bd) @ np.abs(Ad).T, np.abs(ref)) + 1e-30
+        got = np.asarray(s["C"], np.float64).reshape(n, len(rows))
+        err = float((np.abs(got - ref) / denom).max())
+        out[name] = {"rows": rows, "columns": n, "max_rel_err": err, "ok": err < 1e-3}
+    return out
+
+
+def llama_e2e(devices, n_prompt=512, n_gen=128, threads=16, exe=None, extra_env=None, timeout=600):
+    """BASELINE config 5 through llama.cpp-b2430's own llama_decode (see module doc)."""
+    exe = exe or os.path.join(ROOT, "integration", "_build", "llama_e2e_hip")
+    model = os.path.join(os.environ.get("TMPDIR", "/tmp"), "lamm_synth_llama7b_q4_0.gguf")
+    if not os.path.exists(exe):
+        return {"error": f"{exe} missing (build with __graft_entry__.build())"}
+    env = dict(os.environ, **(extra_env or {}))
+    if devices:
+        env["LAMM_HIP_DEVICES"] = ",".join(map(str, devices))
+    try:
+        r = subprocess.run([exe, "-m", model, "-t", str(threads), "-p", str(n_prompt), "-n", str(n_gen)],
+                           capture_output=True, text=True, timeout=timeout, env=env)
+        line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+        if r.returncode != 0 or not line:
+            return {"error": r.stderr[-400:]}
+        d = json.loads(line[-1])
+        d.pop("tokens", None)
+        return d
+    except Exception as e:  # noqa: BLE001 -- reported, never fatal for the main bench line
+        return {"error": str(e)[:300]}
+
+
 def llama_step(fmt):
-    """BASELINE config 5's model on one GPU: the weight matmuls of a Llama-7B step (32 layers x
-    7 projections + the Q6_K output.weight, llama.cpp-b2430's mul_mat sequence) replayed as a
-    hipGraph by la-llama.cpp_amd/llama-matmul-bench, a child process.  Attention, norms and
-    activations are not part of it: tok/s is the bound the weight matmuls set."""
+    """The model's weight matmuls through the device API, hipGraph-replayed (llama-matmul-bench)."""
     exe = os.path.join(ROOT, "la-llama.cpp_amd", "llama-matmul-bench")
-    res = {"note": "weight matmuls only (no attention/norms), synthetic weights, hipGraph replay; "
-                   "decode = 1 token/step (F32 activations fused into the GEMV), prefill = 512 tokens/step "
-                   "with weight-stationary handles; reference: Llama-2-7B Q4_0 on 3A6000 t=4, text-gen "
-                   "4.69 tok/s, prompt 8.27 tok/s (README.md:684,710), whole model"}
+    res = {"note": "weight matmuls only (no attention/norms), synthetic weights, hipGraph replay: the ceiling "
+                   "without the ggml boundary's host round trips"}
     for name, argv in (("decode_n1", ["-n", "1", "-i", "50"]), ("prefill_n512", ["-n", "512", "-i", "5", "-s"])):
         try:
             r = subprocess.run([exe, "-d", fmt] + argv, capture_output=True, text=True, timeout=180)
             line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
             res[name] = json.loads(line[-1]) if r.returncode == 0 and line else {"error": r.stderr[-300:]}
-        except Exception as e:  # noqa: BLE001 -- reported, never fatal for the main bench line
+        except Exception as e:  # noqa: BLE001
             res[name] = {"error": str(e)[:300]}
     return res
 
@@ -278,119 +467,137 @@ def main():
     ap.add_argument("--gemm-N", type=int, default=512)
     ap.add_argument("--no-gemm", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--no-llama", action="store_true", help="skip the Llama-7B weight-matmul step (config 5 model)")
+    ap.add_argument("--no-llama", action="store_true", help="skip config 5 (llama e2e + weight-matmul step)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
-    ap.add_argument("--sweep", action="store_true", help="also time every weight format (config 4)")
+    ap.add_argument("--sweep", action="store_true", help="also every weight format (config 4)")
     args = ap.parse_args()
 
     import torch
-    import torch.distributed as dist
     import lamm_amd as la
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1 and os.environ.get("LAMM_BENCH_REHEARSE") == "1":
-        # rehearsal of the N>1 code path on a one-GPU box: every rank on cuda:0, gloo for the
-        # collectives (numbers meaningless; the driver's multi-GPU runs use RCCL, below)
-        torch.cuda.set_device(0)
-        dist.init_process_group("gloo")
-    elif world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     if la.device_count() == 0:
         raise SystemExit("bench.py: no gfx950 device visible")
+    ctx = Ctx(torch, la)
+    world, rank = ctx.world, ctx.rank
+    M, K, fmt = args.M, args.K, args.fmt
+    unit = gemv_bytes(la, fmt, M, K)
 
-    M, K = args.M, args.K
-    unit = gemv_bytes(la, args.fmt, M, K)
-    slices = max(8, -(-int(1.15 * MALL_BYTES) // unit))     # > MALL per launch
-    per_step, wall_step, kern = run_case(torch, la, dist, args.fmt, M, 1, K, slices, args.steps, args.warmup, world)
-    launch_bytes = slices * unit
-    value = world * launch_bytes / per_step / 1e9
-    achieved = launch_bytes / kern / 1e9
-    traffic = read_traffic(f"{args.fmt}_gemv")
+    g = config2_gemv(ctx, fmt, M, K, args.steps, args.warmup)
+    value = unit / g["per_step"] / 1e9
+    achieved = g["slab_bytes"] / g["kern"] / 1e9
+    traffic = read_traffic(f"{fmt}_gemv_single")
     out = {
         "metric": "Q4_0xQ8_0 GEMM effective GFLOPS @ K=4096; achieved HBM GB/s (GEMV)",
         "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": round(per_step * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+        "ms_per_step": round(g["per_step"] * 1e3, 5), "gpu_ms_per_step": round(g["ev_step"] * 1e3, 5),
+        "higher_is_better": True, "scaling": "strong",
         "vs_baseline": None, "dtype": "i8",
         "data": "synthetic (random block bytes with valid fp16 scales; B = GPU q8 quantizer of N(0,1))",
-        "config": {"workload": f"{args.fmt.upper()}xQ8 GEMV M={M} N=1 K={K} (BASELINE config 2), "
-                               f"{slices} weight slices per launch (ggml ne02=ne12={slices}, "
-                               f"{launch_bytes / 1e6:.1f} MB/launch > 256 MiB MALL)",
-                   "fmt": args.fmt, "M_per_rank": M, "N": 1, "K": K, "slices": slices,
-                   "parallelism": f"rows of A sharded over {world} GPU(s)" + (" + RCCL all-gather of C" if world > 1 else "")},
+        "config": {"workload": f"{fmt.upper()}xQ8 GEMV M={M} N=1 K={K} (BASELINE config 2): ONE call per step, "
+                               f"rotating over {g['R']} weight copies per rank (> 256 MiB MALL)"
+                               + (f"; rows split over {world} GPUs ({g['rows']} on rank 0) + RCCL all-gather of C "
+                                  f"every step" if world > 1 else ""),
+                   "fmt": fmt, "M": M, "N": 1, "K": K, "rows_per_rank": g["rows"],
+                   "parallelism": f"rows of A split over {world} GPU(s)" +
+                                  ((" + all-gather through gloo (one-GPU rehearsal)" if ctx.rehearse else
+                                    " + lamm_hip_allgather_rows (RCCL)") if world > 1 else ""),
+                   "timing": "hipGraph of the K steps, replayed" if g["graphed"] else "eager launches"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic.get("bytes_per_launch") if traffic and traffic.get(
-                         "algorithmic_bytes_per_launch") == launch_bytes else None,
-                     "traffic_source": "profiles/traffic_%s_gemv.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE)" % args.fmt,
-                     "kernel": ("lamm::gemv_stream_dma_kernel" if args.fmt in ("q4_0", "q4_k") else
-                                "lamm::gemv_stream_kernel") + " (csrc/lamm_gemv.hip)",
-                     "per_launch_us": round(kern * 1e6, 3),
-                     "algorithmic_bytes_per_launch": launch_bytes},
+                         "algorithmic_bytes_per_launch") == g["slab_bytes"] else None,
+                     "traffic_source": f"profiles/traffic_{fmt}_gemv_single.json (rocprofv3 --pmc FETCH_SIZE x2 + "
+                                       "WRITE_SIZE, per launch)",
+                     "kernel": "lamm::gemv_rpw_kernel (csrc/lamm_gemv_rpw.hip)",
+                     "per_launch_us": round(g["kern"] * 1e6, 3),
+                     "algorithmic_bytes_per_launch": g["slab_bytes"]},
     }
+    if g["gather_check"] is not None:
+        out["config"]["gather_check"] = g["gather_check"]
+    samples = {"gemv_config2": g["sample"]}
+    extras = {}
+    try:
+        if world == 1:
+            extras["gemv_stacked"] = stacked_gemv(ctx, fmt, M, K, max(5, args.steps // 2))
+    except Exception as e:  # noqa: BLE001
+        extras["gemv_stacked"] = {"error": str(e)[:300]}
     if not args.no_gemm:
-        # BASELINE config 3.  One launch = ggml batch of `gslices` independent 4096x4096 weight
-        # slices (ne02 = ne12), each against its own 512 activation rows, with the weights
-        # stationary (a lamm_hip_weights handle, as the ggml boundary's weight cache holds
-        # them: the fp6 engine's packed weight form is made once, outside the timed region).
-        # The launch is the activation prep + the GEMM main loop; `value` is the whole launch,
-        # `value_repack_each_call` the plain device API that re-packs the weights inside every
-        # call, roofline.achieved the dominant main-loop kernel alone (re-run on the prepared
-        # workspace with LAMM_GEMM_SKIP_PREP=1 and event-timed the same way).
         gN = args.gemm_N
-        out["gemm"] = {}
-        for gslices in (4, 1):
-            g_step, _, g_kern = run_case(torch, la, dist, args.fmt, M, gN, K, gslices, max(3, args.steps // 4), 2,
-                                         world)
-            os.environ["LAMM_GEMM_SKIP_PREP"] = "1"
-            _, _, g_main = run_case(torch, la, dist, args.fmt, M, gN, K, gslices, max(3, args.steps // 4), 2, world,
-                                    warm_first=True)
-            del os.environ["LAMM_GEMM_SKIP_PREP"]
-            r_step, _, _ = run_case(torch, la, dist, args.fmt, M, gN, K, gslices, max(3, args.steps // 4), 2, world,
-                                    stationary=False)
-            ops = 2.0 * M * gN * K * gslices
-            engine = la.gemm_engine(args.fmt, M, gN, K, gslices, stationary=True)
-            out["gemm"][f"slices{gslices}"] = {
-                "workload": f"{args.fmt.upper()}xQ8 GEMM M={M} N={gN} K={K} (BASELINE config 3), "
-                            f"{gslices} slice(s) per launch", "engine": engine,
-                "value": round(world * ops / g_step / 1e9, 1), "unit": "GFLOPS",
-                "value_repack_each_call": round(world * ops / r_step / 1e9, 1),
-                "per_launch_us": round(g_kern * 1e6, 2),
-                "roofline": {"bound": "mfma", "kernel": "lamm::gemm_fp6_kernel (csrc/lamm_gemm_fp6.hip)" if engine == "fp6"
-                             else "lamm::gemm3_kernel (csrc/lamm_gemm.hip)",
-                             "achieved": round(ops / g_main / 1e12, 2), "peak": I8_DENSE_PEAK_TOPS, "unit": "TFLOP/s",
-                             "frac": round(ops / g_main / 1e12 / I8_DENSE_PEAK_TOPS, 4),
-                             "per_launch_us": round(g_main * 1e6, 2)}}
-    if args.sweep:
-        # BASELINE config 4: every weight format, GEMV (HBM GB/s, > MALL per launch) and the
-        # single-slice M=4096 N=512 K=4096 GEMM (effective GFLOPS, stationary weights)
+        gm = {}
+        for gslices in ((4, 1) if world == 1 else (1,)):
+            try:
+                step, kern, main_only, rows, smp = config3_gemm(ctx, fmt, M, gN, K, gslices, max(3, args.steps // 4))
+                ops = 2.0 * M * gN * K * gslices
+                rops = 2.0 * rows * gN * K * gslices
+                engine = la.gemm_engine(fmt, rows, gN, K, gslices, stationary=True)
+                gm[f"slices{gslices}"] = {
+                    "workload": f"{fmt.upper()}xQ8 GEMM M={M} N={gN} K={K} (BASELINE config 3), {gslices} slice(s) "
+                                f"per launch, stationary weights" +
+                                (f"; rows split over {world} GPUs + RCCL all-gather of C" if world > 1 and gslices == 1
+                                 else ""),
+                    "engine": engine, "value": round(ops / step / 1e9, 1), "unit": "GFLOPS",
+                    "ms_per_step": round(step * 1e3, 4),
+                    "roofline": {"bound": "mfma", "scope": "whole launch (activation prep + main loop + split-K "
+                                                           "reduce) of this rank's slab",
+                                 "kernel": "lamm::gemm_fp6_kernel (csrc/lamm_gemm_fp6.hip)" if engine == "fp6"
+                                 else "lamm::gemm3_kernel (csrc/lamm_gemm.hip)",
+                                 "achieved": round(rops / kern / 1e12, 2), "peak": I8_DENSE_PEAK_TOPS,
+                                 "unit": "TFLOP/s", "frac": round(rops / kern / 1e12 / I8_DENSE_PEAK_TOPS, 4),
+                                 "per_launch_us": round(kern * 1e6, 2)},
+                    "main_loop_only": {"per_launch_us": round(main_only * 1e6, 2),
+                                       "TFLOPs": round(rops / main_only / 1e12, 2),
+                                       "note": "LAMM_GEMM_SKIP_PREP=1: the main kernel alone on the prepared "
+                                               "workspace (profiling; not the roofline)"}}
+                if smp:
+                    samples["gemm_config3"] = smp
+            except Exception as e:  # noqa: BLE001
+                gm[f"slices{gslices}"] = {"error": str(e)[:300]}
+        extras["gemm"] = gm
+    if args.sweep and world == 1:
         sw = {}
         for f in ["f32", "f16", "q4_0", "q4_1", "q5_0", "q5_1", "q8_0", "q2_k", "q4_k", "q5_k", "q6_k"]:
-            u = gemv_bytes(la, f, M, K)
-            sl = max(4, -(-int(1.15 * MALL_BYTES) // u))
-            _, _, kk = run_case(torch, la, dist, f, M, 1, K, sl, max(5, args.steps // 2), 2, world)
-            sw[f] = {"gemv_GBs": round(sl * u / kk / 1e9, 1), "gemv_us_per_slice": round(kk / sl * 1e6, 3)}
-            if not args.no_gemm:
-                gN = args.gemm_N
-                _, _, gk = run_case(torch, la, dist, f, M, gN, K, 1, max(3, args.steps // 4), 2, world)
-                engine = la.gemm_engine(f, M, gN, K, 1, stationary=True)
-                sw[f].update({"gemm_GFLOPS": round(2.0 * M * gN * K / gk / 1e9, 1), "gemm_us": round(gk * 1e6, 2),
-                              "gemm_engine": engine})
-        out["sweep"] = sw
-    if rank == 0 and world == 1 and not args.no_llama:
-        out["llama7b_matmul_step"] = llama_step(args.fmt)
+            try:
+                st = stacked_gemv(ctx, f, M, K, max(5, args.steps // 2))
+                sw[f] = {"gemv_stacked_GBs": st["achieved_GBs"]}
+                if not args.no_gemm:
+                    step, kern, _, _, _ = config3_gemm(ctx, f, M, args.gemm_N, K, 1, max(3, args.steps // 4))
+                    sw[f].update({"gemm_GFLOPS": round(2.0 * M * args.gemm_N * K / kern / 1e9, 1),
+                                  "gemm_us": round(kern * 1e6, 2),
+                                  "gemm_engine": la.gemm_engine(f, M, args.gemm_N, K, 1, stationary=True)})
+            except Exception as e:  # noqa: BLE001
+                sw[f] = {"error": str(e)[:200]}
+        extras["sweep"] = sw
+    if not args.no_llama:
+        ctx.barrier()
+        if rank == 0:
+            devs = list(range(world)) if world > 1 and not ctx.rehearse else None
+            e2e = {"note": "BASELINE config 5: llama.cpp-b2430's own llama_decode (integration/_build/llama_e2e_hip: "
+                           "the reference's llama.cpp + ggml, LA_LLAMA hook -> liblamm_hip.so), synthetic "
+                           "Llama-7B-shaped Q4_0 GGUF (Q6_K output, F16 KV cache), pp512 then tg128 greedy; "
+                           "weights device-resident after a warm-up pass; reference published (3A6000, 4 threads, "
+                           "README.md:684,710): prompt 8.27 tok/s, text-gen 4.69 tok/s",
+                   "devices": devs or [ctx.device],
+                   "t16": llama_e2e(devs, threads=16)}
+            if world == 1:
+                extras["llama7b_matmul_step"] = llama_step(fmt)
+            extras["llama7b_e2e"] = e2e
+        ctx.barrier()
+    out.update(extras)
     if rank == 0 and world == 1 and not args.no_cpu:
-        out["cpu_baseline"] = cpu_baseline(args.fmt, M, 1, K, args.cpu_budget, unit)
-        if not args.no_gemm and "gemm" in out:   # the same reference path at BASELINE config 3
-            cb = cpu_baseline(args.fmt, M, args.gemm_N, K, args.cpu_budget, 0)
+        out["cpu_baseline"] = cpu_baseline(fmt, M, 1, K, args.cpu_budget, unit)
+        out["cpu_baseline"]["parity_sample"] = parity_sample(samples)
+        if "gemm" in out:   # the same reference path at BASELINE config 3
+            cb = cpu_baseline(fmt, M, args.gemm_N, K, args.cpu_budget, 0)
             us = cb["median_us"]
             out["gemm"]["cpu_baseline"] = {
                 "value": round(2.0 * M * args.gemm_N * K / (us * 1e-6) / 1e9, 2), "unit": "GFLOPS",
                 "cores": cb["cores"], "kind": cb["kind"], "median_us": round(us, 1), "sample": cb["sample"]}
-    if world > 1:
-        dist.destroy_process_group()
+        if "llama7b_e2e" in out:   # the reference's own llama.cpp + lamm opt-3 on the host cores
+            cpu = llama_e2e(None, n_prompt=64, n_gen=16, threads=out["cpu_baseline"]["cores"],
+                            exe=os.path.join(ROOT, "oracle", "_ref", "llama_e2e_lamm3"))
+            cpu["sample"] = "pp64 + tg16 (bounded sample) of the same model and driver on la-llama.cpp lamm opt 3 AVX2"
+            out["llama7b_e2e"]["cpu_baseline"] = cpu
+    ctx.close()
     if rank == 0:
         print(json.dumps(out), flush=True)
 

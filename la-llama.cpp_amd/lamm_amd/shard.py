@@ -1,27 +1,24 @@
-"""Row sharding of the lamm mul_mat across ranks.
+"""Row sharding of the lamm mul_mat across ranks -- host-side helpers.
 
 Output rows are independent (``C[i, :]`` needs row i of A and all of B,
 src/lamm_impl.hpp:50-53 -- the same contiguous row split ggml hands its threads,
-src/lamm_impl.hpp:38-43), so one process per GPU owns a contiguous slab of weight rows,
-computes ``C[:, r0:r1]`` and the slabs meet in one all-gather of C (RCCL over xGMI with the
-``nccl`` backend, gloo in the CPU tests).  Unlike the reference's ``job_size = M / nth``
-split, the remainder rows are not dropped (SURVEY §8a defect 1).
+src/lamm_impl.hpp:38-43), so each rank owns a contiguous slab of weight rows, computes
+``C[:, r0:r1]`` and the slabs meet in one all-gather of C.  The split itself is the library's
+(lamm_hip_shard_rows: every row exactly once -- the reference's ``job_size = M / nth`` drops
+the remainder rows, SURVEY §8a defect 1); on GPUs the all-gather is the library's RCCL one
+(lamm_amd.Comm.allgather_rows).  ``gather_rows`` is the same exchange through any
+torch.distributed backend on host tensors: the CPU (gloo) tests and bench.py's one-GPU
+rehearsal of the multi-rank path use it.
 """
+import lamm_amd as la
 
 
 def row_shard(M, world, rank, align=1):
-    """Contiguous [r0, r1) of the M weight rows owned by ``rank``.
-
-    Shards are whole multiples of ``align`` rows (the GEMM tile height) except the last
-    one; the ``ceil(M / align)`` tiles are spread as evenly as possible, earlier ranks
-    taking the extra tile."""
+    """Contiguous [r0, r1) of the M weight rows owned by ``rank`` (lamm_hip_shard_rows)."""
     if world < 1 or not 0 <= rank < world:
         raise ValueError(f"rank {rank} outside world {world}")
-    tiles = -(-M // align)
-    base, extra = divmod(tiles, world)
-    t0 = rank * base + min(rank, extra)
-    t1 = t0 + base + (1 if rank < extra else 0)
-    return min(M, t0 * align), min(M, t1 * align)
+    r0, rows = la.shard_rows(M, world, rank, align)
+    return r0, r0 + rows
 
 
 def shard_rows_max(M, world, align=1):
@@ -34,7 +31,7 @@ def gather_rows(dist, c_shard, M, N, world, rank, align=1, out=None):
 
     ``c_shard``: this rank's ``[N][r1 - r0]`` block (torch tensor, contiguous).  Every
     rank sends a ``[N][mmax]`` block (zero-padded), one ``all_gather_into_tensor`` moves
-    them, and a single strided copy interleaves the row slabs into ``[N][M]``."""
+    them, and one strided copy per rank interleaves the row slabs into ``[N][M]``."""
     import torch
 
     mmax = shard_rows_max(M, world, align)
@@ -52,29 +49,3 @@ def gather_rows(dist, c_shard, M, N, world, rank, align=1, out=None):
         a0, a1 = row_shard(M, world, r, align)
         out[:, a0:a1] = recv[r, :, :a1 - a0]
     return out
-
-
-class RowGather:
-    """Preallocated all-gather of equal row slabs (every rank owns ``m`` rows; the bench's
-    weak-scaling case): ``C_shard [R][m]`` (R = slices x N activation rows) -> ``C [R][world*m]``
-    with one ``all_gather_into_tensor`` and one strided copy, no per-step allocation."""
-
-    def __init__(self, dist, R, m, world, dtype, device):
-        import torch
-
-        self.dist, self.R, self.m, self.world = dist, R, m, world
-        self.recv = torch.empty((world, R, m), dtype=dtype, device=device)
-        self.out = torch.empty((R, world * m), dtype=dtype, device=device)
-
-    def __call__(self, c_shard):
-        if self.world > 1 and self.recv.is_cuda and self.dist.get_backend() == "gloo":
-            # gloo is a host backend: stage device slabs through host memory (bench rehearsal)
-            recv = self.recv.cpu()
-            self.dist.all_gather_into_tensor(recv.view(-1), c_shard.reshape(-1).cpu())
-            self.recv.copy_(recv)
-        elif self.world > 1:
-            self.dist.all_gather_into_tensor(self.recv.view(-1), c_shard.reshape(-1))
-        else:
-            self.recv[0].copy_(c_shard.view(self.R, self.m))
-        self.out.view(self.R, self.world, self.m).copy_(self.recv.permute(1, 0, 2))
-        return self.out

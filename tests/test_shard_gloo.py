@@ -1,6 +1,9 @@
 """Multi-rank row sharding + all-gather of C, on CPU with gloo, world_size 2
-and 3: each rank computes its row slab with the oracle and the gathered C must equal the
-single-process result bit for bit (the same per-row arithmetic on both sides)."""
+and 3: the host side of the multi-rank path (the library's row split, lamm_hip_shard_rows,
+and the slab interleave) with each rank's slab computed by the oracle -- no GPU here; the
+gathered C must equal the single-process result bit for bit (the same per-row arithmetic on
+both sides).  The HIP slabs and the library's RCCL all-gather path are covered on the GPU by
+tests/test_gpu_shard.py and bench.py's multi-GPU self-check."""
 import os
 import socket
 import sys
@@ -14,7 +17,7 @@ import torch.multiprocessing as mp  # noqa: E402
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(os.path.dirname(HERE), "la-llama.cpp_amd"))
-from lamm_amd.shard import RowGather, gather_rows, row_shard  # noqa: E402
+from lamm_amd.shard import gather_rows, row_shard  # noqa: E402
 
 
 def test_row_shard_covers_all_rows():
@@ -54,13 +57,8 @@ def _worker(rank, world, port, M, N, K, align, q):
         c = o.mul_mat(ol.Q4_0, r1 - r0, N, K, np.ascontiguousarray(A[r0:r1]), B) if r1 > r0 \
             else np.zeros((N, 0), np.float32)
         full = gather_rows(dist, torch.from_numpy(np.ascontiguousarray(c, dtype=np.float32)), M, N, world, rank, align)
-        # equal-slab variant used by bench.py (weak scaling): pad every slab to M rows
-        cpad = np.zeros((N, M), np.float32)
-        cpad[:, :r1 - r0] = np.asarray(c, np.float32).reshape(N, r1 - r0)
-        rg = RowGather(dist, N, M, world, torch.float32, "cpu")
-        eq = rg(torch.from_numpy(cpad)).numpy()
         if rank == 0:
-            q.put((full.numpy().copy(), eq.copy()))
+            q.put(full.numpy().copy())
     finally:
         dist.destroy_process_group()
 
@@ -76,7 +74,7 @@ def test_gather_rows_gloo(world, M, align):
     procs = [ctx.Process(target=_worker, args=(r, world, port, M, N, K, align, q)) for r in range(world)]
     for p in procs:
         p.start()
-    got, eq = q.get(timeout=120)
+    got = q.get(timeout=120)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -86,6 +84,3 @@ def test_gather_rows_gloo(world, M, align):
     b = rng.standard_normal((N, K), dtype=np.float32)
     want = o.mul_mat(ol.Q4_0, M, N, K, o.quantize(ol.Q4_0, a), o.quantize(ol.Q8_0, b, ol.QUANT_AVX))
     np.testing.assert_array_equal(got, want.reshape(N, M))
-    for r in range(world):   # RowGather: slab r lands at columns [r*M, (r+1)*M)
-        r0, r1 = row_shard(M, world, r, align)
-        np.testing.assert_array_equal(eq[:, r * M:r * M + (r1 - r0)], want.reshape(N, M)[:, r0:r1])

@@ -418,7 +418,9 @@ struct CallStats {
   const char* name;
   uint64_t calls = 0;
   double us = 0;
+  double phase_us[4] = {0, 0, 0, 0};   // fingerprint + lookup, enqueue (copies + launches), sync, C to dst
 };
+const char* kPhase[4] = {"weights lookup", "enqueue", "device sync", "C to dst"};
 CallStats g_stats[4] = {{"weights N<=8"}, {"weights N>8"}, {"views N<=8"}, {"views N>8"}};
 bool stats_on() {
   static const bool on = [] {
@@ -430,13 +432,23 @@ bool stats_on() {
 void print_stats() {
   for (const auto& c : g_stats)
     if (c.calls)
-      fprintf(stderr, "lamm_hip stats: %-13s %8llu calls %12.1f us total %8.2f us/call\n", c.name,
+    {
+      fprintf(stderr, "lamm_hip stats: %-13s %8llu calls %12.1f us total %8.2f us/call  (", c.name,
               (unsigned long long)c.calls, c.us, c.us / (double)c.calls);
+      for (int k = 0; k < 4; ++k) fprintf(stderr, "%s%s %.2f", k ? ", " : "", kPhase[k], c.phase_us[k] / c.calls);
+      fprintf(stderr, ")\n");
+    }
 }
 struct StatScope {
   CallStats* c;
-  std::chrono::steady_clock::time_point t0;
-  explicit StatScope(CallStats* cs) : c(cs), t0(std::chrono::steady_clock::now()) {}
+  std::chrono::steady_clock::time_point t0, tp;
+  explicit StatScope(CallStats* cs) : c(cs), t0(std::chrono::steady_clock::now()), tp(t0) {}
+  void phase(int k) {   // time since the previous mark -> phase k
+    if (!c) return;
+    const auto now = std::chrono::steady_clock::now();
+    c->phase_us[k] += std::chrono::duration<double, std::micro>(now - tp).count();
+    tp = now;
+  }
   ~StatScope() {
     if (c) {
       c->calls++;
@@ -630,16 +642,27 @@ class Runtime {
     return e.prepared;
   }
 
-  // pinned host staging (grow-only): decode-sized B uploads / C downloads as one DMA each
-  // instead of HIP's pageable-copy path; LAMM_HIP_PINNED=0 turns it off (A/B)
+  // pinned host staging (grow-only), mapped into the device's address space: 0 = activations
+  // the kernels read in place (non-coherent: the GPU may cache them in L2; every launch's
+  // acquire drops stale lines), 1 = C the kernels write in place; pinned_dev = the device
+  // address of the same bytes.  LAMM_HIP_PINNED=0 turns staging off (A/B).
   unsigned char* pinned(int which, size_t bytes) {
     if (hcap_[which] < bytes) {
-      if (hbuf_[which]) HIPCHK(hipHostFree(hbuf_[which]));
-      HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&hbuf_[which]), bytes + 256, hipHostMallocDefault));
+      if (hbuf_[which]) {
+        for (Dev& d : devs) {
+          (void)hipSetDevice(d.id);
+          (void)hipStreamSynchronize(d.stream);
+        }
+        HIPCHK(hipHostFree(hbuf_[which]));
+      }
+      const unsigned flags = hipHostMallocMapped | hipHostMallocPortable | (which == 0 ? hipHostMallocNonCoherent : 0u);
+      HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&hbuf_[which]), bytes + 256, flags));
+      HIPCHK(hipHostGetDevicePointer(&hdev_[which], hbuf_[which], 0));
       hcap_[which] = bytes;
     }
     return hbuf_[which];
   }
+  void* pinned_dev(int which) const { return hdev_[which]; }
 
   void clear() {
     for (Dev& d : devs)
@@ -666,6 +689,7 @@ class Runtime {
  private:
   size_t budget_ = 0;
   unsigned char* hbuf_[2] = {nullptr, nullptr};
+  void* hdev_[2] = {nullptr, nullptr};
   size_t hcap_[2] = {0, 0};
 };
 
@@ -718,23 +742,34 @@ bool extra_types_enabled() {
   return !(e && e[0] == '0');
 }
 
-// quantize src1 on the GPU instead of in ggml's INIT phase
-// (LC/ggml.c:10865-10887: serial on thread 0).  The hook then claims the INIT phase too (and
-// does nothing in it), uploads the F32 rows and runs lamm_hip_quantize -- the AVX2 flavour
-// of the x86 reference build, bit-exact, so C is unchanged.  LAMM_HIP_GPU_QUANT=0: ggml's
-// CPU INIT as in the reference, =1: always on the GPU; unset: on the GPU from 8 activation
-// rows up (e2e through the unchanged ggml, profiles/r01/e2e_gpu_quant.txt: Q4_0 4096x512x4096
-// 528 -> 376 us, N=8 44 -> 42 us, but N=1 26 -> 31 us: the extra H2D + launch outweigh
-// quantizing 4096 floats on the host).
-bool gpu_quantizes(const ggml::tensor* src0, const ggml::tensor* src1) {
-  const char* e = getenv("LAMM_HIP_GPU_QUANT");
-  const int64_t rows = src1->ne[1] * src1->ne[2] * src1->ne[3];
-  if (e && e[0] == '0') return false;
-  if (!(e && e[0] == '1') && rows < 8) return false;
+// How an F32 src1 reaches the kernels (ggml's INIT phase quantizes it on thread 0, serially:
+// LC/ggml.c:10865-10887).  Whenever the GPU takes it over, the hook claims the INIT phase too
+// (and does nothing in it) so ggml never quantizes; the INIT and COMPUTE answers come from the
+// same function.
+//   kCpuInit  : ggml's CPU INIT, as in the reference; COMPUTE uploads wdata
+//   kFused    : decode-sized (N <= 8) weight matmuls on q8_0 / q8_1 activations: the GEMV
+//               quantizes the F32 rows while staging them (AVX2 from_float flavour, bit-exact,
+//               lamm_gemv*.hip) -- no quantizer launch, no CPU INIT
+//   kGpuQuant : from 8 activation rows up: F32 rows up, lamm_hip_quantize (AVX2 flavour), then
+//               the GEMM engines (profiles/r01/e2e_gpu_quant.txt: Q4_0 4096x512x4096 528 -> 376 us)
+// LAMM_HIP_GPU_QUANT=0: always ggml's CPU INIT; =1: kGpuQuant for every row count;
+// LAMM_HIP_FUSED=0 turns kFused off (A/B).
+enum ActMode { kCpuInit, kFused, kGpuQuant };
+ActMode act_mode(const ggml::tensor* src0, const ggml::tensor* src1) {
   const int vdt = vec_dot_type(src0->type);
-  return src1->type == kF32 && vdt != kF32 &&
-         (vdt == kQ8_0 || vdt == kQ8_1 || vdt == kQ8_K || vdt == kF16) && src1->nb[0] == sizeof(float) &&
-         (src1->nb[1] & 3) == 0 && (src1->nb[2] & 3) == 0 && (src1->nb[3] & 3) == 0;
+  if (src1->type != kF32 || vdt == kF32) return kCpuInit;
+  const bool f32_rows = src1->nb[0] == sizeof(float) && (src1->nb[1] & 3) == 0 && (src1->nb[2] & 3) == 0 &&
+                        (src1->nb[3] & 3) == 0;
+  if (!f32_rows) return kCpuInit;
+  const char* e = getenv("LAMM_HIP_GPU_QUANT");
+  if (e && e[0] == '0') return kCpuInit;
+  const char* f = getenv("LAMM_HIP_FUSED");
+  if (!(f && f[0] == '0') && !(e && e[0] == '1') && (vdt == kQ8_0 || vdt == kQ8_1) && src1->ne[1] <= 8 &&
+      is_weight(src0))
+    return kFused;
+  const int64_t rows = src1->ne[1] * src1->ne[2] * src1->ne[3];
+  if (!(e && e[0] == '1') && rows < 8) return kCpuInit;
+  return (vdt == kQ8_0 || vdt == kQ8_1 || vdt == kQ8_K || vdt == kF16) ? kGpuQuant : kCpuInit;
 }
 
 }  // namespace
@@ -751,7 +786,7 @@ extern "C" bool lamm_can_mul_mat(const struct ggml_compute_params* vparams, cons
   // :15-17: INIT belongs to ggml (it quantizes src1) unless the GPU quantizes it; the INIT
   // and COMPUTE answers must agree, so INIT re-runs every COMPUTE check below
   if (params->type == ggml::TASK_INIT) {
-    if (!gpu_quantizes(src0, src1)) return false;
+    if (act_mode(src0, src1) == kCpuInit) return false;
   } else if (params->type != ggml::TASK_COMPUTE) {
     return false;
   }
@@ -774,6 +809,31 @@ extern "C" bool lamm_can_mul_mat(const struct ggml_compute_params* vparams, cons
   return probe().count > 0;                                  // no GPU: ggml's CPU loop
 }
 
+namespace {
+
+// Decode-sized calls read their activations from, and write C to, pinned host memory mapped into
+// the device (tools/lat_probe.hip: every HIP copy op costs the host ~5 us to enqueue and the
+// round trip ~2.5 us, against a 10 us floor for one launch + synchronise): one launch + one
+// synchronise per call, host memcpys either side.  LAMM_HIP_ZERO_COPY=0 restores device copies.
+constexpr size_t kZeroCopyMax = (size_t)256 << 10;
+// LAMM_HIP_ZERO_COPY: "both" (default) / "in" / "out" / "0": which direction is read / written
+// in place.  llama.cpp decode through the boundary (tools/ab_zero_copy.sh,
+// profiles/r02/ab_zero_copy.txt, p=32 tg, -t 8): device copies 66 tok/s (34.5 us per matmul
+// call: the D2H into ggml's pageable dst blocks), in only 72, out only 74, both 89 (24.4 us).
+bool zero_copy(size_t bytes, bool in) {
+  static const int mode = [] {
+    const char* e = getenv("LAMM_HIP_ZERO_COPY");
+    const char* p = getenv("LAMM_HIP_PINNED");
+    if ((p && p[0] == '0') || (e && e[0] == '0')) return 0;
+    if (e && !strcmp(e, "in")) return 1;
+    if (e && !strcmp(e, "out")) return 2;
+    return 3;
+  }();
+  return (mode & (in ? 1 : 2)) && bytes <= kZeroCopyMax;
+}
+
+}  // namespace
+
 extern "C" void lamm_mul_mat(const struct ggml_compute_params* vparams, struct ggml_tensor* vdst) {
   const auto* params = reinterpret_cast<const ggml::compute_params*>(vparams);
   auto* dst = reinterpret_cast<ggml::tensor*>(vdst);
@@ -790,7 +850,7 @@ extern "C" void lamm_mul_mat(const struct ggml_compute_params* vparams, struct g
   const size_t a_row = (size_t)kb * block_bytes(t0);
   const size_t b_row = (size_t)kb * block_bytes(vdt);           // ggml_row_size(vdt, ne10)
   const bool use_wdata = src1->type != vdt;
-  const bool gpu_quant = use_wdata && gpu_quantizes(src0, src1);
+  const ActMode act = use_wdata ? act_mode(src0, src1) : kCpuInit;
   const int64_t M = ne01, N = ne11, nslices = ne12 * ne13;
 
   Runtime& rt = Runtime::get();
@@ -802,17 +862,40 @@ extern "C" void lamm_mul_mat(const struct ggml_compute_params* vparams, struct g
   // (KV-cache views, intermediates): uploaded afresh, on the first device
   const int G = weight ? (int)rt.devs.size() : 1;
   const uint64_t fp = weight ? weight_fingerprint(src0, a_row) : 0;
-  const size_t b_bytes = b_row * (size_t)(N * nslices);
-  const unsigned char* b_host = nullptr;   // the activation bytes every device uploads
-  if (use_wdata && !gpu_quant) {
-    b_host = static_cast<const unsigned char*>(params->wdata);
-    if (use_pinned(b_bytes)) {
-      unsigned char* hB = rt.pinned(0, b_bytes);
-      memcpy(hB, params->wdata, b_bytes);
-      b_host = hB;
+  // activation bytes as the kernels read them: F32 rows (kFused, kGpuQuant; packed [slice][N][K])
+  // or vec_dot_type rows (wdata / a vec_dot-typed src1)
+  const int64_t ldx = (ne00 + 3) & ~int64_t(3);                 // the quantizer reads rows as float4
+  const size_t x_row = act == kCpuInit ? b_row : (size_t)ldx * sizeof(float);
+  const size_t x_bytes = x_row * (size_t)(N * nslices);
+  const size_t c_bytes = (size_t)M * N * nslices * sizeof(float);
+  const bool zc_in = G == 1 && zero_copy(x_bytes, true) && act != kGpuQuant;
+  const bool zc_out = G == 1 && zero_copy(c_bytes, false);
+  const unsigned char* x_host = nullptr;   // the bytes every device uploads (or reads in place)
+  auto gather_f32 = [&](unsigned char* out) {   // F32 src1 rows (any strides) -> [slice][N][ldx]
+    for (int64_t i13 = 0; i13 < ne13; ++i13)
+      for (int64_t i12 = 0; i12 < ne12; ++i12)
+        for (int64_t j = 0; j < N; ++j)
+          memcpy(out + ((i13 * ne12 + i12) * N + j) * x_row,
+                 static_cast<const unsigned char*>(src1->data) + i12 * src1->nb[2] + i13 * src1->nb[3] + j * src1->nb[1],
+                 (size_t)ne00 * sizeof(float));
+  };
+  if (zc_in) {
+    unsigned char* h = rt.pinned(0, x_bytes);
+    if (act == kFused) gather_f32(h);
+    else if (use_wdata) memcpy(h, params->wdata, x_bytes);
+    else
+      for (int64_t r = 0; r < N * nslices; ++r)
+        memcpy(h + r * b_row, static_cast<const unsigned char*>(src1->data) + r * src1->nb[1], b_row);
+    x_host = h;
+  } else if (act == kCpuInit && use_wdata) {
+    x_host = static_cast<const unsigned char*>(params->wdata);
+    if (use_pinned(x_bytes)) {
+      unsigned char* h = rt.pinned(0, x_bytes);
+      memcpy(h, params->wdata, x_bytes);
+      x_host = h;
     }
   }
-  const bool pinned_c = G == 1 && use_pinned((size_t)M * N * nslices * sizeof(float));
+  stat.phase(0);
 
   for (int g = 0; g < G; ++g) {
     Dev& d = rt.devs[g];
@@ -839,39 +922,48 @@ extern "C" void lamm_mul_mat(const struct ggml_compute_params* vparams, struct g
       a_s2 = tr.s2;
       a_s3 = tr.s3;
     }
-    // activations: INIT-phase wdata (contiguous rows), a contiguous vec_dot-typed src1, or the
-    // F32 rows quantized here on the GPU
-    void* dB = d.scratch(0, b_bytes + 64);
-    if (gpu_quant) {
-      const int64_t ldx = (ne00 + 3) & ~int64_t(3);   // the quantizer reads rows as float4
-      const size_t xrow = (size_t)ne00 * sizeof(float);
-      float* dX = static_cast<float*>(d.scratch(2, (size_t)ldx * sizeof(float) * (size_t)(N * nslices) + 64));
+    // activations on (or mapped into) the device
+    void* dB;
+    if (zc_in) {
+      dB = rt.pinned_dev(0);
+    } else if (act == kFused || act == kGpuQuant) {
+      float* dX = static_cast<float*>(d.scratch(2, x_bytes + 64));
       for (int64_t i13 = 0; i13 < ne13; ++i13)
         for (int64_t i12 = 0; i12 < ne12; ++i12) {
           const unsigned char* x =
               static_cast<const unsigned char*>(src1->data) + i12 * src1->nb[2] + i13 * src1->nb[3];
-          HIPCHK(hipMemcpy2DAsync(dX + (i13 * ne12 + i12) * N * ldx, (size_t)ldx * sizeof(float), x, src1->nb[1], xrow,
-                                  (size_t)N, hipMemcpyHostToDevice, s));
+          HIPCHK(hipMemcpy2DAsync(dX + (i13 * ne12 + i12) * N * ldx, (size_t)ldx * sizeof(float), x, src1->nb[1],
+                                  (size_t)ne00 * sizeof(float), (size_t)N, hipMemcpyHostToDevice, s));
         }
-      const int qrc = lamm_hip_quantize(vdt, /*AVX2 flavour*/ 1, dX, ldx, dB, kb, (int)ne00, (int)(N * nslices), s);
-      if (qrc != LAMM_OK) {
-        fprintf(stderr, "lamm_hip: lamm_hip_quantize failed (%d): %s\n", qrc, g_err.c_str());
-        std::abort();
+      dB = dX;
+      if (act == kGpuQuant) {
+        void* dq = d.scratch(0, b_row * (size_t)(N * nslices) + 64);
+        const int qrc = lamm_hip_quantize(vdt, /*AVX2 flavour*/ 1, dX, ldx, dq, kb, (int)ne00, (int)(N * nslices), s);
+        if (qrc != LAMM_OK) {
+          fprintf(stderr, "lamm_hip: lamm_hip_quantize failed (%d): %s\n", qrc, g_err.c_str());
+          std::abort();
+        }
+        dB = dq;
       }
     } else if (use_wdata) {
-      HIPCHK(hipMemcpyAsync(dB, b_host, b_bytes, hipMemcpyHostToDevice, s));
+      dB = d.scratch(0, x_bytes + 64);
+      HIPCHK(hipMemcpyAsync(dB, x_host, x_bytes, hipMemcpyHostToDevice, s));
     } else {
+      dB = d.scratch(0, x_bytes + 64);
       HIPCHK(hipMemcpy2DAsync(dB, b_row, src1->data, src1->nb[1], b_row, (size_t)(N * nslices), hipMemcpyHostToDevice,
                               s));
     }
+    const bool b_f32 = act == kFused;
+    const size_t b_pitch = b_f32 ? x_row : b_row;
     const size_t c_slice = (size_t)rows * N * sizeof(float);
-    float* dC = static_cast<float*>(d.scratch(1, c_slice * (size_t)nslices + 64));
+    float* dC = zc_out ? static_cast<float*>((rt.pinned(1, c_bytes), rt.pinned_dev(1)))
+                       : static_cast<float*>(d.scratch(1, c_slice * (size_t)nslices + 64));
 
     lamm_matrix A{a_dev, t0, (int)rows, (int)kb, a_pitch / (int64_t)block_bytes(t0)};
-    lamm_matrix B{dB, vdt, (int)kb, (int)N, (int64_t)kb};
+    lamm_matrix B = b_f32 ? lamm_matrix{dB, kF32, (int)ne00, (int)N, ldx} : lamm_matrix{dB, vdt, (int)kb, (int)N, (int64_t)kb};
     lamm_matrix C{dC, kF32, (int)rows, (int)N, rows};
     lamm_batch bt{ne02, ne03, ne12, ne13, a_s2, a_s3,
-                  b_row * (size_t)N, b_row * (size_t)(N * ne12), c_slice, c_slice * (size_t)ne12};
+                  b_pitch * (size_t)N, b_pitch * (size_t)(N * ne12), c_slice, c_slice * (size_t)ne12};
     // prefill calls on the fp6 / super-block engines reuse the weights' packed form
     GemvArgs pa = weight_args(&A, ne02, ne03, bt.nba2, bt.nba3);
     pa.N = (int)N;
@@ -879,18 +971,16 @@ extern "C" void lamm_mul_mat(const struct ggml_compute_params* vparams, struct g
     pa.ne13 = (int)ne13;
     pa.r2 = (int)(ne12 / ne02);
     pa.r3 = (int)(ne13 / ne03);
-    const bool stationary = weight && N > gemv_max_n(t0) && ((gemm_fp6_supported(t0) && gemm_path(pa, true) == 0) ||
-                                      (gemm_kq_supported(t0) && !getenv_flag0("LAMM_KQ_GEMM")));
+    const bool stationary = weight && !b_f32 && N > gemv_max_n(t0) &&
+                            ((gemm_fp6_supported(t0) && gemm_path(pa, true) == 0) ||
+                             (gemm_kq_supported(t0) && !getenv_flag0("LAMM_KQ_GEMM")));
     const int rc = stationary ? lamm_hip_matmul_weights(rt.prepared(d, *w, A, ne02, ne03), &B, &C, &bt, s)
                               : lamm_hip_matmul_batched(&A, &B, &C, &bt, s);
     if (rc != LAMM_OK) {
       fprintf(stderr, "lamm_hip: lamm_hip_matmul_batched failed (%d): %s\n", rc, g_err.c_str());
       std::abort();
     }
-    if (pinned_c) {   // one DMA into pinned memory; strided host copies after the sync below
-      HIPCHK(hipMemcpyAsync(rt.pinned(1, c_slice * (size_t)nslices), dC, c_slice * (size_t)nslices,
-                            hipMemcpyDeviceToHost, s));
-    } else {   // this device's rows straight into dst
+    if (!zc_out) {   // this device's rows straight into dst
       for (int64_t i13 = 0; i13 < ne13; ++i13)
         for (int64_t i12 = 0; i12 < ne12; ++i12) {
           unsigned char* c_host =
@@ -900,12 +990,14 @@ extern "C" void lamm_mul_mat(const struct ggml_compute_params* vparams, struct g
         }
     }
   }
+  stat.phase(1);
   for (int g = 0; g < G; ++g) {
     HIPCHK(hipSetDevice(rt.devs[g].id));
     HIPCHK(hipStreamSynchronize(rt.devs[g].stream));
   }
-  if (pinned_c) {
-    const unsigned char* hC = rt.pinned(1, (size_t)M * N * nslices * sizeof(float));
+  stat.phase(2);
+  if (zc_out) {
+    const unsigned char* hC = rt.pinned(1, c_bytes);
     const size_t c_slice = (size_t)M * N * sizeof(float);
     for (int64_t i13 = 0; i13 < ne13; ++i13)
       for (int64_t i12 = 0; i12 < ne12; ++i12) {
@@ -915,6 +1007,7 @@ extern "C" void lamm_mul_mat(const struct ggml_compute_params* vparams, struct g
           memcpy(c_host + j * dst->nb[1], src + (size_t)j * M * sizeof(float), M * sizeof(float));
       }
   }
+  stat.phase(3);
 }
 
 extern "C" void lamm_hip_cache_clear(void) {

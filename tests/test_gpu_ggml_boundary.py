@@ -111,13 +111,18 @@ def test_non_compute_phases_and_unsupported(monkeypatch):
     p.ith, p.nth = 0, 1
     p.type = la.TASK_FINALIZE
     assert not la.can_mul_mat(p, dst.t)
-    p.type = la.TASK_INIT        # claimed only when src1 is quantized on the GPU
-    assert not la.can_mul_mat(p, dst.t)          # default: N = 1 stays on ggml's CPU INIT
+    p.type = la.TASK_INIT        # claimed whenever the GPU quantizes src1
+    assert la.can_mul_mat(p, dst.t)              # default: decode-sized q4_0 -> fused into the GEMV
+    monkeypatch.setenv("LAMM_HIP_FUSED", "0")
+    assert not la.can_mul_mat(p, dst.t)          # N = 1 without fusion: ggml's CPU INIT
+    monkeypatch.delenv("LAMM_HIP_FUSED")
     monkeypatch.setenv("LAMM_HIP_GPU_QUANT", "1")
     assert la.can_mul_mat(p, dst.t)
     monkeypatch.setenv("LAMM_HIP_GPU_QUANT", "0")
     assert not la.can_mul_mat(p, dst.t)
     monkeypatch.delenv("LAMM_HIP_GPU_QUANT")
+    s2k, s1k, _, _ = make_node(ol.Q2_K, M, 1, K)   # q8_K activations: no fused path, CPU INIT
+    assert not la.can_mul_mat(p, ggml_emu.mul_mat_node(s2k, s1k).t)
     src0b, src1b, _, _ = make_node(t, M, 8, K)   # from 8 activation rows: GPU quantizer
     dstb = ggml_emu.mul_mat_node(src0b, src1b)
     assert la.can_mul_mat(p, dstb.t)
@@ -272,3 +277,38 @@ def test_boundary_rows_split_over_devices(devices, t, M, N, K, monkeypatch):
         d1 = ggml_emu.mul_mat_node(s0, ggml_emu.Tensor(ol.F32, [K, N], data=b))
         assert ggml_emu.compute(d1, nth=2)
         np.testing.assert_array_equal(d1.buf.view(np.float32).reshape(N, rows), got[:, r0:r0 + rows])
+
+
+@pytest.mark.parametrize("t", [ol.Q4_0, ol.Q4_1, ol.Q8_0, ol.Q6_K], ids=["q4_0", "q4_1", "q8_0", "q6_k"])
+@pytest.mark.parametrize("mode", ["fused", "cpu_init", "device_copies"])
+def test_decode_calls_fresh_every_call(t, mode, monkeypatch):
+    """Decode-sized calls through the boundary, as llama.cpp makes them: the SAME src1 / dst
+    buffers with new contents every call (ggml's compute buffer is reused per token).  Activations
+    are read in place from pinned host memory mapped into the device and C is written back the
+    same way (default), or copied by HIP (LAMM_HIP_ZERO_COPY=0); the activations are quantized by
+    the GEMV (fused, default for q8_0 / q8_1 formats) or by ggml's CPU INIT (LAMM_HIP_FUSED=0).
+    Every call must match the oracle, and the modes must agree bit for bit."""
+    if mode == "cpu_init":
+        monkeypatch.setenv("LAMM_HIP_FUSED", "0")
+    if mode == "device_copies":
+        monkeypatch.setenv("LAMM_HIP_ZERO_COPY", "0")
+    M, N, K = 4096, 1, 4096
+    rng = np.random.default_rng(t)
+    if t in ol.KQ_TYPES:
+        A_q = ol.random_kq_blocks(t, M, K, rng)
+    else:
+        A_q = ORACLE.quantize(t, rng.standard_normal((M, K), dtype=np.float32))
+    src0 = ggml_emu.Tensor(t, [K, M], data=A_q)
+    src1 = ggml_emu.Tensor(ol.F32, [K, N])
+    dst = ggml_emu.mul_mat_node(src0, src1)
+    vt = la.vec_dot_type(t)
+    for it in range(12):
+        x = rng.standard_normal((N, K), dtype=np.float32)
+        src1.buf.view(np.float32)[:] = x.reshape(-1)
+        assert ggml_emu.compute(dst, nth=2)
+        got = dst.buf.view(np.float32).reshape(N, M)
+        B = ORACLE.quantize(vt, x, ol.QUANT_AVX if vt in (ol.Q8_0, ol.Q8_1) else ol.QUANT_REF)
+        want = ORACLE.mul_mat(t, M, N, K, A_q, B)
+        Ad = ORACLE.dequantize(t, A_q, M, K).astype(np.float64)
+        absdot = np.abs(ORACLE.dequantize(vt, B, N, K).astype(np.float64)) @ np.abs(Ad).T
+        assert rel_err(got, want, absdot).max() < 1e-3, it

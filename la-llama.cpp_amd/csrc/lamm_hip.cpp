@@ -466,6 +466,9 @@ struct StatScope {
 struct Dev {
   int id = 0;
   hipStream_t stream = nullptr;
+  unsigned* flag = nullptr;       // pinned, host-coherent completion word (lamm_signal.hip)
+  unsigned* flag_dev = nullptr;   // its device address
+  unsigned seq = 0;
   std::unordered_map<WeightKey, WeightEntry, WeightKeyHash> cache;
   std::list<WeightKey> lru;
   size_t cached = 0;
@@ -589,6 +592,9 @@ class Runtime {
       devs[i].id = ids[i];
       HIPCHK(hipSetDevice(ids[i]));
       HIPCHK(hipStreamCreateWithFlags(&devs[i].stream, hipStreamNonBlocking));
+      HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&devs[i].flag), 64, hipHostMallocCoherent | hipHostMallocMapped));
+      HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&devs[i].flag_dev), devs[i].flag, 0));
+      *(volatile unsigned*)devs[i].flag = 0;
     }
     const char* b = getenv("LAMM_HIP_CACHE_GB");
     budget_ = (size_t)((b ? atof(b) : 64.0) * (1ull << 30));
@@ -676,6 +682,7 @@ class Runtime {
       (void)hipStreamSynchronize(d.stream);
       for (void* b : d.buf)
         if (b) (void)hipFree(b);
+      (void)hipHostFree(d.flag);
       (void)hipStreamDestroy(d.stream);
     }
     devs.clear();
@@ -810,6 +817,28 @@ extern "C" bool lamm_can_mul_mat(const struct ggml_compute_params* vparams, cons
 }
 
 namespace {
+
+// Wait for everything queued on d's stream: a completion flag the GPU writes (lamm_signal.hip),
+// spun on by the host -- ~4 us per call under hipStreamSynchronize.  If the flag has not arrived
+// after a second (a fault, a hang) the stream is synchronised, which reports the error.
+// LAMM_HIP_SPIN=0: hipStreamSynchronize only (A/B).
+void wait_device(Dev& d) {
+  static const bool spin = [] {
+    const char* e = getenv("LAMM_HIP_SPIN");
+    return !(e && e[0] == '0');
+  }();
+  if (spin) {
+    const unsigned seq = ++d.seq;
+    HIPCHK(launch_signal(d.flag_dev, seq, d.stream));
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned it = 0;; ++it) {
+      if (*(volatile unsigned*)d.flag == seq) return;
+      if ((it & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1)) break;
+      __builtin_ia32_pause();
+    }
+  }
+  HIPCHK(hipStreamSynchronize(d.stream));
+}
 
 // Decode-sized calls read their activations from, and write C to, pinned host memory mapped into
 // the device (tools/lat_probe.hip: every HIP copy op costs the host ~5 us to enqueue and the
@@ -993,7 +1022,7 @@ extern "C" void lamm_mul_mat(const struct ggml_compute_params* vparams, struct g
   stat.phase(1);
   for (int g = 0; g < G; ++g) {
     HIPCHK(hipSetDevice(rt.devs[g].id));
-    HIPCHK(hipStreamSynchronize(rt.devs[g].stream));
+    wait_device(rt.devs[g]);
   }
   stat.phase(2);
   if (zc_out) {

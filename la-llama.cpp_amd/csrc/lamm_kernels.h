@@ -50,6 +50,9 @@ bool quantize_weights_supported(int type);
 hipError_t launch_quantize_weights(int type, const float* x, int64_t ldx, void* y, int64_t ldy_bytes, int K, int M,
                                    hipStream_t s);
 
+// completion flag (lamm_signal.hip): stores seq into *flag_dev after everything queued on s
+hipError_t launch_signal(unsigned* flag_dev, unsigned seq, hipStream_t s);
+
 hipError_t launch_gemm(int type, const GemvArgs& p, void* workspace, hipStream_t s);
 size_t gemm_workspace_bytes(int type, const GemvArgs& p);   // device scratch launch_gemm needs
 bool gemm_supported(int type);

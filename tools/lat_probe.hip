@@ -22,6 +22,15 @@
 
 __global__ void empty_kernel() {}
 
+// one lane stores `seq` to a host-mapped flag (system-scope release); the host spins on it
+__global__ void flag_kernel(volatile unsigned* flag, unsigned seq) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    __threadfence_system();
+    *flag = seq;
+    __threadfence_system();
+  }
+}
+
 // one workgroup per 4 KiB: write n floats (C) with plain vector stores
 __global__ void write_kernel(float* __restrict__ c, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -86,6 +95,28 @@ int main(int argc, char** argv) {
            copy_kernel<<<n / 4 / 256, 256, 0, s>>>((const float4*)hcd, (float4*)d1, n / 4);
            write_kernel<<<n / 256, 256, 0, s>>>(hcd, n);
          }, s));
+  unsigned* hflag;
+  unsigned* dflag;
+  CK(hipHostMalloc((void**)&hflag, 64, hipHostMallocCoherent | hipHostMallocMapped));
+  CK(hipHostGetDevicePointer((void**)&dflag, hflag, 0));
+  *hflag = 0;
+  unsigned seq = 0;
+  {   // launch -> host sees the kernel's flag (no stream synchronisation in the timed path)
+    std::vector<double> t(2000);
+    for (int r = -50; r < 2000; ++r) {
+      ++seq;
+      const auto t0 = std::chrono::steady_clock::now();
+      flag_kernel<<<1, 64, 0, s>>>(dflag, seq);
+      while (*(volatile unsigned*)hflag != seq) {
+      }
+      const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+      if (r >= 0) t[r] = us;
+      CK(hipStreamSynchronize(s));
+    }
+    std::sort(t.begin(), t.end());
+    printf(", \"flag_kernel_spin\": %.2f", t[1000]);
+  }
+  printf(", \"flag_kernel_sync\": %.2f", median_us([&] { flag_kernel<<<1, 64, 0, s>>>(dflag, ++seq); }, s));
   printf("}\n");
   return 0;
 }

@@ -1,0 +1,79 @@
+// xfer_probe.hip -- prefill-sized host<->device transfers through the ggml boundary: the
+// activations (512 x 4096 F32 = 8 MiB) up and C (8 MiB) down, from / to ordinary (pageable)
+// host memory as ggml hands it over.  Median of 20 of each, us:
+//   pageable      : hipMemcpyAsync straight from / to the pageable buffer + sync
+//   reg_per_call  : hipHostRegister, hipMemcpyAsync, hipHostUnregister (pinned for the call only)
+//   registered    : hipMemcpyAsync on an already registered buffer (the transfer alone)
+//   via_pinned    : host memcpy into / out of a pinned staging buffer + DMA
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#define CK(x)                                                          \
+  do {                                                                 \
+    hipError_t e = (x);                                                \
+    if (e != hipSuccess) {                                             \
+      fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e));           \
+      exit(1);                                                         \
+    }                                                                  \
+  } while (0)
+
+template <class F>
+double med(F&& f) {
+  std::vector<double> t;
+  for (int r = 0; r < 23; ++r) {
+    const auto t0 = std::chrono::steady_clock::now();
+    f();
+    const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    if (r >= 3) t.push_back(us);
+  }
+  std::sort(t.begin(), t.end());
+  return t[t.size() / 2];
+}
+
+int main() {
+  hipStream_t s;
+  CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  printf("{");
+  const size_t sizes[] = {(size_t)512 << 10, (size_t)8 << 20};
+  for (size_t n : sizes) {
+    void* d;
+    CK(hipMalloc(&d, n));
+    std::vector<unsigned char> page(n + 4096, 1);
+    unsigned char* h = page.data();
+    void* pin;
+    CK(hipHostMalloc(&pin, n, hipHostMallocDefault));
+    for (int dir = 0; dir < 2; ++dir) {
+      const hipMemcpyKind k = dir ? hipMemcpyDeviceToHost : hipMemcpyHostToDevice;
+      auto cp = [&](void* host) {
+        if (dir) CK(hipMemcpyAsync(host, d, n, k, s));
+        else CK(hipMemcpyAsync(d, host, n, k, s));
+        CK(hipStreamSynchronize(s));
+      };
+      const char* name = dir ? "d2h" : "h2d";
+      printf("%s\"%s_%zuK_pageable\": %.1f", (n == sizes[0] && !dir) ? "" : ", ", name, n >> 10, med([&] { cp(h); }));
+      printf(", \"%s_%zuK_reg_per_call\": %.1f", name, n >> 10, med([&] {
+               CK(hipHostRegister(h, n, hipHostRegisterDefault));
+               cp(h);
+               CK(hipHostUnregister(h));
+             }));
+      CK(hipHostRegister(h, n, hipHostRegisterDefault));
+      printf(", \"%s_%zuK_registered\": %.1f", name, n >> 10, med([&] { cp(h); }));
+      CK(hipHostUnregister(h));
+      printf(", \"%s_%zuK_via_pinned\": %.1f", name, n >> 10, med([&] {
+               if (!dir) memcpy(pin, h, n);
+               cp(pin);
+               if (dir) memcpy(h, pin, n);
+             }));
+    }
+    CK(hipHostFree(pin));
+    CK(hipFree(d));
+  }
+  printf("}\n");
+  return 0;
+}

@@ -14,168 +14,12 @@
 //   * the q4_0 / q5_0 offset is applied in the integer domain (sum (q-c) b = sum q b - c sum b);
 //   * the 64 lane partials reduce through DPP + readlane in a fixed order (deterministic).
 // Bytes per call are the algorithmic A + B + C (A streamed once, non-temporal).
-#include "lamm_device.h"
-#include "lamm_kernels.h"
+#include "lamm_rowdot.h"
 
 #include <cstdlib>
 
 namespace lamm {
 namespace {
-
-template <int T> struct RFmt;
-template <> struct RFmt<kQ4_0> { static constexpr int BPB = 18, VBPB = 34; };
-template <> struct RFmt<kQ4_1> { static constexpr int BPB = 20, VBPB = 36; };
-template <> struct RFmt<kQ5_0> { static constexpr int BPB = 22, VBPB = 34; };
-template <> struct RFmt<kQ5_1> { static constexpr int BPB = 24, VBPB = 36; };
-template <> struct RFmt<kQ8_0> { static constexpr int BPB = 34, VBPB = 34; };
-
-// NW consecutive dwords at byte offset `off` (dword aligned) of a buffer resource, as wide
-// buffer loads (b128 / b64 / b32); out-of-range dwords read as 0.
-template <int NW, int AUX>
-__device__ __forceinline__ void load_words(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t (&w)[NW]) {
-  unroll<NW / 4>([&](auto I) {
-    constexpr int i = I;
-    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off + 16 * i, 0, AUX);
-    w[4 * i] = v[0]; w[4 * i + 1] = v[1]; w[4 * i + 2] = v[2]; w[4 * i + 3] = v[3];
-  });
-  constexpr int b = NW / 4 * 4;
-  if constexpr (NW - b >= 2) {
-    const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, off + 4 * b, 0, AUX);
-    w[b] = (uint32_t)v[0];
-    w[b + 1] = (uint32_t)v[1];
-    if constexpr (NW - b == 3) w[b + 2] = __builtin_amdgcn_raw_buffer_load_b32(r, off + 4 * b + 8, 0, AUX);
-  } else if constexpr (NW - b == 1) {
-    w[b] = __builtin_amdgcn_raw_buffer_load_b32(r, off + 4 * b, 0, AUX);
-  }
-}
-
-// bytes [sh, sh + 4*(NW-1)) of w as NW-1 dwords (sh in {0, 1, 2, 3} bytes)
-template <int NW>
-__device__ __forceinline__ void realign(const uint32_t (&w)[NW], uint32_t (&m)[NW - 1], int sh) {
-  unroll<NW - 1>([&](auto K) {
-    constexpr int k = K;
-    m[k] = __builtin_amdgcn_alignbit(w[k + 1], w[k], sh * 8);
-  });
-}
-
-// A 32-element block as the dot needs it: 8 int8 quads (the 4-bit / 5-bit formats unpacked to
-// unsigned bytes) + d (+ m for q4_1 / q5_1)
-template <int T, int NW>
-__device__ __forceinline__ void unpack_a(const uint32_t (&m)[NW], uint32_t (&q)[8], float& da, float& ma) {
-  ma = 0.f;
-  if constexpr (T == kQ8_0) {
-    da = h2f(get16<0>(m));
-    unroll<8>([&](auto K) { q[K] = get32<2 + 4 * K>(m); });
-  } else {
-    constexpr bool AFF = (T == kQ4_1 || T == kQ5_1);
-    constexpr bool FIVE = (T == kQ5_0 || T == kQ5_1);
-    constexpr int QS = (AFF ? 4 : 2) + (FIVE ? 4 : 0);
-    da = h2f(get16<0>(m));
-    if constexpr (AFF) ma = h2f(get16<2>(m));
-    uint32_t qh = 0;
-    if constexpr (FIVE) qh = get32<AFF ? 4 : 2>(m);
-    unroll<4>([&](auto K) {
-      constexpr int k = K;
-      const uint32_t x = get32<QS + 4 * k>(m);
-      q[k] = x & 0x0f0f0f0fu;
-      q[4 + k] = (x >> 4) & 0x0f0f0f0fu;
-      if constexpr (FIVE) {
-        q[k] |= spread4_hi((qh >> (4 * k)) & 0xf);
-        q[4 + k] |= spread4_hi((qh >> (16 + 4 * k)) & 0xf);
-      }
-      // q4_0 / q5_0 quants stay unsigned: their offset is applied to the dot in the integer
-      // domain, sum (q - c) b = sum q b - c sum b, with sum b precomputed per activation block
-    });
-  }
-}
-
-// The activation rows, decoded once per workgroup: per column j and block b, the 8 int8 quads
-// as two 16-byte halves (lanes read consecutive 16-byte slots: conflict-free ds_read_b128),
-// fp32(fp16 d) and, for q8_1, fp32(fp16 s).  F32 rows are quantized here (ggml's AVX2
-// from_float, bit for bit as stage_b_f32 in lamm_gemv.hip).  Split in two so a thread's
-// activation loads can be issued BEFORE its wave's A loads: waiting for them then does not wait
-// for the HBM stream (vmcnt retires in order).
-template <int T, bool BF32>
-struct ActStage {
-  using F = RFmt<T>;
-  static constexpr int NWB = (F::VBPB + 3) / 4 + 1;
-  static constexpr int NW = BF32 ? 32 : NWB;
-  uint32_t w[NW];
-  uint32_t off = 0;
-
-  template <int NC>
-  __device__ __forceinline__ void load(const GemvArgs& p, __amdgpu_buffer_rsrc_t rb, int it) {
-    const int ncols = p.N < NC ? p.N : NC;
-    const int j = it / p.nblk, b = it % p.nblk;
-    const bool ok = j < ncols && it < NC * p.nblk;
-    if constexpr (BF32) {
-      off = ok ? (uint32_t)(j * p.ldb + (int64_t)b * 128) : 0x7ffffff0u;
-      load_words<32, 0>(rb, off, w);
-    } else {
-      off = ok ? (uint32_t)(j * p.ldb + (int64_t)b * F::VBPB) : 0x7ffffff0u;
-      load_words<NWB, 0>(rb, off & ~3u, w);
-    }
-  }
-
-  __device__ __forceinline__ void store(int it, u32x4* q0, u32x4* q1, float* bd, float* bs) const {
-    uint32_t q[8];
-    float d = 0.f, sx = 0.f;
-    if constexpr (BF32) {
-      float amax = 0.f;
-#pragma unroll
-      for (int k = 0; k < 32; ++k) amax = fmaxf(amax, fabsf(__builtin_bit_cast(float, w[k])));
-      const float dd = amax / 127.f;
-      const float id = amax != 0.0f ? 127.f / amax : 0.0f;
-      int sum = 0;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        uint32_t qw = 0;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          int v = (int)__builtin_rintf(__builtin_bit_cast(float, w[4 * k + e]) * id);
-          v = v > 127 ? 127 : (v < -128 ? -128 : v);
-          sum += v;
-          qw |= (uint32_t)(v & 0xff) << (8 * e);
-        }
-        q[k] = qw;
-      }
-      float dh = dd;
-      asm volatile("" : "+v"(dh));
-      d = (float)(_Float16)dh;
-      if constexpr (F::VBPB == 36) {
-        float sd = (float)sum * dd;
-        asm volatile("" : "+v"(sd));
-        sx = (float)(_Float16)sd;
-      }
-    } else {
-      uint32_t m[NWB - 1];
-      realign(w, m, (int)(off & 3u));
-      constexpr int VQS = F::VBPB == 36 ? 4 : 2;
-      unroll<8>([&](auto K) { q[K] = get32<VQS + 4 * K>(m); });
-      d = h2f(m[0] & 0xffff);
-      if constexpr (VQS == 4) sx = h2f(m[0] >> 16);
-    }
-    if constexpr (T == kQ4_0 || T == kQ5_0) {   // sum b (exact int) for the offset term
-      int sb = 0;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) sb = dot4(q[k], 0x01010101u, sb);
-      sx = __builtin_bit_cast(float, sb);
-    }
-    q0[it] = u32x4{q[0], q[1], q[2], q[3]};
-    q1[it] = u32x4{q[4], q[5], q[6], q[7]};
-    bd[it] = d;
-    bs[it] = sx;
-  }
-};
-
-template <int T, int NC, bool BF32>
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t act_rsrc(const GemvArgs& p, const unsigned char* Bz) {
-  using F = RFmt<T>;
-  const int ncols = p.N < NC ? p.N : NC;
-  const int64_t bbytes = BF32 ? (int64_t)(ncols - 1) * p.ldb + (int64_t)p.K * 4
-                              : (int64_t)(ncols - 1) * p.ldb + (int64_t)p.nblk * F::VBPB;
-  return make_rsrc(Bz, (uint32_t)min((bbytes + 3) & ~int64_t(3), (int64_t)0x7fffffff));
-}
 
 // One wave per row: the row's loads for ITER blocks per lane (K <= ITER * 2048) go out at once;
 // each wave also issues its NEXT row's loads before computing the current one (rows strided by

@@ -44,6 +44,16 @@ int fail(int code, const char* fmt, ...) {
   return code;
 }
 
+}  // namespace
+
+// lamm_hip_last_error() for the other translation units of the library (lamm_chain.hip)
+int lamm::report_error(int code, const char* msg) {
+  g_err = msg;
+  return code;
+}
+
+namespace {
+
 struct DeviceProbe {
   int count = 0;          // gfx950 devices visible
   int device = 0;         // device used by the ggml boundary

@@ -19,6 +19,11 @@
 // --batch-proj stores wq|wk|wv and ffn_gate|ffn_up as slices of one tensor each and runs each
 // group as ONE lamm_hip_matmul_batched launch against the shared input (B slice stride 0):
 // 4 launches per layer instead of 7 (a GPU-native layout; llama.cpp-b2430 issues 7 mul_mats).
+// --chain runs the 7 x 32 single-token GEMVs as ONE lamm_hip_chain launch (lamm_chain.hip: a
+// persistent kernel whose waves stream the next op's weight rows while its input is produced;
+// ops wait inside the launch only for the op that produces their input), then the output
+// projection as its own launch; each layer gets its own output buffers (a chain's outputs may
+// not overlap) and layer 0 reads a fixed input.
 // --concurrent keeps llama.cpp's 7 separate tensors but forks wk / wv and ffn_up onto side
 // streams (parallel branches of the captured graph) -- measured SLOWER (decode 1.88 -> 2.14
 // ms): each GEMV grid wants every CU (one 149 KiB-LDS workgroup per CU), so concurrent
@@ -28,6 +33,7 @@
 // --unfused runs the separate lamm_hip_quantize launches instead.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -130,6 +136,8 @@ struct Model {
   std::vector<Tensor> wq, wk, wv, wo, w1, w3, w2, out;
   Act a4096, b4096, c4096, a11008;
   float *q, *k, *v, *o, *g, *u, *d, *logits;
+  lamm_chain* chain = nullptr;   // --chain: every layer's 7 GEMVs as one launch
+  Act last;                      // --chain: the output projection's input (last layer's down)
 };
 
 bool g_fused = true;   // decode (N <= 8): F32 activations straight into the GEMV (INIT fused)
@@ -165,6 +173,12 @@ void matmul(const Tensor& w, const Act& a, float* C, int N, hipStream_t s) {
 // one token step: the mul_mat nodes of build_llama in graph order
 void step(Model& m, int layers, hipStream_t s) {
   const int N = m.N;
+  if (m.chain) {
+    lamm_ok(lamm_hip_chain_run(m.chain, s), "lamm_hip_chain_run");
+    quantize(m.out[0].type, m.last, N, s);
+    matmul(m.out[0], m.last, m.logits, N, s);
+    return;
+  }
   for (int l = 0; l < layers; ++l) {
     quantize(m.wq[l].type, m.a4096, N, s);           // attn_norm output -> wq / wk / wv
     if (m.side[0] && m.wq[l].slices == 1) {          // wk / wv on forked streams, joined before wo
@@ -209,7 +223,7 @@ void step(Model& m, int layers, hipStream_t s) {
 
 int main(int argc, char** argv) {
   int type = 2, N = 1, iters = 20, layers = 32, out_type = 14;
-  bool graph = true, stationary = false, batch_proj = false, concurrent = false;
+  bool graph = true, stationary = false, batch_proj = false, concurrent = false, chain = false;
   for (int i = 1; i < argc; ++i) {
     const std::string a = argv[i];
     auto next = [&]() -> const char* {
@@ -226,8 +240,9 @@ int main(int argc, char** argv) {
     else if (a == "--unfused") g_fused = false;
     else if (a == "--batch-proj") batch_proj = true;
     else if (a == "--concurrent") concurrent = true;
+    else if (a == "--chain") chain = true;
     else {
-      fprintf(stderr, "usage: %s [-d q4_0] [-n tokens] [-i replays] [-l layers] [--no-graph] [-s] [--output-type q6_k] [--unfused] [--batch-proj] [--concurrent]\n",
+      fprintf(stderr, "usage: %s [-d q4_0] [-n tokens] [-i replays] [-l layers] [--no-graph] [-s] [--output-type q6_k] [--unfused] [--batch-proj] [--concurrent] [--chain]\n",
               argv[0]);
       return 1;
     }
@@ -292,10 +307,44 @@ int main(int argc, char** argv) {
   mk_act(m.c4096, H, m.o);
   mk_act(m.a11008, F, batch_proj ? m.g + (size_t)N * F : m.u);   // the up projection's output
 
+  std::vector<void*> chain_bufs;
+  if (chain) {   // per-layer outputs; layer 0 reads a copy of the first input
+    if (batch_proj || N != 1) {
+      fprintf(stderr, "llama-matmul-bench: --chain is a single-token path of separate tensors (no --batch-proj, -n 1)\n");
+      return 1;
+    }
+    auto buf = [&](int M) {
+      float* p = nullptr;
+      hip_ok(hipMalloc(&p, (size_t)M * 4 + 256), "hipMalloc(chain)");
+      hip_ok(hipMemset(p, 0, (size_t)M * 4 + 256), "hipMemset(chain)");
+      chain_bufs.push_back(p);
+      return p;
+    };
+    float* x = buf(H);
+    hip_ok(hipMemcpy(x, m.d, (size_t)H * 4, hipMemcpyDeviceToDevice), "copy x");
+    std::vector<lamm_chain_op> ops;
+    auto op = [&](const Tensor& w, const float* in, float* out) {
+      ops.push_back(lamm_chain_op{lamm_matrix{w.data, w.type, w.M, w.kb, w.ld}, in, out});
+    };
+    for (int l = 0; l < layers; ++l) {
+      float *q = buf(H), *k = buf(H), *v = buf(H), *o = buf(H), *g = buf(F), *u = buf(F), *d = buf(H);
+      op(m.wq[l], x, q);
+      op(m.wk[l], x, k);
+      op(m.wv[l], x, v);
+      op(m.wo[l], q, o);
+      op(m.w1[l], o, g);
+      op(m.w3[l], o, u);
+      op(m.w2[l], u, d);
+      x = d;
+    }
+    lamm_ok(lamm_hip_chain_create(ops.data(), (int)ops.size(), &m.chain), "lamm_hip_chain_create");
+    mk_act(m.last, H, x);
+  }
+
   printf("llama-matmul-bench: Llama-7B weight matmuls, %d layers, weights %s, output.weight %s, "
-         "%.2f GB of weight blocks, %d token(s) per step, %s%s\n",
+         "%.2f GB of weight blocks, %d token(s) per step, %s%s%s\n",
          layers, type_name(type), type_name(out_type), wbytes / 1e9, N, graph ? "hipGraph" : "stream",
-         stationary ? ", weight-stationary handles" : "");
+         stationary ? ", weight-stationary handles" : "", chain ? ", one chain launch for the layers" : "");
 
   // warm-up (workspaces reach their final size before capture), then capture one step
   for (int w = 0; w < 2; ++w) step(m, layers, s);
@@ -332,12 +381,39 @@ int main(int argc, char** argv) {
     fprintf(stderr, "llama-matmul-bench: non-finite logits\n");
     return 1;
   }
+  if (m.chain) lamm_ok(lamm_hip_chain_status(m.chain), "lamm_hip_chain_status");
+  if (m.chain && lamm_hip_chain_trace(m.chain, nullptr, 0)) {   // LAMM_CHAIN_TRACE=1: last launch's phase timeline
+    const int nph = lamm_hip_chain_phases(m.chain), w = 2 * nph + 2;
+    std::vector<uint64_t> tr(lamm_hip_chain_trace(m.chain, nullptr, 0));
+    lamm_hip_chain_trace(m.chain, tr.data(), tr.size());
+    const int grid = (int)(tr.size() / w);
+    uint64_t t0 = ~0ull;
+    for (int g = 0; g < grid; ++g) t0 = std::min(t0, tr[(size_t)g * w]);
+    auto col = [&](int k, std::vector<double>& v) {
+      v.clear();
+      for (int g = 0; g < grid; ++g) v.push_back((tr[(size_t)g * w + k] - t0) * 0.01);   // 100 MHz -> us
+      std::sort(v.begin(), v.end());
+    };
+    std::vector<double> b, e;
+    printf("chain trace (us from the first workgroup's start; staging begin min/max, end min/max):\n");
+    for (int p = 0; p < nph; ++p) {
+      col(1 + 2 * p, b);
+      col(2 + 2 * p, e);
+      if (p < 8 || p >= nph - 4)
+        printf("  phase %3d: begin %8.2f %8.2f  end %8.2f %8.2f\n", p, b.front(), b.back(), e.front(), e.back());
+    }
+    col(w - 1, e);
+    printf("  end: %8.2f %8.2f\n", e.front(), e.back());
+  }
+  const int launches = m.chain ? 2 : (batch_proj ? 4 : 7) * layers + 1;
   printf("step %.3f ms  |  %.1f tok/s  |  weight stream %.1f GB/s  |  %.1f TFLOP/s  |  %d matmul launches + %d quantizations per step  |  logits |sum| %.4g\n",
-         t * 1e3, N / t, wbytes / t / 1e9, 2.0 * params * N / t / 1e12, (batch_proj ? 4 : 7) * layers + 1,
-         fused(type, N) ? 1 : 4 * layers + 1, cs);
+         t * 1e3, N / t, wbytes / t / 1e9, 2.0 * params * N / t / 1e12, launches,
+         m.chain ? 1 : fused(type, N) ? 1 : 4 * layers + 1, cs);
   printf("{\"tool\": \"llama-matmul-bench\", \"layers\": %d, \"tokens_per_step\": %d, \"ms_per_step\": %.4f, \"tok_per_s\": %.2f, "
-         "\"weight_GBps\": %.1f, \"TFLOPs\": %.2f, \"graph\": %s, \"stationary\": %s, \"type\": \"%s\"}\n",
+         "\"weight_GBps\": %.1f, \"TFLOPs\": %.2f, \"graph\": %s, \"stationary\": %s, \"type\": \"%s\", "
+         "\"mode\": \"%s\", \"launches\": %d}\n",
          layers, N, t * 1e3, N / t, wbytes / t / 1e9, 2.0 * params * N / t / 1e12, graph ? "true" : "false",
-         stationary ? "true" : "false", type_name(type));
+         stationary ? "true" : "false", type_name(type),
+         m.chain ? "chain" : batch_proj ? "batch-proj" : concurrent ? "concurrent" : "separate", launches);
   return 0;
 }

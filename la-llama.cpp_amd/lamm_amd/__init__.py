@@ -68,6 +68,11 @@ class Batch(ctypes.Structure):
                 ("nbc3", ctypes.c_size_t)]
 
 
+class ChainOp(ctypes.Structure):
+    """struct lamm_chain_op: y = A x for one token inside a decode chain."""
+    _fields_ = [("A", Matrix), ("x", ctypes.c_void_p), ("y", ctypes.c_void_p)]
+
+
 class GgmlComputeParams(ctypes.Structure):
     """struct ggml_compute_params, LC/ggml.h:668-677 (b2430)."""
     _fields_ = [("type", ctypes.c_int32), ("ith", ctypes.c_int32), ("nth", ctypes.c_int32),
@@ -131,6 +136,12 @@ lib.lamm_hip_comm_last_error.restype = ctypes.c_char_p
 lib.lamm_hip_allgather_rows.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_int64),
                                         ctypes.POINTER(ctypes.c_void_p), ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
                                         ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
+lib.lamm_hip_chain_create.argtypes = [ctypes.POINTER(ChainOp), ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
+lib.lamm_hip_chain_run.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+lib.lamm_hip_chain_status.argtypes = [ctypes.c_void_p]
+lib.lamm_hip_chain_phases.argtypes = [ctypes.c_void_p]
+lib.lamm_hip_chain_destroy.argtypes = [ctypes.c_void_p]
+lib.lamm_hip_chain_destroy.restype = None
 lib.lamm_hip_cache_clear.restype = None
 lib.lamm_hip_cache_bytes.restype = ctypes.c_size_t
 lib.lamm_hip_boundary_reset.restype = None
@@ -370,6 +381,38 @@ class Comm:
     def close(self):
         if self.h:
             lib.lamm_hip_comm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Chain:
+    """lamm_chain: single-token GEMVs y_i = A_i x_i run as ONE persistent launch; an op whose x is
+    an earlier op's y waits for it inside the launch.  ops: [(Matrix A, x pointer, y pointer)]."""
+
+    def __init__(self, ops):
+        arr = (ChainOp * len(ops))(*[ChainOp(A, x, y) for (A, x, y) in ops])
+        self.h = ctypes.c_void_p()
+        _check(lib.lamm_hip_chain_create(arr, len(ops), ctypes.byref(self.h)), "lamm_hip_chain_create")
+
+    @property
+    def phases(self):
+        return lib.lamm_hip_chain_phases(self.h)
+
+    def run(self, stream=0):
+        _check(lib.lamm_hip_chain_run(self.h, stream), "lamm_hip_chain_run")
+
+    def status(self):
+        """After the launch finished: raises if a wait inside it gave up."""
+        _check(lib.lamm_hip_chain_status(self.h), "lamm_hip_chain_status")
+
+    def close(self):
+        if self.h:
+            lib.lamm_hip_chain_destroy(self.h)
             self.h = None
 
     def __del__(self):

@@ -135,3 +135,36 @@ def test_shard_rows_cover_every_row_once(align):
             assert pos == M
             tiles = [-(-rows // align) for _, rows in slabs]
             assert max(tiles) - min(tiles) <= 1
+
+
+def test_chain_create_validation():
+    """lamm_hip_chain_create rejects malformed chains before touching a device."""
+    def op(t, M, K, x, y, base=0x100000):
+        kb = K // 32
+        lda = kb
+        while (lda * la.type_size(t)) % 16:
+            lda += 1
+        return (la.Matrix(base, t, M, kb, lda), x, y)
+
+    def create(ops):
+        arr = (la.ChainOp * len(ops))(*[la.ChainOp(*o) for o in ops])
+        h = ctypes.c_void_p()
+        return la.lib.lamm_hip_chain_create(arr, len(ops), ctypes.byref(h))
+
+    Q4, Q8 = ol.Q4_0, ol.Q8_0
+    assert create([]) == la.LAMM_ERR_SHAPE
+    # one weight type per chain
+    assert create([op(Q4, 64, 64, 0x1000, 0x2000), op(Q8, 64, 64, 0x1000, 0x3000)]) == la.LAMM_ERR_TYPE
+    # unsupported type
+    assert create([op(ol.Q2_K, 64, 256, 0x1000, 0x2000)]) == la.LAMM_ERR_TYPE
+    # outputs overlap
+    assert create([op(Q4, 64, 64, 0x1000, 0x2000), op(Q4, 64, 64, 0x1000, 0x2000 + 128)]) == la.LAMM_ERR_SHAPE
+    # input = an earlier output but K != its rows
+    assert create([op(Q4, 64, 64, 0x1000, 0x2000), op(Q4, 64, 96, 0x2000, 0x3000)]) == la.LAMM_ERR_SHAPE
+    # external input overlapping an output
+    assert create([op(Q4, 64, 64, 0x1000, 0x2000), op(Q4, 64, 64, 0x2000 + 64, 0x3000)]) == la.LAMM_ERR_SHAPE
+    # K beyond 12288
+    assert create([op(Q4, 64, 12320, 0x1000, 0x20000)]) == la.LAMM_ERR_SHAPE
+    # misaligned weights
+    assert create([op(Q4, 64, 64, 0x1000, 0x2000, base=0x100008)]) == la.LAMM_ERR_ALIGN
+    assert "16-byte" in la.last_error()

@@ -4,7 +4,8 @@ wave-group kernels of lamm_gemv.hip) in ONE process, interleaved rounds, two wor
 
   single : BASELINE config 2 as the survey states it -- one M x K GEMV per launch, launches
            rotating over enough distinct weight copies (> 256 MiB MALL), event-timed per launch;
-  stacked: one launch over S slices (> MALL) -- the steady-state rate.
+  stacked: one launch over S slices (> MALL) -- the steady-state rate;
+  single_hot: one weight every call (served from the Infinity Cache) -- what a prefetch buys.
 
 Also each shape with F32 activations (ggml INIT fused).  Checks every variant's C against the
 default within 1e-5 relative.  Prints one JSON line (us per launch, TB/s of A + B + C bytes)."""
@@ -78,7 +79,8 @@ def main():
         Cm = la.Matrix(C.data_ptr(), la.F32, M, 1, M)
         Am = mats[0]
         bt = la.Batch(sl, 1, sl, 1, M * arow, sl * M * arow, brow, sl * brow, 4 * M, 4 * M * sl)
-        res = {v: {"single": [], "single_f32": [], "single_eager": [], "stacked": []} for v in variants}
+        res = {v: {"single": [], "single_f32": [], "single_hot": [], "single_eager": [], "stacked": []}
+               for v in variants}
         outs = {}
         for rnd in range(5):
             for v in variants:
@@ -89,6 +91,8 @@ def main():
                 cs = lambda: torch.cuda.current_stream().cuda_stream   # the capture stream inside graphs
                 res[v]["single"].append(timed(lambda r: la.matmul(mats[r % sl], Bm, Csm, cs()), 200, stream))
                 res[v]["single_f32"].append(timed(lambda r: la.matmul(mats[r % sl], Xm, Csm, cs()), 200, stream))
+                # the same weight every call: served from the 256 MiB Infinity Cache (MALL-hot)
+                res[v]["single_hot"].append(timed(lambda r: la.matmul(mats[0], Xm, Csm, cs()), 200, stream))
                 res[v]["single_eager"].append(timed(lambda r: la.matmul(mats[r % sl], Bm, Csm, cs()), 200, stream, False))
                 res[v]["stacked"].append(timed(lambda r: la.matmul_batched(Am, Bm, Cm, bt, cs()), 20, stream))
                 if rnd == 0:

@@ -1,12 +1,16 @@
-# decode-step GEMV launch A/B on the Llama-7B weight-matmul step (one matrix per call).
-# The record in profiles/r01/llama_decode_gemv_geometry_ab.txt compared LAMM_GEMV_VARIANT 0
-# (8 waves x 2 LDS slots per workgroup) with two temporary builds (14: 4 waves, 15: 2 waves);
-# those variants were not kept (+-2 %).  Today this runs the kept launch choices: 0 (default)
-# and 10 (the VGPR-landing stream kernel).
+# decode-step GEMV A/B on the Llama-7B weight-matmul step (llama-matmul-bench, hipGraph):
+# one launch per projection vs --batch-proj (q|k|v and gate|up as one launch each), across
+# the decode GEMV choices LAMM_GEMV_RPW (unset = default policy, 0 = wave-group kernels,
+# n = row-per-wave kernel with n waves per workgroup).
 set -e
 B=./la-llama.cpp_amd/llama-matmul-bench
-for v in 0 10; do
-  echo "== LAMM_GEMV_VARIANT=$v"
-  LAMM_GEMV_VARIANT=$v timeout -k 10 120 $B -d q4_0 -n 1 -i 50 | grep step
-  LAMM_GEMV_VARIANT=$v timeout -k 10 120 $B -d q4_0 -n 1 -i 50 --batch-proj | grep step
+for v in default 0 4 8 16; do
+  for bp in "" --batch-proj; do
+    echo "== LAMM_GEMV_RPW=$v $bp"
+    if [ "$v" = default ]; then
+      timeout -k 10 120 $B -d q4_0 -n 1 -i 50 $bp | grep step
+    else
+      LAMM_GEMV_RPW=$v timeout -k 10 120 $B -d q4_0 -n 1 -i 50 $bp | grep step
+    fi
+  done
 done

@@ -30,10 +30,14 @@
 //       before unit n's FMAs so the matrix core and the VALU overlap.  q4_1: sum m_a*s_b is
 //       one rank-2 f16 MFMA per K-step.
 // Ragged M / N / K are zero-padded by the prep passes, so the main loop has no bounds checks.
+#include <algorithm>
 #include <cstdlib>
+#include <map>
+#include <mutex>
 
 #include "lamm_device.h"
 #include "lamm_kernels.h"
+#include "lamm_rowdot.h"
 
 namespace lamm {
 namespace {
@@ -222,7 +226,10 @@ __global__ __launch_bounds__(PW_NT) void prep_w_fp6(GemvArgs p, unsigned char* w
 // grid: x = row group of PREP_NT rows * kgroups + kgroup, y = B slice z
 // NB blocks per thread: PREP_NB on batched calls, 1 when a single slice would leave the grid
 // at a few dozen workgroups (one 4096x512 slice: 64 -> 256)
-template <int T, int NB>
+// BF32: B holds F32 rows (ldb bytes apart) -- ggml's INIT quantization (AVX2 flavour, the bits
+// lamm_hip_quantize(.., 1, ..) writes) runs here, straight into the fp6 planes, instead of a
+// separate pass writing q8 rows for this kernel to re-read
+template <int T, int NB, bool BF32>
 __global__ __launch_bounds__(PREP_NT) void prep_b_fp6(GemvArgs p, unsigned char* ws) {
   using F = F6<T>;
   constexpr int VBPB = F::VBPB, VQS = VBPB == 36 ? 4 : 2;
@@ -239,21 +246,36 @@ __global__ __launch_bounds__(PREP_NT) void prep_b_fp6(GemvArgs p, unsigned char*
   const int64_t jw = (int64_t)(blockIdx.x / nkg) * PREP_NT;
   const int64_t nrow = min((int64_t)PREP_NT, (int64_t)p.N - jw);
   const unsigned char* Bz = p.B + (int64_t)i12 * p.sb2 + (int64_t)i13 * p.sb3 + min(jw, (int64_t)p.N) * p.ldb;
-  const int64_t bbytes = nrow > 0 ? (nrow - 1) * p.ldb + (int64_t)p.nblk * VBPB : 0;
+  const int64_t bbytes = nrow > 0 ? (nrow - 1) * p.ldb + (int64_t)p.nblk * (BF32 ? 128 : VBPB) : 0;
   const auto rs = make_rsrc(Bz, (uint32_t)min((bbytes + 3) & ~int64_t(3), (int64_t)0x7fffffff));
   for (int kb = kb0; kb < kb0 + NB && kb < L.nsteps * F6_KB; ++kb) {
     uint32_t chi[32], clo[32];
     uint32_t d = 0, sv = 0;
     if (j < p.N && kb < p.nblk) {
-      uint32_t m[9];
-      load_block<9>(rs, (uint32_t)((j - jw) * p.ldb + (int64_t)kb * VBPB), m);
-      d = m[0] & 0xffffu;
-      if constexpr (VBPB == 36) sv = m[0] >> 16;
+      if constexpr (BF32) {
+        uint32_t x[32], q8[8];
+        uint16_t dh, sh;
+        load_words<32, 0>(rs, (uint32_t)((j - jw) * p.ldb + (int64_t)kb * 128), x);
+        q8_from_f32<VBPB == 36>(x, q8, dh, sh);
+        d = dh;
+        sv = sh;
 #pragma unroll
-      for (int e = 0; e < 32; ++e) {
-        const int q = (int)(int8_t)((m[(VQS + e) >> 2] >> (8 * ((VQS + e) & 3))) & 0xffu);
-        chi[e] = sm_code(q >> 4);   // floor(q / 16) in [-8, 7]
-        clo[e] = (uint32_t)(q & 15);
+        for (int e = 0; e < 32; ++e) {
+          const int q = (int)(int8_t)((q8[e >> 2] >> (8 * (e & 3))) & 0xffu);
+          chi[e] = sm_code(q >> 4);
+          clo[e] = (uint32_t)(q & 15);
+        }
+      } else {
+        uint32_t m[9];
+        load_block<9>(rs, (uint32_t)((j - jw) * p.ldb + (int64_t)kb * VBPB), m);
+        d = m[0] & 0xffffu;
+        if constexpr (VBPB == 36) sv = m[0] >> 16;
+#pragma unroll
+        for (int e = 0; e < 32; ++e) {
+          const int q = (int)(int8_t)((m[(VQS + e) >> 2] >> (8 * ((VQS + e) & 3))) & 0xffu);
+          chi[e] = sm_code(q >> 4);   // floor(q / 16) in [-8, 7]
+          clo[e] = (uint32_t)(q & 15);
+        }
       }
     } else {
 #pragma unroll
@@ -317,7 +339,8 @@ template <int WJ> struct F6Waves {
 // (deterministic).  nsplit == 1 writes C directly.
 template <int T, int V, int WJ>
 __global__ __launch_bounds__(F6Waves<WJ>::NT) void gemm_fp6_kernel(GemvArgs p, const unsigned char* wsA,
-                                                                    const unsigned char* wsB, int nsplit, float* part) {
+                                                                    const unsigned char* wsB, int nsplit, float* part,
+                                                                    unsigned* tile_ctr) {
   using F = F6<T>;
   using WV = F6Waves<WJ>;
   constexpr int F6_NW = WV::NW, F6_PPW = WV::PPW, UPB = 2 * WJ;   // UPB: units per block
@@ -505,17 +528,88 @@ __global__ __launch_bounds__(F6Waves<WJ>::NT) void gemm_fp6_kernel(GemvArgs p, c
     Cz = part + ((int64_t)sp * p.ne12 * p.ne13 + z) * p.N * p.M;
     ldc = p.M;
   }
+  const bool fused = nsplit > 1 && tile_ctr != nullptr;
+  if (!fused) {
+#pragma unroll
+    for (int x = 0; x < WJ; ++x)
+#pragma unroll
+      for (int y = 0; y < 2; ++y) {
+        const int64_t i = (int64_t)it * F6_TI + 64 * wi + 32 * y + lr;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int64_t j = (int64_t)jt * F6_TJ + 32 * WJ * wj + 32 * x + (e & 3) + 8 * (e >> 2) + 4 * h;
+          if (i < p.M && j < p.N) Cz[j * ldc + i] = 0.5f * acc[x][y][e];
+        }
+      }
+    return;
+  }
+  // Split-K fixup inside the launch (no reduce kernel): every split's workgroup publishes its
+  // partial tile, then counts itself in on the tile's counter; the one that arrives last sums
+  // the partials in split order 0..nsplit-1 -- the order f6_reduce adds them in, so C has the
+  // same bits -- and resets the counter for the next launch.  Nobody waits for anybody:
+  // correctness does not depend on which workgroups are resident.  The partials are kept in
+  // the accumulators' own register layout (each lane's 16 values as 4 x 16 B, a wave's
+  // instruction 1 KiB contiguous) and stored write-through (sc1), so the last workgroup reads
+  // them from any XCD with 16-byte loads (4-byte write-through stores cost one fabric write
+  // per lane).
+  constexpr int kAuxSc1 = 16;
+  constexpr int TILE_FLOATS = F6_TI * F6_TJ;
+  const int tile = (int)(((int64_t)z * L.njt + jt) * L.nit + it);
+  const int ntile = L.nit * L.njt * p.ne12 * p.ne13;
+  auto slab = [&](int s_) {   // split s_'s partial of this tile: [wave][x][y][q][lane][4]
+    return make_rsrc(part + ((int64_t)s_ * ntile + tile) * TILE_FLOATS, TILE_FLOATS * 4u);
+  };
+  auto foff = [&](int x, int y, int q) { return (uint32_t)(((((w * WJ + x) * 2 + y) * 4 + q) * 64 + lane) * 16); };
+  {
+    const auto mine = slab(sp);
+#pragma unroll
+    for (int x = 0; x < WJ; ++x)
+#pragma unroll
+      for (int y = 0; y < 2; ++y)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f32x4 v = {0.5f * acc[x][y][4 * q], 0.5f * acc[x][y][4 * q + 1], 0.5f * acc[x][y][4 * q + 2],
+                           0.5f * acc[x][y][4 * q + 3]};
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), mine, foff(x, y, q), 0, kAuxSc1);
+        }
+  }
+  __shared__ int last_arrival;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's partial stores have landed
+  __syncthreads();
+  if (t == 0) last_arrival = atomicAdd(&tile_ctr[tile], 1u) == (unsigned)(nsplit - 1);
+  __syncthreads();
+  if (!last_arrival) return;
+  float* C = p.C + (int64_t)i12 * p.sc2 + (int64_t)i13 * p.sc3;
 #pragma unroll
   for (int x = 0; x < WJ; ++x)
 #pragma unroll
     for (int y = 0; y < 2; ++y) {
+      f32x16 sum;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) sum[e] = sp == 0 ? 0.5f * acc[x][y][e] : 0.f;
+      for (int s2 = (sp == 0 ? 1 : 0); s2 < nsplit; ++s2) {
+        const auto r = slab(s2);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          f32x4 v;
+          if (s2 == sp) {
+            v = f32x4{0.5f * acc[x][y][4 * q], 0.5f * acc[x][y][4 * q + 1], 0.5f * acc[x][y][4 * q + 2],
+                      0.5f * acc[x][y][4 * q + 3]};
+          } else {
+            v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, foff(x, y, q), 0, kAuxSc1));
+          }
+#pragma unroll
+          for (int k = 0; k < 4; ++k) sum[4 * q + k] = s2 == 0 ? v[k] : sum[4 * q + k] + v[k];
+        }
+      }
       const int64_t i = (int64_t)it * F6_TI + 64 * wi + 32 * y + lr;
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int64_t j = (int64_t)jt * F6_TJ + 32 * WJ * wj + 32 * x + (e & 3) + 8 * (e >> 2) + 4 * h;
-        if (i < p.M && j < p.N) Cz[j * ldc + i] = 0.5f * acc[x][y][e];
+        if (i < p.M && j < p.N) C[j * p.ldc + i] = sum[e];
       }
     }
+  if (t == 0) __hip_atomic_store(&tile_ctr[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // C[z][j][i] = sum_{s < nsplit} part[s][z][j][i], in split order; V4: 4 consecutive i per
@@ -553,6 +647,27 @@ void launch_splitk_reduce(const GemvArgs& p, int nsplit, const float* part, hipS
 
 namespace {
 
+// Per (device, stream) tile counters for the in-launch split-K fixup: zeroed once when made,
+// left zero by every launch (the last workgroup of a tile resets its counter).  Launches on one
+// stream are ordered, so one set per stream is never shared by two running launches.
+constexpr size_t kTileCounters = 1 << 16;
+unsigned* tile_counters(hipStream_t s) {
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, unsigned*> bufs;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lock(mu);
+  unsigned*& b = bufs[{dev, s}];
+  if (!b) {
+    if (hipMalloc(&b, kTileCounters * sizeof(unsigned)) != hipSuccess) return b = nullptr;
+    if (hipMemset(b, 0, kTileCounters * sizeof(unsigned)) != hipSuccess) {
+      (void)hipFree(b);
+      return b = nullptr;
+    }
+  }
+  return b;
+}
+
 // K-splits for a grid of `tiles` workgroups: double until 256 CUs have one each, keeping
 // >= 8 K-steps per split, at most 16 (K=11008, 16 tiles: 8 splits 247, 16 splits 288, 21
 // splits 230 TFLOP/s, profiles/r01/ab_driver_split.txt).  LAMM_FP6_SPLIT=n forces n (A/B).
@@ -589,22 +704,36 @@ hipError_t launch_fp6_t(const GemvArgs& p, const void* prepA, void* ws, hipStrea
   if (!(sp && sp[0] == '1')) {
     if (!prepA) launch_prep_w<T>(p, wsA, s);
     const int rgroups = (L.njt * F6_TJ + PREP_NT - 1) / PREP_NT, nb_all = L.nsteps * F6_KB;
-    if ((int64_t)rgroups * ((nb_all + PREP_NB - 1) / PREP_NB) * p.ne12 * p.ne13 >= 256)
-      hipLaunchKernelGGL((prep_b_fp6<T, PREP_NB>),
-                         dim3((unsigned)(rgroups * ((nb_all + PREP_NB - 1) / PREP_NB)), (unsigned)(p.ne12 * p.ne13)),
-                         dim3(PREP_NT), 0, s, p, wsB);
+    auto prep = [&](auto kmulti, auto kone) {
+      if ((int64_t)rgroups * ((nb_all + PREP_NB - 1) / PREP_NB) * p.ne12 * p.ne13 >= 256)
+        hipLaunchKernelGGL(kmulti,
+                           dim3((unsigned)(rgroups * ((nb_all + PREP_NB - 1) / PREP_NB)), (unsigned)(p.ne12 * p.ne13)),
+                           dim3(PREP_NT), 0, s, p, wsB);
+      else
+        hipLaunchKernelGGL(kone, dim3((unsigned)(rgroups * nb_all), (unsigned)(p.ne12 * p.ne13)), dim3(PREP_NT), 0, s,
+                           p, wsB);
+    };
+    if (p.b_f32)
+      prep(prep_b_fp6<T, PREP_NB, true>, prep_b_fp6<T, 1, true>);
     else
-      hipLaunchKernelGGL((prep_b_fp6<T, 1>), dim3((unsigned)(rgroups * nb_all), (unsigned)(p.ne12 * p.ne13)),
-                         dim3(PREP_NT), 0, s, p, wsB);
+      prep(prep_b_fp6<T, PREP_NB, false>, prep_b_fp6<T, 1, false>);
   }
   const size_t lds = (size_t)F6_NBUF * F6_STAGE;
   const int nsplit = f6_nsplit(p, L);
   float* part = reinterpret_cast<float*>(wsB + (size_t)(p.ne12 * p.ne13) * (size_t)L.b_slice);
   const unsigned char* kA = prepA ? static_cast<const unsigned char*>(prepA) : wsA;
+  // LAMM_FP6_FUSED_REDUCE=1: split-K partials summed inside the launch by each tile's last
+  // workgroup instead of the f6_reduce launch.  Measured SLOWER on config 3 (main kernel 25.7 ->
+  // 40.9 us vs 7.7 us for f6_reduce, profiles/r02/fp6_single_slice_ablation.txt): publishing
+  // 128 KiB per workgroup write-through and reading three partials on only the 64 last
+  // workgroups costs more than a reduce pass over all CUs.  Kept as an A/B switch.
+  const int64_t tiles = (int64_t)L.nit * L.njt * p.ne12 * p.ne13;
+  const char* fr = getenv("LAMM_FP6_FUSED_REDUCE");
+  unsigned* ctr = nsplit > 1 && tiles <= (int64_t)kTileCounters && fr && fr[0] == '1' ? tile_counters(s) : nullptr;
   auto go = [&](auto kern, int nt) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(kern, dim3((unsigned)(L.nit * L.njt * p.ne12 * p.ne13 * nsplit)), dim3(nt), lds, s, p, kA,
-                       static_cast<const unsigned char*>(wsB), nsplit, part);
+    hipLaunchKernelGGL(kern, dim3((unsigned)(tiles * nsplit)), dim3(nt), lds, s, p, kA,
+                       static_cast<const unsigned char*>(wsB), nsplit, part, ctr);
   };
   const char* ev = getenv("LAMM_GEMM_VARIANT");
   const char* ew = getenv("LAMM_FP6_WJ");   // A/B: 1 = 16 waves of 32x64
@@ -623,9 +752,7 @@ hipError_t launch_fp6_t(const GemvArgs& p, const void* prepA, void* ws, hipStrea
     case 12: go(gemm_fp6_kernel<T, 12, 2>, NT2); break;
     default: go(gemm_fp6_kernel<T, 0, 2>, NT2);
   }
-  if (nsplit > 1) {
-    launch_splitk_reduce(p, nsplit, part, s);
-  }
+  if (nsplit > 1 && !ctr) launch_splitk_reduce(p, nsplit, part, s);
   return hipGetLastError();
 }
 
@@ -647,7 +774,10 @@ size_t gemm_fp6_workspace_bytes(int type, const GemvArgs& p, bool prepared) {
   (void)type;
   const F6Layout L = F6Layout::of(p);
   const int nsplit = f6_nsplit(p, L);
-  const size_t part = nsplit > 1 ? (size_t)nsplit * p.ne12 * p.ne13 * (size_t)p.N * p.M * sizeof(float) : 0;
+  // split-K partials: C-shaped for f6_reduce, or whole 256 x 128 tiles for the in-launch fixup
+  const size_t tiles = (size_t)L.nit * L.njt * p.ne12 * p.ne13;
+  const size_t per_split = std::max((size_t)p.ne12 * p.ne13 * (size_t)p.N * p.M, tiles * F6_TI * F6_TJ);
+  const size_t part = nsplit > 1 ? (size_t)nsplit * per_split * sizeof(float) : 0;
   return (prepared ? 0 : (size_t)L.a_bytes) + (size_t)(p.ne12 * p.ne13) * (size_t)L.b_slice + part + 256;
 }
 

@@ -99,11 +99,13 @@ struct WsBuf {
 std::mutex g_ws_mu;
 std::unordered_map<WsKey, WsBuf, WsKeyHash> g_ws;
 
-void* workspace(size_t bytes, hipStream_t s) {
+std::unordered_map<WsKey, WsBuf, WsKeyHash> g_ws_act;   // activations quantized for a GEMM (F32 B)
+
+void* workspace(size_t bytes, hipStream_t s, bool act = false) {
   int dev = 0;
   (void)hipGetDevice(&dev);
   std::lock_guard<std::mutex> lock(g_ws_mu);
-  WsBuf& b = g_ws[WsKey{dev, s}];
+  WsBuf& b = (act ? g_ws_act : g_ws)[WsKey{dev, s}];
   if (b.ptr && b.bytes >= bytes) return b.ptr;
   if (b.ptr) {
     (void)hipStreamSynchronize(s);
@@ -196,13 +198,14 @@ int matmul_impl(const lamm_matrix* A, const lamm_matrix* B, const lamm_matrix* C
                 void* hip_stream, const lamm_weights* W) {
   if (!A || !B || !C) return fail(LAMM_ERR_SHAPE, "null matrix");
   if (!is_weight_type(A->type)) return fail(LAMM_ERR_TYPE, "unsupported A type %d", A->type);
-  // F32 activations for a q8_0 / q8_1 weight type (N <= 8): ggml's INIT quantization runs
-  // inside the GEMV launch (stage_b_f32, AVX2 flavour), bit-exact with lamm_hip_quantize + matmul
+  // F32 activations for a q8_0 / q8_1 weight type: ggml's INIT quantization (AVX2 flavour) runs
+  // on the device, bit-exact with lamm_hip_quantize(.., 1, ..) + matmul -- inside the GEMV
+  // launch (N <= 8, stage_b_f32), inside the fp6 GEMM's activation prep (prep_b_fp6), or as a
+  // quantizer launch in front of the other GEMM engines
   const int vdt = vec_dot_type(A->type);
   const bool b_f32 = B->type == kF32 && (vdt == kQ8_0 || vdt == kQ8_1);
-  if (B->type != vdt && !(b_f32 && B->col <= 8))
-    return fail(LAMM_ERR_TYPE, "B type %d is not vec_dot_type(%d)=%d%s", B->type, A->type, vdt,
-                b_f32 ? " (F32 activations only for N <= 8)" : "");
+  if (B->type != vdt && !b_f32)
+    return fail(LAMM_ERR_TYPE, "B type %d is not vec_dot_type(%d)=%d", B->type, A->type, vdt);
   if (C->type != kF32) return fail(LAMM_ERR_TYPE, "C must be f32");
   const int M = A->row, N = B->col, Kb = A->col;
   const int brows = b_f32 ? Kb * block_elems(A->type) : Kb;   // B.row: K in blocks of B's own type
@@ -244,6 +247,26 @@ int matmul_impl(const lamm_matrix* A, const lamm_matrix* B, const lamm_matrix* C
   p.sc3 = (int64_t)(bt.nbc3 / 4);
   p.b_f32 = b_f32 ? 1 : 0;
   hipError_t e;
+  if (b_f32 && N > 8 && !(gemm_fp6_supported(A->type) && gemm_path(p, W && W->packed) == 0)) {
+    if (((uintptr_t)B->data & 15) || (ldb & 15) || (p.sb2 & 15) || (p.sb3 & 15))
+      return fail(LAMM_ERR_ALIGN, "f32 B rows of a GEMM must be 16-byte aligned");
+    // no F32 staging in this engine: quantize the rows (every slice) into a buffer of its own
+    const int64_t qrow = (int64_t)Kb * (int64_t)block_bytes(vdt), qslice = qrow * N;
+    const int64_t slices = (int64_t)p.ne12 * p.ne13;
+    auto* q = static_cast<unsigned char*>(workspace((size_t)(qslice * slices) + 256, s, true));
+    if (!q) return fail(LAMM_ERR_HIP, "activation buffer of %lld bytes", (long long)(qslice * slices));
+    for (int64_t z = 0; z < slices; ++z) {
+      const int64_t i12 = z % p.ne12, i13 = z / p.ne12;
+      const float* x = reinterpret_cast<const float*>(p.B + i12 * p.sb2 + i13 * p.sb3);
+      e = launch_quantize(vdt, 1, x, ldb / 4, q + z * qslice, qrow, p.K, N, s);
+      if (e != hipSuccess) return fail(LAMM_ERR_HIP, "activation quantizer: %s", hipGetErrorString(e));
+    }
+    p.B = q;
+    p.ldb = qrow;
+    p.sb2 = qslice;
+    p.sb3 = qslice * p.ne12;
+    p.b_f32 = 0;
+  }
   if (N <= gemv_max_n(A->type) || (b_f32 && N <= 8)) {
     e = launch_gemv(A->type, p, s);
   } else if (gemm_dense_supported(A->type) && !getenv_flag0("LAMM_DENSE_GEMM")) {
@@ -975,7 +998,9 @@ extern "C" void lamm_mul_mat(const struct ggml_compute_params* vparams, struct g
                                   (size_t)ne00 * sizeof(float), (size_t)N, hipMemcpyHostToDevice, s));
         }
       dB = dX;
-      if (act == kGpuQuant) {
+      // q8_0 / q8_1 activations are quantized by the library inside the GEMM's own activation
+      // prep (fp6 engine) or in front of it; q8_K / f16 ones here
+      if (act == kGpuQuant && vdt != kQ8_0 && vdt != kQ8_1) {
         void* dq = d.scratch(0, b_row * (size_t)(N * nslices) + 64);
         const int qrc = lamm_hip_quantize(vdt, /*AVX2 flavour*/ 1, dX, ldx, dq, kb, (int)ne00, (int)(N * nslices), s);
         if (qrc != LAMM_OK) {
@@ -992,7 +1017,7 @@ extern "C" void lamm_mul_mat(const struct ggml_compute_params* vparams, struct g
       HIPCHK(hipMemcpy2DAsync(dB, b_row, src1->data, src1->nb[1], b_row, (size_t)(N * nslices), hipMemcpyHostToDevice,
                               s));
     }
-    const bool b_f32 = act == kFused;
+    const bool b_f32 = act == kFused || (act == kGpuQuant && (vdt == kQ8_0 || vdt == kQ8_1));
     const size_t b_pitch = b_f32 ? x_row : b_row;
     const size_t c_slice = (size_t)rows * N * sizeof(float);
     float* dC = zc_out ? static_cast<float*>((rt.pinned(1, c_bytes), rt.pinned_dev(1)))
@@ -1010,7 +1035,7 @@ extern "C" void lamm_mul_mat(const struct ggml_compute_params* vparams, struct g
     pa.ne13 = (int)ne13;
     pa.r2 = (int)(ne12 / ne02);
     pa.r3 = (int)(ne13 / ne03);
-    const bool stationary = weight && !b_f32 && N > gemv_max_n(t0) &&
+    const bool stationary = weight && N > gemv_max_n(t0) && (!b_f32 || N > 8) &&
                             ((gemm_fp6_supported(t0) && gemm_path(pa, true) == 0) ||
                              (gemm_kq_supported(t0) && !getenv_flag0("LAMM_KQ_GEMM")));
     const int rc = stationary ? lamm_hip_matmul_weights(rt.prepared(d, *w, A, ne02, ne03), &B, &C, &bt, s)

@@ -77,6 +77,41 @@ __device__ __forceinline__ void unpack_a(const uint32_t (&m)[NW], uint32_t (&q)[
   }
 }
 
+// One 32-element F32 block -> q8_0 / q8_1 the way ggml's AVX2 from_float rounds it
+// (LC/ggml-quants.c quantize_row_q8_0 / _q8_1 AVX2 branches: id = 127/amax, nearest-even,
+// d and s = d * sum as fp16), bit-identical to lamm_hip_quantize(.., flavour 1, ..):
+// q = the 32 int8 quants as 8 little-endian dwords, dh / sh = fp16 bits of d / s.
+template <bool WITH_S>
+__device__ __forceinline__ void q8_from_f32(const uint32_t (&w)[32], uint32_t (&q)[8], uint16_t& dh, uint16_t& sh) {
+  float amax = 0.f;
+#pragma unroll
+  for (int k = 0; k < 32; ++k) amax = fmaxf(amax, fabsf(__builtin_bit_cast(float, w[k])));
+  const float dd = amax / 127.f;
+  const float id = amax != 0.0f ? 127.f / amax : 0.0f;
+  int sum = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    uint32_t qw = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      int v = (int)__builtin_rintf(__builtin_bit_cast(float, w[4 * k + e]) * id);
+      v = v > 127 ? 127 : (v < -128 ? -128 : v);
+      sum += v;
+      qw |= (uint32_t)(v & 0xff) << (8 * e);
+    }
+    q[k] = qw;
+  }
+  float dv = dd;
+  asm volatile("" : "+v"(dv));   // no contraction of the d*sum product below into the division
+  dh = __builtin_bit_cast(uint16_t, (_Float16)dv);
+  sh = 0;
+  if constexpr (WITH_S) {
+    float sd = (float)sum * dd;
+    asm volatile("" : "+v"(sd));
+    sh = __builtin_bit_cast(uint16_t, (_Float16)sd);
+  }
+}
+
 // The activation rows, decoded once per workgroup: per column j and block b, the 8 int8 quads
 // as two 16-byte halves (lanes read consecutive 16-byte slots: conflict-free ds_read_b128),
 // fp32(fp16 d) and, for q8_1, fp32(fp16 s).  F32 rows are quantized here (ggml's AVX2
@@ -109,32 +144,10 @@ struct ActStage {
     uint32_t q[8];
     float d = 0.f, sx = 0.f;
     if constexpr (BF32) {
-      float amax = 0.f;
-#pragma unroll
-      for (int k = 0; k < 32; ++k) amax = fmaxf(amax, fabsf(__builtin_bit_cast(float, w[k])));
-      const float dd = amax / 127.f;
-      const float id = amax != 0.0f ? 127.f / amax : 0.0f;
-      int sum = 0;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        uint32_t qw = 0;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          int v = (int)__builtin_rintf(__builtin_bit_cast(float, w[4 * k + e]) * id);
-          v = v > 127 ? 127 : (v < -128 ? -128 : v);
-          sum += v;
-          qw |= (uint32_t)(v & 0xff) << (8 * e);
-        }
-        q[k] = qw;
-      }
-      float dh = dd;
-      asm volatile("" : "+v"(dh));
-      d = (float)(_Float16)dh;
-      if constexpr (F::VBPB == 36) {
-        float sd = (float)sum * dd;
-        asm volatile("" : "+v"(sd));
-        sx = (float)(_Float16)sd;
-      }
+      uint16_t dh, sh;
+      q8_from_f32<F::VBPB == 36>(w, q, dh, sh);
+      d = h2f(dh);
+      if constexpr (F::VBPB == 36) sx = h2f(sh);
     } else {
       uint32_t m[NWB - 1];
       realign(w, m, (int)(off & 3u));

@@ -266,6 +266,26 @@ def test_gemm_fp6_split_k(t, split, monkeypatch):
     assert np.isnan(np.concatenate([raw[j * (M + 3) + M:(j + 1) * (M + 3)] for j in range(N)])).all()
 
 
+@pytest.mark.parametrize("split", [2, 3, 8])
+@pytest.mark.parametrize("t", FP6_TYPES, ids=[ol.NAMES[t] for t in FP6_TYPES])
+def test_gemm_fp6_split_k_fused_reduce_bitwise(t, split, monkeypatch):
+    """The in-launch split-K fixup (each tile's last workgroup sums the partials) gives the SAME
+    bits as the separate f6_reduce launch (both add in split order), over repeated calls (the
+    tile counters must be left at zero) and a ragged grid; and matches the oracle."""
+    monkeypatch.setenv("LAMM_GEMM_PATH", "fp6")
+    monkeypatch.setenv("LAMM_FP6_SPLIT", str(split))
+    M, N, K = 300, 140, 4096 + 64
+    A_q, B_q = random_case(t, M, N, K, seed=40 + split)
+    runs = []
+    for fused in ("1", "1", "0", "1"):   # 1 = the in-launch fixup (an A/B switch), 0 = f6_reduce
+        monkeypatch.setenv("LAMM_FP6_FUSED_REDUCE", fused)
+        runs.append(gpu_mul_mat(t, A_q, B_q, M, N, K, ldc=M + 3)[0])
+    for r in runs[1:]:
+        assert np.array_equal(r.view(np.uint32), runs[0].view(np.uint32))
+    ref = ORACLE.mul_mat(t, M, N, K, A_q, B_q)
+    assert rel_err(runs[0], ref, absdot(t, A_q, B_q, M, N, K)).max() < TOL
+
+
 @pytest.mark.parametrize("split", ["0", "4"])
 @pytest.mark.parametrize("t", FP6_TYPES, ids=[ol.NAMES[t] for t in FP6_TYPES])
 def test_gemm_fp6_batched_broadcast(t, split, monkeypatch):
@@ -655,14 +675,57 @@ def test_decode_gemv_f32_activations_fused(t, shape):
     assert rel_err(a.reshape(N, M), ref, absdot(t, A_q, B_q, M, N, K)).max() < TOL
 
 
-def test_f32_activations_rejected_beyond_decode():
-    """F32 B is a decode (N <= 8) form only; wider calls must pass quantized rows."""
+GEMM_F32_CASES = [(ol.Q4_0, "fp6"), (ol.Q4_0, "i8"), (ol.Q4_1, "fp6"), (ol.Q4_1, "i8"), (ol.Q5_0, "fp6"),
+                  (ol.Q5_0, "i8"), (ol.Q5_1, "default"), (ol.Q8_0, "default")]
+
+
+@pytest.mark.parametrize("t,path", GEMM_F32_CASES, ids=[f"{ol.NAMES[t]}-{p}" for t, p in GEMM_F32_CASES])
+@pytest.mark.parametrize("N", [9, 140])
+def test_gemm_f32_activations(t, path, N, monkeypatch):
+    """F32 B for N > 8 (ggml's INIT quantization on the device): quantized inside the fp6
+    engine's activation prep, or by a quantizer launch in front of the i8 engine -- C must be
+    BIT-identical to lamm_hip_quantize(flavour 1) + matmul either way, and match the oracle."""
+    if path != "default":
+        monkeypatch.setenv("LAMM_GEMM_PATH", path)
+    M, K = 300, 4096 + 64
+    rng = np.random.default_rng(N + t)
+    A_q = ORACLE.quantize(t, rng.standard_normal((M, K), dtype=np.float32))
+    x = rng.standard_normal((N, K), dtype=np.float32)
+    x[1, 64:96] = 0.0                                  # an all-zero block (d = 0)
+    ldx = K + 4
+    xp = np.full((N, ldx), np.nan, np.float32)
+    xp[:, :K] = x
+    kb = K // 32
+    lda = pitch_blocks(t, kb)
+    dA = dev_bytes(pitched_A(t, A_q, M, kb, lda))
+    dx = torch.from_numpy(xp.reshape(-1)).cuda()
+    s = torch.cuda.current_stream().cuda_stream
+    c1 = torch.full((N * M,), np.nan, dtype=torch.float32, device="cuda")
+    la.matmul(la.Matrix(dA.data_ptr(), t, M, kb, lda), la.Matrix(dx.data_ptr(), la.F32, K, N, ldx),
+              la.Matrix(c1.data_ptr(), la.F32, M, N, M), s)
+    vt = ORACLE.vec_dot_type(t)
+    dq = torch.zeros(N * la.row_bytes(vt, K) + 64, dtype=torch.uint8, device="cuda")
+    la.quantize_torch(vt, dx.view(N, ldx)[:, :K], dq, flavour=1)
+    c2 = torch.full((N * M,), np.nan, dtype=torch.float32, device="cuda")
+    la.matmul(la.Matrix(dA.data_ptr(), t, M, kb, lda), la.Matrix(dq.data_ptr(), vt, kb, N, kb),
+              la.Matrix(c2.data_ptr(), la.F32, M, N, M), s)
+    torch.cuda.synchronize()
+    a, b = c1.cpu().numpy(), c2.cpu().numpy()
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    B_q = ORACLE.quantize(vt, x, ol.QUANT_AVX)
+    ref = ORACLE.mul_mat(t, M, N, K, A_q, B_q)
+    assert rel_err(a.reshape(N, M), ref, absdot(t, A_q, B_q, M, N, K)).max() < TOL
+
+
+def test_gemm_f32_activations_alignment(monkeypatch):
+    """The quantizer in front of the i8 engine reads 16-byte rows: other F32 pitches are refused."""
+    monkeypatch.setenv("LAMM_GEMM_PATH", "i8")
     t, M, K, N = ol.Q4_0, 64, 256, 9
     dA = torch.zeros(M * (K // 32) * 18 + 64, dtype=torch.uint8, device="cuda")
-    dx = torch.zeros(N * K, dtype=torch.float32, device="cuda")
+    dx = torch.zeros(N * (K + 1), dtype=torch.float32, device="cuda")
     c = torch.zeros(N * M, dtype=torch.float32, device="cuda")
     with pytest.raises(la.LammError):
-        la.matmul(la.Matrix(dA.data_ptr(), t, M, K // 32, K // 32), la.Matrix(dx.data_ptr(), la.F32, K, N, K),
+        la.matmul(la.Matrix(dA.data_ptr(), t, M, K // 32, K // 32), la.Matrix(dx.data_ptr(), la.F32, K, N, K + 1),
                   la.Matrix(c.data_ptr(), la.F32, M, N, M), 0)
 
 

@@ -26,14 +26,17 @@ def main():
     W = la.Weights(t, A, M, K)
     splits = os.environ.get("SPLITS", "1,2,4,8").split(",")
     variants = os.environ.get("VARIANTS", "0,1,2,3,6,7").split(",")
-    for sp in splits:
-        for v in variants:
-            os.environ["LAMM_FP6_SPLIT"] = sp
-            os.environ["LAMM_GEMM_VARIANT"] = v
-            for _ in range(20):
-                W.matmul_torch(B, C, N)
-            torch.cuda.synchronize()
-            print(f"split {sp} variant {v} done", flush=True)
+    preps = os.environ.get("PREPS", "1").split(",")   # LAMM_FP6_PREP_TILED (a removed A/B arm)
+    for pr in preps:
+        for sp in splits:
+            for v in variants:
+                os.environ["LAMM_FP6_PREP_TILED"] = pr
+                os.environ["LAMM_FP6_SPLIT"] = sp
+                os.environ["LAMM_GEMM_VARIANT"] = v
+                for _ in range(20):
+                    W.matmul_torch(B, C, N)
+                torch.cuda.synchronize()
+                print(f"prep_tiled {pr} split {sp} variant {v} done", flush=True)
     W.close()
 
 

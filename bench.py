@@ -436,7 +436,11 @@ def llama_step(fmt):
     exe = os.path.join(ROOT, "la-llama.cpp_amd", "llama-matmul-bench")
     res = {"note": "weight matmuls only (no attention/norms), synthetic weights, hipGraph replay: the ceiling "
                    "without the ggml boundary's host round trips"}
-    for name, argv in (("decode_n1", ["-n", "1", "-i", "50"]), ("prefill_n512", ["-n", "512", "-i", "5", "-s"])):
+    # decode_n1: llama.cpp's 7 projection tensors per layer, one launch each; decode_n1_batch_proj:
+    # q|k|v and gate|up stored as one tensor each (4 launches per layer, a GPU-native layout)
+    for name, argv in (("decode_n1", ["-n", "1", "-i", "50"]),
+                       ("decode_n1_batch_proj", ["-n", "1", "-i", "50", "--batch-proj"]),
+                       ("prefill_n512", ["-n", "512", "-i", "5", "-s"])):
         try:
             r = subprocess.run([exe, "-d", fmt] + argv, capture_output=True, text=True, timeout=180)
             line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]

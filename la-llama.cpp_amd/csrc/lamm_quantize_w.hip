@@ -6,12 +6,12 @@
 //   q4_K :2744-2849   q5_K :2992-3090 (make_qkx2_quants, weighted squared error)
 //   q6_K :3301-3380 (make_qx_quants :1774-1841, rmse_type 1)
 // (q8_0 weights are quantize_row_q8_0_reference = lamm_hip_quantize flavour 0.)
-// One thread per block: the k-quant searches are sequential per super-block in the reference
-// and their float sums are order-sensitive, so each thread replays one block's arithmetic in
-// the reference's order.  This file is built with -ffp-contract=off (Makefile): a fused
+// The float sums are order-sensitive, so each thread replays the reference's arithmetic in its
+// order: one thread per 32-element block, and for the k-quants one LANE per sub-block (the
+// reference searches sub-block by sub-block and only then combines their scales).  This file is built with -ffp-contract=off (Makefile): a fused
 // multiply-add would round differently from the reference's separate multiply and add.
 // The quantizer prepares weights once (la-benchmark-matmult quantizes outside its timed loop,
-// src/la-benchmark-matmult.cpp:294-303), so simplicity beats speed here.
+// src/la-benchmark-matmult.cpp:294-303).
 #include "lamm_device.h"
 #include "lamm_formats.h"
 #include "lamm_kernels.h"
@@ -99,12 +99,16 @@ __device__ void quant_affine(const float* x, unsigned char* y) {
 
 // ------------------------------------------------------------------ k-quant searches
 // make_qkx2_quants: affine fit of n values to [0, nmax] minimising the weighted |err|
-// (use_mad) or err^2, scanning nstep+1 candidate scales
-__device__ float make_qkx2(int n, int nmax, const float* x, const float* w, uint8_t* L, float* the_min,
-                           uint8_t* Laux, float rmin, float rdelta, int nstep, bool use_mad) {
+// (use_mad) or err^2, scanning nstep+1 candidate scales.  N is a template constant so the
+// per-value arrays live in registers (every loop over the values is unrolled; the float
+// operations stay in the reference's order).
+template <int N>
+__device__ float make_qkx2(int nmax, const float (&x)[N], const float (&w)[N], uint8_t (&L)[N], float* the_min,
+                           float rmin, float rdelta, int nstep, bool use_mad) {
   float mn = x[0], mx = x[0];
   float sum_w = w[0], sum_x = sum_w * x[0];
-  for (int i = 1; i < n; ++i) {
+#pragma unroll
+  for (int i = 1; i < N; ++i) {
     if (x[i] < mn) mn = x[i];
     if (x[i] > mx) mx = x[i];
     sum_w += w[i];
@@ -112,14 +116,16 @@ __device__ float make_qkx2(int n, int nmax, const float* x, const float* w, uint
   }
   if (mn > 0) mn = 0;
   if (mx == mn) {
-    for (int i = 0; i < n; ++i) L[i] = 0;
+#pragma unroll
+    for (int i = 0; i < N; ++i) L[i] = 0;
     *the_min = -mn;
     return 0.f;
   }
   float iscale = nmax / (mx - mn);
   float scale = 1 / iscale;
   float best = 0;
-  for (int i = 0; i < n; ++i) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
     const int l = nearest_int(iscale * (x[i] - mn));
     L[i] = (uint8_t)(l < 0 ? 0 : (l > nmax ? nmax : l));
     float diff = scale * L[i] + mn - x[i];
@@ -128,8 +134,10 @@ __device__ float make_qkx2(int n, int nmax, const float* x, const float* w, uint
   }
   for (int is = 0; is <= nstep; ++is) {
     iscale = (rmin + rdelta * is + nmax) / (mx - mn);
+    uint8_t Laux[N];
     float sum_l = 0, sum_l2 = 0, sum_xl = 0;
-    for (int i = 0; i < n; ++i) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
       int l = nearest_int(iscale * (x[i] - mn));
       l = l < 0 ? 0 : (l > nmax ? nmax : l);
       Laux[i] = (uint8_t)l;
@@ -146,13 +154,15 @@ __device__ float make_qkx2(int n, int nmax, const float* x, const float* w, uint
         this_scale = sum_xl / sum_l2;
       }
       float mad = 0;
-      for (int i = 0; i < n; ++i) {
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
         float diff = this_scale * Laux[i] + this_min - x[i];
         diff = use_mad ? fabsf(diff) : diff * diff;
         mad += w[i] * diff;
       }
       if (mad < best) {
-        for (int i = 0; i < n; ++i) L[i] = Laux[i];
+#pragma unroll
+        for (int i = 0; i < N; ++i) L[i] = Laux[i];
         best = mad;
         scale = this_scale;
         mn = this_min;
@@ -163,139 +173,24 @@ __device__ float make_qkx2(int n, int nmax, const float* x, const float* w, uint
   return scale;
 }
 
-// q2_K (84 B: scales[16] | qs[64] | d | dmin)
-__device__ void quant_q2_K(const float* x, unsigned char* y) {
-  uint8_t L[256], Laux[16];
-  float w[16], mins[16], scales[16];
-  unsigned char* sc = y;
-  float max_scale = 0, max_min = 0;
-  for (int j = 0; j < 16; ++j) {
-    for (int l = 0; l < 16; ++l) w[l] = fabsf(x[16 * j + l]);
-    scales[j] = make_qkx2(16, 3, x + 16 * j, w, L + 16 * j, &mins[j], Laux, -0.5f, 0.1f, 15, true);
-    if (scales[j] > max_scale) max_scale = scales[j];
-    if (mins[j] > max_min) max_min = mins[j];
-  }
-  uint16_t dh, mh;
-  if (max_scale > 0) {
-    const float iscale = 15.f / max_scale;
-    for (int j = 0; j < 16; ++j) sc[j] = (uint8_t)nearest_int(iscale * scales[j]);
-    dh = f2h(max_scale / 15.f);
-  } else {
-    for (int j = 0; j < 16; ++j) sc[j] = 0;
-    dh = f2h(0.f);
-  }
-  if (max_min > 0) {
-    const float iscale = 15.f / max_min;
-    for (int j = 0; j < 16; ++j) sc[j] |= (uint8_t)(nearest_int(iscale * mins[j]) << 4);
-    mh = f2h(max_min / 15.f);
-  } else {
-    mh = f2h(0.f);
-  }
-  put16(y + 80, dh);
-  put16(y + 82, mh);
-  for (int j = 0; j < 16; ++j) {
-    const float d = hf(dh) * (sc[j] & 0xF);
-    if (!d) continue;
-    const float dm = hf(mh) * (sc[j] >> 4);
-    for (int ii = 0; ii < 16; ++ii) {
-      const int l = nearest_int((x[16 * j + ii] + dm) / d);
-      L[16 * j + ii] = (uint8_t)(l < 0 ? 0 : (l > 3 ? 3 : l));
-    }
-  }
-  for (int j = 0; j < 256; j += 128)
-    for (int l = 0; l < 32; ++l)
-      y[16 + j / 4 + l] = (unsigned char)(L[j + l] | (L[j + l + 32] << 2) | (L[j + l + 64] << 4) | (L[j + l + 96] << 6));
-}
-
-// q4_K (144 B) / q5_K (176 B): 8 sub-blocks of 32, 6-bit scales and mins
-template <bool Q5>
-__device__ void quant_q45_K(const float* x, unsigned char* y) {
-  constexpr int NMAX = Q5 ? 31 : 15;
-  uint8_t L[256], Laux[32];
-  float w[32], mins[8], scales[8];
-  float max_scale = 0, max_min = 0;
-  for (int j = 0; j < 8; ++j) {
-    float sum_x2 = 0;
-    for (int l = 0; l < 32; ++l) sum_x2 += x[32 * j + l] * x[32 * j + l];
-    const float av_x = sqrtf(sum_x2 / 32);
-    for (int l = 0; l < 32; ++l) w[l] = av_x + fabsf(x[32 * j + l]);
-    scales[j] = make_qkx2(32, NMAX, x + 32 * j, w, L + 32 * j, &mins[j], Laux, Q5 ? -0.5f : -1.f, 0.1f,
-                          Q5 ? 15 : 20, false);
-    if (scales[j] > max_scale) max_scale = scales[j];
-    if (mins[j] > max_min) max_min = mins[j];
-  }
-  const float inv_scale = max_scale > 0 ? 63.f / max_scale : 0.f;
-  const float inv_min = max_min > 0 ? 63.f / max_min : 0.f;
-  uint8_t s12[12];
-  for (int j = 0; j < 8; ++j) {
-    uint8_t ls = (uint8_t)nearest_int(inv_scale * scales[j]);
-    uint8_t lm = (uint8_t)nearest_int(inv_min * mins[j]);
-    ls = ls < 63 ? ls : 63;
-    lm = lm < 63 ? lm : 63;
-    if (j < 4) {
-      s12[j] = ls;
-      s12[j + 4] = lm;
-    } else {
-      s12[j + 4] = (uint8_t)((ls & 0xF) | ((lm & 0xF) << 4));
-      s12[j - 4] |= (uint8_t)((ls >> 4) << 6);
-      s12[j] |= (uint8_t)((lm >> 4) << 6);
-    }
-  }
-  const uint16_t dh = f2h(max_scale / 63.f), mh = f2h(max_min / 63.f);
-  for (int j = 0; j < 8; ++j) {   // get_scale_min_k4, LC/ggml-quants.c:2027-2034
-    uint8_t sc, m;
-    if (j < 4) {
-      sc = s12[j] & 63;
-      m = s12[j + 4] & 63;
-    } else {
-      sc = (uint8_t)((s12[j + 4] & 0xF) | ((s12[j - 4] >> 6) << 4));
-      m = (uint8_t)((s12[j + 4] >> 4) | ((s12[j] >> 6) << 4));
-    }
-    const float d = hf(dh) * sc;
-    if (!d) continue;
-    const float dm = hf(mh) * m;
-    for (int ii = 0; ii < 32; ++ii) {
-      const int l = nearest_int((x[32 * j + ii] + dm) / d);
-      L[32 * j + ii] = (uint8_t)(l < 0 ? 0 : (l > NMAX ? NMAX : l));
-    }
-  }
-  put16(y, dh);
-  put16(y + 2, mh);
-  for (int k = 0; k < 12; ++k) y[4 + k] = s12[k];
-  unsigned char* qh = y + 16;
-  unsigned char* ql = y + (Q5 ? 48 : 16);
-  if (Q5)
-    for (int k = 0; k < 32; ++k) qh[k] = 0;
-  uint8_t m1 = 1, m2 = 2;
-  for (int n = 0; n < 256; n += 64) {
-    for (int j = 0; j < 32; ++j) {
-      int l1 = L[n + j], l2 = L[n + j + 32];
-      if (Q5) {
-        if (l1 > 15) { l1 -= 16; qh[j] |= m1; }
-        if (l2 > 15) { l2 -= 16; qh[j] |= m2; }
-      }
-      ql[j] = (unsigned char)(l1 | (l2 << 4));
-    }
-    m1 <<= 2;
-    m2 <<= 2;
-    ql += 32;
-  }
-}
-
 // make_qx_quants(n, nmax, x, L, rmse_type = 1, qw = NULL): symmetric fit with x^2 weights
-__device__ float make_qx_r1(int n, int nmax, const float* x, int8_t* L) {
+template <int N>
+__device__ float make_qx_r1(int nmax, const float (&x)[N], int8_t (&L)[N]) {
   float mx = 0, amax = 0;
-  for (int i = 0; i < n; ++i) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
     const float ax = fabsf(x[i]);
     if (ax > amax) { amax = ax; mx = x[i]; }
   }
   if (amax < 1e-30f) {
-    for (int i = 0; i < n; ++i) L[i] = 0;
+#pragma unroll
+    for (int i = 0; i < N; ++i) L[i] = 0;
     return 0.f;
   }
   float iscale = -nmax / mx;
   float sumlx = 0, suml2 = 0;
-  for (int i = 0; i < n; ++i) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
     int l = nearest_int(iscale * x[i]);
     l = l < -nmax ? -nmax : (l > nmax - 1 ? nmax - 1 : l);
     L[i] = (int8_t)(l + nmax);
@@ -309,7 +204,8 @@ __device__ float make_qx_r1(int n, int nmax, const float* x, int8_t* L) {
     if (is == 0) continue;
     iscale = -(nmax + 0.1f * is) / mx;
     sumlx = suml2 = 0;
-    for (int i = 0; i < n; ++i) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
       int l = nearest_int(iscale * x[i]);
       l = l < -nmax ? -nmax : (l > nmax - 1 ? nmax - 1 : l);
       const float w = x[i] * x[i];
@@ -317,7 +213,8 @@ __device__ float make_qx_r1(int n, int nmax, const float* x, int8_t* L) {
       suml2 += w * l * l;
     }
     if (suml2 > 0 && sumlx * sumlx > best * suml2) {
-      for (int i = 0; i < n; ++i) {
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
         const int l = nearest_int(iscale * x[i]);
         L[i] = (int8_t)(nmax + (l < -nmax ? -nmax : (l > nmax - 1 ? nmax - 1 : l)));
       }
@@ -328,65 +225,243 @@ __device__ float make_qx_r1(int n, int nmax, const float* x, int8_t* L) {
   return scale;
 }
 
-// q6_K (210 B: ql[128] | qh[64] | scales[16] | d)
-__device__ void quant_q6_K(const float* x, unsigned char* y) {
-  int8_t L[256];
-  float scales[16];
-  float max_scale = 0, max_abs_scale = 0;
-  for (int ib = 0; ib < 16; ++ib) {
-    const float scale = make_qx_r1(16, 32, x + 16 * ib, L + 16 * ib);
-    scales[ib] = scale;
-    const float abs_scale = fabsf(scale);
-    if (abs_scale > max_abs_scale) {
-      max_abs_scale = abs_scale;
-      max_scale = scale;
-    }
-  }
-  if (!max_abs_scale) {
-    for (int k = 0; k < 210; ++k) y[k] = 0;
-    put16(y + 208, f2h(0.f));
-    return;
-  }
-  const float iscale = -128.f / max_scale;
-  const uint16_t dh = f2h(1 / iscale);
-  int8_t sc[16];
-  for (int ib = 0; ib < 16; ++ib) {
-    const int v = nearest_int(iscale * scales[ib]);
-    sc[ib] = (int8_t)(v < 127 ? v : 127);
-  }
-  for (int j = 0; j < 16; ++j) {
-    const float d = hf(dh) * sc[j];
-    if (!d) continue;
-    for (int ii = 0; ii < 16; ++ii) {
-      int l = nearest_int(x[16 * j + ii] / d);
-      l = l < -32 ? -32 : (l > 31 ? 31 : l);
-      L[16 * j + ii] = (int8_t)(l + 32);
-    }
-  }
-  unsigned char* ql = y;
-  unsigned char* qh = y + 128;
-  for (int j = 0; j < 256; j += 128) {
-    for (int l = 0; l < 32; ++l) {
-      const uint8_t a = (uint8_t)L[j + l], b = (uint8_t)L[j + l + 32], c = (uint8_t)L[j + l + 64],
-                    e = (uint8_t)L[j + l + 96];
-      ql[l] = (unsigned char)((a & 0xF) | ((c & 0xF) << 4));
-      ql[l + 32] = (unsigned char)((b & 0xF) | ((e & 0xF) << 4));
-      qh[l] = (unsigned char)((a >> 4) | ((b >> 4) << 2) | ((c >> 4) << 4) | ((e >> 4) << 6));
-    }
-    ql += 64;
-    qh += 32;
-  }
-  for (int k = 0; k < 16; ++k) y[192 + k] = (unsigned char)sc[k];
-  put16(y + 208, dh);
+// ------------------------------------------------------------------ k-quants, one lane per sub-block
+// The reference's k-quant search runs per sub-block (16 of 16 values for q2_K / q6_K, 8 of 32
+// for q4_K / q5_K) and only then combines the sub-blocks' scales, so a super-block maps onto a
+// group of SUB lanes: each lane replays its own sub-block's search in the reference's order
+// (make_qkx2 / make_qx_r1 above, same float arithmetic), the group combines the scales with
+// cross-lane max reductions (order-free: max, and for q6_K the first sub-block of largest
+// |scale|), each lane requantizes its own values, and the packed bits -- which interleave
+// sub-blocks -- are assembled through LDS.  64 / SUB super-blocks per wave.
+template <int T> struct KQ;
+template <> struct KQ<kQ2_K> { static constexpr int SUB = 16, N = 16, BPB = 84; };
+template <> struct KQ<kQ4_K> { static constexpr int SUB = 8, N = 32, BPB = 144; };
+template <> struct KQ<kQ5_K> { static constexpr int SUB = 8, N = 32, BPB = 176; };
+template <> struct KQ<kQ6_K> { static constexpr int SUB = 16, N = 16, BPB = 210; };
+
+template <int SUB>
+__device__ __forceinline__ float group_max(float v) {   // max over the lane's group of SUB lanes
+#pragma unroll
+  for (int o = 1; o < SUB; o <<= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
 }
 
-// one thread per block: block b of row j reads x + j*ldx + b*QK, writes y + j*ldy_bytes + b*BPB
+constexpr int KQ_NT = 256;
+
+template <int T>
+__global__ __launch_bounds__(KQ_NT) void quant_kq_wave(const float* __restrict__ x, int64_t ldx,
+                                                       unsigned char* __restrict__ y, int64_t ldy_bytes, int K, int M) {
+  using Q = KQ<T>;
+  constexpr int SUB = Q::SUB, N = Q::N, SB_PER_WG = KQ_NT / SUB;
+  __shared__ uint8_t Ls[SB_PER_WG][256];
+  const int nb = K / 256;
+  const int t = threadIdx.x, j = t % SUB, gl = t / SUB;   // sub-block, super-block within the WG
+  const int64_t g = (int64_t)blockIdx.x * SB_PER_WG + gl;  // super-block index (row-major)
+  const bool live = g < (int64_t)nb * M;
+  const int64_t row = live ? g / nb : 0, b = live ? g % nb : 0;
+  const float* xs = x + row * ldx + b * 256 + N * j;
+  unsigned char* yb = y + row * ldy_bytes + b * Q::BPB;
+  float xv[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) xv[i] = live ? xs[i] : 0.f;
+  uint8_t L[N];
+  uint8_t* Lg = Ls[gl];
+
+  if constexpr (T == kQ6_K) {
+    int8_t Li[N];
+    const float scale = make_qx_r1<N>(32, xv, Li);
+    // the first sub-block with the largest |scale| gives max_scale (its sign included)
+    float ab = fabsf(scale);
+    int who = j;
+#pragma unroll
+    for (int o = 1; o < SUB; o <<= 1) {
+      const float ab2 = __shfl_xor(ab, o);
+      const int who2 = __shfl_xor(who, o);
+      if (ab2 > ab || (ab2 == ab && who2 < who)) { ab = ab2; who = who2; }
+    }
+    const float max_scale = __shfl(scale, (t & ~(SUB - 1) & 63) + who);
+    if (ab == 0.f) {   // !max_abs_scale: the whole super-block is zero, d = +0
+      if (live) {
+        for (int k = j; k < 210; k += SUB) yb[k] = 0;
+        if (j == 0) put16(yb + 208, f2h(0.f));
+      }
+      return;
+    }
+    const float iscale = -128.f / max_scale;
+    const uint16_t dh = f2h(1 / iscale);
+    const int v = nearest_int(iscale * scale);
+    const int8_t sc = (int8_t)(v < 127 ? v : 127);
+    const float d = hf(dh) * sc;
+#pragma unroll
+    for (int ii = 0; ii < N; ++ii) {
+      if (d) {
+        int l = nearest_int(xv[ii] / d);
+        l = l < -32 ? -32 : (l > 31 ? 31 : l);
+        L[ii] = (uint8_t)(l + 32);
+      } else {
+        L[ii] = (uint8_t)Li[ii];
+      }
+    }
+#pragma unroll
+    for (int ii = 0; ii < N; ++ii) Lg[N * j + ii] = L[ii];
+    __syncthreads();
+    if (!live) return;
+    yb[192 + j] = (unsigned char)sc;
+    if (j == 0) put16(yb + 208, dh);
+    // ql[128] | qh[64]: 12 bytes per lane
+    for (int k = j; k < 192; k += SUB) {
+      if (k < 128) {   // ql[64 * h + l] (h: 128-value half, l < 64)
+        const int h = k / 64, l = k % 64, base = 128 * h;
+        const int lo = l < 32 ? base + l : base + l;   // a (l < 32) or b (l >= 32, = L[base + (l-32) + 32])
+        yb[k] = (unsigned char)((Lg[lo] & 0xF) | ((Lg[lo + 64] & 0xF) << 4));
+      } else {
+        const int q = k - 128, h = q / 32, l = q % 32, base = 128 * h;
+        yb[k] = (unsigned char)((Lg[base + l] >> 4) | ((Lg[base + l + 32] >> 4) << 2) | ((Lg[base + l + 64] >> 4) << 4) |
+                                ((Lg[base + l + 96] >> 4) << 6));
+      }
+    }
+  } else {
+    float w[N];
+    float sc_, mn_;
+    if constexpr (T == kQ2_K) {
+#pragma unroll
+      for (int l = 0; l < N; ++l) w[l] = fabsf(xv[l]);
+      sc_ = make_qkx2<N>(3, xv, w, L, &mn_, -0.5f, 0.1f, 15, true);
+    } else {
+      constexpr bool Q5 = T == kQ5_K;
+      float sum_x2 = 0;
+      for (int l = 0; l < 32; ++l) sum_x2 += xv[l] * xv[l];
+      const float av_x = sqrtf(sum_x2 / 32);
+#pragma unroll
+      for (int l = 0; l < 32; ++l) w[l] = av_x + fabsf(xv[l]);
+      sc_ = make_qkx2<N>(Q5 ? 31 : 15, xv, w, L, &mn_, Q5 ? -0.5f : -1.f, 0.1f, Q5 ? 15 : 20, false);
+    }
+    // max_scale / max_min start at 0 in the reference: max with 0
+    // (+0 for non-positive values: fmaxf(-0, +0) may be -0, which would change f16(max / 63))
+    const float max_scale = group_max<SUB>(sc_ > 0.f ? sc_ : 0.f), max_min = group_max<SUB>(mn_ > 0.f ? mn_ : 0.f);
+    if constexpr (T == kQ2_K) {
+      uint8_t scb = 0;
+      uint16_t dh, mh;
+      if (max_scale > 0) {
+        const float iscale = 15.f / max_scale;
+        scb = (uint8_t)nearest_int(iscale * sc_);
+        dh = f2h(max_scale / 15.f);
+      } else {
+        dh = f2h(0.f);
+      }
+      if (max_min > 0) {
+        const float iscale = 15.f / max_min;
+        scb |= (uint8_t)(nearest_int(iscale * mn_) << 4);
+        mh = f2h(max_min / 15.f);
+      } else {
+        mh = f2h(0.f);
+      }
+      const float d = hf(dh) * (scb & 0xF);
+      if (d) {
+        const float dm = hf(mh) * (scb >> 4);
+#pragma unroll
+        for (int ii = 0; ii < N; ++ii) {
+          const int l = nearest_int((xv[ii] + dm) / d);
+          L[ii] = (uint8_t)(l < 0 ? 0 : (l > 3 ? 3 : l));
+        }
+      }
+#pragma unroll
+      for (int ii = 0; ii < N; ++ii) Lg[N * j + ii] = L[ii];
+      __syncthreads();
+      if (!live) return;
+      yb[j] = scb;
+      if (j == 0) {
+        put16(yb + 80, dh);
+        put16(yb + 82, mh);
+      }
+      for (int k = j; k < 64; k += SUB) {   // qs[64]: 4 bytes per lane
+        const int h = k / 32, l = k % 32, base = 128 * h;
+        yb[16 + k] = (unsigned char)(Lg[base + l] | (Lg[base + l + 32] << 2) | (Lg[base + l + 64] << 4) |
+                                     (Lg[base + l + 96] << 6));
+      }
+    } else {
+      constexpr bool Q5 = T == kQ5_K;
+      constexpr int NMAX = Q5 ? 31 : 15;
+      const float inv_scale = max_scale > 0 ? 63.f / max_scale : 0.f;
+      const float inv_min = max_min > 0 ? 63.f / max_min : 0.f;
+      uint8_t ls = (uint8_t)nearest_int(inv_scale * sc_);
+      uint8_t lm = (uint8_t)nearest_int(inv_min * mn_);
+      ls = ls < 63 ? ls : 63;
+      lm = lm < 63 ? lm : 63;
+      const uint16_t dh = f2h(max_scale / 63.f), mh = f2h(max_min / 63.f);
+      // get_scale_min_k4 of the packed scales gives back ls / lm exactly (6-bit values)
+      const float d = hf(dh) * ls;
+      if (d) {
+        const float dm = hf(mh) * lm;
+#pragma unroll
+        for (int ii = 0; ii < N; ++ii) {
+          const int l = nearest_int((xv[ii] + dm) / d);
+          L[ii] = (uint8_t)(l < 0 ? 0 : (l > NMAX ? NMAX : l));
+        }
+      }
+#pragma unroll
+      for (int ii = 0; ii < N; ++ii) Lg[N * j + ii] = L[ii];
+      // the 12 scale bytes: every lane's (ls, lm) to the group's first lane
+      uint8_t lsv[8], lmv[8];
+      const int base_lane = t & 63 & ~(SUB - 1);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        lsv[k] = (uint8_t)__shfl((int)ls, base_lane + k);
+        lmv[k] = (uint8_t)__shfl((int)lm, base_lane + k);
+      }
+      __syncthreads();
+      if (!live) return;
+      if (j == 0) {
+        uint8_t s12[12];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          if (k < 4) {
+            s12[k] = lsv[k];
+            s12[k + 4] = lmv[k];
+          } else {
+            s12[k + 4] = (uint8_t)((lsv[k] & 0xF) | ((lmv[k] & 0xF) << 4));
+            s12[k - 4] |= (uint8_t)((lsv[k] >> 4) << 6);
+            s12[k] |= (uint8_t)((lmv[k] >> 4) << 6);
+          }
+        }
+        put16(yb, dh);
+        put16(yb + 2, mh);
+#pragma unroll
+        for (int k = 0; k < 12; ++k) yb[4 + k] = s12[k];
+      }
+      unsigned char* qh = yb + 16;
+      unsigned char* ql = yb + (Q5 ? 48 : 16);
+      for (int k = j; k < 128; k += SUB) {   // ql[128]: 16 bytes per lane
+        const int n = 64 * (k / 32), jj = k % 32;
+        int l1 = Lg[n + jj], l2 = Lg[n + jj + 32];
+        if (Q5) {
+          l1 &= 15;
+          l2 &= 15;
+        }
+        ql[k] = (unsigned char)(l1 | (l2 << 4));
+      }
+      if constexpr (Q5) {
+        for (int k = j; k < 32; k += SUB) {   // qh[32]: bit 2i / 2i+1 = the 5th bit of chunk i's two halves
+          uint8_t h = 0;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            if (Lg[64 * i + k] > 15) h |= (uint8_t)(1u << (2 * i));
+            if (Lg[64 * i + k + 32] > 15) h |= (uint8_t)(2u << (2 * i));
+          }
+          qh[k] = h;
+        }
+      }
+    }
+  }
+}
+
+// 32-element formats, one thread per block: block b of row j reads x + j*ldx + b*32, writes
+// y + j*ldy_bytes + b*BPB
 template <int T>
 __global__ __launch_bounds__(64) void quant_w(const float* __restrict__ x, int64_t ldx, unsigned char* __restrict__ y,
                                               int64_t ldy_bytes, int K, int M) {
-  constexpr int QK = T == kQ2_K || T == kQ4_K || T == kQ5_K || T == kQ6_K ? 256 : 32;
-  constexpr int BPB = T == kQ4_0 ? 18 : T == kQ4_1 ? 20 : T == kQ5_0 ? 22 : T == kQ5_1 ? 24 : T == kQ2_K ? 84
-                    : T == kQ4_K ? 144 : T == kQ5_K ? 176 : 210;
+  constexpr int QK = 32;
+  constexpr int BPB = T == kQ4_0 ? 18 : T == kQ4_1 ? 20 : T == kQ5_0 ? 22 : 24;
   const int nb = K / QK;
   const int64_t g = (int64_t)blockIdx.x * 64 + threadIdx.x;
   if (g >= (int64_t)nb * M) return;
@@ -396,11 +471,7 @@ __global__ __launch_bounds__(64) void quant_w(const float* __restrict__ x, int64
   if constexpr (T == kQ4_0) quant_sym<4>(xb, yb);
   else if constexpr (T == kQ5_0) quant_sym<5>(xb, yb);
   else if constexpr (T == kQ4_1) quant_affine<4>(xb, yb);
-  else if constexpr (T == kQ5_1) quant_affine<5>(xb, yb);
-  else if constexpr (T == kQ2_K) quant_q2_K(xb, yb);
-  else if constexpr (T == kQ4_K) quant_q45_K<false>(xb, yb);
-  else if constexpr (T == kQ5_K) quant_q45_K<true>(xb, yb);
-  else quant_q6_K(xb, yb);
+  else quant_affine<5>(xb, yb);
 }
 
 }  // namespace
@@ -416,15 +487,21 @@ hipError_t launch_quantize_weights(int type, const float* x, int64_t ldx, void* 
   const int64_t n = (int64_t)(K / block_elems(type)) * M;
   if (n == 0) return hipSuccess;
   const dim3 grid((unsigned)((n + 63) / 64)), blk(64);
+  // k-quants: one lane per sub-block, KQ_NT / SUB super-blocks per workgroup
+  auto kq = [&](auto kern, int sub) {
+    const int per = KQ_NT / sub;
+    hipLaunchKernelGGL(kern, dim3((unsigned)((n + per - 1) / per)), dim3(KQ_NT), 0, s, x, ldx, yb, ldy_bytes, K, M);
+    return hipGetLastError();
+  };
   switch (type) {
     case kQ4_0: hipLaunchKernelGGL(quant_w<kQ4_0>, grid, blk, 0, s, x, ldx, yb, ldy_bytes, K, M); break;
     case kQ4_1: hipLaunchKernelGGL(quant_w<kQ4_1>, grid, blk, 0, s, x, ldx, yb, ldy_bytes, K, M); break;
     case kQ5_0: hipLaunchKernelGGL(quant_w<kQ5_0>, grid, blk, 0, s, x, ldx, yb, ldy_bytes, K, M); break;
     case kQ5_1: hipLaunchKernelGGL(quant_w<kQ5_1>, grid, blk, 0, s, x, ldx, yb, ldy_bytes, K, M); break;
-    case kQ2_K: hipLaunchKernelGGL(quant_w<kQ2_K>, grid, blk, 0, s, x, ldx, yb, ldy_bytes, K, M); break;
-    case kQ4_K: hipLaunchKernelGGL(quant_w<kQ4_K>, grid, blk, 0, s, x, ldx, yb, ldy_bytes, K, M); break;
-    case kQ5_K: hipLaunchKernelGGL(quant_w<kQ5_K>, grid, blk, 0, s, x, ldx, yb, ldy_bytes, K, M); break;
-    case kQ6_K: hipLaunchKernelGGL(quant_w<kQ6_K>, grid, blk, 0, s, x, ldx, yb, ldy_bytes, K, M); break;
+    case kQ2_K: return kq(quant_kq_wave<kQ2_K>, KQ<kQ2_K>::SUB);
+    case kQ4_K: return kq(quant_kq_wave<kQ4_K>, KQ<kQ4_K>::SUB);
+    case kQ5_K: return kq(quant_kq_wave<kQ5_K>, KQ<kQ5_K>::SUB);
+    case kQ6_K: return kq(quant_kq_wave<kQ6_K>, KQ<kQ6_K>::SUB);
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

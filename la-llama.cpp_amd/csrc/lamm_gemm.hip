@@ -24,6 +24,7 @@
 // v_mfma_f32_32x32x16_f16 (K = 16 sub-blocks, exact).
 #include "lamm_device.h"
 #include "lamm_kernels.h"
+#include "lamm_rowdot.h"
 
 namespace lamm {
 namespace {
@@ -122,7 +123,10 @@ struct PrepLayout {
   }
 };
 
-template <int VBPB>   // 34 = q8_0, 36 = q8_1
+// VBPB: 34 = q8_0, 36 = q8_1.  BF32: B holds F32 rows (ldb bytes apart), quantized here the way
+// ggml's INIT does on x86 (AVX2 from_float; the bits of lamm_hip_quantize(.., 1, ..)) -- the
+// activation quantizer fused into this engine's prologue
+template <int VBPB, bool BF32>
 __global__ __launch_bounds__(256) void prep_act_kernel(GemvArgs p, unsigned char* ws) {
   const PrepLayout L = PrepLayout::of(p);
   const int z = blockIdx.y, i12 = z % p.ne12, i13 = z / p.ne12;
@@ -138,10 +142,24 @@ __global__ __launch_bounds__(256) void prep_act_kernel(GemvArgs p, unsigned char
   // every buffer load into a waterfall loop) and offsets < 2^31 for any slice size
   const int64_t jw = ((int64_t)blockIdx.x * 256) / nb_pad;
   const int64_t jl = min((int64_t)p.N - 1, ((int64_t)blockIdx.x * 256 + 255) / nb_pad);
-  const int64_t bbytes = (jl - jw) * p.ldb + (int64_t)p.nblk * VBPB;
+  const int64_t bbytes = (jl - jw) * p.ldb + (int64_t)p.nblk * (BF32 ? 128 : VBPB);
   const auto rs = make_rsrc(Bz + jw * p.ldb, (uint32_t)min((bbytes + 3) & ~int64_t(3), (int64_t)0x7fffffff));
   constexpr int VQS = VBPB == 36 ? 4 : 2;
   const bool ok = b < p.nblk;
+  const int ks = b / KBLK, bb = b % KBLK;
+  const int64_t si = ((int64_t)ks * p.N + j) * KBLK + bb;
+  if constexpr (BF32) {
+    uint32_t x[32], q8[8];
+    uint16_t dh = 0, sh = 0;
+    load_words<32, 0>(rs, ok ? (uint32_t)((j - jw) * p.ldb + (int64_t)b * 128) : 0xfffffff0u, x);
+    q8_from_f32<VBPB == 36>(x, q8, dh, sh);   // a padding block reads zeros: d = 0, quants 0
+    u32x4* dst = (u32x4*)(act + (int64_t)j * L.kpad + 32 * b);
+    dst[0] = u32x4{q8[0], q8[1], q8[2], q8[3]};
+    dst[1] = u32x4{q8[4], q8[5], q8[6], q8[7]};
+    d8[si] = uint2{ok ? (uint32_t)dh : 0u, 0u};
+    if constexpr (VBPB == 36) ssc[si] = __builtin_bit_cast(_Float16, (uint16_t)(ok ? sh : 0));
+    return;
+  }
   const uint32_t off = ok ? (uint32_t)((j - jw) * p.ldb + (int64_t)b * VBPB) : 0xfffffff0u;
   const uint32_t base = off & ~3u;
   const int sh = (int)(off & 3u);
@@ -155,8 +173,6 @@ __global__ __launch_bounds__(256) void prep_act_kernel(GemvArgs p, unsigned char
   dst[0] = ok ? u32x4{get32<VQS>(m), get32<VQS + 4>(m), get32<VQS + 8>(m), get32<VQS + 12>(m)} : u32x4{0, 0, 0, 0};
   dst[1] = ok ? u32x4{get32<VQS + 16>(m), get32<VQS + 20>(m), get32<VQS + 24>(m), get32<VQS + 28>(m)}
               : u32x4{0, 0, 0, 0};
-  const int ks = b / KBLK, bb = b % KBLK;
-  const int64_t si = ((int64_t)ks * p.N + j) * KBLK + bb;
   d8[si] = uint2{ok ? (m[0] & 0xffffu) : 0u, 0u};
   if constexpr (VBPB == 36) ssc[si] = __builtin_bit_cast(_Float16, (uint16_t)(ok ? (m[0] >> 16) : 0));
 }
@@ -555,9 +571,13 @@ hipError_t launch_v3(const GemvArgs& p, void* ws, hipStream_t s) {
   const PrepLayout L = PrepLayout::of(p);
   const int64_t items = (int64_t)p.N * L.nsteps * KBLK;
   const char* sp = getenv("LAMM_GEMM_SKIP_PREP");   // measurement only (bench.py): reuse the prep
-  if (!(sp && sp[0] == '1'))
-    hipLaunchKernelGGL((prep_act_kernel<VBPB>), dim3((unsigned)((items + 255) / 256), p.ne12 * p.ne13), dim3(256), 0,
-                       s, p, static_cast<unsigned char*>(ws));
+  if (!(sp && sp[0] == '1')) {
+    const dim3 g((unsigned)((items + 255) / 256), p.ne12 * p.ne13);
+    if (p.b_f32)
+      hipLaunchKernelGGL((prep_act_kernel<VBPB, true>), g, dim3(256), 0, s, p, static_cast<unsigned char*>(ws));
+    else
+      hipLaunchKernelGGL((prep_act_kernel<VBPB, false>), g, dim3(256), 0, s, p, static_cast<unsigned char*>(ws));
+  }
   constexpr int NB = 2;
   const int nsplit = i8_nsplit(p);
   float* part = reinterpret_cast<float*>(static_cast<unsigned char*>(ws) + i8_part_offset(p));

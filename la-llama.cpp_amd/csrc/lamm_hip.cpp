@@ -99,13 +99,11 @@ struct WsBuf {
 std::mutex g_ws_mu;
 std::unordered_map<WsKey, WsBuf, WsKeyHash> g_ws;
 
-std::unordered_map<WsKey, WsBuf, WsKeyHash> g_ws_act;   // activations quantized for a GEMM (F32 B)
-
-void* workspace(size_t bytes, hipStream_t s, bool act = false) {
+void* workspace(size_t bytes, hipStream_t s) {
   int dev = 0;
   (void)hipGetDevice(&dev);
   std::lock_guard<std::mutex> lock(g_ws_mu);
-  WsBuf& b = (act ? g_ws_act : g_ws)[WsKey{dev, s}];
+  WsBuf& b = g_ws[WsKey{dev, s}];
   if (b.ptr && b.bytes >= bytes) return b.ptr;
   if (b.ptr) {
     (void)hipStreamSynchronize(s);
@@ -199,9 +197,8 @@ int matmul_impl(const lamm_matrix* A, const lamm_matrix* B, const lamm_matrix* C
   if (!A || !B || !C) return fail(LAMM_ERR_SHAPE, "null matrix");
   if (!is_weight_type(A->type)) return fail(LAMM_ERR_TYPE, "unsupported A type %d", A->type);
   // F32 activations for a q8_0 / q8_1 weight type: ggml's INIT quantization (AVX2 flavour) runs
-  // on the device, bit-exact with lamm_hip_quantize(.., 1, ..) + matmul -- inside the GEMV
-  // launch (N <= 8, stage_b_f32), inside the fp6 GEMM's activation prep (prep_b_fp6), or as a
-  // quantizer launch in front of the other GEMM engines
+  // on the device inside the kernels that read B, bit-exact with lamm_hip_quantize(.., 1, ..) +
+  // matmul -- the GEMV's staging (N <= 8), the fp6 / i8 GEMMs' activation prep (N > 8)
   const int vdt = vec_dot_type(A->type);
   const bool b_f32 = B->type == kF32 && (vdt == kQ8_0 || vdt == kQ8_1);
   if (B->type != vdt && !b_f32)
@@ -247,26 +244,6 @@ int matmul_impl(const lamm_matrix* A, const lamm_matrix* B, const lamm_matrix* C
   p.sc3 = (int64_t)(bt.nbc3 / 4);
   p.b_f32 = b_f32 ? 1 : 0;
   hipError_t e;
-  if (b_f32 && N > 8 && !(gemm_fp6_supported(A->type) && gemm_path(p, W && W->packed) == 0)) {
-    if (((uintptr_t)B->data & 15) || (ldb & 15) || (p.sb2 & 15) || (p.sb3 & 15))
-      return fail(LAMM_ERR_ALIGN, "f32 B rows of a GEMM must be 16-byte aligned");
-    // no F32 staging in this engine: quantize the rows (every slice) into a buffer of its own
-    const int64_t qrow = (int64_t)Kb * (int64_t)block_bytes(vdt), qslice = qrow * N;
-    const int64_t slices = (int64_t)p.ne12 * p.ne13;
-    auto* q = static_cast<unsigned char*>(workspace((size_t)(qslice * slices) + 256, s, true));
-    if (!q) return fail(LAMM_ERR_HIP, "activation buffer of %lld bytes", (long long)(qslice * slices));
-    for (int64_t z = 0; z < slices; ++z) {
-      const int64_t i12 = z % p.ne12, i13 = z / p.ne12;
-      const float* x = reinterpret_cast<const float*>(p.B + i12 * p.sb2 + i13 * p.sb3);
-      e = launch_quantize(vdt, 1, x, ldb / 4, q + z * qslice, qrow, p.K, N, s);
-      if (e != hipSuccess) return fail(LAMM_ERR_HIP, "activation quantizer: %s", hipGetErrorString(e));
-    }
-    p.B = q;
-    p.ldb = qrow;
-    p.sb2 = qslice;
-    p.sb3 = qslice * p.ne12;
-    p.b_f32 = 0;
-  }
   if (N <= gemv_max_n(A->type) || (b_f32 && N <= 8)) {
     e = launch_gemv(A->type, p, s);
   } else if (gemm_dense_supported(A->type) && !getenv_flag0("LAMM_DENSE_GEMM")) {
@@ -998,8 +975,8 @@ extern "C" void lamm_mul_mat(const struct ggml_compute_params* vparams, struct g
                                   (size_t)ne00 * sizeof(float), (size_t)N, hipMemcpyHostToDevice, s));
         }
       dB = dX;
-      // q8_0 / q8_1 activations are quantized by the library inside the GEMM's own activation
-      // prep (fp6 engine) or in front of it; q8_K / f16 ones here
+      // q8_0 / q8_1 activations are quantized by the library inside the kernels that read them;
+      // q8_K / f16 ones here
       if (act == kGpuQuant && vdt != kQ8_0 && vdt != kQ8_1) {
         void* dq = d.scratch(0, b_row * (size_t)(N * nslices) + 64);
         const int qrc = lamm_hip_quantize(vdt, /*AVX2 flavour*/ 1, dX, ldx, dq, kb, (int)ne00, (int)(N * nslices), s);

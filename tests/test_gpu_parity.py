@@ -682,9 +682,9 @@ GEMM_F32_CASES = [(ol.Q4_0, "fp6"), (ol.Q4_0, "i8"), (ol.Q4_1, "fp6"), (ol.Q4_1,
 @pytest.mark.parametrize("t,path", GEMM_F32_CASES, ids=[f"{ol.NAMES[t]}-{p}" for t, p in GEMM_F32_CASES])
 @pytest.mark.parametrize("N", [9, 140])
 def test_gemm_f32_activations(t, path, N, monkeypatch):
-    """F32 B for N > 8 (ggml's INIT quantization on the device): quantized inside the fp6
-    engine's activation prep, or by a quantizer launch in front of the i8 engine -- C must be
-    BIT-identical to lamm_hip_quantize(flavour 1) + matmul either way, and match the oracle."""
+    """F32 B for N > 8 (ggml's INIT quantization on the device): quantized inside the fp6 and
+    i8 engines' activation preps -- C must be BIT-identical to lamm_hip_quantize(flavour 1) +
+    matmul either way, and match the oracle."""
     if path != "default":
         monkeypatch.setenv("LAMM_GEMM_PATH", path)
     M, K = 300, 4096 + 64
@@ -692,7 +692,7 @@ def test_gemm_f32_activations(t, path, N, monkeypatch):
     A_q = ORACLE.quantize(t, rng.standard_normal((M, K), dtype=np.float32))
     x = rng.standard_normal((N, K), dtype=np.float32)
     x[1, 64:96] = 0.0                                  # an all-zero block (d = 0)
-    ldx = K + 4
+    ldx = K + 4 if N > 100 else K + 1                  # NaN-padded rows; odd pitch: 4-byte aligned only
     xp = np.full((N, ldx), np.nan, np.float32)
     xp[:, :K] = x
     kb = K // 32
@@ -705,7 +705,7 @@ def test_gemm_f32_activations(t, path, N, monkeypatch):
               la.Matrix(c1.data_ptr(), la.F32, M, N, M), s)
     vt = ORACLE.vec_dot_type(t)
     dq = torch.zeros(N * la.row_bytes(vt, K) + 64, dtype=torch.uint8, device="cuda")
-    la.quantize_torch(vt, dx.view(N, ldx)[:, :K], dq, flavour=1)
+    la.quantize_torch(vt, dx.view(N, ldx)[:, :K].contiguous(), dq, flavour=1)   # the quantizer wants 16-byte rows
     c2 = torch.full((N * M,), np.nan, dtype=torch.float32, device="cuda")
     la.matmul(la.Matrix(dA.data_ptr(), t, M, kb, lda), la.Matrix(dq.data_ptr(), vt, kb, N, kb),
               la.Matrix(c2.data_ptr(), la.F32, M, N, M), s)
@@ -715,18 +715,6 @@ def test_gemm_f32_activations(t, path, N, monkeypatch):
     B_q = ORACLE.quantize(vt, x, ol.QUANT_AVX)
     ref = ORACLE.mul_mat(t, M, N, K, A_q, B_q)
     assert rel_err(a.reshape(N, M), ref, absdot(t, A_q, B_q, M, N, K)).max() < TOL
-
-
-def test_gemm_f32_activations_alignment(monkeypatch):
-    """The quantizer in front of the i8 engine reads 16-byte rows: other F32 pitches are refused."""
-    monkeypatch.setenv("LAMM_GEMM_PATH", "i8")
-    t, M, K, N = ol.Q4_0, 64, 256, 9
-    dA = torch.zeros(M * (K // 32) * 18 + 64, dtype=torch.uint8, device="cuda")
-    dx = torch.zeros(N * (K + 1), dtype=torch.float32, device="cuda")
-    c = torch.zeros(N * M, dtype=torch.float32, device="cuda")
-    with pytest.raises(la.LammError):
-        la.matmul(la.Matrix(dA.data_ptr(), t, M, K // 32, K // 32), la.Matrix(dx.data_ptr(), la.F32, K, N, K + 1),
-                  la.Matrix(c.data_ptr(), la.F32, M, N, M), 0)
 
 
 # ---------------------------------------------------------------- BASELINE config 3, full size

@@ -29,7 +29,8 @@
 // ms): each GEMV grid wants every CU (one 149 KiB-LDS workgroup per CU), so concurrent
 // branches only contend; batching (--batch-proj) is the way to share the launch cost.
 // Single-token decode steps (N = 1) hand the F32 activations of q8_0/q8_1-typed weights straight to the
-// GEMV, which quantizes them while staging (bit-exact with the separate quantizer);
+// GEMV, which quantizes them while staging (bit-exact with the separate quantizer), and prefill
+// steps (N > 8) to the GEMMs, which quantize them in their activation prep;
 // --unfused runs the separate lamm_hip_quantize launches instead.
 #include <hip/hip_runtime.h>
 
@@ -144,9 +145,10 @@ bool g_fused = true;   // decode (N <= 8): F32 activations straight into the GEM
 
 bool fused(int wtype, int N) {
   const int vt = lamm_vec_dot_type(wtype);
-  // one column only: with 8 columns every workgroup re-quantizes 8 rows before its first
-  // dot and the step gets slower (3.87 -> 4.66 ms at N = 8; N = 1: 2.05 -> 1.89 ms)
-  return g_fused && N == 1 && (vt == 8 || vt == 9);
+  // GEMV: one column only -- with 8 columns every workgroup re-quantizes 8 rows before its
+  // first dot and the step gets slower (3.87 -> 4.66 ms at N = 8; N = 1: 2.05 -> 1.89 ms).
+  // GEMM (N > 8): the engines quantize F32 rows inside their activation prep, one pass fewer.
+  return g_fused && (N == 1 || N > 8) && (vt == 8 || vt == 9);
 }
 
 void quantize(int wtype, Act& a, int N, hipStream_t s) {

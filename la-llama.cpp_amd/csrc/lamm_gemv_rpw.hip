@@ -24,7 +24,7 @@ namespace {
 // One wave per row: the row's loads for ITER blocks per lane (K <= ITER * 2048) go out at once;
 // each wave also issues its NEXT row's loads before computing the current one (rows strided by
 // the grid), so a persistent grid keeps HBM busy across rows.
-template <int T, int NC, int WAVES, bool BF32, int ITER>
+template <int T, int NC, int WAVES, bool BF32, int ITER, bool LB>
 __global__ __launch_bounds__(64 * WAVES) void gemv_rpw_kernel(GemvArgs p) {
   using F = RFmt<T>;
   constexpr int NWA = (F::BPB + 3) / 4 + 1;     // A dwords per block incl. realignment slack
@@ -54,6 +54,13 @@ __global__ __launch_bounds__(64 * WAVES) void gemv_rpw_kernel(GemvArgs p) {
       load_words<NWA, 2>(ra, off, wa[it]);   // non-temporal: A is read once
     }
   };
+  // LANEB (q8 activations, one column, K <= 4096): each lane holds the two activation blocks its
+  // own weight blocks meet, loaded straight from L2 -- no LDS staging, no workgroup barrier
+  // (profiles/r02/rpw_probe.txt: the staging + barrier cost 0.36 us of a 3.6 us launch, per-lane
+  // loads 0.2).  Same bytes, same block arithmetic: C is bit-identical either way.
+  constexpr bool LANEB = LB && !BF32 && NC == 1 && ITER == 2;
+  uint32_t lq[ITER][8];
+  float ld[ITER], ls[ITER];
   auto compute = [&](int64_t row, const uint32_t (&wa)[ITER][NWA]) {
     float acc[NC];
 #pragma unroll
@@ -69,15 +76,26 @@ __global__ __launch_bounds__(64 * WAVES) void gemv_rpw_kernel(GemvArgs p) {
         unpack_a<T>(m, q, da, ma);
 #pragma unroll
         for (int j = 0; j < NC; ++j) {
-          const u32x4 b0 = sq0[j * nb + b], b1 = sq1[j * nb + b];
+          u32x4 b0, b1;
+          float db, bsv;
+          if constexpr (LANEB) {
+            b0 = u32x4{lq[it][0], lq[it][1], lq[it][2], lq[it][3]};
+            b1 = u32x4{lq[it][4], lq[it][5], lq[it][6], lq[it][7]};
+            db = ld[it];
+            bsv = ls[it];
+          } else {
+            b0 = sq0[j * nb + b];
+            b1 = sq1[j * nb + b];
+            db = sbd[j * nb + b];
+            bsv = sbs[j * nb + b];
+          }
           int s = 0;
           s = dot4(q[0], b0[0], s); s = dot4(q[1], b0[1], s); s = dot4(q[2], b0[2], s); s = dot4(q[3], b0[3], s);
           s = dot4(q[4], b1[0], s); s = dot4(q[5], b1[1], s); s = dot4(q[6], b1[2], s); s = dot4(q[7], b1[3], s);
-          const float db = sbd[j * nb + b];
-          if constexpr (T == kQ4_0) s -= 8 * __builtin_bit_cast(int, sbs[j * nb + b]);
-          if constexpr (T == kQ5_0) s -= 16 * __builtin_bit_cast(int, sbs[j * nb + b]);
+          if constexpr (T == kQ4_0) s -= 8 * __builtin_bit_cast(int, bsv);
+          if constexpr (T == kQ5_0) s -= 16 * __builtin_bit_cast(int, bsv);
           if constexpr (T == kQ4_1 || T == kQ5_1)
-            acc[j] = __builtin_fmaf(da * db, (float)s, __builtin_fmaf(ma, sbs[j * nb + b], acc[j]));
+            acc[j] = __builtin_fmaf(da * db, (float)s, __builtin_fmaf(ma, bsv, acc[j]));
           else
             acc[j] = __builtin_fmaf(da * db, (float)s, acc[j]);
         }
@@ -98,18 +116,29 @@ __global__ __launch_bounds__(64 * WAVES) void gemv_rpw_kernel(GemvArgs p) {
   const int nact = NC * nb;
   ActStage<T, BF32> st;
   const int t0 = threadIdx.x;
-  // straight-line (no branch between them), so the activation loads stay ahead of the row's
-  // HBM stream and waiting for them does not wait for A; out-of-range loads read zeros
-  st.template load<NC>(p, rb, t0);
-  __builtin_amdgcn_sched_barrier(0);   // keep the activation loads first in the vmcnt order
-  issue(row < p.M ? row : 0, wa0);
-  __builtin_amdgcn_sched_barrier(0);
-  if (t0 < nact) st.store(t0, sq0, sq1, sbd, sbs);
-  for (int it = t0 + blockDim.x; it < nact; it += blockDim.x) {
-    st.template load<NC>(p, rb, it);
-    st.store(it, sq0, sq1, sbd, sbs);
+  if constexpr (LANEB) {
+    ActStage<T, BF32> st1;
+    st.template load<NC>(p, rb, lane);        // this lane's activation blocks lane, lane + 64
+    st1.template load<NC>(p, rb, lane + 64);
+    __builtin_amdgcn_sched_barrier(0);   // ahead of the row's HBM stream in the vmcnt order
+    issue(row < p.M ? row : 0, wa0);
+    __builtin_amdgcn_sched_barrier(0);
+    st.decode(lq[0], ld[0], ls[0]);
+    st1.decode(lq[1], ld[1], ls[1]);
+  } else {
+    // straight-line (no branch between them), so the activation loads stay ahead of the row's
+    // HBM stream and waiting for them does not wait for A; out-of-range loads read zeros
+    st.template load<NC>(p, rb, t0);
+    __builtin_amdgcn_sched_barrier(0);   // keep the activation loads first in the vmcnt order
+    issue(row < p.M ? row : 0, wa0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (t0 < nact) st.store(t0, sq0, sq1, sbd, sbs);
+    for (int it = t0 + blockDim.x; it < nact; it += blockDim.x) {
+      st.template load<NC>(p, rb, it);
+      st.store(it, sq0, sq1, sbd, sbs);
+    }
+    __syncthreads();
   }
-  __syncthreads();
   while (row < p.M) {
     int64_t next = row + stride;
     if (next < p.M) issue(next, wa1);
@@ -125,14 +154,21 @@ __global__ __launch_bounds__(64 * WAVES) void gemv_rpw_kernel(GemvArgs p) {
 
 template <int T, int NC, int WAVES, bool BF32, int ITER>
 hipError_t launch_rpw_k(const GemvArgs& p, hipStream_t s) {
-  const size_t lds = (size_t)NC * p.nblk * 40;
+  // LAMM_GEMV_LANEB=1: per-lane activation blocks for q8 single-column calls (A/B)
+  const char* lb = getenv("LAMM_GEMV_LANEB");
+  const bool laneb = !BF32 && NC == 1 && ITER == 2 && lb && lb[0] == '1';
+  const size_t lds = laneb ? 0 : (size_t)NC * p.nblk * 40;
   const int slices = p.ne12 * p.ne13;
   const int gmax = (p.M + WAVES - 1) / WAVES;
   // one round of workgroups over the chip: ~2 per CU in total across the slices
   int gx = (512 + slices - 1) / slices;
   gx = gx < 1 ? 1 : (gx > gmax ? gmax : gx);
   if (lds > 64 * 1024) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((gemv_rpw_kernel<T, NC, WAVES, BF32, ITER>), dim3(gx, slices), dim3(64 * WAVES), lds, s, p);
+  if (laneb)
+    hipLaunchKernelGGL((gemv_rpw_kernel<T, NC, WAVES, BF32, ITER, true>), dim3(gx, slices), dim3(64 * WAVES), lds, s, p);
+  else
+    hipLaunchKernelGGL((gemv_rpw_kernel<T, NC, WAVES, BF32, ITER, false>), dim3(gx, slices), dim3(64 * WAVES), lds, s,
+                       p);
   return hipGetLastError();
 }
 

@@ -142,7 +142,18 @@ struct ActStage {
 
   __device__ __forceinline__ void store(int it, u32x4* q0, u32x4* q1, float* bd, float* bs) const {
     uint32_t q[8];
-    float d = 0.f, sx = 0.f;
+    float d, sx;
+    decode(q, d, sx);
+    q0[it] = u32x4{q[0], q[1], q[2], q[3]};
+    q1[it] = u32x4{q[4], q[5], q[6], q[7]};
+    bd[it] = d;
+    bs[it] = sx;
+  }
+
+  // the block as the dot needs it: 8 quads, d, and s (q8_1) or the bit pattern of sum b (q4_0 / q5_0)
+  __device__ __forceinline__ void decode(uint32_t (&q)[8], float& d, float& sx) const {
+    d = 0.f;
+    sx = 0.f;
     if constexpr (BF32) {
       uint16_t dh, sh;
       q8_from_f32<F::VBPB == 36>(w, q, dh, sh);
@@ -162,10 +173,6 @@ struct ActStage {
       for (int k = 0; k < 8; ++k) sb = dot4(q[k], 0x01010101u, sb);
       sx = __builtin_bit_cast(float, sb);
     }
-    q0[it] = u32x4{q[0], q[1], q[2], q[3]};
-    q1[it] = u32x4{q[4], q[5], q[6], q[7]};
-    bd[it] = d;
-    bs[it] = sx;
   }
 };
 

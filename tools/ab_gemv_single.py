@@ -84,10 +84,13 @@ def main():
         outs = {}
         for rnd in range(5):
             for v in variants:
-                if v == "auto":
+                # "<waves>b": the same with per-lane activation blocks (LAMM_GEMV_LANEB=1)
+                os.environ["LAMM_GEMV_LANEB"] = "1" if v.endswith("b") else "0"
+                w = v.rstrip("b")
+                if w == "auto":
                     os.environ.pop("LAMM_GEMV_RPW", None)
                 else:
-                    os.environ["LAMM_GEMV_RPW"] = v
+                    os.environ["LAMM_GEMV_RPW"] = w
                 cs = lambda: torch.cuda.current_stream().cuda_stream   # the capture stream inside graphs
                 res[v]["single"].append(timed(lambda r: la.matmul(mats[r % sl], Bm, Csm, cs()), 200, stream))
                 res[v]["single_f32"].append(timed(lambda r: la.matmul(mats[r % sl], Xm, Csm, cs()), 200, stream))
@@ -101,6 +104,7 @@ def main():
                     torch.cuda.synchronize()
                     outs[v] = (Cs.clone(), C[:M].clone())
         os.environ.pop("LAMM_GEMV_RPW", None)
+        os.environ.pop("LAMM_GEMV_LANEB", None)
         summ = {}
         for v in variants:
             d = {}

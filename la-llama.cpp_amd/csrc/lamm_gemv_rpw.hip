@@ -125,6 +125,17 @@ __global__ __launch_bounds__(64 * WAVES) void gemv_rpw_kernel(GemvArgs p) {
     __builtin_amdgcn_sched_barrier(0);
     st.decode(lq[0], ld[0], ls[0]);
     st1.decode(lq[1], ld[1], ls[1]);
+  } else if (BF32 && 4 * nact <= (int)blockDim.x) {
+    // F32 rows in one pass, four lanes per block (ActStage4): 4096 x 4096 F32 5.12 -> 4.30 us.
+    // (Longer rows keep one lane per block: three passes with every load up front measured
+    // slower on every shape, profiles/r02/ab_gemv_f32_staging.txt.)
+    ActStage4<T> s4;
+    s4.template load<NC>(p, rb, t0);
+    __builtin_amdgcn_sched_barrier(0);   // keep the activation loads first in the vmcnt order
+    issue(row < p.M ? row : 0, wa0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (t0 < 4 * nact) s4.store(t0, sq0, sq1, sbd, sbs);
+    __syncthreads();
   } else {
     // straight-line (no branch between them), so the activation loads stay ahead of the row's
     // HBM stream and waiting for them does not wait for A; out-of-range loads read zeros

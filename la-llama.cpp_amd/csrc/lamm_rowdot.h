@@ -176,6 +176,71 @@ struct ActStage {
   }
 };
 
+// F32 activation rows staged by FOUR lanes per 32-element block (8 values each): the block's
+// |max| and sum of quants are combined across the lane quad with DPP, every value is rounded by
+// the lane that holds it -- the same bytes as ActStage<T, true> / q8_from_f32 (max and integer
+// sums do not depend on the order), with a quarter of the latency per block and 4x the
+// threads working.  Thread t handles block t / 4, values 8 (t % 4) .. 8 (t % 4) + 7; all four
+// lanes of a quad must call store() together (they do: t runs over whole quads).
+template <int T>
+struct ActStage4 {
+  using F = RFmt<T>;
+  uint32_t w[8];
+
+  template <int NC>
+  __device__ __forceinline__ void load(const GemvArgs& p, __amdgpu_buffer_rsrc_t rb, int t) {
+    const int ncols = p.N < NC ? p.N : NC;
+    const int it = t >> 2, part = t & 3;
+    const int j = it / p.nblk, b = it % p.nblk;
+    const bool ok = j < ncols && it < NC * p.nblk;
+    load_words<8, 0>(rb, ok ? (uint32_t)(j * p.ldb + (int64_t)b * 128 + 32 * part) : 0x7ffffff0u, w);
+  }
+
+  __device__ __forceinline__ void store(int t, u32x4* q0, u32x4* q1, float* bd, float* bs) const {
+    const int it = t >> 2, part = t & 3;
+    float amax = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) amax = fmaxf(amax, fabsf(__builtin_bit_cast(float, w[k])));
+    amax = fmaxf(amax, dpp_get<0xB1>(amax));   // quad_perm [1,0,3,2]
+    amax = fmaxf(amax, dpp_get<0x4E>(amax));   // quad_perm [2,3,0,1]
+    const float dd = amax / 127.f;
+    const float id = amax != 0.0f ? 127.f / amax : 0.0f;
+    int sum = 0;
+    uint32_t q[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      uint32_t qw = 0;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        int v = (int)__builtin_rintf(__builtin_bit_cast(float, w[4 * k + e]) * id);
+        v = v > 127 ? 127 : (v < -128 ? -128 : v);
+        sum += v;
+        qw |= (uint32_t)(v & 0xff) << (8 * e);
+      }
+      q[k] = qw;
+    }
+    sum += __builtin_bit_cast(int, dpp_get<0xB1>(__builtin_bit_cast(float, sum)));
+    sum += __builtin_bit_cast(int, dpp_get<0x4E>(__builtin_bit_cast(float, sum)));
+    // quads 2 part .. 2 part + 1 of the block: words 0-3 in q0, 4-7 in q1
+    uint32_t* dst = reinterpret_cast<uint32_t*>(part < 2 ? &q0[it] : &q1[it]) + 2 * (part & 1);
+    dst[0] = q[0];
+    dst[1] = q[1];
+    if (part == 0) {
+      float dv = dd;
+      asm volatile("" : "+v"(dv));
+      bd[it] = h2f(__builtin_bit_cast(uint16_t, (_Float16)dv));
+      float sx = 0.f;
+      if constexpr (F::VBPB == 36) {
+        float sd = (float)sum * dd;
+        asm volatile("" : "+v"(sd));
+        sx = h2f(__builtin_bit_cast(uint16_t, (_Float16)sd));
+      }
+      if constexpr (T == kQ4_0 || T == kQ5_0) sx = __builtin_bit_cast(float, sum);   // sum b, exact
+      bs[it] = sx;
+    }
+  }
+};
+
 template <int T, int NC, bool BF32>
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t act_rsrc(const GemvArgs& p, const unsigned char* Bz) {
   using F = RFmt<T>;

@@ -1240,15 +1240,18 @@ size_t gemv_lds_bytes(int type, int nc) {
 // once several slices share a launch.  hipGraph-replayed single calls, q4_0 (tools/
 // ab_gemv_single.py, profiles/r02/ab_gemv_single.json): 4096x4096 6.03 -> 4.67 us, 11008x4096
 // 8.81 -> 7.78, 4096x11008 11.34 -> 8.25; 33 stacked slices stay on the wave-group kernel
-// (52 vs 75 us).  Workgroup size: 8 waves for K > 4096; otherwise 16 up to 12288 rows per launch
-// (4096 with F32 activations, which every workgroup quantizes once), 8 beyond.
+// (52 vs 75 us).  Workgroup size: for K > 4096 8 waves (16 with F32 activations); otherwise 16 up
+// to 12288 rows per launch (4096 with F32 activations, which every workgroup quantizes once), 8
+// beyond.
 // LAMM_GEMV_RPW=0 off, =4/8/16 forces.
 int rpw_waves(const GemvArgs& p) {
   const char* e = getenv("LAMM_GEMV_RPW");
   if (e) return atoi(e);
   const int64_t rows = (int64_t)p.M * p.ne12 * p.ne13;
   if (rows > 32768) return 0;
-  if (p.nblk > 128) return 8;
+  // K > 4096: 8 waves; F32 rows 16, so two lanes per block stage the row in one pass
+  // (4096 x 11008 F32 9.8 -> 8.7 us, profiles/r02/ab_gemv_f32_staging.txt)
+  if (p.nblk > 128) return p.b_f32 ? 16 : 8;
   // waves per workgroup by rows per launch (profiles/r02/ab_gemv_waves.json, interleaved A/B):
   // q8 rows 4096 x 4096 16 waves 4.17 us (4: 4.53), 11008 16, 22016 8; F32 rows 4096 16, more 8
   return rows <= (p.b_f32 ? 4096 : 12288) ? 16 : 8;

@@ -125,16 +125,23 @@ __global__ __launch_bounds__(64 * WAVES) void gemv_rpw_kernel(GemvArgs p) {
     __builtin_amdgcn_sched_barrier(0);
     st.decode(lq[0], ld[0], ls[0]);
     st1.decode(lq[1], ld[1], ls[1]);
-  } else if (BF32 && 4 * nact <= (int)blockDim.x) {
-    // F32 rows in one pass, four lanes per block (ActStage4): 4096 x 4096 F32 5.12 -> 4.30 us.
-    // (Longer rows keep one lane per block: three passes with every load up front measured
-    // slower on every shape, profiles/r02/ab_gemv_f32_staging.txt.)
-    ActStage4<T> s4;
-    s4.template load<NC>(p, rb, t0);
-    __builtin_amdgcn_sched_barrier(0);   // keep the activation loads first in the vmcnt order
-    issue(row < p.M ? row : 0, wa0);
-    __builtin_amdgcn_sched_barrier(0);
-    if (t0 < 4 * nact) s4.store(t0, sq0, sq1, sbd, sbs);
+  } else if (BF32 && 2 * nact <= (int)blockDim.x) {
+    // F32 rows in one pass, several lanes per block (ActStageL): 4 when the threads cover it
+    // (4096 x 4096 F32 5.12 -> 4.41 us), else 2.  (Three passes with every load up front
+    // measured slower on every shape, profiles/r02/ab_gemv_f32_staging.txt.)
+    auto stage = [&](auto lanes) {
+      constexpr int LN = decltype(lanes)::value;
+      ActStageL<T, LN> sl;
+      sl.template load<NC>(p, rb, t0);
+      __builtin_amdgcn_sched_barrier(0);   // keep the activation loads first in the vmcnt order
+      issue(row < p.M ? row : 0, wa0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (t0 < LN * nact) sl.store(t0, sq0, sq1, sbd, sbs);
+    };
+    if (4 * nact <= (int)blockDim.x)
+      stage(std::integral_constant<int, 4>{});
+    else
+      stage(std::integral_constant<int, 2>{});
     __syncthreads();
   } else {
     // straight-line (no branch between them), so the activation loads stay ahead of the row's
@@ -191,6 +198,7 @@ hipError_t launch_rpw_nc(const GemvArgs& p, hipStream_t s, int waves) {
     if (waves >= 8) return bf ? launch_rpw_k<T, NC, 8, true, 2>(p, s) : launch_rpw_k<T, NC, 8, false, 2>(p, s);
     return bf ? launch_rpw_k<T, NC, 4, true, 2>(p, s) : launch_rpw_k<T, NC, 4, false, 2>(p, s);
   }
+  if (waves >= 16 && bf) return launch_rpw_k<T, NC, 16, true, 6>(p, s);   // F32: staging in one pass
   if (waves >= 8) return bf ? launch_rpw_k<T, NC, 8, true, 6>(p, s) : launch_rpw_k<T, NC, 8, false, 6>(p, s);
   return bf ? launch_rpw_k<T, NC, 4, true, 6>(p, s) : launch_rpw_k<T, NC, 4, false, 6>(p, s);
 }

@@ -176,39 +176,41 @@ struct ActStage {
   }
 };
 
-// F32 activation rows staged by FOUR lanes per 32-element block (8 values each): the block's
-// |max| and sum of quants are combined across the lane quad with DPP, every value is rounded by
-// the lane that holds it -- the same bytes as ActStage<T, true> / q8_from_f32 (max and integer
-// sums do not depend on the order), with a quarter of the latency per block and 4x the
-// threads working.  Thread t handles block t / 4, values 8 (t % 4) .. 8 (t % 4) + 7; all four
-// lanes of a quad must call store() together (they do: t runs over whole quads).
-template <int T>
-struct ActStage4 {
+// F32 activation rows staged by L lanes per 32-element block (L = 2 or 4; 32 / L values each):
+// the block's |max| and sum of quants are combined across the L lanes with DPP, every value is
+// rounded by the lane that holds it -- the same bytes as ActStage<T, true> / q8_from_f32 (max
+// and integer sums do not depend on the order), with 1 / L of the latency per block.  Thread t
+// handles block t / L, values (32 / L) (t % L) ..; all L lanes of a block must call store()
+// together (they do: t runs over whole groups).
+template <int T, int L>
+struct ActStageL {
+  static_assert(L == 2 || L == 4, "lanes per block");
   using F = RFmt<T>;
-  uint32_t w[8];
+  static constexpr int NV = 32 / L;   // values per lane
+  uint32_t w[NV];
 
   template <int NC>
   __device__ __forceinline__ void load(const GemvArgs& p, __amdgpu_buffer_rsrc_t rb, int t) {
     const int ncols = p.N < NC ? p.N : NC;
-    const int it = t >> 2, part = t & 3;
+    const int it = t / L, part = t % L;
     const int j = it / p.nblk, b = it % p.nblk;
     const bool ok = j < ncols && it < NC * p.nblk;
-    load_words<8, 0>(rb, ok ? (uint32_t)(j * p.ldb + (int64_t)b * 128 + 32 * part) : 0x7ffffff0u, w);
+    load_words<NV, 0>(rb, ok ? (uint32_t)(j * p.ldb + (int64_t)b * 128 + 4 * NV * part) : 0x7ffffff0u, w);
   }
 
   __device__ __forceinline__ void store(int t, u32x4* q0, u32x4* q1, float* bd, float* bs) const {
-    const int it = t >> 2, part = t & 3;
+    const int it = t / L, part = t % L;
     float amax = 0.f;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) amax = fmaxf(amax, fabsf(__builtin_bit_cast(float, w[k])));
-    amax = fmaxf(amax, dpp_get<0xB1>(amax));   // quad_perm [1,0,3,2]
-    amax = fmaxf(amax, dpp_get<0x4E>(amax));   // quad_perm [2,3,0,1]
+    for (int k = 0; k < NV; ++k) amax = fmaxf(amax, fabsf(__builtin_bit_cast(float, w[k])));
+    amax = fmaxf(amax, dpp_get<0xB1>(amax));                  // quad_perm [1,0,3,2]
+    if constexpr (L == 4) amax = fmaxf(amax, dpp_get<0x4E>(amax));   // quad_perm [2,3,0,1]
     const float dd = amax / 127.f;
     const float id = amax != 0.0f ? 127.f / amax : 0.0f;
     int sum = 0;
-    uint32_t q[2];
+    uint32_t q[NV / 4];
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < NV / 4; ++k) {
       uint32_t qw = 0;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -220,11 +222,12 @@ struct ActStage4 {
       q[k] = qw;
     }
     sum += __builtin_bit_cast(int, dpp_get<0xB1>(__builtin_bit_cast(float, sum)));
-    sum += __builtin_bit_cast(int, dpp_get<0x4E>(__builtin_bit_cast(float, sum)));
-    // quads 2 part .. 2 part + 1 of the block: words 0-3 in q0, 4-7 in q1
-    uint32_t* dst = reinterpret_cast<uint32_t*>(part < 2 ? &q0[it] : &q1[it]) + 2 * (part & 1);
-    dst[0] = q[0];
-    dst[1] = q[1];
+    if constexpr (L == 4) sum += __builtin_bit_cast(int, dpp_get<0x4E>(__builtin_bit_cast(float, sum)));
+    // quad words (NV / 4 per lane) of the block: words 0-3 in q0, 4-7 in q1
+    const int w0 = (NV / 4) * part;
+    uint32_t* dst = reinterpret_cast<uint32_t*>(w0 < 4 ? &q0[it] : &q1[it]) + (w0 & 3);
+#pragma unroll
+    for (int k = 0; k < NV / 4; ++k) dst[k] = q[k];
     if (part == 0) {
       float dv = dd;
       asm volatile("" : "+v"(dv));

@@ -28,7 +28,7 @@ Bm = la.Matrix(B.data_ptr(), la.Q8_0, kb, 1, kb)
 for r in range(20):
     la.matmul(la.Matrix(A.data_ptr() + (r % sl) * M * arow, t, M, kb, kb), Bm, la.Matrix(C.data_ptr(), la.F32, M, 1, M), s)
 torch.cuda.synchronize()
-os.environ["LAMM_GEMV_RPW"] = "4"   # the same kernel over 33 slices in one launch
+os.environ["LAMM_GEMV_RPW"] = "16"   # the same kernel (16 waves, as the single calls) over 33 slices in one launch
 bt = la.Batch(sl, 1, sl, 1, M * arow, sl * M * arow, 34 * kb, sl * 34 * kb, 4 * M, 4 * M * sl)
 for _ in range(5):
     la.matmul_batched(la.Matrix(A.data_ptr(), t, M, kb, kb), Bm, la.Matrix(C.data_ptr(), la.F32, M, 1, M), bt, s)

@@ -1252,6 +1252,9 @@ int rpw_waves(const GemvArgs& p) {
   // K > 4096: 8 waves; F32 rows 16, so two lanes per block stage the row in one pass
   // (4096 x 11008 F32 9.8 -> 8.7 us, profiles/r02/ab_gemv_f32_staging.txt)
   if (p.nblk > 128) return p.b_f32 ? 16 : 8;
+  // fewer rows than one per wave of 256 sixteen-wave workgroups (a row slab of a sharded
+  // weight, bench.py --gpus N): smaller workgroups spread the rows over more CUs
+  if (rows < 4096) return rows >= 2048 ? 8 : 4;
   // waves per workgroup by rows per launch (profiles/r02/ab_gemv_waves.json, interleaved A/B):
   // q8 rows 4096 x 4096 16 waves 4.17 us (4: 4.53), 11008 16, 22016 8; F32 rows 4096 16, more 8
   return rows <= (p.b_f32 ? 4096 : 12288) ? 16 : 8;

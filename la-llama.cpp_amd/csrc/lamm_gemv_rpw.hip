@@ -168,6 +168,15 @@ __global__ __launch_bounds__(64 * WAVES) void gemv_rpw_kernel(GemvArgs p) {
     compute(row, wa1);
     row = next;
   }
+  if (p.flag) {   // completion signal: the last workgroup to finish tells the host (see GemvArgs)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's C stores have completed
+    __syncthreads();
+    if (threadIdx.x == 0 && atomicAdd(p.done_ctr, 1u) == gridDim.x * gridDim.y - 1) {
+      __hip_atomic_store(p.done_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __threadfence_system();
+      __hip_atomic_store(p.flag, p.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
 }
 
 template <int T, int NC, int WAVES, bool BF32, int ITER>

@@ -192,8 +192,21 @@ int gemv_max_n(int type) {
   return n < 1 ? 1 : (n > 8 ? 8 : n);
 }
 
+// A completion signal the ggml boundary asks of the next matmul on this thread (decode calls):
+// the row-per-wave GEMV writes it itself when it takes the call (signaled = true); otherwise the
+// boundary launches the signal kernel after the call.
+struct Completion {
+  unsigned* ctr;
+  unsigned* flag;
+  unsigned seq;
+  bool signaled;
+};
+thread_local Completion* g_completion = nullptr;
+
 int matmul_impl(const lamm_matrix* A, const lamm_matrix* B, const lamm_matrix* C, const lamm_batch* batch,
                 void* hip_stream, const lamm_weights* W) {
+  Completion* done = g_completion;
+  g_completion = nullptr;
   if (!A || !B || !C) return fail(LAMM_ERR_SHAPE, "null matrix");
   if (!is_weight_type(A->type)) return fail(LAMM_ERR_TYPE, "unsupported A type %d", A->type);
   // F32 activations for a q8_0 / q8_1 weight type: ggml's INIT quantization (AVX2 flavour) runs
@@ -245,6 +258,12 @@ int matmul_impl(const lamm_matrix* A, const lamm_matrix* B, const lamm_matrix* C
   p.b_f32 = b_f32 ? 1 : 0;
   hipError_t e;
   if (N <= gemv_max_n(A->type) || (b_f32 && N <= 8)) {
+    if (done && gemv_rpw_supported(A->type, p) && rpw_waves(p) > 0) {
+      p.done_ctr = done->ctr;
+      p.flag = done->flag;
+      p.seq = done->seq;
+      done->signaled = true;
+    }
     e = launch_gemv(A->type, p, s);
   } else if (gemm_dense_supported(A->type) && !getenv_flag0("LAMM_DENSE_GEMM")) {
     const size_t wsb = gemm_dense_workspace_bytes(A->type, p);
@@ -479,6 +498,8 @@ struct Dev {
   unsigned* flag = nullptr;       // pinned, host-coherent completion word (lamm_signal.hip)
   unsigned* flag_dev = nullptr;   // its device address
   unsigned seq = 0;
+  unsigned* done_ctr = nullptr;   // device counter for the GEMV's own completion signal
+  unsigned pending = 0;           // seq the last call's kernel signals itself (0: none)
   std::unordered_map<WeightKey, WeightEntry, WeightKeyHash> cache;
   std::list<WeightKey> lru;
   size_t cached = 0;
@@ -605,6 +626,8 @@ class Runtime {
       HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&devs[i].flag), 64, hipHostMallocCoherent | hipHostMallocMapped));
       HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&devs[i].flag_dev), devs[i].flag, 0));
       *(volatile unsigned*)devs[i].flag = 0;
+      HIPCHK(hipMalloc(reinterpret_cast<void**>(&devs[i].done_ctr), 64));
+      HIPCHK(hipMemset(devs[i].done_ctr, 0, 64));
     }
     const char* b = getenv("LAMM_HIP_CACHE_GB");
     budget_ = (size_t)((b ? atof(b) : 64.0) * (1ull << 30));
@@ -693,6 +716,7 @@ class Runtime {
       for (void* b : d.buf)
         if (b) (void)hipFree(b);
       (void)hipHostFree(d.flag);
+      if (d.done_ctr) (void)hipFree(d.done_ctr);
       (void)hipStreamDestroy(d.stream);
     }
     devs.clear();
@@ -832,14 +856,36 @@ namespace {
 // spun on by the host -- ~4 us per call under hipStreamSynchronize.  If the flag has not arrived
 // after a second (a fault, a hang) the stream is synchronised, which reports the error.
 // LAMM_HIP_SPIN=0: hipStreamSynchronize only (A/B).
-void wait_device(Dev& d) {
+bool spin_enabled() {
   static const bool spin = [] {
     const char* e = getenv("LAMM_HIP_SPIN");
     return !(e && e[0] == '0');
   }();
-  if (spin) {
-    const unsigned seq = ++d.seq;
-    HIPCHK(launch_signal(d.flag_dev, seq, d.stream));
+  return spin;
+}
+
+// LAMM_HIP_KERNEL_SIGNAL=1: the GEMV's last workgroup writes the completion flag itself instead
+// of a signal launch behind it.  Measured no faster through llama.cpp (profiles/r02/
+// ab_kernel_signal.txt: device wait 15.8 vs 15.1 us per decode call) -- the last workgroup's
+// counter round trip and system fence cost what the second launch costs -- so it is an A/B switch.
+bool kernel_signal_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("LAMM_HIP_KERNEL_SIGNAL");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
+void wait_device(Dev& d) {
+  if (spin_enabled()) {
+    // with LAMM_HIP_KERNEL_SIGNAL=1 the call's GEMV signals completion itself when it can
+    // (Completion: zero-copy C with nothing queued behind it)
+    unsigned seq = d.pending;
+    d.pending = 0;
+    if (!seq) {
+      seq = ++d.seq;
+      HIPCHK(launch_signal(d.flag_dev, seq, d.stream));
+    }
     const auto t0 = std::chrono::steady_clock::now();
     for (unsigned it = 0;; ++it) {
       if (*(volatile unsigned*)d.flag == seq) return;
@@ -1015,8 +1061,15 @@ extern "C" void lamm_mul_mat(const struct ggml_compute_params* vparams, struct g
     const bool stationary = weight && N > gemv_max_n(t0) && (!b_f32 || N > 8) &&
                             ((gemm_fp6_supported(t0) && gemm_path(pa, true) == 0) ||
                              (gemm_kq_supported(t0) && !getenv_flag0("LAMM_KQ_GEMM")));
+    Completion comp{d.done_ctr, d.flag_dev, 0, false};
+    if (zc_out && spin_enabled() && kernel_signal_enabled()) {   // nothing is queued behind the matmul
+      comp.seq = ++d.seq;
+      g_completion = &comp;
+    }
     const int rc = stationary ? lamm_hip_matmul_weights(rt.prepared(d, *w, A, ne02, ne03), &B, &C, &bt, s)
                               : lamm_hip_matmul_batched(&A, &B, &C, &bt, s);
+    g_completion = nullptr;
+    d.pending = comp.signaled ? comp.seq : 0;
     if (rc != LAMM_OK) {
       fprintf(stderr, "lamm_hip: lamm_hip_matmul_batched failed (%d): %s\n", rc, g_err.c_str());
       std::abort();

@@ -21,12 +21,18 @@ struct GemvArgs {
   // GEMV only, q8_0 / q8_1 activations: B holds F32 rows (ldb in bytes) that the kernel
   // quantizes while staging them (ggml's INIT fused into the launch, AVX2 flavour, bit-exact)
   int b_f32 = 0;
+  // completion signal (row-per-wave GEMV only, the ggml boundary's decode calls): the last
+  // workgroup to finish stores seq into *flag (host-mapped) -- no separate signal launch
+  unsigned* done_ctr = nullptr;   // device counter, zero between launches
+  unsigned* flag = nullptr;
+  unsigned seq = 0;
 };
 
 hipError_t launch_gemv(int type, const GemvArgs& p, hipStream_t s);
 // row-per-wave decode GEMV (lamm_gemv_rpw.hip): 32-element block formats, N <= 2, K <= 12288;
 // `waves` per workgroup (4 / 8 / 16; 8 at most for K > 4096)
 bool gemv_rpw_supported(int type, const GemvArgs& p);
+int rpw_waves(const GemvArgs& p);   // 0: the wave-group kernels (lamm_gemv.hip) take the call
 hipError_t launch_gemv_rpw(int type, const GemvArgs& p, hipStream_t s, int waves);
 size_t gemv_lds_bytes(int type, int nc);
 hipError_t launch_gemv_dense(int type, const GemvArgs& p, hipStream_t s);   // F32 / F16 rows

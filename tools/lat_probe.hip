@@ -117,6 +117,40 @@ int main(int argc, char** argv) {
     printf(", \"flag_kernel_spin\": %.2f", t[1000]);
   }
   printf(", \"flag_kernel_sync\": %.2f", median_us([&] { flag_kernel<<<1, 64, 0, s>>>(dflag, ++seq); }, s));
+  // the same completion signal written by the command processor (hipStreamWriteValue32), no kernel
+  {
+    std::vector<double> t(2000);
+    for (int r = -50; r < 2000; ++r) {
+      ++seq;
+      const auto t0 = std::chrono::steady_clock::now();
+      CK(hipStreamWriteValue32(s, dflag, seq, 0));
+      while (*(volatile unsigned*)hflag != seq) {
+      }
+      const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+      if (r >= 0) t[r] = us;
+      CK(hipStreamSynchronize(s));
+    }
+    std::sort(t.begin(), t.end());
+    printf(", \"write_value_spin\": %.2f", t[1000]);
+  }
+  // a 256-workgroup kernel then the completion signal: signal kernel vs stream write-value
+  for (int mode = 0; mode < 2; ++mode) {
+    std::vector<double> t(2000);
+    for (int r = -50; r < 2000; ++r) {
+      ++seq;
+      const auto t0 = std::chrono::steady_clock::now();
+      write_kernel<<<n / 256, 256, 0, s>>>(d0, n);
+      if (mode == 0) flag_kernel<<<1, 64, 0, s>>>(dflag, seq);
+      else CK(hipStreamWriteValue32(s, dflag, seq, 0));
+      while (*(volatile unsigned*)hflag != seq) {
+      }
+      const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+      if (r >= 0) t[r] = us;
+      CK(hipStreamSynchronize(s));
+    }
+    std::sort(t.begin(), t.end());
+    printf(mode == 0 ? ", \"kernel_then_flag_kernel_spin\": %.2f" : ", \"kernel_then_write_value_spin\": %.2f", t[1000]);
+  }
   printf("}\n");
   return 0;
 }

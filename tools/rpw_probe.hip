@@ -9,6 +9,10 @@
 //   2 + staging : mode 1 + the activation row (q8_0, 4352 B) staged into LDS by 128 threads and a
 //                 workgroup barrier before the reduce
 //   3 + compute : mode 2 + the real q4_0 x q8_0 block dots, fixed-order wave reduction, C store
+//   4 blocks + per-lane B : mode 1 + each lane loading its own two activation blocks (L2-served)
+//                 instead of the LDS staging and barrier
+//   5 coalesced + LDS     : mode 0's loads, the row written to a per-wave LDS slice, each lane then
+//                 reading its two blocks back (dword reads + realignment), xor-reduce
 //   hipcc --offload-arch=gfx950 -O3 tools/rpw_probe.hip -o tools/rpw_probe && tools/rpw_probe
 #include <hip/hip_runtime.h>
 
@@ -48,14 +52,29 @@ __global__ __launch_bounds__(64 * WAVES) void probe(const unsigned char* A, cons
   const auto ra = rsrc(A + (size_t)row * ROW, ROW);
   uint32_t w[2][6];
   u32x4 c[3];
-  if constexpr (MODE == 0) {
+  __shared__ uint32_t rowbuf[WAVES][ROW / 4 + 16];
+  uint32_t bw[2][10];
+  if constexpr (MODE == 4) {   // activation blocks l and l+64 straight into registers (before A)
+    const auto rb = rsrc(B, NB * 34);
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const uint32_t off = ((lane + 64 * it) * 34) & ~3u;
+      const u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(rb, off, 0, 0);
+      const u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(rb, off + 16, 0, 0);
+      const u32x2 v2 = __builtin_amdgcn_raw_buffer_load_b64(rb, off + 32, 0, 0);
+      bw[it][0] = v0[0]; bw[it][1] = v0[1]; bw[it][2] = v0[2]; bw[it][3] = v0[3];
+      bw[it][4] = v1[0]; bw[it][5] = v1[1]; bw[it][6] = v1[2]; bw[it][7] = v1[3];
+      bw[it][8] = v2[0]; bw[it][9] = v2[1];
+    }
+  }
+  if constexpr (MODE == 0 || MODE == 5) {
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       const int ch = lane + 64 * k;
       c[k] = __builtin_amdgcn_raw_buffer_load_b128(ra, ch < ROW / 16 ? ch * 16 : 0x7ffffff0, 0, 2);
     }
   } else {
-    if constexpr (MODE >= 2) {   // activation loads first (vmcnt order), like the kernel
+    if constexpr (MODE == 2 || MODE == 3) {   // activation loads first (vmcnt order), like the kernel
       if (threadIdx.x < NB) {
         const auto rb = rsrc(B, NB * 34);
         const uint32_t off = (threadIdx.x * 34) & ~3u;
@@ -70,10 +89,34 @@ __global__ __launch_bounds__(64 * WAVES) void probe(const unsigned char* A, cons
       const u32x2 u = __builtin_amdgcn_raw_buffer_load_b64(ra, off + 16, 0, 2);
       w[it][0] = v[0]; w[it][1] = v[1]; w[it][2] = v[2]; w[it][3] = v[3]; w[it][4] = u[0]; w[it][5] = u[1];
     }
-    if constexpr (MODE >= 2) __syncthreads();
+    if constexpr (MODE == 2 || MODE == 3) __syncthreads();
   }
   float acc = 0.f;
-  if constexpr (MODE == 0) {
+  if constexpr (MODE == 5) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int ch = lane + 64 * k;
+      if (ch < ROW / 16)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) rowbuf[wave][ch * 4 + q] = c[k][q];
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's LDS writes done (wave-local slice)
+    uint32_t x = 0;
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int o = ((lane + 64 * it) * BPB) >> 2;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) x ^= rowbuf[wave][o + k];
+    }
+    acc = (float)(x & 0xff);
+  } else if constexpr (MODE == 4) {
+    uint32_t x = 0;
+#pragma unroll
+    for (int it = 0; it < 2; ++it)
+#pragma unroll
+      for (int k = 0; k < 6; ++k) x ^= w[it][k] ^ bw[it][k] ^ bw[it][k + 4];
+    acc = (float)(x & 0xff);
+  } else if constexpr (MODE == 0) {
     uint32_t x = 0;
 #pragma unroll
     for (int k = 0; k < 3; ++k) x ^= c[k][0] ^ c[k][1] ^ c[k][2] ^ c[k][3];
@@ -152,6 +195,8 @@ int main() {
   printf(", \"blocks_us\": %.3f", time_us([&](int r) { probe<1><<<g, b, 0, s>>>(pool + (r % slots) * bytes, B, C); }));
   printf(", \"blocks_staging_us\": %.3f", time_us([&](int r) { probe<2><<<g, b, 0, s>>>(pool + (r % slots) * bytes, B, C); }));
   printf(", \"blocks_staging_compute_us\": %.3f", time_us([&](int r) { probe<3><<<g, b, 0, s>>>(pool + (r % slots) * bytes, B, C); }));
+  printf(", \"blocks_lane_b_us\": %.3f", time_us([&](int r) { probe<4><<<g, b, 0, s>>>(pool + (r % slots) * bytes, B, C); }));
+  printf(", \"coalesced_lds_transpose_us\": %.3f", time_us([&](int r) { probe<5><<<g, b, 0, s>>>(pool + (r % slots) * bytes, B, C); }));
   printf(", \"bytes_per_launch\": %zu}\n", bytes);
   return 0;
 }

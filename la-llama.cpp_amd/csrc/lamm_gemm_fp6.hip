@@ -73,8 +73,6 @@ template <> struct F6<kQ5_0> { static constexpr int ABPB = 22, VBPB = 34; static
 // (h = k-group: 0 = hi codes, 1 = lo codes; both copies carry d_b and s_b)
 constexpr int F6_A_BYTES = 2 * F6_KB * F6_TI * 16;
 constexpr int F6_B_BYTES = 2 * F6_KB * 2 * F6_TJ * 16;
-constexpr int F6_STAGE = F6_A_BYTES + F6_B_BYTES;
-constexpr int F6_PA = F6_A_BYTES / F6_PIECE;
 
 // byte offset of plane p (16 bytes) of the fragment of (block b, [k-group h,] row r).  Planes
 // are separate arrays, so the 32 lanes of a half-wave read 512 contiguous bytes per plane:
@@ -326,24 +324,42 @@ __device__ __forceinline__ half4 f6_dq(const F6Frag& f) {   // {d, 0, 0, 0}
 // V: ablations for tools/ab_gemm.py (0 production, 1 no compute, 2 no DMA, 3 no epilogue FMAs,
 //    4 no DMA + no LDS fragment reads (operands from registers), 5 no DMA + no barrier,
 //    6 no P-MFMA, 7 no S-MFMA)
-// WJ: 32-row activation sub-tiles per wave (2: 8 waves of 64x64; 1: 16 waves of 32x64)
-template <int WJ> struct F6Waves {
-  static constexpr int NWJ = F6_TJ / (32 * WJ), NWI = F6_TI / 64, NW = NWJ * NWI, NT = 64 * NW;
-  static_assert(F6_STAGE % (NW * F6_PIECE) == 0, "every wave moves the same number of DMA pieces");
-  static constexpr int PPW = F6_STAGE / F6_PIECE / NW;   // DMA pieces per wave per stage
+// WJ: 32-row activation sub-tiles per wave (2: 64x64 per wave; 1: 32x64).
+// SI / SJ: the workgroup's tile is 1/SI x 1/SJ of a packed 256 x 128 chunk (the packed layout,
+// and so the stationary weights, stay the same: a sub-tile's rows of one plane are contiguous
+// 1 KiB DMA pieces).  KG: K-groups -- the workgroup's waves form KG groups that compute
+// consecutive K-steps of the same output tile side by side (one LDS stage = KG K-steps) and
+// sum their accumulators through LDS at the end in group order: small grids fill the chip
+// without split-K partials in HBM or a reduce launch.
+template <int WJ, int SI = 1, int SJ = 1, int KG = 1> struct F6Waves {
+  static constexpr int TI = F6_TI / SI, TJ = F6_TJ / SJ;   // workgroup tile
+  static constexpr int NWJ = TJ / (32 * WJ), NWI = TI / 64, NWG = NWJ * NWI, NW = NWG * KG, NT = 64 * NW;
+  static constexpr int A_SUB = 2 * F6_KB * TI * 16, B_SUB = 2 * F6_KB * 2 * TJ * 16, SUB = A_SUB + B_SUB;
+  static constexpr int STAGE = KG * SUB;
+  static constexpr int NBUF = STAGE * F6_NBUF <= 128 * 1024 ? F6_NBUF : 128 * 1024 / STAGE;
+  static constexpr int PA = A_SUB / F6_PIECE, PSUB = SUB / F6_PIECE;
+  static_assert(TI % 64 == 0 && TJ % 64 == 0 && NWJ >= 1, "tile");
+  static_assert(NBUF >= 2, "LDS stages");
+  static_assert(STAGE % (NW * F6_PIECE) == 0, "every wave moves the same number of DMA pieces");
+  static_assert((KG - 1) * NWG * WJ * 8192 <= NBUF * STAGE, "K-group sums fit the stages");
+  static constexpr int PPW = STAGE / F6_PIECE / NW;   // DMA pieces per wave per stage
+  // LDS byte offsets inside one K-step's sub-stage (the chunk image with TI / TJ rows)
+  __device__ static constexpr int aoff(int p, int b, int r) { return ((p * F6_KB + b) * TI + r) * 16; }
+  __device__ static constexpr int boff(int p, int b, int h, int r) { return A_SUB + (((p * F6_KB + b) * 2 + h) * TJ + r) * 16; }
 };
 
-// Split-K (grids with too few 256x128 tiles to fill 256 CUs, e.g. ONE 4096x512 GEMM = 64
-// tiles): split s of nsplit runs K-steps [s*nsteps/nsplit, (s+1)*nsteps/nsplit) and writes its
-// partial tile to part[s][z][j][i]; f6_reduce then sums the splits in order 0..nsplit-1
-// (deterministic).  nsplit == 1 writes C directly.
-template <int T, int V, int WJ>
-__global__ __launch_bounds__(F6Waves<WJ>::NT) void gemm_fp6_kernel(GemvArgs p, const unsigned char* wsA,
-                                                                    const unsigned char* wsB, int nsplit, float* part,
-                                                                    unsigned* tile_ctr) {
+// Split-K (grids with too few 256x128 tiles to fill 256 CUs and no sub-tile plan): split s of
+// nsplit runs K-steps [s*nsteps/nsplit, (s+1)*nsteps/nsplit) and writes its partial tile to
+// part[s][z][j][i]; f6_reduce then sums the splits in order 0..nsplit-1 (deterministic).
+// nsplit == 1 writes C directly.
+template <int T, int V, int WJ, int SI = 1, int SJ = 1, int KG = 1>
+__global__ __launch_bounds__((F6Waves<WJ, SI, SJ, KG>::NT)) void gemm_fp6_kernel(GemvArgs p, const unsigned char* wsA,
+                                                                                const unsigned char* wsB, int nsplit,
+                                                                                float* part, unsigned* tile_ctr) {
   using F = F6<T>;
-  using WV = F6Waves<WJ>;
+  using WV = F6Waves<WJ, SI, SJ, KG>;
   constexpr int F6_NW = WV::NW, F6_PPW = WV::PPW, UPB = 2 * WJ;   // UPB: units per block
+  constexpr int NBUF = WV::NBUF, TI = WV::TI, TJ = WV::TJ;
   constexpr bool AFF = F::AFF;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const F6Layout L = F6Layout::of(p);
@@ -351,46 +367,60 @@ __global__ __launch_bounds__(F6Waves<WJ>::NT) void gemm_fp6_kernel(GemvArgs p, c
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int lr = lane & 31, h = lane >> 5;
-  const int wj = w % WV::NWJ, wi = w / WV::NWJ;   // NWJ (j) x 4 (i) waves
+  const int g = w / WV::NWG, wl = w % WV::NWG;   // K-group, wave within the group
+  const int wj = wl % WV::NWJ, wi = wl / WV::NWJ;   // NWJ (j) x NWI (i) waves
   // XCD-aware tile order: workgroup id -> tile index so that the workgroups one XCD runs at
   // once are neighbouring tiles of one slice (their DMA chunks meet in that XCD's L2).
-  int it, jt, z, sp;
+  const int nsi = (p.M + TI - 1) / TI, nsj = (p.N + TJ - 1) / TJ;   // workgroup tiles per slice
+  int ti, tj, z, sp;
   {
-    const int ntile = L.nit * L.njt * p.ne12 * p.ne13;
+    const int ntile = nsi * nsj * p.ne12 * p.ne13;
     const int nwg = ntile * nsplit;
     const int id = blockIdx.x, x = id & 7, k = id >> 3, q = nwg >> 3, rmd = nwg & 7;
     int wv = x < rmd ? x * (q + 1) + k : rmd * (q + 1) + (x - rmd) * q + k;
     sp = wv / ntile;   // split-major: one XCD's neighbouring tiles share a K range
     wv %= ntile;
-    const int per = L.nit * L.njt;
+    const int per = nsi * nsj;
     z = wv / per;
-    const int ws_ = wv % per, ib = ws_ / (8 * L.njt), rem = ws_ % (8 * L.njt);
-    const int width = min(8, L.nit - ib * 8);
-    jt = rem / width;
-    it = ib * 8 + rem % width;
+    const int ws_ = wv % per, ib = ws_ / (8 * nsj), rem = ws_ % (8 * nsj);
+    const int width = min(8, nsi - ib * 8);
+    tj = rem / width;
+    ti = ib * 8 + rem % width;
   }
+  const int it = ti / SI, jt = tj / SJ;   // packed chunk and the tile's rows inside it
+  const int ri0 = (ti % SI) * TI, rj0 = (tj % SJ) * TJ;
   const int i12 = z % p.ne12, i13 = z / p.ne12;
   const int ne02 = p.ne12 / p.r2, a = (i12 / p.r2) + (i13 / p.r3) * ne02;
   const unsigned char* wa = wsA + (int64_t)a * L.a_slice + (int64_t)it * L.nsteps * F6_A_BYTES;
   const unsigned char* wb = wsB + (int64_t)z * L.b_slice + (int64_t)jt * L.nsteps * F6_B_BYTES;
   const int nsteps = L.nsteps;
   const int k0 = (int)((int64_t)sp * nsteps / nsplit), k1 = (int)((int64_t)(sp + 1) * nsteps / nsplit);
+  // stages: KG consecutive K-steps each (KG > 1 runs unsplit)
+  const int s0 = KG == 1 ? k0 : 0, s1 = KG == 1 ? k1 : (nsteps + KG - 1) / KG;
 
-  // ---- LDS-DMA: piece pc = k*NW + w of a stage (A chunk pieces first, then B) ----
+  // ---- LDS-DMA: piece pc = k*NW + w of a stage = K-group pc / PSUB, piece pc % PSUB of its
+  // K-step (A pieces first, then B); a K-step past the end re-loads the last one (its group
+  // skips the compute), so every wave moves PPW pieces per stage and the vmcnt counts hold.
+  // The piece's offset is wave-uniform (soffset); the lane's 16 bytes are the only VGPR ----
   const auto ra = make_rsrc(wa, (uint32_t)(nsteps * F6_A_BYTES));
   const auto rb = make_rsrc(wb, (uint32_t)(nsteps * F6_B_BYTES));
-  auto issue = [&](int ks) {
-    unsigned char* dst = smem + (ks % F6_NBUF) * F6_STAGE;
+  auto issue = [&](int ss) {
+    unsigned char* dst = smem + (ss % NBUF) * WV::STAGE;
 #pragma unroll
     for (int k = 0; k < F6_PPW; ++k) {
       const int pc = k * F6_NW + w;   // wave-uniform
-      if (pc < F6_PA)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (__attribute__((address_space(3))) void*)(dst + pc * F6_PIECE),
-                                                 16, (uint32_t)(ks * F6_A_BYTES + pc * F6_PIECE + lane * 16), 0, 0, 0);
-      else
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            rb, (__attribute__((address_space(3))) void*)(dst + pc * F6_PIECE), 16,
-            (uint32_t)(ks * F6_B_BYTES + (pc - F6_PA) * F6_PIECE + lane * 16), 0, 0, 0);
+      const int kg = pc / WV::PSUB, q = pc % WV::PSUB;
+      const int ks = min(KG * ss + kg, nsteps - 1);
+      auto* d = (__attribute__((address_space(3))) void*)(dst + pc * F6_PIECE);
+      if (q < WV::PA) {
+        const int plane = q / (TI / 64), part_ = q % (TI / 64);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, d, 16, lane * 16,
+                                                 ks * F6_A_BYTES + (plane * F6_TI + ri0 + 64 * part_) * 16, 0, 0);
+      } else {
+        const int plane = (q - WV::PA) / (TJ / 64), part_ = (q - WV::PA) % (TJ / 64);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, d, 16, lane * 16,
+                                                 ks * F6_B_BYTES + (plane * F6_TJ + rj0 + 64 * part_) * 16, 0, 0);
+      }
     }
   };
 
@@ -406,7 +436,7 @@ __global__ __launch_bounds__(F6Waves<WJ>::NT) void gemm_fp6_kernel(GemvArgs p, c
 
   constexpr bool NODMA = V == 2 || V == 4 || V == 5;
   if (!NODMA)
-    for (int k = k0; k < k0 + F6_NBUF - 1 && k < k1; ++k) issue(k);
+    for (int k = s0; k < s0 + NBUF - 1 && k < s1; ++k) issue(k);
   F6Frag fb[2][WJ], fa[2][2];   // [block slot][sub-tile]
   F6Res rr[F6_PD + 1];   // results of the units in flight
   constexpr int NU = UPB * F6_KB;   // units per K-step
@@ -428,35 +458,37 @@ __global__ __launch_bounds__(F6Waves<WJ>::NT) void gemm_fp6_kernel(GemvArgs p, c
     if (w >= 4) __builtin_amdgcn_s_setprio(1);
   }
   bool pend = false;
-  for (int ks = k0; ks < k1; ++ks) {
-    if (!NODMA) {   // this wave's pieces of stage ks landed (younger stages may stay in flight)
-      const int ahead = min(F6_NBUF - 2, k1 - 1 - ks);
+  for (int ss = s0; ss < s1; ++ss) {
+    if (!NODMA) {   // this wave's pieces of stage ss landed (younger stages may stay in flight)
+      const int ahead = min(NBUF - 2, s1 - 1 - ss);
       if (ahead >= 2) f6_wait_vm<2 * F6_PPW>();
       else if (ahead == 1) f6_wait_vm<F6_PPW>();
       else f6_wait_vm<0>();
     }
-    if (V != 5) f6_barrier();   // stage ks visible to all waves; stage ks-1 no longer read
-    if (!NODMA && ks + F6_NBUF - 1 < k1) issue(ks + F6_NBUF - 1);
+    if (V != 5) f6_barrier();   // stage ss visible to all waves; stage ss-1 no longer read
+    if (!NODMA && ss + NBUF - 1 < s1) issue(ss + NBUF - 1);
     if constexpr (V == 1) continue;
-    const unsigned char* sA = smem + (ks % F6_NBUF) * F6_STAGE;
-    const unsigned char* sB = sA + F6_A_BYTES;
+    const int ks = KG * ss + g;
+    if (KG > 1 && ks >= nsteps) continue;   // this group's K-step is past the end (wave-uniform)
+    const unsigned char* sA = smem + (ss % NBUF) * WV::STAGE + g * WV::SUB;
+    const unsigned char* sB = sA;
 
     // fragments are read from LDS one block ahead of their MFMAs, not as one burst per K-step
     // (8 waves x 4*KB ds_read_b128 pairs right after the barrier queue hundreds of LDS cycles
     // in front of every wave's first MFMA).  Block b lives in register slot b & 1.
     auto ldB = [&](int b, int x) {
       if constexpr (V == 4) {
-        if (ks > k0) return;
+        if (ss > s0) return;
       }
       const int r = 32 * WJ * wj + 32 * x + lr;
-      f6_load(fb[b & 1][x], sB + f6_boff(0, b, h, r), sB + f6_boff(1, b, h, r));
+      f6_load(fb[b & 1][x], sB + WV::boff(0, b, h, r), sB + WV::boff(1, b, h, r));
     };
     auto ldA = [&](int b, int y) {
       if constexpr (V == 4) {
-        if (ks > k0) return;
+        if (ss > s0) return;
       }
       const int r = 64 * wi + 32 * y + lr;
-      f6_load(fa[b & 1][y], sA + f6_aoff(0, b, r), sA + f6_aoff(1, b, r));
+      f6_load(fa[b & 1][y], sA + WV::aoff(0, b, r), sA + WV::aoff(1, b, r));
     };
     // unit n = (block n / UPB, j sub-tile (n / 2) % WJ, i sub-tile n % 2)
     auto ld_unit = [&](int n) {   // the fragments unit n uses first
@@ -519,6 +551,33 @@ __global__ __launch_bounds__(F6Waves<WJ>::NT) void gemm_fp6_kernel(GemvArgs p, c
   }
 
   if (pend) epi(NU - 1, rr[(NU - 1) % (F6_PD + 1)]);
+  if constexpr (KG > 1) {
+    // K-groups 1..KG-1 hand their sums to group 0 through the (now idle) stages; group 0 adds
+    // them in group order.  Layout [group-1][wave][x][y][e][lane]: a wave's dword per lane,
+    // conflict-free.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);
+    auto at = [&](int g_, int x, int y, int e) { return ((((g_ - 1) * WV::NWG + wl) * WJ + x) * 2 + y) * 16 * 64 + e * 64 + lane; };
+    if (g > 0) {
+#pragma unroll
+      for (int x = 0; x < WJ; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) red[at(g, x, y, e)] = acc[x][y][e];
+    }
+    __syncthreads();
+    if (g > 0) return;
+#pragma unroll 1
+    for (int g_ = 1; g_ < KG; ++g_)
+#pragma unroll
+      for (int x = 0; x < WJ; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) acc[x][y][e] += red[at(g_, x, y, e)];
+  }
   float* Cz;
   int64_t ldc;
   if (nsplit == 1) {
@@ -528,16 +587,16 @@ __global__ __launch_bounds__(F6Waves<WJ>::NT) void gemm_fp6_kernel(GemvArgs p, c
     Cz = part + ((int64_t)sp * p.ne12 * p.ne13 + z) * p.N * p.M;
     ldc = p.M;
   }
-  const bool fused = nsplit > 1 && tile_ctr != nullptr;
+  const bool fused = SI == 1 && SJ == 1 && KG == 1 && nsplit > 1 && tile_ctr != nullptr;
   if (!fused) {
 #pragma unroll
     for (int x = 0; x < WJ; ++x)
 #pragma unroll
       for (int y = 0; y < 2; ++y) {
-        const int64_t i = (int64_t)it * F6_TI + 64 * wi + 32 * y + lr;
+        const int64_t i = (int64_t)ti * TI + 64 * wi + 32 * y + lr;
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-          const int64_t j = (int64_t)jt * F6_TJ + 32 * WJ * wj + 32 * x + (e & 3) + 8 * (e >> 2) + 4 * h;
+          const int64_t j = (int64_t)tj * TJ + 32 * WJ * wj + 32 * x + (e & 3) + 8 * (e >> 2) + 4 * h;
           if (i < p.M && j < p.N) Cz[j * ldc + i] = 0.5f * acc[x][y][e];
         }
       }
@@ -671,7 +730,7 @@ unsigned* tile_counters(hipStream_t s) {
 // K-splits for a grid of `tiles` workgroups: double until 256 CUs have one each, keeping
 // >= 8 K-steps per split, at most 16 (K=11008, 16 tiles: 8 splits 247, 16 splits 288, 21
 // splits 230 TFLOP/s, profiles/r01/ab_driver_split.txt).  LAMM_FP6_SPLIT=n forces n (A/B).
-int f6_nsplit(const GemvArgs& p, const F6Layout& L) {
+int f6_nsplit_for(const GemvArgs& p, const F6Layout& L) {
   const char* e = getenv("LAMM_FP6_SPLIT");
   const int tiles = L.nit * L.njt * p.ne12 * p.ne13;
   int n = 1;
@@ -682,6 +741,31 @@ int f6_nsplit(const GemvArgs& p, const F6Layout& L) {
   }
   return n < 1 ? 1 : (n > L.nsteps ? L.nsteps : n);
 }
+
+// Launch plan.  A grid of fewer 256x128 tiles than CUs runs 128x64 workgroup tiles with
+// K-groups (F6Waves) when that fills the chip -- no split-K partials, no reduce launch -- and
+// splits K otherwise.  LAMM_FP6_SUB=0 keeps split-K (A/B), =2 picks the 2-group / 32x64-wave
+// form instead of the 4-group / 64x64-wave one; LAMM_FP6_SPLIT=n forces split-K with n.
+struct F6Plan {
+  int sub;      // 0: 256x128 tiles (+ split-K), 1: 128x64 tiles x 4 K-groups, 2: 128x64 x 2 K-groups
+  int nsplit;
+  int grid;
+};
+constexpr int kSubTilesMin = 256;
+F6Plan f6_plan(const GemvArgs& p, const F6Layout& L) {
+  const int tiles = L.nit * L.njt * p.ne12 * p.ne13;
+  const char* es = getenv("LAMM_FP6_SUB");
+  const char* ek = getenv("LAMM_FP6_SPLIT");
+  const int sub = es ? atoi(es) : -1;   // -1: automatic; 1 / 2 force that form (tests, A/B)
+  const int64_t subt = (int64_t)((p.M + 127) / 128) * ((p.N + 63) / 64) * p.ne12 * p.ne13;
+  if (!(ek && atoi(ek) > 0) && sub != 0 && subt < (1 << 30)) {
+    if (sub > 0) return {sub == 2 ? 2 : 1, 1, (int)subt};
+    if (tiles < 256 && subt >= kSubTilesMin) return {1, 1, (int)subt};
+  }
+  const int n = f6_nsplit_for(p, L);
+  return {0, n, tiles * n};
+}
+int f6_nsplit(const GemvArgs& p, const F6Layout& L) { return f6_plan(p, L).nsplit; }
 
 template <int T>
 void launch_prep_w(const GemvArgs& p, unsigned char* wsA, hipStream_t s) {
@@ -718,8 +802,8 @@ hipError_t launch_fp6_t(const GemvArgs& p, const void* prepA, void* ws, hipStrea
     else
       prep(prep_b_fp6<T, PREP_NB, false>, prep_b_fp6<T, 1, false>);
   }
-  const size_t lds = (size_t)F6_NBUF * F6_STAGE;
-  const int nsplit = f6_nsplit(p, L);
+  const F6Plan plan = f6_plan(p, L);
+  const int nsplit = plan.nsplit;
   float* part = reinterpret_cast<float*>(wsB + (size_t)(p.ne12 * p.ne13) * (size_t)L.b_slice);
   const unsigned char* kA = prepA ? static_cast<const unsigned char*>(prepA) : wsA;
   // LAMM_FP6_FUSED_REDUCE=1: split-K partials summed inside the launch by each tile's last
@@ -730,27 +814,37 @@ hipError_t launch_fp6_t(const GemvArgs& p, const void* prepA, void* ws, hipStrea
   const int64_t tiles = (int64_t)L.nit * L.njt * p.ne12 * p.ne13;
   const char* fr = getenv("LAMM_FP6_FUSED_REDUCE");
   unsigned* ctr = nsplit > 1 && tiles <= (int64_t)kTileCounters && fr && fr[0] == '1' ? tile_counters(s) : nullptr;
-  auto go = [&](auto kern, int nt) {
+  auto go = [&](auto kern, auto waves) {
+    using WV = decltype(waves);
+    const size_t lds = (size_t)WV::NBUF * WV::STAGE;
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(kern, dim3((unsigned)(tiles * nsplit)), dim3(nt), lds, s, p, kA,
+    hipLaunchKernelGGL(kern, dim3((unsigned)plan.grid), dim3(WV::NT), lds, s, p, kA,
                        static_cast<const unsigned char*>(wsB), nsplit, part, ctr);
   };
+  if (plan.sub == 1) {
+    go(gemm_fp6_kernel<T, 0, 2, 2, 2, 4>, F6Waves<2, 2, 2, 4>{});
+    return hipGetLastError();
+  }
+  if (plan.sub == 2) {
+    go(gemm_fp6_kernel<T, 0, 1, 2, 2, 2>, F6Waves<1, 2, 2, 2>{});
+    return hipGetLastError();
+  }
   const char* ev = getenv("LAMM_GEMM_VARIANT");
   const char* ew = getenv("LAMM_FP6_WJ");   // A/B: 1 = 16 waves of 32x64
   const int wjv = ew ? atoi(ew) : 2;
-  constexpr int NT2 = F6Waves<2>::NT;
+  using W2 = F6Waves<2>;
   switch (wjv == 1 ? -1 : ev ? atoi(ev) : 0) {
-    case -1: go(gemm_fp6_kernel<T, 0, 1>, F6Waves<1>::NT); break;
-    case 1: go(gemm_fp6_kernel<T, 1, 2>, NT2); break;
-    case 2: go(gemm_fp6_kernel<T, 2, 2>, NT2); break;
-    case 3: go(gemm_fp6_kernel<T, 3, 2>, NT2); break;
-    case 5: go(gemm_fp6_kernel<T, 5, 2>, NT2); break;
-    case 6: go(gemm_fp6_kernel<T, 6, 2>, NT2); break;
-    case 7: go(gemm_fp6_kernel<T, 7, 2>, NT2); break;
-    case 8: go(gemm_fp6_kernel<T, 8, 2>, NT2); break;
-    case 10: go(gemm_fp6_kernel<T, 10, 2>, NT2); break;
-    case 12: go(gemm_fp6_kernel<T, 12, 2>, NT2); break;
-    default: go(gemm_fp6_kernel<T, 0, 2>, NT2);
+    case -1: go(gemm_fp6_kernel<T, 0, 1>, F6Waves<1>{}); break;
+    case 1: go(gemm_fp6_kernel<T, 1, 2>, W2{}); break;
+    case 2: go(gemm_fp6_kernel<T, 2, 2>, W2{}); break;
+    case 3: go(gemm_fp6_kernel<T, 3, 2>, W2{}); break;
+    case 5: go(gemm_fp6_kernel<T, 5, 2>, W2{}); break;
+    case 6: go(gemm_fp6_kernel<T, 6, 2>, W2{}); break;
+    case 7: go(gemm_fp6_kernel<T, 7, 2>, W2{}); break;
+    case 8: go(gemm_fp6_kernel<T, 8, 2>, W2{}); break;
+    case 10: go(gemm_fp6_kernel<T, 10, 2>, W2{}); break;
+    case 12: go(gemm_fp6_kernel<T, 12, 2>, W2{}); break;
+    default: go(gemm_fp6_kernel<T, 0, 2>, W2{});
   }
   if (nsplit > 1 && !ctr) launch_splitk_reduce(p, nsplit, part, s);
   return hipGetLastError();
@@ -767,7 +861,7 @@ int gemm_fp6_tiles(const GemvArgs& p) {
 
 int gemm_fp6_grid(const GemvArgs& p) {
   const F6Layout L = F6Layout::of(p);
-  return L.nit * L.njt * p.ne12 * p.ne13 * f6_nsplit(p, L);
+  return f6_plan(p, L).grid;
 }
 
 size_t gemm_fp6_workspace_bytes(int type, const GemvArgs& p, bool prepared) {

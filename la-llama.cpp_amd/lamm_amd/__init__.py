@@ -288,7 +288,8 @@ def quantize_torch(vtype, x, y, flavour=1, stream=None):
 def gemm_engine(fmt, M, N, K, slices=1, stationary=False):
     """Which prefill engine lamm_hip_matmul* picks for N > 8 (mirrors gemm_path() in
     csrc/lamm_hip.cpp): "fp6" (q4_0/q4_1/q5_0 when its 256x128 tiles fill >= 256 CUs -- or,
-    for stationary weights (la.Weights), its tiles x K-splits do), "i8" (K-split on small grids)
+    for stationary weights (la.Weights), its 128x64 K-group tiles or tiles x K-splits do), "i8"
+    (K-split on small grids)
     otherwise; LAMM_GEMM_PATH overrides."""
     t = BY_NAME[fmt] if isinstance(fmt, str) else fmt
     env_n = os.environ.get("LAMM_GEMV_MAX_N")   # gemv_max_n() in csrc/lamm_hip.cpp
@@ -309,11 +310,16 @@ def gemm_engine(fmt, M, N, K, slices=1, stationary=False):
     tiles = -(-M // 256) * -(-N // 128) * slices
     nsteps = -(-(K // 32) // 2)
     split = int(os.environ.get("LAMM_FP6_SPLIT", "0") or 0)
-    if split <= 0:   # f6_nsplit(): double until 256 workgroups, >= 8 K-steps per split, <= 16
-        split = 1
-        while tiles * split < 256 and split < 16 and nsteps // (2 * split) >= 8:
-            split *= 2
-    grid = tiles * max(1, min(split, nsteps))
+    sub = int(os.environ.get("LAMM_FP6_SUB", "-1") or -1)
+    subt = -(-M // 128) * -(-N // 64) * slices   # f6_plan(): 128x64 tiles with K-groups
+    if split <= 0 and sub != 0 and (sub > 0 or (tiles < 256 and subt >= 256)):
+        grid = subt
+    else:
+        if split <= 0:   # f6_nsplit_for(): double until 256 workgroups, >= 8 K-steps per split, <= 16
+            split = 1
+            while tiles * split < 256 and split < 16 and nsteps // (2 * split) >= 8:
+                split *= 2
+        grid = tiles * max(1, min(split, nsteps))
     return "fp6" if (grid if stationary else tiles) >= 256 else "i8"
 
 

@@ -26,7 +26,8 @@ def _env_choices(t, N):
         return [{}]
     if t in (ol.Q4_0, ol.Q4_1, ol.Q5_0):
         return [{}, {"LAMM_GEMM_PATH": "i8"}, {"LAMM_GEMM_PATH": "fp6", "LAMM_FP6_SPLIT": "1"},
-                {"LAMM_GEMM_PATH": "fp6", "LAMM_FP6_SPLIT": "3"}]
+                {"LAMM_GEMM_PATH": "fp6", "LAMM_FP6_SPLIT": "3"}, {"LAMM_GEMM_PATH": "fp6", "LAMM_FP6_SUB": "1"},
+                {"LAMM_GEMM_PATH": "fp6", "LAMM_FP6_SUB": "2"}]
     if t in SUPER:
         return [{}, {"LAMM_KQ_VARIANT": "1"}, {"LAMM_KQ_GEMM": "0"}]
     if t in (ol.F32, ol.F16):

@@ -266,6 +266,27 @@ def test_gemm_fp6_split_k(t, split, monkeypatch):
     assert np.isnan(np.concatenate([raw[j * (M + 3) + M:(j + 1) * (M + 3)] for j in range(N)])).all()
 
 
+FP6_KG_SHAPES = [(300, 140, 4096 + 64), (257, 129, 96), (33, 17, 1024), (130, 9, 8192 + 512), (64, 64, 64)]
+
+
+@pytest.mark.parametrize("form", ["1", "2"])
+@pytest.mark.parametrize("t", FP6_TYPES, ids=[ol.NAMES[t] for t in FP6_TYPES])
+@pytest.mark.parametrize("shape", FP6_KG_SHAPES, ids=[f"{m}x{n}x{k}" for m, n, k in FP6_KG_SHAPES])
+def test_gemm_fp6_k_groups(t, shape, form, monkeypatch):
+    """fp6 engine on 128x64 workgroup tiles whose waves split K into groups summed through LDS
+    (LAMM_FP6_SUB=1: 4 groups of 64x64 waves, 2: 2 groups of 32x64 waves; automatic for grids
+    of < 256 big tiles): K-step counts that leave groups with nothing in the last stage (65,
+    2, 136 K-steps), tiles cut by M / N, C with a padded pitch."""
+    monkeypatch.setenv("LAMM_GEMM_PATH", "fp6")
+    monkeypatch.setenv("LAMM_FP6_SUB", form)
+    M, N, K = shape
+    A_q, B_q = random_case(t, M, N, K, seed=M + N + K + int(form))
+    c, raw = gpu_mul_mat(t, A_q, B_q, M, N, K, ldc=M + 3)
+    ref = ORACLE.mul_mat(t, M, N, K, A_q, B_q)
+    assert rel_err(c, ref, absdot(t, A_q, B_q, M, N, K)).max() < TOL
+    assert np.isnan(np.concatenate([raw[j * (M + 3) + M:(j + 1) * (M + 3)] for j in range(N)])).all()
+
+
 @pytest.mark.parametrize("split", [2, 3, 8])
 @pytest.mark.parametrize("t", FP6_TYPES, ids=[ol.NAMES[t] for t in FP6_TYPES])
 def test_gemm_fp6_split_k_fused_reduce_bitwise(t, split, monkeypatch):
@@ -286,14 +307,17 @@ def test_gemm_fp6_split_k_fused_reduce_bitwise(t, split, monkeypatch):
     assert rel_err(runs[0], ref, absdot(t, A_q, B_q, M, N, K)).max() < TOL
 
 
-@pytest.mark.parametrize("split", ["0", "4"])
+@pytest.mark.parametrize("split", ["0", "4", "kg1", "kg2"])
 @pytest.mark.parametrize("t", FP6_TYPES, ids=[ol.NAMES[t] for t in FP6_TYPES])
 def test_gemm_fp6_batched_broadcast(t, split, monkeypatch):
     """fp6 engine with ggml batch dims: 2 weight slices broadcast over 4 activation slices
     (r2 = 2), the unique-A-slice prep indexing of lamm_gemm_fp6.hip; split-K partials
-    indexed per slice."""
+    indexed per slice; the K-group forms' tile order over slices."""
     monkeypatch.setenv("LAMM_GEMM_PATH", "fp6")
-    monkeypatch.setenv("LAMM_FP6_SPLIT", split)
+    if split.startswith("kg"):
+        monkeypatch.setenv("LAMM_FP6_SUB", split[2:])
+    else:
+        monkeypatch.setenv("LAMM_FP6_SPLIT", split)
     M, N, K = 70, 20, 512
     kb = K // la.blck_size(t)
     vt = la.vec_dot_type(t)
@@ -743,16 +767,22 @@ def _config3_check(c, A_q, B_q, rows):
 CONFIG3_ROWS = np.unique(np.concatenate([np.arange(0, 4096, 16), [1, 127, 128, 255, 256, 2047, 2048, 4095]]))
 
 
-@pytest.mark.parametrize("path", ["stationary_fp6_auto_split", "per_call_default", "per_call_fp6", "per_call_i8"])
+@pytest.mark.parametrize("path", ["stationary_fp6_auto", "stationary_fp6_split_k", "stationary_fp6_kgroups2",
+                                  "per_call_default", "per_call_fp6", "per_call_i8"])
 def test_config3_full_size_gemm(path, monkeypatch):
     """BASELINE config 3 at its real size: Q4_0 x Q8_0 M=4096 N=512 K=4096, one slice.
-    Paths: the weight-stationary handle (the ggml boundary's and bench.py's; fp6 engine with its
-    automatic K-split over 64 tiles), the per-call API's default engine (i8, split-K), and both
-    engines forced per call.  >= 256 sampled rows x all 512 columns vs the oracle."""
+    Paths: the weight-stationary handle (the ggml boundary's and bench.py's; fp6 engine, by
+    default 256 128x64 tiles with 4 K-groups each, or forced: K split over the 64 256x128 tiles,
+    2 K-groups), the per-call API's default engine, and both engines forced per call.  >= 256
+    sampled rows x all 512 columns vs the oracle."""
     M, N, K = 4096, 512, 4096
     (A_q,), (B_q,) = _config3_operands(2024, 1)
     if path in ("per_call_fp6", "per_call_i8"):
         monkeypatch.setenv("LAMM_GEMM_PATH", path.rsplit("_", 1)[1])
+    if path == "stationary_fp6_split_k":
+        monkeypatch.setenv("LAMM_FP6_SUB", "0")
+    if path == "stationary_fp6_kgroups2":
+        monkeypatch.setenv("LAMM_FP6_SUB", "2")
     A = dev_bytes(np.concatenate([A_q, np.zeros(64, np.uint8)]))
     B = dev_bytes(B_q)
     C = torch.full((N * M,), float("nan"), dtype=torch.float32, device="cuda")

@@ -44,6 +44,7 @@ namespace {
 
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 #ifndef F6_KB_CFG
 #define F6_KB_CFG 2
@@ -341,7 +342,12 @@ template <int WJ, int SI = 1, int SJ = 1, int KG = 1> struct F6Waves {
   static_assert(TI % 64 == 0 && TJ % 64 == 0 && NWJ >= 1, "tile");
   static_assert(NBUF >= 2, "LDS stages");
   static_assert(STAGE % (NW * F6_PIECE) == 0, "every wave moves the same number of DMA pieces");
-  static_assert((KG - 1) * NWG * WJ * 8192 <= NBUF * STAGE, "K-group sums fit the stages");
+  // K-group epilogue: every wave's partial tile as [group][j][i] rows padded by 8 floats (the
+  // two half-waves' rows j and j+4 then fall on disjoint banks)
+  static constexpr int RED = KG > 1 ? KG * TJ * (TI + 8) * 4 : 0;
+  static constexpr int LDS = NBUF * STAGE > RED ? NBUF * STAGE : RED;
+  static_assert(LDS <= 160 * 1024, "LDS");
+  static_assert(KG == 1 || (TI == 128 && TJ % NW == 0), "K-group epilogue: a lane stores 2 of a 128-float row");
   static constexpr int PPW = STAGE / F6_PIECE / NW;   // DMA pieces per wave per stage
   // LDS byte offsets inside one K-step's sub-stage (the chunk image with TI / TJ rows)
   __device__ static constexpr int aoff(int p, int b, int r) { return ((p * F6_KB + b) * TI + r) * 16; }
@@ -352,10 +358,16 @@ template <int WJ, int SI = 1, int SJ = 1, int KG = 1> struct F6Waves {
 // nsplit runs K-steps [s*nsteps/nsplit, (s+1)*nsteps/nsplit) and writes its partial tile to
 // part[s][z][j][i]; f6_reduce then sums the splits in order 0..nsplit-1 (deterministic).
 // nsplit == 1 writes C directly.
-template <int T, int V, int WJ, int SI = 1, int SJ = 1, int KG = 1>
+template <int T, int V_, int WJ, int SI = 1, int SJ = 1, int KG = 1>
 __global__ __launch_bounds__((F6Waves<WJ, SI, SJ, KG>::NT)) void gemm_fp6_kernel(GemvArgs p, const unsigned char* wsA,
                                                                                 const unsigned char* wsB, int nsplit,
                                                                                 float* part, unsigned* tile_ctr) {
+  // V_ >= 20: clock probe of ablation V_ - 20 (tools/clk_probe.py): instead of C, thread 0 of
+  // workgroup b writes C[2b] = shader clocks (s_memtime) and C[2b+1] = 100 MHz ticks
+  // (s_memrealtime) spent from entry to the end of the main loop
+  constexpr int V = V_ >= 20 ? V_ - 20 : V_;
+  constexpr bool CLK = V_ >= 20;
+  const uint64_t clk0 = CLK ? __builtin_readcyclecounter() : 0, rt0 = CLK ? __builtin_amdgcn_s_memrealtime() : 0;
   using F = F6<T>;
   using WV = F6Waves<WJ, SI, SJ, KG>;
   constexpr int F6_NW = WV::NW, F6_PPW = WV::PPW, UPB = 2 * WJ;   // UPB: units per block
@@ -551,32 +563,65 @@ __global__ __launch_bounds__((F6Waves<WJ, SI, SJ, KG>::NT)) void gemm_fp6_kernel
   }
 
   if (pend) epi(NU - 1, rr[(NU - 1) % (F6_PD + 1)]);
+  if constexpr (CLK) {
+    float sink = 0.f;   // keep the main loop's arithmetic alive and ordered before the stamp
+#pragma unroll
+    for (int x = 0; x < WJ; ++x)
+#pragma unroll
+      for (int y = 0; y < 2; ++y)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) sink += acc[x][y][e];
+    asm volatile("s_nop 0" ::"v"(sink) : "memory");
+    const uint64_t clk1 = __builtin_readcyclecounter(), rt1 = __builtin_amdgcn_s_memrealtime();
+    if (sink == -1.2345e-30f) p.C[4096 + t] = sink;
+    if (t == 0) {
+      p.C[2 * blockIdx.x] = (float)(clk1 - clk0);
+      p.C[2 * blockIdx.x + 1] = (float)(rt1 - rt0);
+    }
+    return;
+  }
   if constexpr (KG > 1) {
-    // K-groups 1..KG-1 hand their sums to group 0 through the (now idle) stages; group 0 adds
-    // them in group order.  Layout [group-1][wave][x][y][e][lane]: a wave's dword per lane,
-    // conflict-free.
+    // Every wave parks its partial tile in the (now idle) stages; then the tile's rows are split
+    // over ALL waves: wave w sums rows j = w*RPW.. over the groups in group order (the bits of
+    // "group 0 adds groups 1, 2, 3"), and stores them as 512-byte runs of C (2 floats a lane)
+    // -- instead of group 0's two waves alone adding and storing 4-byte pieces
+    // (profiles/r02/fp6_kgroups_ablation.txt: that epilogue cost ~4 us of a 30 us kernel).
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     float* red = reinterpret_cast<float*>(smem);
-    auto at = [&](int g_, int x, int y, int e) { return ((((g_ - 1) * WV::NWG + wl) * WJ + x) * 2 + y) * 16 * 64 + e * 64 + lane; };
-    if (g > 0) {
+    constexpr int PI = TI + 8, RPW = TJ / F6_NW;
 #pragma unroll
-      for (int x = 0; x < WJ; ++x)
+    for (int x = 0; x < WJ; ++x)
 #pragma unroll
-        for (int y = 0; y < 2; ++y)
+      for (int y = 0; y < 2; ++y)
 #pragma unroll
-          for (int e = 0; e < 16; ++e) red[at(g, x, y, e)] = acc[x][y][e];
-    }
+        for (int e = 0; e < 16; ++e) {
+          const int i = 64 * wi + 32 * y + lr, j = 32 * WJ * wj + 32 * x + (e & 3) + 8 * (e >> 2) + 4 * h;
+          red[(g * TJ + j) * PI + i] = acc[x][y][e];
+        }
     __syncthreads();
-    if (g > 0) return;
-#pragma unroll 1
-    for (int g_ = 1; g_ < KG; ++g_)
+    float* C = p.C + (int64_t)i12 * p.sc2 + (int64_t)i13 * p.sc3;
+    const int64_t i = (int64_t)ti * TI + 2 * lane;
+    const bool pair = i + 1 < p.M && (p.ldc & 1) == 0 && ((uintptr_t)C & 7) == 0;
 #pragma unroll
-      for (int x = 0; x < WJ; ++x)
+    for (int q = 0; q < RPW; ++q) {
+      const int jl = w * RPW + q;
+      const int64_t j = (int64_t)tj * TJ + jl;
+      f32x2 v = *reinterpret_cast<const f32x2*>(&red[jl * PI + 2 * lane]);
 #pragma unroll
-        for (int y = 0; y < 2; ++y)
-#pragma unroll
-          for (int e = 0; e < 16; ++e) acc[x][y][e] += red[at(g_, x, y, e)];
+      for (int g_ = 1; g_ < KG; ++g_) v += *reinterpret_cast<const f32x2*>(&red[(g_ * TJ + jl) * PI + 2 * lane]);
+      v *= 0.5f;
+      if (j < p.N) {
+        float* c = C + j * p.ldc + i;
+        if (pair) {
+          *reinterpret_cast<f32x2*>(c) = v;
+        } else {
+          if (i < p.M) c[0] = v[0];
+          if (i + 1 < p.M) c[1] = v[1];
+        }
+      }
+    }
+    return;
   }
   float* Cz;
   int64_t ldc;
@@ -816,20 +861,36 @@ hipError_t launch_fp6_t(const GemvArgs& p, const void* prepA, void* ws, hipStrea
   unsigned* ctr = nsplit > 1 && tiles <= (int64_t)kTileCounters && fr && fr[0] == '1' ? tile_counters(s) : nullptr;
   auto go = [&](auto kern, auto waves) {
     using WV = decltype(waves);
-    const size_t lds = (size_t)WV::NBUF * WV::STAGE;
+    const size_t lds = (size_t)WV::LDS;
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(kern, dim3((unsigned)plan.grid), dim3(WV::NT), lds, s, p, kA,
                        static_cast<const unsigned char*>(wsB), nsplit, part, ctr);
   };
+  const char* ev = getenv("LAMM_GEMM_VARIANT");
   if (plan.sub == 1) {
-    go(gemm_fp6_kernel<T, 0, 2, 2, 2, 4>, F6Waves<2, 2, 2, 4>{});
+    using WK = F6Waves<2, 2, 2, 4>;
+    // ablations of the K-group form (q4_0 only, tools/ab_kg.sh, profiles/r02/fp6_kgroups_ablation.txt):
+    // 1 no compute, 2 no DMA, 3 no epilogue FMAs, 4 no DMA + no LDS fragment reads, 6 no P-MFMA,
+    // 7 no S-MFMA
+    switch (T == kQ4_0 && ev ? atoi(ev) : 0) {
+      case 1: go(gemm_fp6_kernel<T, 1, 2, 2, 2, 4>, WK{}); break;
+      case 2: go(gemm_fp6_kernel<T, 2, 2, 2, 2, 4>, WK{}); break;
+      case 3: go(gemm_fp6_kernel<T, 3, 2, 2, 2, 4>, WK{}); break;
+      case 4: go(gemm_fp6_kernel<T, 4, 2, 2, 2, 4>, WK{}); break;
+      case 6: go(gemm_fp6_kernel<T, 6, 2, 2, 2, 4>, WK{}); break;
+      case 7: go(gemm_fp6_kernel<T, 7, 2, 2, 2, 4>, WK{}); break;
+      case 20: go(gemm_fp6_kernel<T, 20, 2, 2, 2, 4>, WK{}); break;
+      case 21: go(gemm_fp6_kernel<T, 21, 2, 2, 2, 4>, WK{}); break;
+      case 22: go(gemm_fp6_kernel<T, 22, 2, 2, 2, 4>, WK{}); break;
+      case 24: go(gemm_fp6_kernel<T, 24, 2, 2, 2, 4>, WK{}); break;
+      default: go(gemm_fp6_kernel<T, 0, 2, 2, 2, 4>, WK{});
+    }
     return hipGetLastError();
   }
   if (plan.sub == 2) {
     go(gemm_fp6_kernel<T, 0, 1, 2, 2, 2>, F6Waves<1, 2, 2, 2>{});
     return hipGetLastError();
   }
-  const char* ev = getenv("LAMM_GEMM_VARIANT");
   const char* ew = getenv("LAMM_FP6_WJ");   // A/B: 1 = 16 waves of 32x64
   const int wjv = ew ? atoi(ew) : 2;
   using W2 = F6Waves<2>;

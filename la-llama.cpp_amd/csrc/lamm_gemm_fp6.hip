@@ -122,8 +122,7 @@ __device__ __forceinline__ void load_block(__amdgpu_buffer_rsrc_t r, uint32_t of
   const uint32_t base = off & ~3u;
   const int sh = (int)(off & 3u) * 8;
   uint32_t w[NW + 1];
-#pragma unroll
-  for (int k = 0; k <= NW; ++k) w[k] = bload4(r, base + 4 * k);
+  load_words<NW + 1, 0>(r, base, w);   // wide loads (b128 / b64 / b32) from the dword below
 #pragma unroll
   for (int k = 0; k < NW; ++k) m[k] = __builtin_amdgcn_alignbit(w[k + 1], w[k], sh);
 }

@@ -800,6 +800,36 @@ def test_config3_full_size_gemm(path, monkeypatch):
     assert err < TOL
 
 
+@pytest.mark.parametrize("act", ["q8", "f32"])
+def test_config3_repeated_calls_fresh_activations(act, monkeypatch):
+    """Config 3, three calls with DIFFERENT activations into the same per-stream workspace (B1,
+    B2, B1): the packed activation tiles the prep writes there and the main kernel reads back
+    must never be served stale from an earlier call.  q8 rows through the weight-stationary
+    handle, or F32 rows (quantized on the device) through the per-call API."""
+    M, N, K = 4096, 512, 4096
+    rng = np.random.default_rng(77)
+    (A_q,), _ = _config3_operands(2025, 1)
+    xs = [rng.standard_normal((N, K), dtype=np.float32) for _ in range(2)]
+    Bq = [ORACLE.quantize(ol.Q8_0, x, ol.QUANT_AVX) for x in xs]
+    A = dev_bytes(np.concatenate([A_q, np.zeros(64, np.uint8)]))
+    W = la.Weights(ol.Q4_0, A, M, K)
+    rows = CONFIG3_ROWS[::2]
+    s = torch.cuda.current_stream().cuda_stream
+    monkeypatch.setenv("LAMM_GEMM_PATH", "fp6")   # the F32 calls go through the per-call API
+    for k in (0, 1, 0):
+        C = torch.full((N * M,), float("nan"), dtype=torch.float32, device="cuda")
+        if act == "q8":
+            W.matmul_torch(dev_bytes(Bq[k]), C, N)
+        else:
+            X = torch.from_numpy(xs[k]).cuda()
+            la.matmul(la.Matrix(A.data_ptr(), ol.Q4_0, M, K // 32, K // 32), la.Matrix(X.data_ptr(), la.F32, K, N, K),
+                      la.Matrix(C.data_ptr(), la.F32, M, N, M), s)
+        torch.cuda.synchronize()
+        err = _config3_check(C.cpu().numpy().reshape(N, M), A_q, Bq[k], rows)
+        assert err < TOL, (k, err)
+    W.close()
+
+
 def test_config3_four_slice_batched_launch():
     """The 4-slice batched launch bench.py times (ne02 = ne12 = 4, stationary weights, fp6
     engine with 256 tiles): every slice's sampled rows x all columns vs the oracle."""

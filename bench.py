@@ -251,8 +251,10 @@ def config2_gemv(ctx, fmt, M, K, steps, warmup):
         a = A[(last % R) * slab_bytes:(last % R + 1) * slab_bytes].view(M, arow)
         sample.update(A=a[sample["rows"]].cpu().numpy(), B=B[:la.row_bytes(vt, K)].cpu().numpy(),
                       C=gathered[sample["rows"]].cpu().numpy())
-    # the rank's kernel alone (no collective): roofline numerator
-    _, kern, _ = time_steps(ctx, gemv, max(steps, 50), 3)
+    # the rank's kernel alone (no collective): roofline numerator.  1000 launches per graph: the
+    # replay's own start-up (~20-30 us before the first kernel runs) spread over 50 launches of a
+    # ~4 us kernel added ~0.6 us to every launch (profiles/r02/ab_gemv_waves.json: 4.17 us at 200)
+    _, kern, _ = time_steps(ctx, gemv, max(steps, 1000), 3)
     res = dict(per_step=per_step, ev_step=ev_step, kern=kern, graphed=graphed, R=R, rows=rows,
                slab_bytes=slab_bytes + la.row_bytes(vt, K) + 4 * rows, gather_check=check, sample=sample)
     del A, B, C
@@ -325,7 +327,7 @@ def config3_gemm(ctx, fmt, M, N, K, slices, steps):
                                     [torch.cuda.current_stream().cuda_stream])
 
     per_step, _, _ = time_steps(ctx, step, steps, 2, graph=not ctx.rehearse)
-    _, kern, _ = time_steps(ctx, gemm, steps, 2)
+    _, kern, _ = time_steps(ctx, gemm, max(steps, 200), 2)   # (graph start-up amortized, as for config 2)
     # main loop alone: LAMM_GEMM_SKIP_PREP re-runs the main kernel on the prepared workspace
     os.environ["LAMM_GEMM_SKIP_PREP"] = "1"
     try:

@@ -488,14 +488,14 @@ __global__ __launch_bounds__((F6Waves<WJ, SI, SJ, KG>::NT)) void gemm_fp6_kernel
     // (8 waves x 4*KB ds_read_b128 pairs right after the barrier queue hundreds of LDS cycles
     // in front of every wave's first MFMA).  Block b lives in register slot b & 1.
     auto ldB = [&](int b, int x) {
-      if constexpr (V == 4) {
+      if constexpr (V == 4 || V == 11) {   // 11: DMA on, fragments read once
         if (ss > s0) return;
       }
       const int r = 32 * WJ * wj + 32 * x + lr;
       f6_load(fb[b & 1][x], sB + WV::boff(0, b, h, r), sB + WV::boff(1, b, h, r));
     };
     auto ldA = [&](int b, int y) {
-      if constexpr (V == 4) {
+      if constexpr (V == 4 || V == 11) {   // 11: DMA on, fragments read once
         if (ss > s0) return;
       }
       const int r = 64 * wi + 32 * y + lr;
@@ -870,7 +870,7 @@ hipError_t launch_fp6_t(const GemvArgs& p, const void* prepA, void* ws, hipStrea
     using WK = F6Waves<2, 2, 2, 4>;
     // ablations of the K-group form (q4_0 only, tools/ab_kg.sh, profiles/r02/fp6_kgroups_ablation.txt):
     // 1 no compute, 2 no DMA, 3 no epilogue FMAs, 4 no DMA + no LDS fragment reads, 6 no P-MFMA,
-    // 7 no S-MFMA
+    // 7 no S-MFMA, 11 DMA but no LDS fragment reads; 20 + V: in-kernel clock probe of V
     switch (T == kQ4_0 && ev ? atoi(ev) : 0) {
       case 1: go(gemm_fp6_kernel<T, 1, 2, 2, 2, 4>, WK{}); break;
       case 2: go(gemm_fp6_kernel<T, 2, 2, 2, 2, 4>, WK{}); break;
@@ -882,6 +882,8 @@ hipError_t launch_fp6_t(const GemvArgs& p, const void* prepA, void* ws, hipStrea
       case 21: go(gemm_fp6_kernel<T, 21, 2, 2, 2, 4>, WK{}); break;
       case 22: go(gemm_fp6_kernel<T, 22, 2, 2, 2, 4>, WK{}); break;
       case 24: go(gemm_fp6_kernel<T, 24, 2, 2, 2, 4>, WK{}); break;
+      case 11: go(gemm_fp6_kernel<T, 11, 2, 2, 2, 4>, WK{}); break;
+      case 31: go(gemm_fp6_kernel<T, 31, 2, 2, 2, 4>, WK{}); break;
       default: go(gemm_fp6_kernel<T, 0, 2, 2, 2, 4>, WK{});
     }
     return hipGetLastError();

@@ -27,7 +27,7 @@ def main():
     C = torch.zeros(N * M, dtype=torch.float32, device="cuda")
     W = la.Weights(la.Q4_0, A, M, K)
     out = {}
-    for v in (0, 1, 2, 4):
+    for v in (0, 1, 2, 4, 11):
         os.environ["LAMM_GEMM_VARIANT"] = str(20 + v)
         runs = []
         for rep in range(12):

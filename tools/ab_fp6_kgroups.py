@@ -3,7 +3,7 @@
 workgroup tiles with K-groups (1: 4 groups of 64x64 waves, 2: 2 groups of 32x64 waves), on
 config 3 (4096x512x4096, one slice and four) and the Llama-7B prefill shapes (N=512: q/k/v/o
 4096x4096, gate/up 11008x4096, down 4096x11008).  hipGraph-replayed whole launches (bench.py's
-time_steps), interleaved arms, medians; one JSON line."""
+time_steps), interleaved arms, medians; one JSON line.  ABVAR / ARMS pick another switch."""
 import json
 import os
 import statistics
@@ -20,6 +20,7 @@ import bench  # noqa: E402
 SHAPES = [("config3_1slice", 4096, 512, 4096, 1), ("config3_4slices", 4096, 512, 4096, 4),
           ("gate_up", 11008, 512, 4096, 1), ("down", 4096, 512, 11008, 1)]
 ARMS = os.environ.get("ARMS", "0,1,2").split(",")
+ABVAR = os.environ.get("ABVAR", "LAMM_FP6_SUB")   # the switch the arms set (e.g. LAMM_PREP_HSPLIT)
 
 
 def main():
@@ -40,7 +41,7 @@ def main():
         ref = None
         for rep in range(5):
             for arm in ARMS:
-                os.environ["LAMM_FP6_SUB"] = arm
+                os.environ[ABVAR] = arm
 
                 def step(i):
                     W.matmul_torch(B, C, N, batch=bt, stream=torch.cuda.current_stream().cuda_stream)
@@ -62,7 +63,7 @@ def main():
         W.close()
         del A, B, C, W
         torch.cuda.empty_cache()
-    os.environ.pop("LAMM_FP6_SUB", None)
+    os.environ.pop(ABVAR, None)
     print(json.dumps(out))
 
 

@@ -58,6 +58,9 @@ constexpr int F6_TJ = 128;      // activation rows per tile
 constexpr int F6_PIECE = 1024;  // bytes one wave moves per LDS-DMA instruction (64 lanes x 16 B)
 constexpr int F6_NBUF = F6_NBUF_CFG;   // LDS stages (3 K-steps of DMA in flight)
 constexpr int SCALE_W = 130, SCALE_HI = 134, SCALE_LO = 130;   // E8M0: 2^(s-127)
+#ifndef F6_C_NT
+#define F6_C_NT 0   // 1: the K-group epilogue's C stores non-temporal (A/B build, tools/ab_c_nt.sh)
+#endif
 #ifndef F6_PD
 #define F6_PD 1   // MFMA pipeline depth: unit n+PD's MFMAs are issued before unit n's FMAs (2: no gain, +20 VGPRs)
 #endif
@@ -288,87 +291,6 @@ __global__ __launch_bounds__(PREP_NT) void prep_b_fp6(GemvArgs p, unsigned char*
     *(u32x4*)(ch + f6_boff(1, b, 0, r)) = u32x4{oh[4], oh[5], d, sv};
     *(u32x4*)(ch + f6_boff(0, b, 1, r)) = u32x4{ol[0], ol[1], ol[2], ol[3]};
     *(u32x4*)(ch + f6_boff(1, b, 1, r)) = u32x4{ol[4], ol[5], d, sv};
-  }
-}
-
-// Plane-split activation prep (default): the same bytes as prep_b_fp6, but each wave writes
-// ONE k-group plane (wave-uniform h: 0 = hi codes, 1 = lo codes) of 64 rows, so a workgroup of
-// PREP_NT threads covers PREP_RW = PREP_NT / 2 rows and the grid has twice the waves (config 3:
-// 1 -> 2 per SIMD), and the codes are built four at a time in SWAR form (byte lanes of a dword)
-// instead of one element at a time:
-//   lo code  = q & 15                                  -> w & 0x0f0f0f0f
-//   hi code  = sm_code(q >> 4): u = high nibble (0..15), u < 8 -> u, else 32 | (16 - u) = 48 - u
-//   4 byte codes -> 24 bits (6 bits each), 8 groups -> the 192-bit fragment (code e at bit 6e).
-constexpr int PREP_RW = PREP_NT / 2;
-
-__device__ __forceinline__ uint32_t f6_hi_codes4(uint32_t w) {
-  const uint32_t u = (w >> 4) & 0x0f0f0f0fu;
-  const uint32_t neg = ((u >> 3) & 0x01010101u) * 0xffu;   // byte mask: u >= 8
-  return ((0x30303030u - u) & neg) | (u & ~neg);           // no borrows: u <= 15 < 48
-}
-__device__ __forceinline__ uint32_t f6_group24(uint32_t x) {   // bytes (6-bit codes) -> 24 bits
-  x = (x & 0x003f003fu) | ((x >> 2) & 0x0fc00fc0u);
-  return (x & 0x00000fffu) | ((x >> 4) & 0x00fff000u);
-}
-__device__ __forceinline__ void f6_pack_groups(const uint32_t (&c4)[8], uint32_t (&o)[6]) {
-  uint32_t g[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) g[k] = f6_group24(c4[k]);
-  o[0] = g[0] | (g[1] << 24);
-  o[1] = (g[1] >> 8) | (g[2] << 16);
-  o[2] = (g[2] >> 16) | (g[3] << 8);
-  o[3] = g[4] | (g[5] << 24);
-  o[4] = (g[5] >> 8) | (g[6] << 16);
-  o[5] = (g[6] >> 16) | (g[7] << 8);
-}
-
-template <int T, int NB, bool BF32>
-__global__ __launch_bounds__(PREP_NT) void prep_b_fp6_hs(GemvArgs p, unsigned char* ws) {
-  using F = F6<T>;
-  constexpr int VBPB = F::VBPB, VQS = VBPB == 36 ? 4 : 2;
-  const F6Layout L = F6Layout::of(p);
-  const int nkg = (L.nsteps * F6_KB + NB - 1) / NB;
-  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int h = __builtin_amdgcn_readfirstlane(wv & 1);
-  const int64_t jw = (int64_t)(blockIdx.x / nkg) * PREP_RW;
-  const int64_t j = jw + (wv >> 1) * 64 + lane;
-  const int kb0 = (blockIdx.x % nkg) * NB;
-  const int z = blockIdx.y, i12 = z % p.ne12, i13 = z / p.ne12;
-  if (j >= (int64_t)L.njt * F6_TJ) return;
-  const int jt = (int)(j / F6_TJ), r = (int)(j % F6_TJ);
-  unsigned char* wsb = ws + (int64_t)z * L.b_slice + (int64_t)jt * L.nsteps * F6_B_BYTES;
-  // resource based at the workgroup's first row (wave-uniform, offsets < 2^31), as prep_b_fp6
-  const int64_t nrow = min((int64_t)PREP_RW, (int64_t)p.N - jw);
-  const unsigned char* Bz = p.B + (int64_t)i12 * p.sb2 + (int64_t)i13 * p.sb3 + min(jw, (int64_t)p.N) * p.ldb;
-  const int64_t bbytes = nrow > 0 ? (nrow - 1) * p.ldb + (int64_t)p.nblk * (BF32 ? 128 : VBPB) : 0;
-  const auto rs = make_rsrc(Bz, (uint32_t)min((bbytes + 3) & ~int64_t(3), (int64_t)0x7fffffff));
-  for (int kb = kb0; kb < kb0 + NB && kb < L.nsteps * F6_KB; ++kb) {
-    uint32_t q8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    uint32_t d = 0, sv = 0;
-    if (j < p.N && kb < p.nblk) {
-      if constexpr (BF32) {
-        uint32_t x[32];
-        uint16_t dh, sh;
-        load_words<32, 0>(rs, (uint32_t)((j - jw) * p.ldb + (int64_t)kb * 128), x);
-        q8_from_f32<VBPB == 36>(x, q8, dh, sh);
-        d = dh;
-        sv = sh;
-      } else {
-        uint32_t m[9];
-        load_block<9>(rs, (uint32_t)((j - jw) * p.ldb + (int64_t)kb * VBPB), m);
-        d = m[0] & 0xffffu;
-        if constexpr (VBPB == 36) sv = m[0] >> 16;
-        unroll<8>([&](auto K) { q8[K] = get32<VQS + 4 * K>(m); });
-      }
-    }
-    uint32_t c4[8], o[6];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) c4[k] = h == 0 ? f6_hi_codes4(q8[k]) : (q8[k] & 0x0f0f0f0fu);
-    f6_pack_groups(c4, o);
-    unsigned char* ch = wsb + (int64_t)(kb / F6_KB) * F6_B_BYTES;
-    const int b = kb % F6_KB;
-    *(u32x4*)(ch + f6_boff(0, b, h, r)) = u32x4{o[0], o[1], o[2], o[3]};
-    *(u32x4*)(ch + f6_boff(1, b, h, r)) = u32x4{o[4], o[5], d, sv};
   }
 }
 
@@ -694,7 +616,11 @@ __global__ __launch_bounds__((F6Waves<WJ, SI, SJ, KG>::NT)) void gemm_fp6_kernel
       if (j < p.N) {
         float* c = C + j * p.ldc + i;
         if (pair) {
+#if F6_C_NT
+          __builtin_nontemporal_store(v, reinterpret_cast<f32x2*>(c));
+#else
           *reinterpret_cast<f32x2*>(c) = v;
+#endif
         } else {
           if (i < p.M) c[0] = v[0];
           if (i + 1 < p.M) c[1] = v[1];
@@ -912,12 +838,7 @@ hipError_t launch_fp6_t(const GemvArgs& p, const void* prepA, void* ws, hipStrea
   const char* sp = getenv("LAMM_GEMM_SKIP_PREP");
   if (!(sp && sp[0] == '1')) {
     if (!prepA) launch_prep_w<T>(p, wsA, s);
-    // LAMM_PREP_HSPLIT=1: the plane-split prep (A/B against the one-thread-per-(row, block)
-    // prep; same bytes)
-    const char* ehs = getenv("LAMM_PREP_HSPLIT");
-    const bool hs = ehs && ehs[0] == '1';
-    const int rw = hs ? PREP_RW : PREP_NT;
-    const int rgroups = (L.njt * F6_TJ + rw - 1) / rw, nb_all = L.nsteps * F6_KB;
+    const int rgroups = (L.njt * F6_TJ + PREP_NT - 1) / PREP_NT, nb_all = L.nsteps * F6_KB;
     auto prep = [&](auto kmulti, auto kone) {
       if ((int64_t)rgroups * ((nb_all + PREP_NB - 1) / PREP_NB) * p.ne12 * p.ne13 >= 256)
         hipLaunchKernelGGL(kmulti,
@@ -927,16 +848,10 @@ hipError_t launch_fp6_t(const GemvArgs& p, const void* prepA, void* ws, hipStrea
         hipLaunchKernelGGL(kone, dim3((unsigned)(rgroups * nb_all), (unsigned)(p.ne12 * p.ne13)), dim3(PREP_NT), 0, s,
                            p, wsB);
     };
-    if (hs) {
-      if (p.b_f32)
-        prep(prep_b_fp6_hs<T, PREP_NB, true>, prep_b_fp6_hs<T, 1, true>);
-      else
-        prep(prep_b_fp6_hs<T, PREP_NB, false>, prep_b_fp6_hs<T, 1, false>);
-    } else if (p.b_f32) {
+    if (p.b_f32)
       prep(prep_b_fp6<T, PREP_NB, true>, prep_b_fp6<T, 1, true>);
-    } else {
+    else
       prep(prep_b_fp6<T, PREP_NB, false>, prep_b_fp6<T, 1, false>);
-    }
   }
   const F6Plan plan = f6_plan(p, L);
   const int nsplit = plan.nsplit;

@@ -741,47 +741,6 @@ def test_gemm_f32_activations(t, path, N, monkeypatch):
     assert rel_err(a.reshape(N, M), ref, absdot(t, A_q, B_q, M, N, K)).max() < TOL
 
 
-PREP_HS_CASES = [(t, f32, N) for t in (ol.Q4_0, ol.Q4_1, ol.Q5_0) for f32 in (False, True) for N in (9, 200, 700)]
-
-
-@pytest.mark.parametrize("t,f32,N", PREP_HS_CASES,
-                         ids=[f"{ol.NAMES[t]}-{'f32' if f else 'q8'}-N{N}" for t, f, N in PREP_HS_CASES])
-def test_fp6_prep_plane_split_bitwise(t, f32, N, monkeypatch):
-    """The plane-split fp6 activation prep (prep_b_fp6_hs: one k-group plane per wave, SWAR
-    codes; default) writes the same workspace bytes as the one-thread-per-block prep
-    (LAMM_PREP_HSPLIT=0): C bit-identical, ragged N / K (zero-padded rows and blocks), q8 and F32
-    activations, single-row-group (N < 128) and multi-block-per-thread (N = 700) grids."""
-    monkeypatch.setenv("LAMM_GEMM_PATH", "fp6")
-    M, K = 300, 4096 + 96
-    rng = np.random.default_rng(N * 7 + t)
-    A_q = ORACLE.quantize(t, rng.standard_normal((M, K), dtype=np.float32))
-    x = rng.standard_normal((N, K), dtype=np.float32) * 3.0
-    x[1, 64:96] = 0.0                                  # an all-zero block (d = 0)
-    kb = K // 32
-    lda = pitch_blocks(t, kb)
-    dA = dev_bytes(pitched_A(t, A_q, M, kb, lda))
-    vt = ORACLE.vec_dot_type(t)
-    if f32:
-        dB = torch.from_numpy(x.reshape(-1)).cuda()
-        Bm = la.Matrix(dB.data_ptr(), la.F32, K, N, K)
-        B_q = ORACLE.quantize(vt, x, ol.QUANT_AVX)
-    else:
-        B_q = ORACLE.quantize(vt, x, ol.QUANT_AVX)
-        dB = dev_bytes(B_q)
-        Bm = la.Matrix(dB.data_ptr(), vt, kb, N, kb)
-    s = torch.cuda.current_stream().cuda_stream
-    outs = []
-    for hs in ("1", "0"):
-        monkeypatch.setenv("LAMM_PREP_HSPLIT", hs)
-        c = torch.full((N * M,), np.nan, dtype=torch.float32, device="cuda")
-        la.matmul(la.Matrix(dA.data_ptr(), t, M, kb, lda), Bm, la.Matrix(c.data_ptr(), la.F32, M, N, M), s)
-        torch.cuda.synchronize()
-        outs.append(c.cpu().numpy())
-    assert np.array_equal(outs[0].view(np.uint32), outs[1].view(np.uint32))
-    ref = ORACLE.mul_mat(t, M, N, K, A_q, B_q)
-    assert rel_err(outs[0].reshape(N, M), ref, absdot(t, A_q, B_q, M, N, K)).max() < TOL
-
-
 # ---------------------------------------------------------------- BASELINE config 3, full size
 def _config3_operands(seed, slices):
     """Q4_0 A (4096 x 4096, `slices` distinct slices) quantized from N(0,1) by the oracle's

@@ -59,7 +59,11 @@ constexpr int F6_PIECE = 1024;  // bytes one wave moves per LDS-DMA instruction 
 constexpr int F6_NBUF = F6_NBUF_CFG;   // LDS stages (3 K-steps of DMA in flight)
 constexpr int SCALE_W = 130, SCALE_HI = 134, SCALE_LO = 130;   // E8M0: 2^(s-127)
 #ifndef F6_C_NT
-#define F6_C_NT 0   // 1: the K-group epilogue's C stores non-temporal (A/B build, tools/ab_c_nt.sh)
+// The K-group epilogue's C stores are non-temporal: C is written once and not re-read by this
+// launch, so streaming it past L2 leaves the end-of-launch L2 write-back nothing of it to flush
+// (config 3, one slice: whole launch 36.2 -> 35.1 us on one box, profiles/r02/ab_c_nt/).
+// 0: cached stores (A/B build, tools/ab_c_nt.sh).
+#define F6_C_NT 1
 #endif
 #ifndef F6_PD
 #define F6_PD 1   // MFMA pipeline depth: unit n+PD's MFMAs are issued before unit n's FMAs (2: no gain, +20 VGPRs)

@@ -26,7 +26,10 @@ ABVAR = os.environ.get("ABVAR", "LAMM_FP6_SUB")   # the switch the arms set (e.g
 def main():
     ctx = bench.Ctx(torch, la)
     out = {}
+    only = os.environ.get("SHAPES")   # comma-separated subset of the shape names
     for name, M, N, K, slices in SHAPES:
+        if only and name not in only.split(","):
+            continue
         t = la.Q4_0
         gen = torch.Generator(device="cuda")
         gen.manual_seed(5)

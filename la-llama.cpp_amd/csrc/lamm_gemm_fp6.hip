@@ -65,6 +65,12 @@ constexpr int SCALE_W = 130, SCALE_HI = 134, SCALE_LO = 130;   // E8M0: 2^(s-127
 // 0: cached stores (A/B build, tools/ab_c_nt.sh).
 #define F6_C_NT 1
 #endif
+#ifndef F6_CT_NT
+// The whole-tile (KG = 1) epilogue's C / split-K partial stores are non-temporal too (config 3,
+// four slices: 93.0 -> 89.7 us whole launch, mean of 3 alternating pairs on one box,
+// profiles/r02/ab_c_nt/ab_ct_nt.txt).  0: cached stores (A/B build, tools/ab_ct_nt.sh).
+#define F6_CT_NT 1
+#endif
 #ifndef F6_PD
 #define F6_PD 1   // MFMA pipeline depth: unit n+PD's MFMAs are issued before unit n's FMAs (2: no gain, +20 VGPRs)
 #endif
@@ -652,7 +658,13 @@ __global__ __launch_bounds__((F6Waves<WJ, SI, SJ, KG>::NT)) void gemm_fp6_kernel
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
           const int64_t j = (int64_t)tj * TJ + 32 * WJ * wj + 32 * x + (e & 3) + 8 * (e >> 2) + 4 * h;
-          if (i < p.M && j < p.N) Cz[j * ldc + i] = 0.5f * acc[x][y][e];
+          if (i < p.M && j < p.N) {
+#if F6_CT_NT
+            __builtin_nontemporal_store(0.5f * acc[x][y][e], &Cz[j * ldc + i]);
+#else
+            Cz[j * ldc + i] = 0.5f * acc[x][y][e];
+#endif
+          }
         }
       }
     return;

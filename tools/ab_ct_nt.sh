@@ -1,4 +1,5 @@
-# fp6 GEMM whole-tile (KG = 1, 256x128 tiles: batched slices, split-K partials) epilogue stores:
+# fp6 GEMM whole-tile (KG = 1, 256x128 tiles: batched slices, split-K partials) epilogue stores
+# (first run, before non-temporal became the default; VAR then = the -DF6_CT_NT=1 build):
 # non-temporal (VAR = build_var/liblamm_hip_ctnt.so, -DF6_CT_NT=1) vs the default cached stores.
 # Parity of the variant on the fp6 / config-3 tests, then alternating processes of the
 # whole-launch timing (ab_fp6_kgroups.py, automatic plan), REPS times.

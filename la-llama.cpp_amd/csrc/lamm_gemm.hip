@@ -381,7 +381,9 @@ __device__ __forceinline__ void gemm3_body(const GemvArgs& p, const unsigned cha
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
     const int64_t j = j0 + jb + (e & 3) + 8 * (e >> 2) + 4 * h;
-    if (i < p.M && j < p.N) Cz[j * ldc + i] = 0.5f * acc[e] + (AFF ? macc[e] : 0.f);
+    // non-temporal C / split-K partial stores (q8_0 4096x512x4096: 47.3 -> 46.7 us whole launch,
+    // profiles/r02/ab_gemm_store.txt)
+    if (i < p.M && j < p.N) __builtin_nontemporal_store(0.5f * acc[e] + (AFF ? macc[e] : 0.f), &Cz[j * ldc + i]);
   }
 }
 

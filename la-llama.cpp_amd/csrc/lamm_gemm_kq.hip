@@ -568,7 +568,9 @@ __global__ __launch_bounds__(KQ_T) void gemm_kq_kernel(GemvArgs p, const unsigne
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int64_t j = (int64_t)jt * KQ_TJ + 64 * wj + 32 * rt + (r & 3) + 8 * (r >> 2) + 4 * h;
-      if (i < p.M && j < p.N) Cz[j * ldc + i] = acc[rt][r];
+      // non-temporal: C is written once (Q6_K output.weight 32000x512: 292 -> 280 us whole
+      // launch, profiles/r02/ab_gemm_store.txt)
+      if (i < p.M && j < p.N) __builtin_nontemporal_store(acc[rt][r], &Cz[j * ldc + i]);
     }
 }
 

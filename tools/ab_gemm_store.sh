@@ -1,5 +1,6 @@
 # non-temporal C stores in the i8 (gemm3_kernel) and super-block (gemm_kq_kernel) GEMM epilogues:
-# VAR = build_var/liblamm_hip_gnt.so (built from a copy of the sources with those stores NT) vs
+# (run before they became the default) VAR = build_var/liblamm_hip_gnt.so (built from a copy of
+# the sources with those stores NT) vs
 # the default build.  Parity of the variant on the i8 / super-block tests, then REPS alternating
 # process pairs of tools/ab_gemm_store.py.
 set -e

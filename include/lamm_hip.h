@@ -175,35 +175,6 @@ const char *lamm_hip_comm_last_error(void);
 int lamm_hip_allgather_rows(lamm_comm *c, const float *const *slabs, const int64_t *ld_slab, float *const *C,
                             int64_t ldc, int64_t M, int N, int align, void *const *streams);
 
-/* ---- 4. decode chains: a sequence of single-token GEMVs as ONE persistent launch --------
- * The weight matmuls of a decode step (per Llama layer: wq|wk|wv -> wo -> ffn_gate|ffn_up ->
- * ffn_down; build_llama, LC/llama.cpp:5708-5830) are launch-bound one by one.  A chain runs them
- * in one launch: op i computes y_i = A_i x_i (one token, F32 x quantized like ggml's INIT with
- * the AVX2 rounding, so y_i is bit-identical to lamm_hip_matmul(A_i, F32 x_i)).  x_i is either
- * written before the launch or IS the y of an earlier op (same pointer, K == that op's rows);
- * consecutive ops on one input form a phase and run together; a phase waits only for the op
- * that produces its input.  Weights: q4_0/q4_1/q5_0/q5_1/q8_0 (one type per chain), K <= 12288,
- * 16-byte aligned rows.  Outputs must not overlap one another or an external input.  One launch
- * of a chain at a time (it keeps its sequence number on the device); graph capture is fine.
- * create runs synchronously on the current device. */
-typedef struct lamm_chain lamm_chain;
-typedef struct lamm_chain_op {
-  lamm_matrix A;        /* weights: A.row rows of A.col blocks, A.ld blocks apart */
-  const float *x;       /* input, F32 [A.col * 32] */
-  float *y;             /* output, F32 [A.row] */
-} lamm_chain_op;
-int lamm_hip_chain_create(const lamm_chain_op *ops, int nops, lamm_chain **out);
-int lamm_hip_chain_run(lamm_chain *c, void *hip_stream);
-/* after the launch has finished: LAMM_OK, or LAMM_ERR_HIP if a wait inside it gave up (its
- * outputs are then invalid); clears the error */
-int lamm_hip_chain_status(lamm_chain *c);
-int lamm_hip_chain_phases(const lamm_chain *c);
-/* Diagnostics: with LAMM_CHAIN_TRACE=1 at create, each launch records per workgroup the device
- * clock (100 MHz) at its start, at the start and end of every phase's input staging, and at its
- * end: [workgroup][2 * phases + 2].  Returns the count; copies it when out holds that many. */
-size_t lamm_hip_chain_trace(const lamm_chain *c, uint64_t *out, size_t n);
-void lamm_hip_chain_destroy(lamm_chain *c);
-
 /* Device weight residency used by the ggml boundary (keyed by src0->data/type/
  * shape/strides plus a sampled fingerprint of the bytes). */
 void lamm_hip_cache_clear(void);
@@ -214,6 +185,11 @@ size_t lamm_hip_cache_bytes(void);
  * dst -- the host consumes C, no collective.  Read at the first call; reset drops
  * every device's cache and stream so the next call reads the environment again. */
 void lamm_hip_boundary_reset(void);
+
+/* Every LAMM_* environment switch (engine/plan overrides for A/B runs and tests, the boundary's
+ * policies) is read once, at the first call that needs it; this re-reads them all.
+ * lamm_hip_boundary_reset() re-reads them too. */
+void lamm_hip_reload_env(void);
 
 #ifdef __cplusplus
 }

@@ -15,7 +15,9 @@
 // RCCL is loaded with dlopen at the first communicator (a process that already holds it --
 // PyTorch's copy -- shares that one; liblamm_hip.so itself has no link-time dependency on it).
 // Ranks that share ONE device (a rehearsal on a one-GPU box; RCCL refuses duplicate devices)
-// run in loopback mode: the same pack / unpack kernels, the exchange done by device copies.
+// run in loopback mode: the same pack / unpack kernels, the exchange done by device copies whose
+// ordering is expressed with events only (no host synchronisation), so a loopback all-gather
+// can be captured into a hipGraph like the RCCL one.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -113,6 +115,8 @@ struct lamm_comm {
   std::vector<ncclComm_t> comms;    // per local rank (empty in loopback mode)
   std::vector<float*> gbuf;         // per local rank: [world][N][maxrows] gather buffer
   std::vector<size_t> gcap;
+  // loopback: per local rank, "my segment is packed" and "my reads of the others are done"
+  std::vector<hipEvent_t> packed, done;
   std::mutex mu;
 };
 
@@ -196,6 +200,8 @@ extern "C" void lamm_hip_comm_destroy(lamm_comm* c) {
     (void)hipSetDevice(c->devices[i]);
     (void)hipDeviceSynchronize();
     if (c->gbuf[i]) (void)hipFree(c->gbuf[i]);
+    if (i < c->packed.size()) (void)hipEventDestroy(c->packed[i]);
+    if (i < c->done.size()) (void)hipEventDestroy(c->done[i]);
   }
   if (!c->comms.empty() && rccl().ok)
     for (ncclComm_t k : c->comms) rccl().CommDestroy(k);
@@ -253,23 +259,45 @@ extern "C" int lamm_hip_allgather_rows(lamm_comm* c, const float* const* slabs, 
     }
   }
   // 2. exchange
-  if (c->loopback) {
+  if (c->loopback && nl > 1) {
+    // events only (graph-capturable): every stream copies the other ranks' segments once they are
+    // packed, then every stream waits until all the others have finished reading ITS buffers --
+    // the caller's next matmul on stream k overwrites C[k] / gbuf[k] (without that
+    // wait a reader of the previous contents could race it)
+    if (c->packed.empty()) {
+      c->packed.resize(nl);
+      c->done.resize(nl);
+      for (int i = 0; i < nl; ++i) {
+        (void)hipSetDevice(c->devices[i]);
+        if (hipEventCreateWithFlags(&c->packed[i], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&c->done[i], hipEventDisableTiming) != hipSuccess)
+          return cfail(LAMM_ERR_HIP, "hipEventCreate");
+      }
+    }
+    auto ok = [](hipError_t e) { return e == hipSuccess; };
     for (int i = 0; i < nl; ++i) {
       (void)hipSetDevice(c->devices[i]);
-      if (hipStreamSynchronize(st(i)) != hipSuccess) return cfail(LAMM_ERR_HIP, "stream sync");
+      if (!ok(hipEventRecord(c->packed[i], st(i)))) return cfail(LAMM_ERR_HIP, "hipEventRecord");
     }
     for (int i = 0; i < nl; ++i) {
       (void)hipSetDevice(c->devices[i]);
       float* dst = direct ? C[i] : c->gbuf[i];
       for (int k = 0; k < nl; ++k) {
         if (k == i) continue;
+        if (!ok(hipStreamWaitEvent(st(i), c->packed[k], 0))) return cfail(LAMM_ERR_HIP, "hipStreamWaitEvent");
         const float* src = direct ? C[k] : c->gbuf[k];
         const size_t off = (size_t)(c->rank0 + k) * count;
-        if (hipMemcpyAsync(dst + off, src + off, count * sizeof(float), hipMemcpyDeviceToDevice, st(i)) != hipSuccess)
+        if (!ok(hipMemcpyAsync(dst + off, src + off, count * sizeof(float), hipMemcpyDeviceToDevice, st(i))))
           return cfail(LAMM_ERR_HIP, "loopback copy");
       }
+      if (!ok(hipEventRecord(c->done[i], st(i)))) return cfail(LAMM_ERR_HIP, "hipEventRecord");
     }
-  } else {
+    for (int k = 0; k < nl; ++k) {
+      (void)hipSetDevice(c->devices[k]);
+      for (int i = 0; i < nl; ++i)
+        if (i != k && !ok(hipStreamWaitEvent(st(k), c->done[i], 0))) return cfail(LAMM_ERR_HIP, "hipStreamWaitEvent");
+    }
+  } else if (!c->loopback) {
     const Rccl& r = rccl();
     r.GroupStart();
     for (int i = 0; i < nl; ++i) {

@@ -25,6 +25,7 @@
 #include "lamm_device.h"
 #include "lamm_kernels.h"
 #include "lamm_rowdot.h"
+#include "lamm_knobs.h"
 
 namespace lamm {
 namespace {
@@ -536,15 +537,17 @@ __global__ __launch_bounds__(GT) void gemm_q2k_kernel(GemvArgs p) {
 template <class K>
 hipError_t launch_with(K kern, size_t lds, int threads, const GemvArgs& p, hipStream_t s) {
   const dim3 grid((unsigned)((p.M + TI - 1) / TI), (unsigned)((p.N + TJ - 1) / TJ), (unsigned)(p.ne12 * p.ne13));
-  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  set_max_lds((const void*)kern, (int)lds);
   hipLaunchKernelGGL(kern, grid, dim3(threads), lds, s, p);
   return hipGetLastError();
 }
 
-int gemm_variant() {   // A/B and ablation switch for tools/ab_gemm.py; 0 in production
+#ifdef LAMM_AB_VARIANTS
+int gemm_variant() {   // A/B and ablation switch for tools/ab_gemm.py (variant build only)
   const char* e = getenv("LAMM_GEMM_VARIANT");
   return e ? atoi(e) : 0;
 }
+#endif
 
 // K-splits of the i8 GEMM: its 64x128 tiles have no other way to fill 256 CUs on a small grid
 // (one 4096 x 128 GEMM = 64 tiles); double until 256 workgroups, >= 4 K-steps (32 blocks) per
@@ -552,10 +555,9 @@ int gemm_variant() {   // A/B and ablation switch for tools/ab_gemm.py; 0 in pro
 int i8_nsplit(const GemvArgs& p) {
   const PrepLayout L = PrepLayout::of(p);
   const int tiles = ((p.M + TI - 1) / TI) * ((p.N + TJ - 1) / TJ) * p.ne12 * p.ne13;
-  const char* e = getenv("LAMM_I8_SPLIT");
   int n = 1;
-  if (e && atoi(e) > 0) {
-    n = atoi(e);
+  if (knobs().i8_split > 0) {
+    n = knobs().i8_split;
   } else {
     while (tiles * n < 256 && n < 16 && L.nsteps / (2 * n) >= 4) n *= 2;
   }
@@ -572,8 +574,11 @@ hipError_t launch_v3(const GemvArgs& p, void* ws, hipStream_t s) {
   constexpr int VBPB = GF<T>::VBPB;
   const PrepLayout L = PrepLayout::of(p);
   const int64_t items = (int64_t)p.N * L.nsteps * KBLK;
-  const char* sp = getenv("LAMM_GEMM_SKIP_PREP");   // measurement only (bench.py): reuse the prep
-  if (!(sp && sp[0] == '1')) {
+#ifdef LAMM_AB_VARIANTS
+  const char* sp = getenv("LAMM_GEMM_SKIP_PREP");   // variant build only: re-run on the previous prep
+  if (!(sp && sp[0] == '1'))
+#endif
+  {
     const dim3 g((unsigned)((items + 255) / 256), p.ne12 * p.ne13);
     if (p.b_f32)
       hipLaunchKernelGGL((prep_act_kernel<VBPB, true>), g, dim3(256), 0, s, p, static_cast<unsigned char*>(ws));
@@ -588,18 +593,22 @@ hipError_t launch_v3(const GemvArgs& p, void* ws, hipStream_t s) {
   const auto* wsc = static_cast<const unsigned char*>(ws);
   auto go = [&](auto kern, size_t lds_bytes = 0) {
     const size_t lds = lds_bytes ? lds_bytes : sizeof(Smem3<T, NB>);
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    set_max_lds((const void*)kern, (int)lds);
     hipLaunchKernelGGL(kern, grid, dim3(GT8), lds, s, p, wsc, nsplit, part);
   };
+#ifdef LAMM_AB_VARIANTS
   switch (gemm_variant()) {
     case 1: go(gemm3_kernel<T, NB, 1>); break;
     case 2: go(gemm3_kernel<T, NB, 2>); break;
     case 3: go(gemm3_kernel<T, NB, 3>); break;
-    case 4: break;   // prep pass only
+    case 4: return hipGetLastError();   // prep pass only
     case 5: go(gemm3_kernel<T, 1, 0>, sizeof(Smem3<T, 1>)); break;   // single-buffered
     default: go(gemm3_kernel<T, NB, 0>);
   }
-  if (nsplit > 1 && gemm_variant() != 4) launch_splitk_reduce(p, nsplit, part, s);
+#else
+  go(gemm3_kernel<T, NB, 0>);
+#endif
+  if (nsplit > 1) launch_splitk_reduce(p, nsplit, part, s);
   return hipGetLastError();
 }
 

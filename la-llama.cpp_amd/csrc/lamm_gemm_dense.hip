@@ -21,6 +21,7 @@
 
 #include "lamm_device.h"
 #include "lamm_kernels.h"
+#include "lamm_knobs.h"
 
 namespace lamm {
 namespace {
@@ -211,10 +212,9 @@ int dg_nsplit(const GemvArgs& p, int eb) {
   const int nit = (p.M + DG_T - 1) / DG_T, njt = (p.N + DG_T - 1) / DG_T;
   const int tiles = nit * njt * p.ne12 * p.ne13;
   const int nsteps = (p.K + 128 / eb - 1) / (128 / eb);
-  const char* e = getenv("LAMM_DENSE_SPLIT");
   int n = 1;
-  if (e && atoi(e) > 0) {
-    n = atoi(e);
+  if (knobs().dense_split > 0) {
+    n = knobs().dense_split;
   } else {
     while (tiles * n < 256 && n < 8 && nsteps / (2 * n) >= 4) n *= 2;
   }
@@ -229,12 +229,7 @@ hipError_t launch_dg(const GemvArgs& p, void* ws, hipStream_t s) {
   float* part = static_cast<float*>(ws);
   if (nwg > 0x7fffffff) return hipErrorInvalidValue;
   constexpr size_t lds = 2 * DG_STAGE;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)gemm_dense_kernel<T, BAL>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
-    attr_set = true;
-  }
+  set_max_lds((const void*)gemm_dense_kernel<T, BAL>, (int)lds);
   hipLaunchKernelGGL((gemm_dense_kernel<T, BAL>), dim3((unsigned)nwg), dim3(DG_NT), lds, s, p, nsplit, part);
   if (nsplit > 1) launch_splitk_reduce(p, nsplit, part, s);
   return hipGetLastError();

@@ -37,6 +37,7 @@
 
 #include "lamm_device.h"
 #include "lamm_kernels.h"
+#include "lamm_knobs.h"
 #include "lamm_rowdot.h"
 
 namespace lamm {
@@ -798,11 +799,10 @@ unsigned* tile_counters(hipStream_t s) {
 // >= 8 K-steps per split, at most 16 (K=11008, 16 tiles: 8 splits 247, 16 splits 288, 21
 // splits 230 TFLOP/s, profiles/r01/ab_driver_split.txt).  LAMM_FP6_SPLIT=n forces n (A/B).
 int f6_nsplit_for(const GemvArgs& p, const F6Layout& L) {
-  const char* e = getenv("LAMM_FP6_SPLIT");
   const int tiles = L.nit * L.njt * p.ne12 * p.ne13;
   int n = 1;
-  if (e && atoi(e) > 0) {
-    n = atoi(e);
+  if (knobs().fp6_split > 0) {
+    n = knobs().fp6_split;
   } else {
     while (tiles * n < 256 && n < 16 && L.nsteps / (2 * n) >= 8) n *= 2;
   }
@@ -821,11 +821,9 @@ struct F6Plan {
 constexpr int kSubTilesMin = 256;
 F6Plan f6_plan(const GemvArgs& p, const F6Layout& L) {
   const int tiles = L.nit * L.njt * p.ne12 * p.ne13;
-  const char* es = getenv("LAMM_FP6_SUB");
-  const char* ek = getenv("LAMM_FP6_SPLIT");
-  const int sub = es ? atoi(es) : -1;   // -1: automatic; 1 / 2 force that form (tests, A/B)
+  const int sub = knobs().fp6_sub;   // -1: automatic; 1 / 2 force that form (tests, A/B)
   const int64_t subt = (int64_t)((p.M + 127) / 128) * ((p.N + 63) / 64) * p.ne12 * p.ne13;
-  if (!(ek && atoi(ek) > 0) && sub != 0 && subt < (1 << 30)) {
+  if (knobs().fp6_split <= 0 && sub != 0 && subt < (1 << 30)) {
     if (sub > 0) return {sub == 2 ? 2 : 1, 1, (int)subt};
     if (tiles < 256 && subt >= kSubTilesMin) return {1, 1, (int)subt};
   }
@@ -849,10 +847,13 @@ hipError_t launch_fp6_t(const GemvArgs& p, const void* prepA, void* ws, hipStrea
   auto* w = static_cast<unsigned char*>(ws);
   unsigned char* wsA = prepA ? nullptr : w;
   unsigned char* wsB = w + (prepA ? 0 : L.a_bytes);
-  // LAMM_GEMM_SKIP_PREP=1 (measurement only, bench.py): re-run the main kernel on the
-  // workspace the previous identical call prepared, so its own duration can be event-timed
+#ifdef LAMM_AB_VARIANTS
+  // LAMM_GEMM_SKIP_PREP=1 (variant build only): re-run the main kernel on the workspace the
+  // previous identical call prepared, so its own duration can be event-timed
   const char* sp = getenv("LAMM_GEMM_SKIP_PREP");
-  if (!(sp && sp[0] == '1')) {
+  if (!(sp && sp[0] == '1'))
+#endif
+  {
     if (!prepA) launch_prep_w<T>(p, wsA, s);
     const int rgroups = (L.njt * F6_TJ + PREP_NT - 1) / PREP_NT, nb_all = L.nsteps * F6_KB;
     auto prep = [&](auto kmulti, auto kone) {
@@ -879,21 +880,24 @@ hipError_t launch_fp6_t(const GemvArgs& p, const void* prepA, void* ws, hipStrea
   // 128 KiB per workgroup write-through and reading three partials on only the 64 last
   // workgroups costs more than a reduce pass over all CUs.  Kept as an A/B switch.
   const int64_t tiles = (int64_t)L.nit * L.njt * p.ne12 * p.ne13;
-  const char* fr = getenv("LAMM_FP6_FUSED_REDUCE");
-  unsigned* ctr = nsplit > 1 && tiles <= (int64_t)kTileCounters && fr && fr[0] == '1' ? tile_counters(s) : nullptr;
+  unsigned* ctr = nsplit > 1 && tiles <= (int64_t)kTileCounters && knobs().fp6_fused_reduce ? tile_counters(s) : nullptr;
   auto go = [&](auto kern, auto waves) {
     using WV = decltype(waves);
     const size_t lds = (size_t)WV::LDS;
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    set_max_lds((const void*)kern, (int)lds);
     hipLaunchKernelGGL(kern, dim3((unsigned)plan.grid), dim3(WV::NT), lds, s, p, kA,
                        static_cast<const unsigned char*>(wsB), nsplit, part, ctr);
   };
+#ifdef LAMM_AB_VARIANTS
   const char* ev = getenv("LAMM_GEMM_VARIANT");
+#endif
   if (plan.sub == 1) {
     using WK = F6Waves<2, 2, 2, 4>;
-    // ablations of the K-group form (q4_0 only, tools/ab_kg.sh, profiles/r02/fp6_kgroups_ablation.txt):
-    // 1 no compute, 2 no DMA, 3 no epilogue FMAs, 4 no DMA + no LDS fragment reads, 6 no P-MFMA,
-    // 7 no S-MFMA, 11 DMA but no LDS fragment reads; 20 + V: in-kernel clock probe of V
+#ifdef LAMM_AB_VARIANTS
+    // ablations of the K-group form (variant build, q4_0 only, tools/ab_kg.sh,
+    // profiles/r02/fp6_kgroups_ablation.txt): 1 no compute, 2 no DMA, 3 no epilogue FMAs,
+    // 4 no DMA + no LDS fragment reads, 6 no P-MFMA, 7 no S-MFMA, 11 DMA but no LDS fragment
+    // reads; 20 + V: in-kernel clock probe of V
     switch (T == kQ4_0 && ev ? atoi(ev) : 0) {
       case 1: go(gemm_fp6_kernel<T, 1, 2, 2, 2, 4>, WK{}); break;
       case 2: go(gemm_fp6_kernel<T, 2, 2, 2, 2, 4>, WK{}); break;
@@ -909,17 +913,21 @@ hipError_t launch_fp6_t(const GemvArgs& p, const void* prepA, void* ws, hipStrea
       case 31: go(gemm_fp6_kernel<T, 31, 2, 2, 2, 4>, WK{}); break;
       default: go(gemm_fp6_kernel<T, 0, 2, 2, 2, 4>, WK{});
     }
+#else
+    go(gemm_fp6_kernel<T, 0, 2, 2, 2, 4>, WK{});
+#endif
     return hipGetLastError();
   }
   if (plan.sub == 2) {
     go(gemm_fp6_kernel<T, 0, 1, 2, 2, 2>, F6Waves<1, 2, 2, 2>{});
     return hipGetLastError();
   }
-  const char* ew = getenv("LAMM_FP6_WJ");   // A/B: 1 = 16 waves of 32x64
-  const int wjv = ew ? atoi(ew) : 2;
   using W2 = F6Waves<2>;
-  switch (wjv == 1 ? -1 : ev ? atoi(ev) : 0) {
-    case -1: go(gemm_fp6_kernel<T, 0, 1>, F6Waves<1>{}); break;
+  if (knobs().fp6_wj == 1) {   // A/B: 16 waves of 32x64
+    go(gemm_fp6_kernel<T, 0, 1>, F6Waves<1>{});
+  } else {
+#ifdef LAMM_AB_VARIANTS
+  switch (ev ? atoi(ev) : 0) {
     case 1: go(gemm_fp6_kernel<T, 1, 2>, W2{}); break;
     case 2: go(gemm_fp6_kernel<T, 2, 2>, W2{}); break;
     case 3: go(gemm_fp6_kernel<T, 3, 2>, W2{}); break;
@@ -930,6 +938,10 @@ hipError_t launch_fp6_t(const GemvArgs& p, const void* prepA, void* ws, hipStrea
     case 10: go(gemm_fp6_kernel<T, 10, 2>, W2{}); break;
     case 12: go(gemm_fp6_kernel<T, 12, 2>, W2{}); break;
     default: go(gemm_fp6_kernel<T, 0, 2>, W2{});
+  }
+#else
+  go(gemm_fp6_kernel<T, 0, 2>, W2{});
+#endif
   }
   if (nsplit > 1 && !ctr) launch_splitk_reduce(p, nsplit, part, s);
   return hipGetLastError();

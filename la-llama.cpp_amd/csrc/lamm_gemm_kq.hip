@@ -29,6 +29,7 @@
 
 #include "lamm_device.h"
 #include "lamm_kernels.h"
+#include "lamm_knobs.h"
 
 namespace lamm {
 namespace {
@@ -260,8 +261,7 @@ hipError_t launch_kq_simple(const GemvArgs& p, hipStream_t s) {
                   (unsigned)(p.ne12 * p.ne13));
   constexpr size_t lds = sizeof(KQSmem<T>);
   static_assert(lds <= 160 * 1024, "LDS");
-  (void)hipFuncSetAttribute((const void*)gemm_kq_simple_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)lds);
+  set_max_lds((const void*)gemm_kq_simple_kernel<T>, (int)lds);
   hipLaunchKernelGGL(gemm_kq_simple_kernel<T>, grid, dim3(KQ_T), lds, s, p);
   return hipGetLastError();
 }
@@ -579,10 +579,9 @@ __global__ __launch_bounds__(KQ_T) void gemm_kq_kernel(GemvArgs p, const unsigne
 int kq_nsplit(const GemvArgs& p) {
   const KQLayout L = KQLayout::of(p);
   const int tiles = L.nit * L.njt * p.ne12 * p.ne13;
-  const char* e = getenv("LAMM_KQ_SPLIT");
   int n = 1;
-  if (e && atoi(e) > 0) {
-    n = atoi(e);
+  if (knobs().kq_split > 0) {
+    n = knobs().kq_split;
   } else {
     while (tiles * n < 256 && n < 16 && L.nsb / (2 * n) >= 4) n *= 2;
   }
@@ -613,7 +612,7 @@ hipError_t launch_kq(const GemvArgs& p, const void* prepA, void* ws, hipStream_t
                      wsB);
   constexpr size_t lds = 2 * (KQC_A + KQC_B);
   static_assert(lds <= 160 * 1024, "LDS");
-  (void)hipFuncSetAttribute((const void*)gemm_kq_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  set_max_lds((const void*)gemm_kq_kernel<T>, (int)lds);
   const int nsplit = kq_nsplit(p);
   float* part = reinterpret_cast<float*>(w + kq_part_offset(p, prepA != nullptr));
   hipLaunchKernelGGL(gemm_kq_kernel<T>, dim3((unsigned)L.nit, (unsigned)L.njt, (unsigned)(p.ne12 * p.ne13 * nsplit)),
@@ -655,8 +654,7 @@ hipError_t prepare_kq_weights(int type, const GemvArgs& p, void* wsA, hipStream_
 hipError_t launch_gemm_kq(int type, const GemvArgs& p, const void* prepA, void* ws, hipStream_t s) {
   if (p.M == 0 || p.N == 0) return hipSuccess;
   if ((p.ldb & 3) || ((uintptr_t)p.B & 3) || (p.sb2 & 3) || (p.sb3 & 3)) return hipErrorInvalidValue;
-  const char* ev = getenv("LAMM_KQ_VARIANT");
-  if (ev && atoi(ev) == 1 && type != kQ2_K) {
+  if (knobs().kq_variant == 1 && type != kQ2_K) {
     switch (type) {
       case kQ4_K: return launch_kq_simple<kQ4_K>(p, s);
       case kQ5_K: return launch_kq_simple<kQ5_K>(p, s);

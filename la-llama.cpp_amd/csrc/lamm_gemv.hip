@@ -22,6 +22,7 @@
 #include "lamm_kernels.h"
 
 #include <cstdlib>
+#include "lamm_knobs.h"
 
 namespace lamm {
 namespace {
@@ -814,8 +815,7 @@ hipError_t launch_stream_dma(const GemvArgs& p, hipStream_t s) {
   int gx = (256 * per_cu) / slices;
   const int gmax = (ngroups + WAVES - 1) / WAVES;
   gx = gx < 1 ? 1 : (gx > gmax ? gmax : gx);
-  (void)hipFuncSetAttribute((const void*)gemv_stream_dma_kernel<T, NC, WAVES, NS>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  set_max_lds((const void*)gemv_stream_dma_kernel<T, NC, WAVES, NS>, (int)lds);
   hipLaunchKernelGGL((gemv_stream_dma_kernel<T, NC, WAVES, NS>), dim3(gx, slices), dim3(64 * WAVES), lds, s, p);
   return hipGetLastError();
 }
@@ -955,8 +955,7 @@ hipError_t launch_seg_dma(const GemvArgs& p, hipStream_t s) {
   int gx = 256 / slices;
   const int gmax = (ngroups + WAVES - 1) / WAVES;
   gx = gx < 1 ? 1 : (gx > gmax ? gmax : gx);
-  (void)hipFuncSetAttribute((const void*)gemv_seg_dma_kernel<T, NC, WAVES, NS, NSEG>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  set_max_lds((const void*)gemv_seg_dma_kernel<T, NC, WAVES, NS, NSEG>, (int)lds);
   hipLaunchKernelGGL((gemv_seg_dma_kernel<T, NC, WAVES, NS, NSEG>), dim3(gx, slices), dim3(64 * WAVES), lds, s, p);
   return hipGetLastError();
 }
@@ -1102,8 +1101,7 @@ bool launch_flat_dma(const GemvArgs& p, hipStream_t s, hipError_t* err) {
   const int nwg = 256;
   if (total < (int64_t)nwg * WAVES * 2 || total >= (int64_t)1 << 31) return false;   // small calls: the 2-D grid
   if ((total + nwg - 1) / nwg > ngroups) return false;         // a range would span > 2 slices
-  (void)hipFuncSetAttribute((const void*)gemv_flat_dma_kernel<T, NC, WAVES, NS>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  set_max_lds((const void*)gemv_flat_dma_kernel<T, NC, WAVES, NS>, (int)lds);
   hipLaunchKernelGGL((gemv_flat_dma_kernel<T, NC, WAVES, NS>), dim3(nwg), dim3(64 * WAVES), lds, s, p);
   *err = hipGetLastError();
   return true;
@@ -1115,12 +1113,7 @@ constexpr bool stream_fits() { return sizeof(SmemStream<T, NC, WAVES>) <= 160 * 
 template <int T, int NC, int WAVES>
 hipError_t launch_stream_w(const GemvArgs& p, hipStream_t s, int gx) {
   const size_t lds = sizeof(SmemStream<T, NC, WAVES>);
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)gemv_stream_kernel<T, NC, WAVES>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attr_set = true;
-  }
+  set_max_lds((const void*)gemv_stream_kernel<T, NC, WAVES>, (int)lds);
   hipLaunchKernelGGL((gemv_stream_kernel<T, NC, WAVES>), dim3(gx, p.ne12 * p.ne13), dim3(64 * WAVES), lds, s, p);
   return hipGetLastError();
 }
@@ -1151,20 +1144,12 @@ hipError_t launch_v(const GemvArgs& p, hipStream_t s) {
   const size_t lds = sizeof(Smem<T, NC>);
   const int grid = (int)((p.M + kRows - 1) / kRows);
   if (grid == 0) return hipSuccess;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)gemv_kernel<T, NC, V>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
-    attr_set = true;
-  }
+  set_max_lds((const void*)gemv_kernel<T, NC, V>, (int)lds);
   hipLaunchKernelGGL((gemv_kernel<T, NC, V>), dim3(grid, p.ne12 * p.ne13), dim3(kThreads), lds, s, p);
   return hipGetLastError();
 }
 
-int variant() {
-  const char* e = getenv("LAMM_GEMV_VARIANT");
-  return e ? atoi(e) : 0;
-}
+int variant() { return knobs().gemv_variant; }
 
 template <int T, int NC>
 hipError_t launch_t(const GemvArgs& p, hipStream_t s) {
@@ -1198,15 +1183,16 @@ hipError_t launch_t(const GemvArgs& p, hipStream_t s) {
   }
   if constexpr (T == kQ4_0 && NC == 1) {
     if (v == 8) return launch_stream_dma<T, NC, 4, 4>(p, s);   // A/B: LDS-DMA streaming, 4 waves x 4 slots
-    switch (v) {
+#ifdef LAMM_AB_VARIANTS
+    switch (v) {   // variant build only
       case 1: return launch_v<T, NC, 1>(p, s);
       case 2: return launch_v<T, NC, 2>(p, s);
       case 3: return launch_v<T, NC, 3>(p, s);
       case 4: return launch_v<T, NC, 4>(p, s);   // ablation: no compute (timing only)
       case 5: return launch_v<T, NC, 5>(p, s);   // ablation: no B staging (timing only)
-      case 7: return launch_v<T, NC, 0>(p, s);   // force the segmented kernel
       default: break;
     }
+#endif
   }
   return launch_v<T, NC, 0>(p, s);
 }
@@ -1245,8 +1231,7 @@ size_t gemv_lds_bytes(int type, int nc) {
 // beyond.
 // LAMM_GEMV_RPW=0 off, =4/8/16 forces.
 int rpw_waves(const GemvArgs& p) {
-  const char* e = getenv("LAMM_GEMV_RPW");
-  if (e) return atoi(e);
+  if (knobs().gemv_rpw >= 0) return knobs().gemv_rpw;
   const int64_t rows = (int64_t)p.M * p.ne12 * p.ne13;
   if (rows > 32768) return 0;
   // K > 4096: 8 waves; F32 rows 16, so two lanes per block stage the row in one pass

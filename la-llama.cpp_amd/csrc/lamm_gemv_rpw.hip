@@ -17,6 +17,7 @@
 #include "lamm_rowdot.h"
 
 #include <cstdlib>
+#include "lamm_knobs.h"
 
 namespace lamm {
 namespace {
@@ -182,8 +183,7 @@ __global__ __launch_bounds__(64 * WAVES) void gemv_rpw_kernel(GemvArgs p) {
 template <int T, int NC, int WAVES, bool BF32, int ITER>
 hipError_t launch_rpw_k(const GemvArgs& p, hipStream_t s) {
   // LAMM_GEMV_LANEB=1: per-lane activation blocks for q8 single-column calls (A/B)
-  const char* lb = getenv("LAMM_GEMV_LANEB");
-  const bool laneb = !BF32 && NC == 1 && ITER == 2 && lb && lb[0] == '1';
+  const bool laneb = !BF32 && NC == 1 && ITER == 2 && knobs().gemv_laneb;
   const size_t lds = laneb ? 0 : (size_t)NC * p.nblk * 40;
   const int slices = p.ne12 * p.ne13;
   const int gmax = (p.M + WAVES - 1) / WAVES;

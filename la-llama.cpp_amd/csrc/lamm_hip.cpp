@@ -22,6 +22,7 @@
 #include "ggml_b2430_abi.h"
 #include "lamm_formats.h"
 #include "lamm_kernels.h"
+#include "lamm_knobs.h"
 
 namespace lamm {
 hipError_t launch_quantize(int vec_type, int flavour, const float* x, int64_t ldx, void* y,
@@ -46,17 +47,11 @@ int fail(int code, const char* fmt, ...) {
 
 }  // namespace
 
-// lamm_hip_last_error() for the other translation units of the library (lamm_chain.hip)
-int lamm::report_error(int code, const char* msg) {
-  g_err = msg;
-  return code;
-}
-
 namespace {
 
 struct DeviceProbe {
   int count = 0;          // gfx950 devices visible
-  int device = 0;         // device used by the ggml boundary
+  int device = 0;         // the first of them (the ggml boundary's default device)
   std::vector<int> ids;   // every gfx950 device
 };
 
@@ -73,8 +68,6 @@ const DeviceProbe& probe() {
         d.ids.push_back(i);
       }
     }
-    const char* env = getenv("LAMM_HIP_DEVICE");
-    if (env && d.count) d.device = atoi(env);
     return d;
   }();
   return p;
@@ -116,12 +109,6 @@ void* workspace(size_t bytes, hipStream_t s) {
   return b.ptr;
 }
 
-// env var set to "0" (A/B switches that turn a default path off)
-bool getenv_flag0(const char* name) {
-  const char* e = getenv(name);
-  return e && !strcmp(e, "0");
-}
-
 // GEMM engine for the q4_0 / q4_1 / q5_0 prefill path: 0 = block-scaled fp6 MFMA
 // (lamm_gemm_fp6.hip), 1 = MFMA-i8 (lamm_gemm.hip).  The fp6 kernel's 256x128 tiles only pay
 // off once they fill the chip (>= one tile per CU); smaller calls take the i8 kernel's
@@ -134,13 +121,23 @@ bool getenv_flag0(const char* name) {
 // splits (93 unsplit), 199 on fp6 re-packing per call at 16 splits, 286 with the packed weights
 // resident (profiles/r01/ab_driver_split.txt).  LAMM_GEMM_PATH=fp6 / i8 forces one (A/B).
 int gemm_path(const GemvArgs& p, bool stationary) {
-  const char* e = getenv("LAMM_GEMM_PATH");
-  if (e && (!strcmp(e, "i8") || !strcmp(e, "1"))) return 1;
-  if (e && (!strcmp(e, "fp6") || !strcmp(e, "0"))) return 0;
+  if (knobs().gemm_path >= 0) return knobs().gemm_path;
   return (stationary ? gemm_fp6_grid(p) : gemm_fp6_tiles(p)) >= 256 ? 0 : 1;
 }
 
 }  // namespace
+
+void lamm::set_max_lds(const void* kernel, int bytes) {
+  static std::mutex mu;
+  static std::unordered_map<const void*, int> done[64];   // per device: the largest size set
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lock(mu);
+  int& have = done[dev & 63][kernel];
+  if (have >= bytes) return;
+  (void)hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  have = bytes;
+}
 
 // =============================================================== traits
 extern "C" int lamm_blck_size(int type) { return block_bytes(type) ? block_elems(type) : 0; }
@@ -183,9 +180,8 @@ GemvArgs weight_args(const lamm_matrix* A, int64_t ne02, int64_t ne03, size_t nb
 // the 32-block formats stay on the GEMV up to 8 (q4_0 N = 8: 4.74 vs 6.50).
 // LAMM_GEMV_MAX_N=n overrides (A/B).
 int gemv_max_n(int type) {
-  const char* e = getenv("LAMM_GEMV_MAX_N");
   int n = 8;
-  if (e) n = atoi(e);
+  if (knobs().gemv_max_n > 0) n = knobs().gemv_max_n;
   else if (type == kQ2_K) n = 5;
   else if (type == kQ4_K) n = 6;
   else if (type == kQ5_K || type == kQ6_K || type == kF16) n = 4;
@@ -265,12 +261,12 @@ int matmul_impl(const lamm_matrix* A, const lamm_matrix* B, const lamm_matrix* C
       done->signaled = true;
     }
     e = launch_gemv(A->type, p, s);
-  } else if (gemm_dense_supported(A->type) && !getenv_flag0("LAMM_DENSE_GEMM")) {
+  } else if (gemm_dense_supported(A->type) && knobs().dense_gemm) {
     const size_t wsb = gemm_dense_workspace_bytes(A->type, p);
     void* ws = nullptr;
     if (wsb && !(ws = workspace(wsb, s))) return fail(LAMM_ERR_HIP, "workspace allocation of %zu bytes failed", wsb);
     e = launch_gemm_dense(A->type, p, ws, s);
-  } else if (gemm_kq_supported(A->type) && !getenv_flag0("LAMM_KQ_GEMM") && (ldb & 3) == 0 &&
+  } else if (gemm_kq_supported(A->type) && knobs().kq_gemm && (ldb & 3) == 0 &&
              ((uintptr_t)B->data & 3) == 0 && (bt.nbb2 & 3) == 0 && (bt.nbb3 & 3) == 0) {
     const void* prepA = W ? W->packed : nullptr;
     const size_t wsb = gemm_kq_workspace_bytes(A->type, p, prepA != nullptr);
@@ -451,13 +447,7 @@ struct CallStats {
 };
 const char* kPhase[4] = {"weights lookup", "enqueue", "device sync", "C to dst"};
 CallStats g_stats[4] = {{"weights N<=8"}, {"weights N>8"}, {"views N<=8"}, {"views N>8"}};
-bool stats_on() {
-  static const bool on = [] {
-    const char* e = getenv("LAMM_HIP_STATS");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
+bool stats_on() { return knobs().stats; }
 void print_stats() {
   for (const auto& c : g_stats)
     if (c.calls)
@@ -599,7 +589,7 @@ class Runtime {
   void ensure_init() {
     if (!devs.empty()) return;
     std::vector<int> ids;
-    const char* e = getenv("LAMM_HIP_DEVICES");
+    const char* e = knobs().devices;
     int nvis = 0;
     (void)hipGetDeviceCount(&nvis);
     if (e && !strcmp(e, "all")) {
@@ -617,7 +607,7 @@ class Runtime {
         c = *end == ',' ? end + 1 : end;
       }
     }
-    if (ids.empty()) ids.push_back(probe().device);
+    if (ids.empty()) ids.push_back(knobs().device >= 0 ? knobs().device : probe().device);
     devs.resize(ids.size());
     for (size_t i = 0; i < ids.size(); ++i) {
       devs[i].id = ids[i];
@@ -629,9 +619,12 @@ class Runtime {
       HIPCHK(hipMalloc(reinterpret_cast<void**>(&devs[i].done_ctr), 64));
       HIPCHK(hipMemset(devs[i].done_ctr, 0, 64));
     }
-    const char* b = getenv("LAMM_HIP_CACHE_GB");
-    budget_ = (size_t)((b ? atof(b) : 64.0) * (1ull << 30));
-    if (stats_on()) atexit(print_stats);
+    budget_ = (size_t)(knobs().cache_gb * (1ull << 30));
+    static bool stats_registered = false;
+    if (stats_on() && !stats_registered) {
+      stats_registered = true;
+      atexit(print_stats);
+    }
   }
 
   // rows [r0, r0 + rows) of every (i02, i03) slice of a weight on device d, re-pitched to 16 B
@@ -735,10 +728,7 @@ class Runtime {
 };
 
 bool use_pinned(size_t bytes) {
-  static const bool on = [] {
-    const char* e = getenv("LAMM_HIP_PINNED");
-    return !(e && e[0] == '0');
-  }();
+  const bool on = knobs().pinned;
   // decode-sized transfers only: through the unchanged ggml (tools/ab_pinned.sh,
   // profiles/r01/ab_pinned.txt) Q4_0 4096x1x4096 27.7 -> 23.3 us, but N = 8 (128 KiB of C)
   // 41.8 -> 46 us and N = 512 (8 MiB) 367 -> 691 us: the host-side strided copy out of the
@@ -746,13 +736,7 @@ bool use_pinned(size_t bytes) {
   return on && bytes <= ((size_t)32 << 10);
 }
 
-int opt_level() {
-  static int lvl = [] {
-    const char* e = getenv("LAMM_OPT_LEVEL");
-    return e ? atoi(e) : 3;
-  }();
-  return lvl;
-}
+int opt_level() { return knobs().opt_level; }
 
 bool is_contiguous(const ggml::tensor* t) {
   const size_t ts = block_bytes(t->type);
@@ -772,16 +756,11 @@ bool is_weight(const ggml::tensor* t) { return t->view_src == nullptr && t->op =
 constexpr int64_t kViewMinRows = 8;
 bool views_accepted(const ggml::tensor* src0, const ggml::tensor* src1) {
   if (is_weight(src0)) return true;
-  const char* e = getenv("LAMM_HIP_VIEWS");
-  if (e && e[0] == '0') return false;
-  if (e && e[0] == '1') return true;
+  if (knobs().views >= 0) return knobs().views == 1;
   return src1->ne[1] >= kViewMinRows;
 }
 
-bool extra_types_enabled() {
-  const char* e = getenv("LAMM_HIP_EXTRA_TYPES");
-  return !(e && e[0] == '0');
-}
+bool extra_types_enabled() { return knobs().extra_types; }
 
 // How an F32 src1 reaches the kernels (ggml's INIT phase quantizes it on thread 0, serially:
 // LC/ggml.c:10865-10887).  Whenever the GPU takes it over, the hook claims the INIT phase too
@@ -802,14 +781,12 @@ ActMode act_mode(const ggml::tensor* src0, const ggml::tensor* src1) {
   const bool f32_rows = src1->nb[0] == sizeof(float) && (src1->nb[1] & 3) == 0 && (src1->nb[2] & 3) == 0 &&
                         (src1->nb[3] & 3) == 0;
   if (!f32_rows) return kCpuInit;
-  const char* e = getenv("LAMM_HIP_GPU_QUANT");
-  if (e && e[0] == '0') return kCpuInit;
-  const char* f = getenv("LAMM_HIP_FUSED");
-  if (!(f && f[0] == '0') && !(e && e[0] == '1') && (vdt == kQ8_0 || vdt == kQ8_1) && src1->ne[1] <= 8 &&
-      is_weight(src0))
+  const int gq = knobs().gpu_quant;
+  if (gq == 0) return kCpuInit;
+  if (knobs().fused && gq != 1 && (vdt == kQ8_0 || vdt == kQ8_1) && src1->ne[1] <= 8 && is_weight(src0))
     return kFused;
   const int64_t rows = src1->ne[1] * src1->ne[2] * src1->ne[3];
-  if (!(e && e[0] == '1') && rows < 8) return kCpuInit;
+  if (gq != 1 && rows < 8) return kCpuInit;
   return (vdt == kQ8_0 || vdt == kQ8_1 || vdt == kQ8_K || vdt == kF16) ? kGpuQuant : kCpuInit;
 }
 
@@ -856,25 +833,13 @@ namespace {
 // spun on by the host -- ~4 us per call under hipStreamSynchronize.  If the flag has not arrived
 // after a second (a fault, a hang) the stream is synchronised, which reports the error.
 // LAMM_HIP_SPIN=0: hipStreamSynchronize only (A/B).
-bool spin_enabled() {
-  static const bool spin = [] {
-    const char* e = getenv("LAMM_HIP_SPIN");
-    return !(e && e[0] == '0');
-  }();
-  return spin;
-}
+bool spin_enabled() { return knobs().spin; }
 
 // LAMM_HIP_KERNEL_SIGNAL=1: the GEMV's last workgroup writes the completion flag itself instead
 // of a signal launch behind it.  Measured no faster through llama.cpp (profiles/r02/
 // ab_kernel_signal.txt: device wait 15.8 vs 15.1 us per decode call) -- the last workgroup's
 // counter round trip and system fence cost what the second launch costs -- so it is an A/B switch.
-bool kernel_signal_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("LAMM_HIP_KERNEL_SIGNAL");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
+bool kernel_signal_enabled() { return knobs().kernel_signal; }
 
 void wait_device(Dev& d) {
   if (spin_enabled()) {
@@ -905,17 +870,7 @@ constexpr size_t kZeroCopyMax = (size_t)256 << 10;
 // in place.  llama.cpp decode through the boundary (tools/ab_zero_copy.sh,
 // profiles/r02/ab_zero_copy.txt, p=32 tg, -t 8): device copies 66 tok/s (34.5 us per matmul
 // call: the D2H into ggml's pageable dst blocks), in only 72, out only 74, both 89 (24.4 us).
-bool zero_copy(size_t bytes, bool in) {
-  static const int mode = [] {
-    const char* e = getenv("LAMM_HIP_ZERO_COPY");
-    const char* p = getenv("LAMM_HIP_PINNED");
-    if ((p && p[0] == '0') || (e && e[0] == '0')) return 0;
-    if (e && !strcmp(e, "in")) return 1;
-    if (e && !strcmp(e, "out")) return 2;
-    return 3;
-  }();
-  return (mode & (in ? 1 : 2)) && bytes <= kZeroCopyMax;
-}
+bool zero_copy(size_t bytes, bool in) { return (knobs().zero_copy & (in ? 1 : 2)) && bytes <= kZeroCopyMax; }
 
 }  // namespace
 
@@ -1060,7 +1015,7 @@ extern "C" void lamm_mul_mat(const struct ggml_compute_params* vparams, struct g
     pa.r3 = (int)(ne13 / ne03);
     const bool stationary = weight && N > gemv_max_n(t0) && (!b_f32 || N > 8) &&
                             ((gemm_fp6_supported(t0) && gemm_path(pa, true) == 0) ||
-                             (gemm_kq_supported(t0) && !getenv_flag0("LAMM_KQ_GEMM")));
+                             (gemm_kq_supported(t0) && knobs().kq_gemm));
     Completion comp{d.done_ctr, d.flag_dev, 0, false};
     if (zc_out && spin_enabled() && kernel_signal_enabled()) {   // nothing is queued behind the matmul
       comp.seq = ++d.seq;
@@ -1114,6 +1069,7 @@ extern "C" void lamm_hip_boundary_reset(void) {
   Runtime& rt = Runtime::get();
   std::lock_guard<std::mutex> lock(rt.mu);
   rt.reset();
+  reload_knobs();   // the next call sees the environment as it is now
 }
 
 extern "C" size_t lamm_hip_cache_bytes(void) {

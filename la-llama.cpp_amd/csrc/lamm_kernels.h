@@ -56,11 +56,12 @@ bool quantize_weights_supported(int type);
 hipError_t launch_quantize_weights(int type, const float* x, int64_t ldx, void* y, int64_t ldy_bytes, int K, int M,
                                    hipStream_t s);
 
+// hipFuncSetAttribute(kernel, MaxDynamicSharedMemorySize, bytes) once per (device, kernel) and
+// size: a launch path that set it every call would pay the runtime call on every launch
+void set_max_lds(const void* kernel, int bytes);
+
 // completion flag (lamm_signal.hip): stores seq into *flag_dev after everything queued on s
 hipError_t launch_signal(unsigned* flag_dev, unsigned seq, hipStream_t s);
-
-// sets lamm_hip_last_error() (lamm_hip.cpp) and returns code
-int report_error(int code, const char* msg);
 
 hipError_t launch_gemm(int type, const GemvArgs& p, void* workspace, hipStream_t s);
 size_t gemm_workspace_bytes(int type, const GemvArgs& p);   // device scratch launch_gemm needs

@@ -1,0 +1,47 @@
+// lamm_knobs.h -- every LAMM_* environment switch of liblamm_hip.so, read ONCE: at the first
+// call that needs one, again only at lamm_hip_reload_env() (and lamm_hip_boundary_reset()).
+// No launch path calls getenv.  The production defaults are the zero / -1 values; every switch
+// only forces an alternative engine, plan or boundary policy (A/B measurements, tests).
+#pragma once
+
+namespace lamm {
+
+struct Knobs {
+  // ---- operator API: engine and plan selection
+  int gemm_path = -1;          // LAMM_GEMM_PATH: fp6|0 / i8|1 forces the q4_0/q4_1/q5_0 prefill engine
+  int gemv_max_n = 0;          // LAMM_GEMV_MAX_N: widest N on the decode GEMV (0: per-type default)
+  bool dense_gemm = true;      // LAMM_DENSE_GEMM=0: F32/F16 prefill on the grouped GEMV instead
+  bool kq_gemm = true;         // LAMM_KQ_GEMM=0: k-quant prefill on the grouped GEMV / i8 engine
+  int fp6_split = 0;           // LAMM_FP6_SPLIT=n: split-K plan with n splits
+  int fp6_sub = -1;            // LAMM_FP6_SUB: 0 split-K plan, 1 4-group K-group plan, 2 2-group plan
+  bool fp6_fused_reduce = false;   // LAMM_FP6_FUSED_REDUCE=1: split-K partials summed in-launch
+  int fp6_wj = 2;              // LAMM_FP6_WJ=1: 16 waves of 32x64 on the 256x128 plan
+  int i8_split = 0;            // LAMM_I8_SPLIT=n
+  int dense_split = 0;         // LAMM_DENSE_SPLIT=n
+  int kq_split = 0;            // LAMM_KQ_SPLIT=n
+  int kq_variant = 0;          // LAMM_KQ_VARIANT=1: single-pass super-block kernel
+  int gemv_variant = 0;        // LAMM_GEMV_VARIANT: 7 segmented, 8 DMA 4x4, 10 VGPR stream, 12 flat, 13 staged seg
+  int gemv_rpw = -1;           // LAMM_GEMV_RPW: 0 off, 4 / 8 / 16 waves forced
+  bool gemv_laneb = false;     // LAMM_GEMV_LANEB=1: per-lane activation blocks in the row-per-wave GEMV
+  // ---- ggml boundary
+  int opt_level = 3;           // LAMM_OPT_LEVEL=0: lamm_can_mul_mat always false
+  int device = -1;             // LAMM_HIP_DEVICE: the boundary's device (-1: first gfx950)
+  char devices[256] = {0};     // LAMM_HIP_DEVICES: "all" or "0,1,2,3" (empty: one device)
+  bool stats = false;          // LAMM_HIP_STATS=1
+  double cache_gb = 64.0;      // LAMM_HIP_CACHE_GB
+  bool pinned = true;          // LAMM_HIP_PINNED=0: no pinned staging (and no zero copy)
+  int views = -1;              // LAMM_HIP_VIEWS: 0 never, 1 always, -1 prefill only
+  bool extra_types = true;     // LAMM_HIP_EXTRA_TYPES=0: only the reference's 7 pairs
+  int gpu_quant = -1;          // LAMM_HIP_GPU_QUANT: 0 CPU INIT, 1 GPU for every row count
+  bool fused = true;           // LAMM_HIP_FUSED=0: no fused INIT in the decode GEMV
+  bool spin = true;            // LAMM_HIP_SPIN=0: hipStreamSynchronize instead of the flag spin
+  bool kernel_signal = false;  // LAMM_HIP_KERNEL_SIGNAL=1: the GEMV writes the completion flag
+  int zero_copy = 3;           // LAMM_HIP_ZERO_COPY: 0 off, 1 in, 2 out, 3 both
+};
+
+// The current switches (read from the environment at the first call).
+const Knobs& knobs();
+// Re-read the environment (tests, A/B tools); earlier references stay valid.
+void reload_knobs();
+
+}  // namespace lamm

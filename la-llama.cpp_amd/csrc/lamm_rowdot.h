@@ -1,5 +1,5 @@
-// lamm_rowdot.h -- the row-per-wave block-dot pieces shared by the decode GEMV
-// (lamm_gemv_rpw.hip) and the decode chain (lamm_chain.hip): block layouts, wide buffer loads
+// lamm_rowdot.h -- the row-per-wave block-dot pieces of the decode GEMV (lamm_gemv_rpw.hip) and
+// the fp6 GEMM's activation prep (lamm_gemm_fp6.hip): block layouts, wide buffer loads
 // with realignment, the A-block unpack and the activation staging (ggml's AVX2 from_float for
 // F32 rows, bit for bit).  The arithmetic is the reference's lamm_kernel_q*.hpp block dot:
 // exact int32 dots, d_a*d_b*S [+ m_a*s_b] in fp32.

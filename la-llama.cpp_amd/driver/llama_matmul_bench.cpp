@@ -19,11 +19,18 @@
 // --batch-proj stores wq|wk|wv and ffn_gate|ffn_up as slices of one tensor each and runs each
 // group as ONE lamm_hip_matmul_batched launch against the shared input (B slice stride 0):
 // 4 launches per layer instead of 7 (a GPU-native layout; llama.cpp-b2430 issues 7 mul_mats).
-// --chain runs the 7 x 32 single-token GEMVs as ONE lamm_hip_chain launch (lamm_chain.hip: a
-// persistent kernel whose waves stream the next op's weight rows while its input is produced;
-// ops wait inside the launch only for the op that produces their input), then the output
-// projection as its own launch; each layer gets its own output buffers (a chain's outputs may
-// not overlap) and layer 0 reads a fixed input.
+// Row-sharded multi-GPU form (BASELINE config 5: "weight rows sharded 8xMI355X + RCCL
+// all-gather"; the reference's row split over threads, src/lamm_impl.hpp:38-43 / :107-112,
+// mapped onto GPUs): every weight's rows split over the ranks (lamm_hip_shard_rows),
+// each rank computes its rows of every projection into its full-size output and one
+// lamm_hip_allgather_rows per projection gives every rank the whole vector for the next matmul.
+//   --shard G [--devices 0,1,..]   one process, G local ranks (lamm_hip_comm_init_all; device ids
+//                                  may repeat: the loopback rehearsal on one GPU)
+//   --rank r --world w --comm-id HEX [--device d]   one process per GPU (lamm_hip_comm_init_rank)
+// --batch-proj in the sharded form stores q|k|v and gate|up as ONE tall weight each (12288 and
+// 22016 rows) so their rows shard like any other weight.  The whole step (matmuls + all-gathers)
+// is captured into one hipGraph per process.  --dump FILE writes rank 0's logits (f32) after
+// the timed replays (bit-for-bit comparison of a sharded run against one GPU).
 // --concurrent keeps llama.cpp's 7 separate tensors but forks wk / wv and ffn_up onto side
 // streams (parallel branches of the captured graph) -- measured SLOWER (decode 1.88 -> 2.14
 // ms): each GEMV grid wants every CU (one 149 KiB-LDS workgroup per CU), so concurrent
@@ -79,14 +86,14 @@ int parse_type(const char* s) {
 struct Tensor {
   int type = 0, M = 0, K = 0, kb = 0, slices = 1;   // slices: projections sharing one input
   int64_t ld = 0;
+  int64_t r0 = 0, Mfull = 0;   // sharded form: this slab is rows [r0, r0 + M) of a Mfull-row weight
   void* data = nullptr;
   lamm_weights* handle = nullptr;
   size_t bytes() const { return (size_t)ld * lamm_type_size(type) * M; }   // one slice
 };
 
-// random F32 values (fixed LCG) quantized on the GPU into `copies` distinct tensors
-std::vector<Tensor> make_weights(int type, int M, int K, int copies, bool stationary, hipStream_t s,
-                                 int slices = 1) {
+// random F32 values (fixed LCG, seeded by the shape) of an M x K weight
+std::vector<float> host_weights(int M, int K) {
   std::vector<float> h((size_t)M * K);
   uint32_t st = 0x9e3779b9u ^ (uint32_t)(M * 131 + K);
   for (float& v : h) {
@@ -95,6 +102,13 @@ std::vector<Tensor> make_weights(int type, int M, int K, int copies, bool statio
   }
   const float amp = std::sqrt(3.0f / K);   // unit gain per matmul: activations stay O(1) over 32 layers
   for (float& v : h) v *= amp;
+  return h;
+}
+
+// host_weights(M, K) quantized on the GPU into `copies` distinct tensors
+std::vector<Tensor> make_weights(int type, int M, int K, int copies, bool stationary, hipStream_t s,
+                                 int slices = 1) {
+  const std::vector<float> h = host_weights(M, K);
   float* dx = nullptr;
   hip_ok(hipMalloc(&dx, h.size() * 4), "hipMalloc");
   hip_ok(hipMemcpy(dx, h.data(), h.size() * 4, hipMemcpyHostToDevice), "upload");
@@ -137,8 +151,6 @@ struct Model {
   std::vector<Tensor> wq, wk, wv, wo, w1, w3, w2, out;
   Act a4096, b4096, c4096, a11008;
   float *q, *k, *v, *o, *g, *u, *d, *logits;
-  lamm_chain* chain = nullptr;   // --chain: every layer's 7 GEMVs as one launch
-  Act last;                      // --chain: the output projection's input (last layer's down)
 };
 
 bool g_fused = true;   // decode (N <= 8): F32 activations straight into the GEMV (INIT fused)
@@ -175,12 +187,6 @@ void matmul(const Tensor& w, const Act& a, float* C, int N, hipStream_t s) {
 // one token step: the mul_mat nodes of build_llama in graph order
 void step(Model& m, int layers, hipStream_t s) {
   const int N = m.N;
-  if (m.chain) {
-    lamm_ok(lamm_hip_chain_run(m.chain, s), "lamm_hip_chain_run");
-    quantize(m.out[0].type, m.last, N, s);
-    matmul(m.out[0], m.last, m.logits, N, s);
-    return;
-  }
   for (int l = 0; l < layers; ++l) {
     quantize(m.wq[l].type, m.a4096, N, s);           // attn_norm output -> wq / wk / wv
     if (m.side[0] && m.wq[l].slices == 1) {          // wk / wv on forked streams, joined before wo
@@ -221,11 +227,288 @@ void step(Model& m, int layers, hipStream_t s) {
   matmul(m.out[0], m.a4096, m.logits, N, s);
 }
 
+// ---------------------------------------------------------------- row-sharded form
+constexpr int kShardAlign = 16;   // row granularity of the split (lamm_hip_shard_rows)
+
+// rows [r0, r0 + rows) of a `rep` x M-row weight stacked from host_weights(M, K) (rep = 3: q|k|v,
+// 2: gate|up), quantized on this device into `copies` distinct slabs
+std::vector<Tensor> make_slabs(int type, int M, int K, int rep, int64_t r0, int64_t rows, int copies, bool stationary,
+                               hipStream_t s) {
+  const std::vector<float> h = host_weights(M, K);
+  std::vector<float> part((size_t)std::max<int64_t>(rows, 1) * K);
+  for (int64_t i = 0; i < rows; ++i)
+    memcpy(&part[(size_t)i * K], &h[(size_t)((r0 + i) % M) * K], (size_t)K * 4);
+  float* dx = nullptr;
+  hip_ok(hipMalloc(&dx, part.size() * 4), "hipMalloc");
+  hip_ok(hipMemcpy(dx, part.data(), part.size() * 4, hipMemcpyHostToDevice), "upload");
+  std::vector<Tensor> out;
+  for (int c = 0; c < copies; ++c) {
+    Tensor t;
+    t.type = type;
+    t.M = (int)rows;
+    t.K = K;
+    t.kb = K / lamm_blck_size(type);
+    t.ld = t.kb;
+    while ((t.ld * lamm_type_size(type)) % 16) ++t.ld;
+    t.r0 = r0;
+    t.Mfull = (int64_t)rep * M;
+    hip_ok(hipMalloc(&t.data, t.bytes() + 256), "hipMalloc(weights)");
+    if (rows > 0) {
+      lamm_ok(lamm_hip_quantize(type, 0, dx, K, t.data, t.ld, K, (int)rows, s), "lamm_hip_quantize(weights)");
+      if (stationary) {
+        lamm_matrix A{t.data, type, (int)rows, t.kb, t.ld};
+        lamm_ok(lamm_hip_weights_create(&A, 1, 1, 0, 0, s, &t.handle), "lamm_hip_weights_create");
+      }
+    }
+    out.push_back(t);
+  }
+  hip_ok(hipStreamSynchronize(s), "quantize weights");
+  hip_ok(hipFree(dx), "hipFree");
+  return out;
+}
+
+// one local rank of a sharded run: its device, stream, weight slabs, and full-size vectors
+struct Rank {
+  int dev = 0, grank = 0;
+  hipStream_t s = nullptr;
+  std::vector<Tensor> wq, wk, wv, wo, w1, w3, w2, out;   // tall form: wq = q|k|v, w1 = gate|up
+  float *q = nullptr, *k = nullptr, *v = nullptr, *o = nullptr, *g = nullptr, *u = nullptr, *d = nullptr,
+        *logits = nullptr;
+  Act a4096, b4096, c4096, a11008;
+};
+
+// this rank's rows of C = w . a, written at their place in the full output C (column stride Mfull)
+void matmul_rows(const Tensor& w, Act& a, float* C, int N, hipStream_t s) {
+  if (w.M == 0) return;
+  quantize(w.type, a, N, s);
+  const int vt = lamm_vec_dot_type(w.type);
+  lamm_matrix B{vt == 0 ? (void*)a.x : a.q, vt, w.kb, N, (int64_t)(a.K / lamm_blck_size(vt))};
+  if (fused(w.type, N)) B = lamm_matrix{a.x, 0, a.K, N, (int64_t)a.K};
+  lamm_matrix Cm{C + w.r0, 0, w.M, N, w.Mfull};
+  if (w.handle) {
+    lamm_ok(lamm_hip_matmul_weights(w.handle, &B, &Cm, nullptr, s), "lamm_hip_matmul_weights");
+  } else {
+    lamm_matrix A{w.data, w.type, w.M, w.kb, w.ld};
+    lamm_ok(lamm_hip_matmul(&A, &B, &Cm, s), "lamm_hip_matmul");
+  }
+}
+
+// every local rank: its rows of one projection; then one all-gather of that output
+template <class W, class In, class Out>
+void project(std::vector<Rank>& R, lamm_comm* comm, int N, W wsel, In insel, Out outsel) {
+  std::vector<const float*> slabs;
+  std::vector<int64_t> ld;
+  std::vector<float*> Cs;
+  std::vector<void*> streams;
+  int64_t Mfull = 0;
+  for (Rank& r : R) {
+    hip_ok(hipSetDevice(r.dev), "hipSetDevice");
+    const Tensor& w = wsel(r);
+    float* C = outsel(r);
+    matmul_rows(w, insel(r), C, N, r.s);
+    Mfull = w.Mfull;
+    slabs.push_back(C + w.r0);
+    ld.push_back(w.Mfull);
+    Cs.push_back(C);
+    streams.push_back(r.s);
+  }
+  lamm_ok(lamm_hip_allgather_rows(comm, slabs.data(), ld.data(), Cs.data(), Mfull, Mfull, N, kShardAlign,
+                                  streams.data()),
+          "lamm_hip_allgather_rows");
+}
+
+void step_sharded(std::vector<Rank>& R, lamm_comm* comm, int layers, int N, bool tall) {
+  for (int l = 0; l < layers; ++l) {
+    project(R, comm, N, [&](Rank& r) -> const Tensor& { return r.wq[l]; }, [](Rank& r) -> Act& { return r.a4096; },
+            [](Rank& r) { return r.q; });
+    if (!tall) {
+      project(R, comm, N, [&](Rank& r) -> const Tensor& { return r.wk[l]; }, [](Rank& r) -> Act& { return r.a4096; },
+              [](Rank& r) { return r.k; });
+      project(R, comm, N, [&](Rank& r) -> const Tensor& { return r.wv[l]; }, [](Rank& r) -> Act& { return r.a4096; },
+              [](Rank& r) { return r.v; });
+    }
+    project(R, comm, N, [&](Rank& r) -> const Tensor& { return r.wo[l]; }, [](Rank& r) -> Act& { return r.b4096; },
+            [](Rank& r) { return r.o; });
+    project(R, comm, N, [&](Rank& r) -> const Tensor& { return r.w1[l]; }, [](Rank& r) -> Act& { return r.c4096; },
+            [](Rank& r) { return r.g; });
+    if (!tall)
+      project(R, comm, N, [&](Rank& r) -> const Tensor& { return r.w3[l]; }, [](Rank& r) -> Act& { return r.c4096; },
+              [](Rank& r) { return r.u; });
+    project(R, comm, N, [&](Rank& r) -> const Tensor& { return r.w2[l]; }, [](Rank& r) -> Act& { return r.a11008; },
+            [](Rank& r) { return r.d; });
+  }
+  project(R, comm, N, [](Rank& r) -> const Tensor& { return r.out[0]; }, [](Rank& r) -> Act& { return r.a4096; },
+          [](Rank& r) { return r.logits; });
+}
+
+struct ShardOpts {
+  int world = 0;            // > 0: sharded
+  std::vector<int> devices; // local ranks' devices (--shard / --devices), or the one device (--rank)
+  int rank = -1;            // >= 0: one rank per process
+  std::string comm_id;      // hex (2 * LAMM_COMM_ID_BYTES digits) or "auto" (world 1 only)
+  std::string dump;
+};
+
+int run_sharded(const ShardOpts& o, int type, int out_type, int N, int iters, int layers, bool stationary, bool tall) {
+  constexpr int H = 4096, F = 11008, V = 32000;
+  lamm_comm* comm = nullptr;
+  std::vector<Rank> R(o.devices.size());
+  if (o.rank >= 0) {
+    unsigned char id[LAMM_COMM_ID_BYTES] = {0};
+    if (o.comm_id == "auto") {
+      if (o.world != 1) { fprintf(stderr, "llama-matmul-bench: --comm-id auto needs --world 1\n"); return 1; }
+      lamm_ok(lamm_hip_comm_unique_id(id), "lamm_hip_comm_unique_id");
+    } else {
+      if (o.comm_id.size() != 2 * LAMM_COMM_ID_BYTES) { fprintf(stderr, "llama-matmul-bench: bad --comm-id\n"); return 1; }
+      for (int i = 0; i < LAMM_COMM_ID_BYTES; ++i) id[i] = (unsigned char)std::stoi(o.comm_id.substr(2 * i, 2), nullptr, 16);
+    }
+    if (lamm_hip_comm_init_rank(&comm, o.world, o.rank, id, o.devices[0]) != LAMM_OK) {
+      fprintf(stderr, "llama-matmul-bench: lamm_hip_comm_init_rank: %s\n", lamm_hip_comm_last_error());
+      return 1;
+    }
+    R[0].grank = o.rank;
+  } else {
+    if (lamm_hip_comm_init_all(&comm, (int)o.devices.size(), o.devices.data()) != LAMM_OK) {
+      fprintf(stderr, "llama-matmul-bench: lamm_hip_comm_init_all: %s\n", lamm_hip_comm_last_error());
+      return 1;
+    }
+    for (size_t i = 0; i < R.size(); ++i) R[i].grank = (int)i;
+  }
+  const int world = o.world;
+  size_t wbytes = 0;
+  double params = 0;
+  for (size_t i = 0; i < R.size(); ++i) {
+    Rank& r = R[i];
+    r.dev = o.devices[i];
+    hip_ok(hipSetDevice(r.dev), "hipSetDevice");
+    hip_ok(hipStreamCreateWithFlags(&r.s, hipStreamNonBlocking), "hipStreamCreate");
+    auto slabs = [&](int ty, int M, int K, int rep, int copies) {
+      int64_t r0, rows;
+      lamm_hip_shard_rows((int64_t)rep * M, world, r.grank, kShardAlign, &r0, &rows);
+      auto v = make_slabs(ty, M, K, rep, r0, rows, copies, stationary, r.s);
+      if (i == 0) {   // whole-model bytes / params (every rank's slabs add up to one model)
+        wbytes += (size_t)v.size() * (size_t)(K / lamm_blck_size(ty)) * lamm_type_size(ty) * (size_t)rep * M;
+        params += (double)v.size() * rep * M * K;
+      }
+      return v;
+    };
+    if (tall) {
+      r.wq = slabs(type, H, H, 3, layers);
+      r.w1 = slabs(type, F, H, 2, layers);
+    } else {
+      r.wq = slabs(type, H, H, 1, layers);
+      r.wk = slabs(type, H, H, 1, layers);
+      r.wv = slabs(type, H, H, 1, layers);
+      r.w1 = slabs(type, F, H, 1, layers);
+      r.w3 = slabs(type, F, H, 1, layers);
+    }
+    r.wo = slabs(type, H, H, 1, layers);
+    r.w2 = slabs(type, H, F, 1, layers);
+    r.out = slabs(out_type, V, H, 1, 1);
+    auto mk_out = [&](float*& p, int M) {
+      hip_ok(hipMalloc(&p, (size_t)N * M * 4 + 256), "hipMalloc(out)");
+      hip_ok(hipMemsetAsync(p, 0, (size_t)N * M * 4 + 256, r.s), "hipMemsetAsync");
+    };
+    mk_out(r.q, 3 * H); mk_out(r.k, H); mk_out(r.v, H); mk_out(r.o, H);
+    mk_out(r.g, 2 * F); mk_out(r.u, F); mk_out(r.d, H); mk_out(r.logits, V);
+    std::vector<float> x((size_t)N * H);
+    for (size_t j = 0; j < x.size(); ++j) x[j] = std::sin(0.37f * (float)j);   // the single-GPU run's input
+    hip_ok(hipStreamSynchronize(r.s), "memsets");
+    hip_ok(hipMemcpy(r.d, x.data(), x.size() * 4, hipMemcpyHostToDevice), "upload x");
+    auto mk_act = [&](Act& a, int K, float* alias) {
+      a.K = K;
+      a.x = alias;
+      hip_ok(hipMalloc(&a.q, (size_t)N * K * 2 + 4096), "hipMalloc(q act)");
+    };
+    // tall form at N > 1: q|k|v rows interleave per column ([N][12288]), so wo's input is not the
+    // first N x 4096 block -- the bench only needs a well-formed input, so it reads those floats
+    mk_act(r.a4096, H, r.d);
+    mk_act(r.b4096, H, r.q);
+    mk_act(r.c4096, H, r.o);
+    mk_act(r.a11008, F, tall ? r.g + (size_t)F : r.u);
+  }
+  printf("llama-matmul-bench: Llama-7B weight matmuls, %d layers, weights %s, output.weight %s, %.2f GB of weight "
+         "blocks, %d token(s) per step, rows sharded over %d rank(s) (%s; this process: %zu), hipGraph%s%s\n",
+         layers, type_name(type), type_name(out_type), wbytes / 1e9, N, world,
+         o.rank >= 0 ? "one process per GPU, RCCL" : (lamm_hip_comm_local_ranks(comm) > 1 ? "one process" : "one rank"),
+         R.size(), stationary ? ", weight-stationary handles" : "", tall ? ", q|k|v and gate|up as tall weights" : "");
+  for (int w = 0; w < 2; ++w) step_sharded(R, comm, layers, N, tall);
+  for (Rank& r : R) {
+    hip_ok(hipSetDevice(r.dev), "hipSetDevice");
+    hip_ok(hipStreamSynchronize(r.s), "warm-up");
+  }
+  // one graph: the step on rank 0's stream, the other local ranks' streams forked from it
+  hip_ok(hipSetDevice(R[0].dev), "hipSetDevice");
+  hipEvent_t fork;
+  std::vector<hipEvent_t> join(R.size());
+  hip_ok(hipEventCreateWithFlags(&fork, hipEventDisableTiming), "hipEventCreate");
+  for (size_t i = 1; i < R.size(); ++i) {
+    hip_ok(hipSetDevice(R[i].dev), "hipSetDevice");
+    hip_ok(hipEventCreateWithFlags(&join[i], hipEventDisableTiming), "hipEventCreate");
+  }
+  hip_ok(hipSetDevice(R[0].dev), "hipSetDevice");
+  hipGraph_t g;
+  hipGraphExec_t exec = nullptr;
+  hip_ok(hipStreamBeginCapture(R[0].s, hipStreamCaptureModeRelaxed), "hipStreamBeginCapture");
+  hip_ok(hipEventRecord(fork, R[0].s), "hipEventRecord");
+  for (size_t i = 1; i < R.size(); ++i) hip_ok(hipStreamWaitEvent(R[i].s, fork, 0), "hipStreamWaitEvent");
+  step_sharded(R, comm, layers, N, tall);
+  for (size_t i = 1; i < R.size(); ++i) {
+    hip_ok(hipSetDevice(R[i].dev), "hipSetDevice");
+    hip_ok(hipEventRecord(join[i], R[i].s), "hipEventRecord");
+    hip_ok(hipSetDevice(R[0].dev), "hipSetDevice");
+    hip_ok(hipStreamWaitEvent(R[0].s, join[i], 0), "hipStreamWaitEvent");
+  }
+  hip_ok(hipStreamEndCapture(R[0].s, &g), "hipStreamEndCapture");
+  hip_ok(hipGraphInstantiate(&exec, g, nullptr, nullptr, 0), "hipGraphInstantiate");
+  hip_ok(hipGraphDestroy(g), "hipGraphDestroy");
+  hip_ok(hipGraphLaunch(exec, R[0].s), "hipGraphLaunch");
+  hip_ok(hipStreamSynchronize(R[0].s), "graph warm-up");
+  hipEvent_t e0, e1;
+  hip_ok(hipEventCreate(&e0), "hipEventCreate");
+  hip_ok(hipEventCreate(&e1), "hipEventCreate");
+  hip_ok(hipEventRecord(e0, R[0].s), "hipEventRecord");
+  for (int it = 0; it < iters; ++it) hip_ok(hipGraphLaunch(exec, R[0].s), "hipGraphLaunch");
+  hip_ok(hipEventRecord(e1, R[0].s), "hipEventRecord");
+  hip_ok(hipEventSynchronize(e1), "hipEventSynchronize");
+  float ms = 0;
+  hip_ok(hipEventElapsedTime(&ms, e0, e1), "hipEventElapsedTime");
+  const double t = ms * 1e-3 / iters;
+  std::vector<float> lg((size_t)N * V);
+  hip_ok(hipMemcpy(lg.data(), R[0].logits, lg.size() * 4, hipMemcpyDeviceToHost), "download logits");
+  double cs = 0;
+  for (float v : lg) cs += std::fabs(v);
+  if (!std::isfinite(cs)) {
+    fprintf(stderr, "llama-matmul-bench: non-finite logits\n");
+    return 1;
+  }
+  if (!o.dump.empty()) {
+    FILE* f = fopen(o.dump.c_str(), "wb");
+    if (!f || fwrite(lg.data(), 4, lg.size(), f) != lg.size()) { fprintf(stderr, "llama-matmul-bench: --dump failed\n"); return 1; }
+    fclose(f);
+  }
+  const int projections = (tall ? 4 : 7) * layers + 1;
+  printf("step %.3f ms  |  %.1f tok/s  |  weight stream %.1f GB/s (whole model)  |  %d matmuls + %d all-gathers per rank "
+         "per step  |  logits |sum| %.6g\n",
+         t * 1e3, N / t, wbytes / t / 1e9, projections, projections, cs);
+  printf("{\"tool\": \"llama-matmul-bench\", \"layers\": %d, \"tokens_per_step\": %d, \"ms_per_step\": %.4f, "
+         "\"tok_per_s\": %.2f, \"weight_GBps\": %.1f, \"TFLOPs\": %.2f, \"graph\": true, \"stationary\": %s, "
+         "\"type\": \"%s\", \"mode\": \"%s\", \"launches\": %d, \"world\": %d, \"rank\": %d, \"local_ranks\": %zu, "
+         "\"allgathers\": %d, \"logits_abs_sum\": %.9g}\n",
+         layers, N, t * 1e3, N / t, wbytes / t / 1e9, 2.0 * params * N / t / 1e12, stationary ? "true" : "false",
+         type_name(type), tall ? "sharded-batch-proj" : "sharded", projections, world, o.rank >= 0 ? o.rank : 0,
+         R.size(), projections, cs);
+  lamm_hip_comm_destroy(comm);
+  return 0;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
   int type = 2, N = 1, iters = 20, layers = 32, out_type = 14;
-  bool graph = true, stationary = false, batch_proj = false, concurrent = false, chain = false;
+  bool graph = true, stationary = false, batch_proj = false, concurrent = false;
+  ShardOpts so;
+  int shard = 0;
   for (int i = 1; i < argc; ++i) {
     const std::string a = argv[i];
     auto next = [&]() -> const char* {
@@ -242,9 +525,25 @@ int main(int argc, char** argv) {
     else if (a == "--unfused") g_fused = false;
     else if (a == "--batch-proj") batch_proj = true;
     else if (a == "--concurrent") concurrent = true;
-    else if (a == "--chain") chain = true;
+    else if (a == "--shard") shard = atoi(next());
+    else if (a == "--devices") {
+      so.devices.clear();
+      for (const char* c = next(); *c;) {
+        char* end = nullptr;
+        so.devices.push_back((int)strtol(c, &end, 10));
+        if (end == c) break;
+        c = *end == ',' ? end + 1 : end;
+      }
+    }
+    else if (a == "--rank") so.rank = atoi(next());
+    else if (a == "--world") so.world = atoi(next());
+    else if (a == "--comm-id") so.comm_id = next();
+    else if (a == "--device") so.devices = {atoi(next())};
+    else if (a == "--dump") so.dump = next();
     else {
-      fprintf(stderr, "usage: %s [-d q4_0] [-n tokens] [-i replays] [-l layers] [--no-graph] [-s] [--output-type q6_k] [--unfused] [--batch-proj] [--concurrent] [--chain]\n",
+      fprintf(stderr, "usage: %s [-d q4_0] [-n tokens] [-i replays] [-l layers] [--no-graph] [-s] [--output-type q6_k] "
+                      "[--unfused] [--batch-proj] [--concurrent] [--shard G [--devices 0,1,..]] "
+                      "[--rank r --world w --comm-id HEX|auto [--device d]] [--dump FILE]\n",
               argv[0]);
       return 1;
     }
@@ -252,6 +551,26 @@ int main(int argc, char** argv) {
   if (lamm_hip_device_count() <= 0) {
     fprintf(stderr, "llama-matmul-bench: no gfx950 device (%s)\n", lamm_hip_last_error());
     return 1;
+  }
+  if (so.rank >= 0 || shard > 0 || !so.devices.empty() || !so.dump.empty()) {   // the row-sharded form
+    if (so.rank >= 0) {
+      if (so.world < 1 || so.rank >= so.world || so.comm_id.empty()) {
+        fprintf(stderr, "llama-matmul-bench: --rank needs --world > rank and --comm-id\n");
+        return 1;
+      }
+      if (so.devices.empty()) so.devices = {so.rank % lamm_hip_device_count()};
+    } else {
+      if (so.devices.empty()) {   // G local ranks on devices 0..G-1 (repeating when fewer: loopback)
+        const int G = shard > 0 ? shard : 1;
+        for (int i = 0; i < G; ++i) so.devices.push_back(i % lamm_hip_device_count());
+      }
+      so.world = (int)so.devices.size();
+    }
+    if (concurrent || !graph) {
+      fprintf(stderr, "llama-matmul-bench: the sharded form is graph-captured, without --concurrent\n");
+      return 1;
+    }
+    return run_sharded(so, type, out_type, N, iters, layers, stationary, batch_proj);
   }
   constexpr int H = 4096, F = 11008, V = 32000;
   hipStream_t s;
@@ -309,44 +628,10 @@ int main(int argc, char** argv) {
   mk_act(m.c4096, H, m.o);
   mk_act(m.a11008, F, batch_proj ? m.g + (size_t)N * F : m.u);   // the up projection's output
 
-  std::vector<void*> chain_bufs;
-  if (chain) {   // per-layer outputs; layer 0 reads a copy of the first input
-    if (batch_proj || N != 1) {
-      fprintf(stderr, "llama-matmul-bench: --chain is a single-token path of separate tensors (no --batch-proj, -n 1)\n");
-      return 1;
-    }
-    auto buf = [&](int M) {
-      float* p = nullptr;
-      hip_ok(hipMalloc(&p, (size_t)M * 4 + 256), "hipMalloc(chain)");
-      hip_ok(hipMemset(p, 0, (size_t)M * 4 + 256), "hipMemset(chain)");
-      chain_bufs.push_back(p);
-      return p;
-    };
-    float* x = buf(H);
-    hip_ok(hipMemcpy(x, m.d, (size_t)H * 4, hipMemcpyDeviceToDevice), "copy x");
-    std::vector<lamm_chain_op> ops;
-    auto op = [&](const Tensor& w, const float* in, float* out) {
-      ops.push_back(lamm_chain_op{lamm_matrix{w.data, w.type, w.M, w.kb, w.ld}, in, out});
-    };
-    for (int l = 0; l < layers; ++l) {
-      float *q = buf(H), *k = buf(H), *v = buf(H), *o = buf(H), *g = buf(F), *u = buf(F), *d = buf(H);
-      op(m.wq[l], x, q);
-      op(m.wk[l], x, k);
-      op(m.wv[l], x, v);
-      op(m.wo[l], q, o);
-      op(m.w1[l], o, g);
-      op(m.w3[l], o, u);
-      op(m.w2[l], u, d);
-      x = d;
-    }
-    lamm_ok(lamm_hip_chain_create(ops.data(), (int)ops.size(), &m.chain), "lamm_hip_chain_create");
-    mk_act(m.last, H, x);
-  }
-
   printf("llama-matmul-bench: Llama-7B weight matmuls, %d layers, weights %s, output.weight %s, "
-         "%.2f GB of weight blocks, %d token(s) per step, %s%s%s\n",
+         "%.2f GB of weight blocks, %d token(s) per step, %s%s\n",
          layers, type_name(type), type_name(out_type), wbytes / 1e9, N, graph ? "hipGraph" : "stream",
-         stationary ? ", weight-stationary handles" : "", chain ? ", one chain launch for the layers" : "");
+         stationary ? ", weight-stationary handles" : "");
 
   // warm-up (workspaces reach their final size before capture), then capture one step
   for (int w = 0; w < 2; ++w) step(m, layers, s);
@@ -383,39 +668,15 @@ int main(int argc, char** argv) {
     fprintf(stderr, "llama-matmul-bench: non-finite logits\n");
     return 1;
   }
-  if (m.chain) lamm_ok(lamm_hip_chain_status(m.chain), "lamm_hip_chain_status");
-  if (m.chain && lamm_hip_chain_trace(m.chain, nullptr, 0)) {   // LAMM_CHAIN_TRACE=1: last launch's phase timeline
-    const int nph = lamm_hip_chain_phases(m.chain), w = 2 * nph + 2;
-    std::vector<uint64_t> tr(lamm_hip_chain_trace(m.chain, nullptr, 0));
-    lamm_hip_chain_trace(m.chain, tr.data(), tr.size());
-    const int grid = (int)(tr.size() / w);
-    uint64_t t0 = ~0ull;
-    for (int g = 0; g < grid; ++g) t0 = std::min(t0, tr[(size_t)g * w]);
-    auto col = [&](int k, std::vector<double>& v) {
-      v.clear();
-      for (int g = 0; g < grid; ++g) v.push_back((tr[(size_t)g * w + k] - t0) * 0.01);   // 100 MHz -> us
-      std::sort(v.begin(), v.end());
-    };
-    std::vector<double> b, e;
-    printf("chain trace (us from the first workgroup's start; staging begin min/max, end min/max):\n");
-    for (int p = 0; p < nph; ++p) {
-      col(1 + 2 * p, b);
-      col(2 + 2 * p, e);
-      if (p < 8 || p >= nph - 4)
-        printf("  phase %3d: begin %8.2f %8.2f  end %8.2f %8.2f\n", p, b.front(), b.back(), e.front(), e.back());
-    }
-    col(w - 1, e);
-    printf("  end: %8.2f %8.2f\n", e.front(), e.back());
-  }
-  const int launches = m.chain ? 2 : (batch_proj ? 4 : 7) * layers + 1;
+  const int launches = (batch_proj ? 4 : 7) * layers + 1;
   printf("step %.3f ms  |  %.1f tok/s  |  weight stream %.1f GB/s  |  %.1f TFLOP/s  |  %d matmul launches + %d quantizations per step  |  logits |sum| %.4g\n",
          t * 1e3, N / t, wbytes / t / 1e9, 2.0 * params * N / t / 1e12, launches,
-         m.chain ? 1 : fused(type, N) ? 1 : 4 * layers + 1, cs);
+         fused(type, N) ? 1 : 4 * layers + 1, cs);
   printf("{\"tool\": \"llama-matmul-bench\", \"layers\": %d, \"tokens_per_step\": %d, \"ms_per_step\": %.4f, \"tok_per_s\": %.2f, "
          "\"weight_GBps\": %.1f, \"TFLOPs\": %.2f, \"graph\": %s, \"stationary\": %s, \"type\": \"%s\", "
          "\"mode\": \"%s\", \"launches\": %d}\n",
          layers, N, t * 1e3, N / t, wbytes / t / 1e9, 2.0 * params * N / t / 1e12, graph ? "true" : "false",
          stationary ? "true" : "false", type_name(type),
-         m.chain ? "chain" : batch_proj ? "batch-proj" : concurrent ? "concurrent" : "separate", launches);
+         batch_proj ? "batch-proj" : concurrent ? "concurrent" : "separate", launches);
   return 0;
 }

@@ -68,11 +68,6 @@ class Batch(ctypes.Structure):
                 ("nbc3", ctypes.c_size_t)]
 
 
-class ChainOp(ctypes.Structure):
-    """struct lamm_chain_op: y = A x for one token inside a decode chain."""
-    _fields_ = [("A", Matrix), ("x", ctypes.c_void_p), ("y", ctypes.c_void_p)]
-
-
 class GgmlComputeParams(ctypes.Structure):
     """struct ggml_compute_params, LC/ggml.h:668-677 (b2430)."""
     _fields_ = [("type", ctypes.c_int32), ("ith", ctypes.c_int32), ("nth", ctypes.c_int32),
@@ -136,15 +131,31 @@ lib.lamm_hip_comm_last_error.restype = ctypes.c_char_p
 lib.lamm_hip_allgather_rows.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_int64),
                                         ctypes.POINTER(ctypes.c_void_p), ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
                                         ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
-lib.lamm_hip_chain_create.argtypes = [ctypes.POINTER(ChainOp), ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
-lib.lamm_hip_chain_run.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
-lib.lamm_hip_chain_status.argtypes = [ctypes.c_void_p]
-lib.lamm_hip_chain_phases.argtypes = [ctypes.c_void_p]
-lib.lamm_hip_chain_destroy.argtypes = [ctypes.c_void_p]
-lib.lamm_hip_chain_destroy.restype = None
 lib.lamm_hip_cache_clear.restype = None
 lib.lamm_hip_cache_bytes.restype = ctypes.c_size_t
 lib.lamm_hip_boundary_reset.restype = None
+lib.lamm_hip_reload_env.restype = None
+
+# The library reads its LAMM_* switches once (lamm_hip_reload_env re-reads them).  Tests and A/B
+# tools flip them through os.environ between calls, so every entry point below re-syncs the
+# library when the LAMM_* part of the environment changed since the last call.
+_env_seen = None
+
+
+def _sync_env():
+    global _env_seen
+    cur = tuple(sorted((k, v) for k, v in os.environ.items() if k.startswith("LAMM_")))
+    if cur != _env_seen:
+        if _env_seen is not None:
+            lib.lamm_hip_reload_env()
+        _env_seen = cur
+
+
+def reload_env():
+    """Re-read every LAMM_* switch now (lamm_hip_reload_env)."""
+    global _env_seen
+    _env_seen = tuple(sorted((k, v) for k, v in os.environ.items() if k.startswith("LAMM_")))
+    lib.lamm_hip_reload_env()
 
 
 def blck_size(t):
@@ -199,11 +210,13 @@ def _check(rc, what):
 
 def matmul(A, B, C, stream=0):
     """LAMMImpl<T>::matmul on device memory; A, B, C are ``Matrix`` (device pointers)."""
+    _sync_env()
     _check(lib.lamm_hip_matmul(ctypes.byref(A), ctypes.byref(B), ctypes.byref(C), ctypes.c_void_p(stream)),
            "lamm_hip_matmul")
 
 
 def matmul_batched(A, B, C, batch, stream=0):
+    _sync_env()
     _check(lib.lamm_hip_matmul_batched(ctypes.byref(A), ctypes.byref(B), ctypes.byref(C), ctypes.byref(batch),
                                        ctypes.c_void_p(stream)), "lamm_hip_matmul_batched")
 
@@ -241,6 +254,7 @@ class Weights:
         self.ne02, self.ne03, self.nba2, self.nba3 = ne02, ne03, nba2, nba3
         self._a = a   # keep the blocks alive
         self.A = Matrix(a.data_ptr(), wtype, M, kb, lda if lda is not None else kb)
+        _sync_env()
         h = ctypes.c_void_p()
         _check(lib.lamm_hip_weights_create(ctypes.byref(self.A), ne02, ne03, nba2, nba3, ctypes.c_void_p(stream),
                                            ctypes.byref(h)), "lamm_hip_weights_create")
@@ -257,6 +271,7 @@ class Weights:
         vt = vec_dot_type(self.wtype)
         B = Matrix(b.data_ptr(), vt, self.kb, N, ldb if ldb is not None else self.kb)
         C = Matrix(c.data_ptr(), F32, self.M, N, ldc if ldc is not None else self.M)
+        _sync_env()
         _check(lib.lamm_hip_matmul_weights(self.h, ctypes.byref(B), ctypes.byref(C),
                                            ctypes.byref(batch) if batch is not None else None,
                                            ctypes.c_void_p(stream)), "lamm_hip_matmul_weights")
@@ -280,6 +295,7 @@ def quantize_torch(vtype, x, y, flavour=1, stream=None):
     if stream is None:
         stream = torch.cuda.current_stream().cuda_stream
     ldy = K // blck_size(vtype)
+    _sync_env()
     _check(lib.lamm_hip_quantize(vtype, flavour, ctypes.c_void_p(x.data_ptr()), x.stride(0),
                                  ctypes.c_void_p(y.data_ptr()), ldy, K, N, ctypes.c_void_p(stream)),
            "lamm_hip_quantize")
@@ -396,47 +412,18 @@ class Comm:
             pass
 
 
-class Chain:
-    """lamm_chain: single-token GEMVs y_i = A_i x_i run as ONE persistent launch; an op whose x is
-    an earlier op's y waits for it inside the launch.  ops: [(Matrix A, x pointer, y pointer)]."""
-
-    def __init__(self, ops):
-        arr = (ChainOp * len(ops))(*[ChainOp(A, x, y) for (A, x, y) in ops])
-        self.h = ctypes.c_void_p()
-        _check(lib.lamm_hip_chain_create(arr, len(ops), ctypes.byref(self.h)), "lamm_hip_chain_create")
-
-    @property
-    def phases(self):
-        return lib.lamm_hip_chain_phases(self.h)
-
-    def run(self, stream=0):
-        _check(lib.lamm_hip_chain_run(self.h, stream), "lamm_hip_chain_run")
-
-    def status(self):
-        """After the launch finished: raises if a wait inside it gave up."""
-        _check(lib.lamm_hip_chain_status(self.h), "lamm_hip_chain_status")
-
-    def close(self):
-        if self.h:
-            lib.lamm_hip_chain_destroy(self.h)
-            self.h = None
-
-    def __del__(self):
-        try:
-            self.close()
-        except Exception:
-            pass
-
-
 def can_mul_mat(params, dst):
+    _sync_env()
     return bool(lib.lamm_can_mul_mat(ctypes.byref(params), ctypes.byref(dst)))
 
 
 def mul_mat(params, dst):
+    _sync_env()
     lib.lamm_mul_mat(ctypes.byref(params), ctypes.byref(dst))
 
 
 def get_opt_level():
+    _sync_env()
     return lib.lamm_get_opt_level()
 
 
@@ -449,5 +436,8 @@ def cache_bytes():
 
 
 def boundary_reset():
-    """Drop the ggml boundary's devices (caches, streams); the next call re-reads LAMM_HIP_DEVICES."""
+    """Drop the ggml boundary's devices (caches, streams) and re-read every LAMM_* switch; the next
+    call re-reads LAMM_HIP_DEVICES."""
+    global _env_seen
+    _env_seen = tuple(sorted((k, v) for k, v in os.environ.items() if k.startswith("LAMM_")))
     lib.lamm_hip_boundary_reset()

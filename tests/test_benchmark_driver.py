@@ -52,6 +52,19 @@ def test_driver_default_shape_average(extra):
     assert len(rows) == 3 and all("; 11008;  4096;   128;" in ln for ln in rows), rows
 
 
+@pytest.mark.gpu
+def test_driver_config1_f32_512():
+    """BASELINE config 1: la-benchmark-matmult -d f32 at M=N=K=512 (the reference's plumbing
+    config, src/la-benchmark-matmult.cpp:257-276) with the --debug random inputs: the driver's own
+    sum check (within 1e-2 of the analytic sum, else ABORT / exit 1) and the Average line."""
+    r = run("--debug", "-d", "f32", "-M", "512", "-N", "512", "-K", "512", "-t", "1", "-i", "3")
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "ABORT" not in r.stdout
+    m = AVERAGE.search(r.stdout)
+    assert m and float(m.group(1)) > 0
+    assert any(";   512;   512;   512;" in ln for ln in r.stdout.splitlines()), r.stdout[-800:]
+
+
 LLAMA = os.path.join(ROOT, "la-llama.cpp_amd", "llama-matmul-bench")
 
 

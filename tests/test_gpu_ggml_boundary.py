@@ -279,36 +279,56 @@ def test_boundary_rows_split_over_devices(devices, t, M, N, K, monkeypatch):
         np.testing.assert_array_equal(d1.buf.view(np.float32).reshape(N, rows), got[:, r0:r0 + rows])
 
 
+DECODE_MODES = {"fused": {}, "cpu_init": {"LAMM_HIP_FUSED": "0"}, "device_copies": {"LAMM_HIP_ZERO_COPY": "0"},
+                "kernel_signal": {"LAMM_HIP_KERNEL_SIGNAL": "1"}, "no_spin": {"LAMM_HIP_SPIN": "0"}}
+
+
 @pytest.mark.parametrize("t", [ol.Q4_0, ol.Q4_1, ol.Q8_0, ol.Q6_K], ids=["q4_0", "q4_1", "q8_0", "q6_k"])
-@pytest.mark.parametrize("mode", ["fused", "cpu_init", "device_copies"])
-def test_decode_calls_fresh_every_call(t, mode, monkeypatch):
+def test_decode_calls_fresh_every_call(t, monkeypatch):
     """Decode-sized calls through the boundary, as llama.cpp makes them: the SAME src1 / dst
-    buffers with new contents every call (ggml's compute buffer is reused per token).  Activations
-    are read in place from pinned host memory mapped into the device and C is written back the
-    same way (default), or copied by HIP (LAMM_HIP_ZERO_COPY=0); the activations are quantized by
-    the GEMV (fused, default for q8_0 / q8_1 formats) or by ggml's CPU INIT (LAMM_HIP_FUSED=0).
-    Every call must match the oracle, and the modes must agree bit for bit."""
-    if mode == "cpu_init":
-        monkeypatch.setenv("LAMM_HIP_FUSED", "0")
-    if mode == "device_copies":
-        monkeypatch.setenv("LAMM_HIP_ZERO_COPY", "0")
+    buffers with new contents every call (ggml's compute buffer is reused per token).  Modes:
+    activations read in place from pinned host memory mapped into the device and C written back
+    the same way (default), or copied by HIP (LAMM_HIP_ZERO_COPY=0); the activations quantized by
+    the GEMV (fused, default for q8_0 / q8_1 formats) or by ggml's CPU INIT (LAMM_HIP_FUSED=0);
+    completion by the signal launch (default), by the GEMV's own last workgroup
+    (LAMM_HIP_KERNEL_SIGNAL=1) or by hipStreamSynchronize (LAMM_HIP_SPIN=0).  The boundary re-reads
+    its switches at lamm_hip_boundary_reset (they used to be frozen at the first call).
+    Every call must match the oracle, and every mode must give the same bits."""
     M, N, K = 4096, 1, 4096
     rng = np.random.default_rng(t)
     if t in ol.KQ_TYPES:
         A_q = ol.random_kq_blocks(t, M, K, rng)
     else:
         A_q = ORACLE.quantize(t, rng.standard_normal((M, K), dtype=np.float32))
-    src0 = ggml_emu.Tensor(t, [K, M], data=A_q)
-    src1 = ggml_emu.Tensor(ol.F32, [K, N])
-    dst = ggml_emu.mul_mat_node(src0, src1)
+    xs = [rng.standard_normal((N, K), dtype=np.float32) for _ in range(6)]
     vt = la.vec_dot_type(t)
-    for it in range(12):
-        x = rng.standard_normal((N, K), dtype=np.float32)
-        src1.buf.view(np.float32)[:] = x.reshape(-1)
-        assert ggml_emu.compute(dst, nth=2)
-        got = dst.buf.view(np.float32).reshape(N, M)
-        B = ORACLE.quantize(vt, x, ol.QUANT_AVX if vt in (ol.Q8_0, ol.Q8_1) else ol.QUANT_REF)
-        want = ORACLE.mul_mat(t, M, N, K, A_q, B)
-        Ad = ORACLE.dequantize(t, A_q, M, K).astype(np.float64)
-        absdot = np.abs(ORACLE.dequantize(vt, B, N, K).astype(np.float64)) @ np.abs(Ad).T
-        assert rel_err(got, want, absdot).max() < 1e-3, it
+    Ad = ORACLE.dequantize(t, A_q, M, K).astype(np.float64)
+    results = {}
+    try:
+        for mode, env in DECODE_MODES.items():
+            for k in ("LAMM_HIP_FUSED", "LAMM_HIP_ZERO_COPY", "LAMM_HIP_KERNEL_SIGNAL", "LAMM_HIP_SPIN"):
+                monkeypatch.delenv(k, raising=False)
+            for k, v in env.items():
+                monkeypatch.setenv(k, v)
+            la.boundary_reset()
+            src0 = ggml_emu.Tensor(t, [K, M], data=A_q)
+            src1 = ggml_emu.Tensor(ol.F32, [K, N])
+            dst = ggml_emu.mul_mat_node(src0, src1)
+            outs = []
+            for it, x in enumerate(xs):
+                src1.buf.view(np.float32)[:] = x.reshape(-1)
+                assert ggml_emu.compute(dst, nth=2)
+                got = dst.buf.view(np.float32).reshape(N, M).copy()
+                B = ORACLE.quantize(vt, x, ol.QUANT_AVX if vt in (ol.Q8_0, ol.Q8_1) else ol.QUANT_REF)
+                want = ORACLE.mul_mat(t, M, N, K, A_q, B)
+                absdot = np.abs(ORACLE.dequantize(vt, B, N, K).astype(np.float64)) @ np.abs(Ad).T
+                assert rel_err(got, want, absdot).max() < 1e-3, (mode, it)
+                outs.append(got)
+            results[mode] = np.stack(outs)
+    finally:
+        for k in ("LAMM_HIP_FUSED", "LAMM_HIP_ZERO_COPY", "LAMM_HIP_KERNEL_SIGNAL", "LAMM_HIP_SPIN"):
+            monkeypatch.delenv(k, raising=False)
+        la.boundary_reset()
+    first = results["fused"].view(np.uint32)
+    for mode, r in results.items():
+        np.testing.assert_array_equal(r.view(np.uint32), first, err_msg=mode)

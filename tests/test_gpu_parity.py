@@ -367,9 +367,13 @@ def test_known_answer_constant(t):
     assert abs(c.sum(dtype=np.float64) - want) / want < 1e-2
 
 
-@pytest.mark.parametrize("t", [ol.Q4_0, ol.Q8_0, ol.Q2_K], ids=["q4_0", "q8_0", "q2_k"])
+GEMV_FULL_TYPES = [ol.Q4_0, ol.Q4_1, ol.Q5_0, ol.Q5_1, ol.Q8_0, ol.Q2_K]
+
+
+@pytest.mark.parametrize("t", GEMV_FULL_TYPES, ids=[ol.NAMES[t] for t in GEMV_FULL_TYPES])
 def test_full_size_gemv_4096(t):
-    """BASELINE config 2 shape (M=4096, N=1, K=4096): every row vs the oracle."""
+    """BASELINE config 2 shape (M=4096, N=1, K=4096) for Q4_0 and every config-4 format
+    (src/la-benchmark-matmult.cpp:26-36): every row vs the oracle."""
     M, N, K = 4096, 1, 4096
     A_q, B_q = random_case(t, M, N, K, seed=42)
     c, _ = gpu_mul_mat(t, A_q, B_q, M, N, K)
@@ -906,3 +910,69 @@ def test_gemv_row_per_wave_batched_broadcast(monkeypatch):
     for z in range(4):
         ref = ORACLE.mul_mat(t, M, N, K, As[z // 2], Bs[z])
         assert rel_err(c[z], ref, absdot(t, As[z // 2], Bs[z], M, N, K)).max() < TOL, z
+
+
+# ---------------------------------------------------------------- BASELINE config 4, full size
+CONFIG4_TYPES = [ol.Q4_1, ol.Q5_0, ol.Q5_1, ol.Q8_0, ol.Q2_K]   # src/la-benchmark-matmult.cpp:26-36
+_CONFIG4_CACHE = {}
+
+
+def _config4_operands(t):
+    """A = t-quantized N(0,1) 4096 x 4096 (the oracle's reference quantizer), B = 512 rows of
+    vec_dot_type(t) (AVX2 flavour for q8_0 / q8_1, as ggml's INIT on x86)."""
+    if t not in _CONFIG4_CACHE:
+        M, N, K = 4096, 512, 4096
+        rng = np.random.default_rng(4000 + t)
+        vt = la.vec_dot_type(t)
+        A_q = ORACLE.quantize(t, rng.standard_normal((M, K), dtype=np.float32))
+        B_q = ORACLE.quantize(vt, rng.standard_normal((N, K), dtype=np.float32),
+                              ol.QUANT_AVX if vt in (ol.Q8_0, ol.Q8_1) else ol.QUANT_REF)
+        _CONFIG4_CACHE.clear()
+        _CONFIG4_CACHE[t] = (A_q, B_q)
+    return _CONFIG4_CACHE[t]
+
+
+@pytest.mark.parametrize("mode", ["stationary", "per_call"])
+@pytest.mark.parametrize("t", CONFIG4_TYPES, ids=[ol.NAMES[t] for t in CONFIG4_TYPES])
+def test_config4_full_size_gemm(t, mode):
+    """BASELINE config 4 at its real size: every sweep format at M=4096 N=512 K=4096 on its
+    default prefill engine (q4_1 / q5_0: fp6, q5_1 / q8_0: MFMA-i8, q2_K: the super-block
+    engine), through the weight-stationary handle (the ggml boundary's and bench.py's path) and
+    the per-call API.  >= 256 sampled rows x all 512 columns vs the oracle."""
+    M, N, K = 4096, 512, 4096
+    A_q, B_q = _config4_operands(t)
+    A = dev_bytes(np.concatenate([A_q, np.zeros(64, np.uint8)]))
+    B = dev_bytes(B_q)
+    C = torch.full((N * M,), float("nan"), dtype=torch.float32, device="cuda")
+    if mode == "stationary":
+        W = la.Weights(t, A, M, K)
+        W.matmul_torch(B, C, N)
+        torch.cuda.synchronize()
+        W.close()
+    else:
+        la.mul_mat_torch(t, A, B, C, M, N, K)
+        torch.cuda.synchronize()
+    c = C.cpu().numpy().reshape(N, M)
+    assert np.isfinite(c).all()
+    arow = la.row_bytes(t, K)
+    rows = CONFIG3_ROWS
+    a = np.concatenate([A_q[r * arow:(r + 1) * arow] for r in rows])
+    ref = ORACLE.mul_mat(t, len(rows), N, K, a, B_q)
+    err = rel_err(c[:, rows], ref, absdot(t, a, B_q, len(rows), N, K)).max()
+    print(f"config 4 {ol.NAMES[t]} {mode} [{la.gemm_engine(t, M, N, K, 1, stationary=mode == 'stationary')}]: "
+          f"max rel err {err:.2e} over {len(rows)} rows x {N}")
+    assert err < TOL
+
+
+# ---------------------------------------------------------------- BASELINE config 1
+def test_config1_f32_512_cube():
+    """BASELINE config 1 (la-benchmark-matmult F32 M=N=K=512, src/la-benchmark-matmult.cpp:257-276)
+    on the GPU's F32 path (the dense prefill GEMM): every output vs the oracle's F32 dot."""
+    M = N = K = 512
+    rng = np.random.default_rng(512)
+    a = rng.standard_normal((M, K), dtype=np.float32)
+    b = rng.standard_normal((N, K), dtype=np.float32)
+    c, _ = gpu_mul_mat(ol.F32, a.view(np.uint8), b.view(np.uint8), M, N, K)
+    ref = ORACLE.mul_mat(ol.F32, M, N, K, a.view(np.uint8), b.view(np.uint8))
+    absd = np.abs(b.astype(np.float64)) @ np.abs(a.astype(np.float64)).T
+    assert rel_err(c, ref, absd).max() < TOL

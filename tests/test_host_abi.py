@@ -137,34 +137,40 @@ def test_shard_rows_cover_every_row_once(align):
             assert max(tiles) - min(tiles) <= 1
 
 
-def test_chain_create_validation():
-    """lamm_hip_chain_create rejects malformed chains before touching a device."""
-    def op(t, M, K, x, y, base=0x100000):
-        kb = K // 32
-        lda = kb
-        while (lda * la.type_size(t)) % 16:
-            lda += 1
-        return (la.Matrix(base, t, M, kb, lda), x, y)
+def test_env_switches_read_once_and_reloaded(monkeypatch):
+    """The library reads its LAMM_* switches once (lamm_knobs.cpp) and again only on
+    lamm_hip_reload_env / lamm_hip_boundary_reset; the Python binding re-syncs when os.environ's
+    LAMM_* part changes.  LAMM_OPT_LEVEL=0 is visible through lamm_get_opt_level() (0 without a
+    GPU either way, so this checks the sync path, and on a GPU box the switch itself)."""
+    base = la.get_opt_level()
+    monkeypatch.setenv("LAMM_OPT_LEVEL", "0")
+    assert la.get_opt_level() == 0          # _sync_env saw the change and reloaded
+    monkeypatch.delenv("LAMM_OPT_LEVEL")
+    assert la.get_opt_level() == base
+    # a raw change without the binding's sync stays invisible until reload_env()
+    os.environ["LAMM_OPT_LEVEL"] = "0"
+    try:
+        assert la.lib.lamm_get_opt_level() == base
+        la.reload_env()
+        assert la.lib.lamm_get_opt_level() == 0
+    finally:
+        del os.environ["LAMM_OPT_LEVEL"]
+        la.reload_env()
+    assert la.lib.lamm_get_opt_level() == base
 
-    def create(ops):
-        arr = (la.ChainOp * len(ops))(*[la.ChainOp(*o) for o in ops])
-        h = ctypes.c_void_p()
-        return la.lib.lamm_hip_chain_create(arr, len(ops), ctypes.byref(h))
 
-    Q4, Q8 = ol.Q4_0, ol.Q8_0
-    assert create([]) == la.LAMM_ERR_SHAPE
-    # one weight type per chain
-    assert create([op(Q4, 64, 64, 0x1000, 0x2000), op(Q8, 64, 64, 0x1000, 0x3000)]) == la.LAMM_ERR_TYPE
-    # unsupported type
-    assert create([op(ol.Q2_K, 64, 256, 0x1000, 0x2000)]) == la.LAMM_ERR_TYPE
-    # outputs overlap
-    assert create([op(Q4, 64, 64, 0x1000, 0x2000), op(Q4, 64, 64, 0x1000, 0x2000 + 128)]) == la.LAMM_ERR_SHAPE
-    # input = an earlier output but K != its rows
-    assert create([op(Q4, 64, 64, 0x1000, 0x2000), op(Q4, 64, 96, 0x2000, 0x3000)]) == la.LAMM_ERR_SHAPE
-    # external input overlapping an output
-    assert create([op(Q4, 64, 64, 0x1000, 0x2000), op(Q4, 64, 64, 0x2000 + 64, 0x3000)]) == la.LAMM_ERR_SHAPE
-    # K beyond 12288
-    assert create([op(Q4, 64, 12320, 0x1000, 0x20000)]) == la.LAMM_ERR_SHAPE
-    # misaligned weights
-    assert create([op(Q4, 64, 64, 0x1000, 0x2000, base=0x100008)]) == la.LAMM_ERR_ALIGN
-    assert "16-byte" in la.last_error()
+def test_no_getenv_on_launch_paths():
+    """Product-path hygiene: only lamm_knobs.cpp reads the environment; ablation switches
+    (LAMM_GEMM_VARIANT, LAMM_GEMM_SKIP_PREP, ...) exist only in the LAMM_AB_VARIANTS build."""
+    csrc = os.path.join(ROOT, "la-llama.cpp_amd", "csrc")
+    for f in sorted(os.listdir(csrc)):
+        if not f.endswith((".hip", ".cpp", ".h")) or f == "lamm_knobs.cpp":
+            continue
+        depth = 0
+        for ln in open(os.path.join(csrc, f)):
+            if ln.startswith("#ifdef LAMM_AB_VARIANTS"):
+                depth += 1
+            elif depth and ln.startswith("#endif"):
+                depth -= 1
+            elif "getenv(" in ln:
+                assert depth > 0, f"{f}: getenv outside the variant build: {ln.strip()}"

@@ -18,18 +18,26 @@ Beside it (same JSON line):
   gemv_stacked  : 33 4096x4096 slices in ONE launch (steady-state streaming rate), N = 1
   gemm          : BASELINE config 3 (M=4096 N=512 K=4096, stationary weights): one slice and
                   a 4-slice batch; roofline = the WHOLE launch (activation prep + main loop +
-                  split-K reduce); `main_loop_only` separately labelled.  N > 1: the slice's
-                  rows split over the ranks + the RCCL all-gather of C (8 MiB)
+                  split-K reduce).  N > 1: the slice's rows split over the ranks + the RCCL
+                  all-gather of C (8 MiB)
+  config1       : BASELINE config 1 (F32 M=N=K=512, la-benchmark-matmult's plumbing shape): the
+                  GPU's F32 path and the reference's CPU path side by side
+  sweep         : BASELINE config 4 (Q4_1 / Q5_0 / Q5_1 / Q8_0 / Q2_K at K=4096): per format the
+                  single-call GEMV (config 2's measurement) and the config-3-shaped GEMM
   llama7b_e2e   : BASELINE config 5 through the unchanged caller -- llama.cpp-b2430's own
                   llama_decode (integration/_build/llama_e2e_hip: the reference's llama.cpp and
                   ggml with the LA_LLAMA hook linked to liblamm_hip.so), synthetic Llama-7B Q4_0
                   GGUF, pp512 / tg128; with N GPUs the boundary splits every weight's rows over
                   all N (LAMM_HIP_DEVICES)
   llama7b_matmul_step : the same model's weight matmuls through the device API (hipGraph) --
-                  the ceiling without the ggml boundary's host round trips
+                  the ceiling without the ggml boundary's host round trips; with N GPUs every
+                  weight's rows sharded over the N ranks (one llama-matmul-bench process per GPU,
+                  RCCL all-gather after every projection, hipGraph-captured)
   cpu_baseline  : the reference itself (oracle/_ref: la-llama.cpp lamm opt-3 AVX2 build) on this
-                  host's cores, rank 0, N = 1; the same leg checks a sample of the GPU outputs
-                  above against the oracle (`parity_sample`)
+                  host's cores (the CPUs this process may use: affinity, cgroup quota,
+                  OMP_NUM_THREADS -- the GPU box's share), rank 0, N = 1; the same leg checks a
+                  sample of the GPU outputs above against the oracle (`parity_sample`) and runs
+                  config 5's greedy-token parity (GPU build vs the reference, pp64 / tg16)
 
 Synthetic data: A bytes random with valid fp16 scales; B = the GPU activation quantizer applied
 to N(0,1) floats.  Inputs are resident in HBM before the timed region.
@@ -57,6 +65,25 @@ FP16_FIELDS = {  # byte offsets of fp16 scale fields inside one block (lamm_form
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def host_cores():
+    """CPUs this process may run on: the affinity mask, capped by a cgroup CPU quota and by
+    OMP_NUM_THREADS (the GPU box exports its CPU share there: its nproc shows the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    src = f"affinity {n}"
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if quota != "max":
+            q = max(1, int(int(quota) / int(period)))
+            if q < n:
+                n, src = q, f"cgroup cpu.max {q}"
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and 0 < int(omp) < n:
+        n, src = int(omp), f"OMP_NUM_THREADS={omp} (the box's CPU share)"
+    return n, src
 
 
 def make_weights(torch, la, fmt, slices, M, K, gen):
@@ -328,13 +355,6 @@ def config3_gemm(ctx, fmt, M, N, K, slices, steps):
 
     per_step, _, _ = time_steps(ctx, step, steps, 2, graph=not ctx.rehearse)
     _, kern, _ = time_steps(ctx, gemm, max(steps, 200), 2)   # (graph start-up amortized, as for config 2)
-    # main loop alone: LAMM_GEMM_SKIP_PREP re-runs the main kernel on the prepared workspace
-    os.environ["LAMM_GEMM_SKIP_PREP"] = "1"
-    try:
-        _, main_only, _ = time_steps(ctx, gemm, steps, 1, graph=False)
-    finally:
-        del os.environ["LAMM_GEMM_SKIP_PREP"]
-    gemm(0)   # a correct result again (the skip-prep launches leave C undefined)
     torch.cuda.synchronize()
     sample = None
     if world == 1 and slices == 1:
@@ -345,14 +365,65 @@ def config3_gemm(ctx, fmt, M, N, K, slices, steps):
     W.close()
     del A, B, C, slab, W
     torch.cuda.empty_cache()
-    return per_step, kern, main_only, rows, sample
+    return per_step, kern, rows, sample
+
+
+def config1_f32(ctx, steps):
+    """BASELINE config 1: F32 M=N=K=512 (la-benchmark-matmult's plumbing shape) on the GPU's F32
+    path (the dense prefill GEMM), hipGraph-replayed, inputs resident."""
+    torch, la = ctx.torch, ctx.la
+    n = 512
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(512)
+    A = torch.randn(n * n, device="cuda", generator=gen)
+    B = torch.randn(n * n, device="cuda", generator=gen)
+    C = torch.zeros(n * n, device="cuda")
+    Am, Bm, Cm = la.Matrix(A.data_ptr(), la.F32, n, n, n), la.Matrix(B.data_ptr(), la.F32, n, n, n), \
+        la.Matrix(C.data_ptr(), la.F32, n, n, n)
+    _, kern, _ = time_steps(ctx, lambda i: la.matmul(Am, Bm, Cm, torch.cuda.current_stream().cuda_stream),
+                            max(steps, 200), 3)
+    ref = (B.view(n, n) @ A.view(n, n).T).reshape(-1)
+    err = float((C - ref).abs().max() / ref.abs().max())
+    del A, B, C
+    return {"workload": "F32 M=N=K=512 (BASELINE config 1, la-benchmark-matmult -d f32 shape), one call per step",
+            "kernel": "lamm::gemm_dense_kernel (csrc/lamm_gemm_dense.hip)", "per_launch_us": round(kern * 1e6, 3),
+            "GFLOPS": round(2.0 * n ** 3 / kern / 1e9, 1), "max_rel_err_vs_torch_fp32": err}
+
+
+def llama_step_sharded(ctx, fmt):
+    """Config 5's weight matmuls with every weight's rows sharded over the job's ranks: one
+    llama-matmul-bench process per GPU (--rank / --world / --comm-id; RCCL all-gather of every
+    projection's output, the whole step one hipGraph per process).  Returns rank 0's view with the
+    step time maxed over ranks."""
+    exe = os.path.join(ROOT, "la-llama.cpp_amd", "llama-matmul-bench")
+    uid = [ctx.la.comm_unique_id().hex() if ctx.rank == 0 else None]
+    if ctx.world > 1:
+        ctx.dist.broadcast_object_list(uid, src=0)
+    out = {"note": f"weight rows sharded over {ctx.world} GPU(s), one process per GPU, RCCL all-gather after every "
+                   "projection (hipGraph per process); synthetic weights, weight matmuls only"}
+    for name, argv in (("decode_n1_batch_proj", ["-n", "1", "-i", "50", "--batch-proj"]),
+                       ("prefill_n512", ["-n", "512", "-i", "5", "-s", "--batch-proj"])):
+        res = {}
+        try:
+            r = subprocess.run([exe, "-d", fmt, "--rank", str(ctx.rank), "--world", str(ctx.world), "--comm-id", uid[0],
+                                "--device", str(ctx.device)] + argv, capture_output=True, text=True, timeout=300)
+            line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+            res = json.loads(line[-1]) if r.returncode == 0 and line else {"error": r.stderr[-300:]}
+        except Exception as e:  # noqa: BLE001
+            res = {"error": str(e)[:300]}
+        ms = res.get("ms_per_step", float("inf"))
+        (ms_max,) = ctx.max(ms)
+        if "error" not in res:
+            res["ms_per_step_max_over_ranks"] = round(ms_max, 4)
+            res["tok_per_s"] = round(res["tokens_per_step"] / (ms_max * 1e-3), 2)
+        out[name] = res
+    return out
 
 
 def cpu_baseline(fmt, M, N, K, budget_s, unit_bytes):
     """The real reference (lamm opt=3, AVX2; Q8_0 uses opt=0 stock ggml because lamm's AVX2 Q8_0
     is numerically wrong) timed like la-benchmark-matmult."""
-    threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    threads = max(1, min(threads, 16))
+    threads, cores_src = host_cores()
     variant = "lamm0" if fmt == "q8_0" else "lamm3"
     exe = os.path.join(ROOT, "oracle", "_ref", f"ref_driver_{variant}")
     if os.path.exists(exe):
@@ -362,6 +433,7 @@ def cpu_baseline(fmt, M, N, K, budget_s, unit_bytes):
             r = json.loads(out.stdout.strip().splitlines()[-1])
             us = r["median_us"]
             return {"value": round(unit_bytes / (us * 1e-6) / 1e9, 3), "unit": "GB/s", "cores": threads,
+                    "cores_source": cores_src,
                     "kind": "reference", "median_us": us, "gflops": r["gflops"],
                     "sample": f"{r['iters']} x {fmt} mul_mat M={M} N={N} K={K} via ggml_graph_compute "
                               f"(ref_driver_{variant}: la-llama.cpp lamm opt {3 if variant == 'lamm3' else 0} "
@@ -411,7 +483,7 @@ def parity_sample(samples):
     return out
 
 
-def llama_e2e(devices, n_prompt=512, n_gen=128, threads=16, exe=None, extra_env=None, timeout=600):
+def llama_e2e(devices, n_prompt=512, n_gen=128, threads=16, exe=None, extra_env=None, timeout=600, keep_tokens=False):
     """BASELINE config 5 through llama.cpp-b2430's own llama_decode (see module doc)."""
     exe = exe or os.path.join(ROOT, "integration", "_build", "llama_e2e_hip")
     model = os.path.join(os.environ.get("TMPDIR", "/tmp"), "lamm_synth_llama7b_q4_0.gguf")
@@ -427,7 +499,8 @@ def llama_e2e(devices, n_prompt=512, n_gen=128, threads=16, exe=None, extra_env=
         if r.returncode != 0 or not line:
             return {"error": r.stderr[-400:]}
         d = json.loads(line[-1])
-        d.pop("tokens", None)
+        if not keep_tokens:
+            d.pop("tokens", None)
         return d
     except Exception as e:  # noqa: BLE001 -- reported, never fatal for the main bench line
         return {"error": str(e)[:300]}
@@ -475,7 +548,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-llama", action="store_true", help="skip config 5 (llama e2e + weight-matmul step)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
-    ap.add_argument("--sweep", action="store_true", help="also every weight format (config 4)")
+    ap.add_argument("--sweep", action="store_true", help="also every weight format's stacked GEMV + GEMM")
+    ap.add_argument("--no-config1", action="store_true", help="skip config 1 (F32 512^3)")
+    ap.add_argument("--no-config4", action="store_true", help="skip config 4 (the per-format sweep)")
     args = ap.parse_args()
 
     import torch
@@ -532,7 +607,7 @@ def main():
         gm = {}
         for gslices in ((4, 1) if world == 1 else (1,)):
             try:
-                step, kern, main_only, rows, smp = config3_gemm(ctx, fmt, M, gN, K, gslices, max(3, args.steps // 4))
+                step, kern, rows, smp = config3_gemm(ctx, fmt, M, gN, K, gslices, max(3, args.steps // 4))
                 ops = 2.0 * M * gN * K * gslices
                 rops = 2.0 * rows * gN * K * gslices
                 engine = la.gemm_engine(fmt, rows, gN, K, gslices, stationary=True)
@@ -549,16 +624,39 @@ def main():
                                  else "lamm::gemm3_kernel (csrc/lamm_gemm.hip)",
                                  "achieved": round(rops / kern / 1e12, 2), "peak": I8_DENSE_PEAK_TOPS,
                                  "unit": "TFLOP/s", "frac": round(rops / kern / 1e12 / I8_DENSE_PEAK_TOPS, 4),
-                                 "per_launch_us": round(kern * 1e6, 2)},
-                    "main_loop_only": {"per_launch_us": round(main_only * 1e6, 2),
-                                       "TFLOPs": round(rops / main_only / 1e12, 2),
-                                       "note": "LAMM_GEMM_SKIP_PREP=1: the main kernel alone on the prepared "
-                                               "workspace (profiling; not the roofline)"}}
+                                 "per_launch_us": round(kern * 1e6, 2)}}
                 if smp:
                     samples["gemm_config3"] = smp
             except Exception as e:  # noqa: BLE001
                 gm[f"slices{gslices}"] = {"error": str(e)[:300]}
         extras["gemm"] = gm
+    if world == 1 and not args.no_config1:
+        try:
+            extras["config1"] = config1_f32(ctx, args.steps)
+        except Exception as e:  # noqa: BLE001
+            extras["config1"] = {"error": str(e)[:300]}
+    if world == 1 and not args.no_config4:
+        c4 = {"workload": "BASELINE config 4: per format, ONE M=4096 N=1 K=4096 GEMV per step (config 2's "
+                          "measurement, weights rotated > MALL) and the M=4096 N=512 K=4096 GEMM (config 3's, "
+                          "stationary weights, whole launch)"}
+        for f in ("q4_1", "q5_0", "q5_1", "q8_0", "q2_k"):
+            try:
+                g4 = config2_gemv(ctx, f, M, K, args.steps, args.warmup)
+                ent = {"gemv_per_launch_us": round(g4["kern"] * 1e6, 3),
+                       "gemv_GBs": round(g4["slab_bytes"] / g4["kern"] / 1e9, 1),
+                       "gemv_frac": round(g4["slab_bytes"] / g4["kern"] / 1e9 / HBM_PEAK_GBS, 4),
+                       "gemv_bytes": g4["slab_bytes"]}
+                if not args.no_gemm:
+                    _, kern4, _, _ = config3_gemm(ctx, f, M, args.gemm_N, K, 1, max(3, args.steps // 4))
+                    ops4 = 2.0 * M * args.gemm_N * K
+                    ent.update({"gemm_engine": la.gemm_engine(f, M, args.gemm_N, K, 1, stationary=True),
+                                "gemm_per_launch_us": round(kern4 * 1e6, 2),
+                                "gemm_TFLOPs": round(ops4 / kern4 / 1e12, 2),
+                                "gemm_frac": round(ops4 / kern4 / 1e12 / I8_DENSE_PEAK_TOPS, 4)})
+                c4[f] = ent
+            except Exception as e:  # noqa: BLE001
+                c4[f] = {"error": str(e)[:200]}
+        extras["config4"] = c4
     if args.sweep and world == 1:
         sw = {}
         for f in ["f32", "f16", "q4_0", "q4_1", "q5_0", "q5_1", "q8_0", "q2_k", "q4_k", "q5_k", "q6_k"]:
@@ -566,7 +664,7 @@ def main():
                 st = stacked_gemv(ctx, f, M, K, max(5, args.steps // 2))
                 sw[f] = {"gemv_stacked_GBs": st["achieved_GBs"]}
                 if not args.no_gemm:
-                    step, kern, _, _, _ = config3_gemm(ctx, f, M, args.gemm_N, K, 1, max(3, args.steps // 4))
+                    step, kern, _, _ = config3_gemm(ctx, f, M, args.gemm_N, K, 1, max(3, args.steps // 4))
                     sw[f].update({"gemm_GFLOPS": round(2.0 * M * args.gemm_N * K / kern / 1e9, 1),
                                   "gemm_us": round(kern * 1e6, 2),
                                   "gemm_engine": la.gemm_engine(f, M, args.gemm_N, K, 1, stationary=True)})
@@ -574,6 +672,7 @@ def main():
                 sw[f] = {"error": str(e)[:200]}
         extras["sweep"] = sw
     if not args.no_llama:
+        extras["llama7b_matmul_step_sharded"] = llama_step_sharded(ctx, fmt)
         ctx.barrier()
         if rank == 0:
             devs = list(range(world)) if world > 1 and not ctx.rehearse else None
@@ -583,7 +682,7 @@ def main():
                            "weights device-resident after a warm-up pass; reference published (3A6000, 4 threads, "
                            "README.md:684,710): prompt 8.27 tok/s, text-gen 4.69 tok/s",
                    "devices": devs or [ctx.device],
-                   "t16": llama_e2e(devs, threads=16)}
+                   "t16": llama_e2e(devs, threads=min(16, host_cores()[0]))}
             if world == 1:
                 extras["llama7b_matmul_step"] = llama_step(fmt)
             extras["llama7b_e2e"] = e2e
@@ -598,11 +697,28 @@ def main():
             out["gemm"]["cpu_baseline"] = {
                 "value": round(2.0 * M * args.gemm_N * K / (us * 1e-6) / 1e9, 2), "unit": "GFLOPS",
                 "cores": cb["cores"], "kind": cb["kind"], "median_us": round(us, 1), "sample": cb["sample"]}
+        if "config1" in out and "error" not in out["config1"]:   # the reference's CPU path at config 1
+            cb = cpu_baseline("f32", 512, 512, 512, min(args.cpu_budget, 5.0), 0)
+            us = cb["median_us"]
+            out["config1"]["cpu_baseline"] = {"value": round(2.0 * 512 ** 3 / (us * 1e-6) / 1e9, 2), "unit": "GFLOPS",
+                                              "cores": cb["cores"], "kind": cb["kind"], "median_us": round(us, 1),
+                                              "sample": cb["sample"]}
         if "llama7b_e2e" in out:   # the reference's own llama.cpp + lamm opt-3 on the host cores
-            cpu = llama_e2e(None, n_prompt=64, n_gen=16, threads=out["cpu_baseline"]["cores"],
-                            exe=os.path.join(ROOT, "oracle", "_ref", "llama_e2e_lamm3"))
-            cpu["sample"] = "pp64 + tg16 (bounded sample) of the same model and driver on la-llama.cpp lamm opt 3 AVX2"
+            ref_exe = os.path.join(ROOT, "oracle", "_ref", "llama_e2e_lamm3")
+            cpu = llama_e2e(None, n_prompt=512, n_gen=128, threads=out["cpu_baseline"]["cores"], exe=ref_exe)
+            cpu["sample"] = "pp512 + tg128 (the GPU run's workload) of the same model and driver on la-llama.cpp lamm " \
+                            "opt 3 AVX2"
             out["llama7b_e2e"]["cpu_baseline"] = cpu
+            # greedy-token parity of the full 32-layer model: the GPU build vs the reference, pp64 / tg16
+            g = llama_e2e(None, n_prompt=64, n_gen=16, threads=min(16, host_cores()[0]), keep_tokens=True)
+            c = llama_e2e(None, n_prompt=64, n_gen=16, threads=out["cpu_baseline"]["cores"], exe=ref_exe,
+                          keep_tokens=True)
+            gt, ct = g.get("tokens"), c.get("tokens")
+            out["llama7b_e2e"]["parity_32_layers"] = {
+                "run": "pp64 + tg16 greedy, same synthetic 32-layer model: llama_e2e_hip vs llama_e2e_lamm3 (reference)",
+                "tokens_gpu": gt, "tokens_reference": ct,
+                "greedy_tokens_match": gt is not None and gt == ct,
+                "first_divergence": next((i for i, (x, y) in enumerate(zip(gt or [], ct or [])) if x != y), None)}
     ctx.close()
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -305,6 +305,102 @@ __global__ __launch_bounds__(PREP_NT) void prep_b_fp6(GemvArgs p, unsigned char*
   }
 }
 
+// Activation prep, q8 rows (the default path), tiled: a workgroup takes 32 rows x 8 blocks; the
+// rows' raw block bytes come in by coalesced 16-byte loads (consecutive lanes, consecutive bytes
+// of one row) through LDS, then thread (row r, block b) encodes one block.  The per-row kernel
+// above reads 34 bytes per lane at a 4352-byte lane stride -- every lane a different cache line,
+// 3 instructions per block -- which made it 6.4 us for config 3's 2.2 MB (profiles/r02/
+// full_run_6/kernel_stats_bench.csv).  Codes by SWAR, 4 per dword:
+//   lo = q & 15 (e2m3 code n/8 = n for 0 <= n <= 15)
+//   hi = u < 8 ? u : 48 - u, u = q >> 4 as a nibble (sign | |h| for h = floor(q / 16) in [-8, 7])
+constexpr int PB_ROWS = 32, PB_NB = 8, PB_NT = 256;
+
+// 32 six-bit codes held as bytes (code e = byte e % 4 of c[e / 4]) -> the 192-bit fragment
+__device__ __forceinline__ void pack_fp6_bytes(const uint32_t (&c)[8], uint32_t (&o)[6]) {
+  uint32_t t[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const uint32_t x = c[k];
+    t[k] = (x & 0x3fu) | ((x >> 2) & 0xfc0u) | ((x >> 4) & 0x3f000u) | ((x >> 6) & 0xfc0000u);
+  }
+  o[0] = t[0] | (t[1] << 24);
+  o[1] = (t[1] >> 8) | (t[2] << 16);
+  o[2] = (t[2] >> 16) | (t[3] << 8);
+  o[3] = t[4] | (t[5] << 24);
+  o[4] = (t[5] >> 8) | (t[6] << 16);
+  o[5] = (t[6] >> 16) | (t[7] << 8);
+}
+
+// one activation block (32 int8 quants as 8 dwords, fp16 d / s bits) -> its hi / lo fragments
+__device__ __forceinline__ void store_b_fp6(unsigned char* ch, int b, int r, const uint32_t (&q)[8], uint32_t d,
+                                            uint32_t sv) {
+  uint32_t hi[8], lo[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    lo[k] = q[k] & 0x0f0f0f0fu;
+    const uint32_t u = (q[k] >> 4) & 0x0f0f0f0fu;
+    const uint32_t neg = ((u >> 3) & 0x01010101u) * 0xffu;
+    hi[k] = u + ((0x30303030u - (u << 1)) & neg);
+  }
+  uint32_t oh[6], ol[6];
+  pack_fp6_bytes(hi, oh);
+  pack_fp6_bytes(lo, ol);
+  *(u32x4*)(ch + f6_boff(0, b, 0, r)) = u32x4{oh[0], oh[1], oh[2], oh[3]};
+  *(u32x4*)(ch + f6_boff(1, b, 0, r)) = u32x4{oh[4], oh[5], d, sv};
+  *(u32x4*)(ch + f6_boff(0, b, 1, r)) = u32x4{ol[0], ol[1], ol[2], ol[3]};
+  *(u32x4*)(ch + f6_boff(1, b, 1, r)) = u32x4{ol[4], ol[5], d, sv};
+}
+
+template <int T>
+__global__ __launch_bounds__(PB_NT) void prep_b_fp6_tile(GemvArgs p, unsigned char* ws) {
+  using F = F6<T>;
+  constexpr int VBPB = F::VBPB, VQS = VBPB == 36 ? 4 : 2;
+  constexpr int SEG = PB_NB * VBPB;                // bytes of a row's 8 blocks (272 / 288)
+  constexpr int PIECES = (SEG + 3 + 15) / 16;      // 16-byte pieces from the dword below the start
+  constexpr int SEGW = PIECES * 4 + 4;             // dwords per LDS row: 16-byte aligned, realign slack
+  __shared__ uint32_t raw[PB_ROWS * SEGW];
+  const F6Layout L = F6Layout::of(p);
+  const int nbg = (L.nsteps * F6_KB + PB_NB - 1) / PB_NB;
+  const int64_t j0 = (int64_t)(blockIdx.x / nbg) * PB_ROWS;
+  const int kb0 = (blockIdx.x % nbg) * PB_NB;
+  const int z = blockIdx.y, i12 = z % p.ne12, i13 = z / p.ne12;
+  const unsigned char* Bz = p.B + (int64_t)i12 * p.sb2 + (int64_t)i13 * p.sb3;
+  const int64_t nrow = min((int64_t)PB_ROWS, (int64_t)p.N - j0);
+  // resource from the tile's first row: offsets < 2^31 for any slice size
+  const int64_t base = min(j0, (int64_t)p.N) * p.ldb;
+  const int64_t bbytes = nrow > 0 ? (nrow - 1) * p.ldb + (int64_t)p.nblk * VBPB : 0;
+  const auto rs = make_rsrc(Bz + base, (uint32_t)min((bbytes + 3) & ~int64_t(3), (int64_t)0x7fffffff));
+  const int t = threadIdx.x;
+  for (int idx = t; idx < PB_ROWS * PIECES; idx += PB_NT) {
+    const int r = idx / PIECES, o = idx % PIECES;
+    const uint32_t start = (uint32_t)((int64_t)r * p.ldb + (int64_t)kb0 * VBPB);
+    const uint32_t off = r < nrow && kb0 < p.nblk ? (start & ~3u) + 16 * o : 0x7ffffff0u;
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+    *reinterpret_cast<u32x4*>(&raw[r * SEGW + 4 * o]) = v;
+  }
+  __syncthreads();
+  const int r = t % PB_ROWS, bl = t / PB_ROWS;
+  const int64_t j = j0 + r;
+  const int kb = kb0 + bl;
+  if (j >= (int64_t)L.njt * F6_TJ || kb >= L.nsteps * F6_KB) return;
+  uint32_t q[8] = {0, 0, 0, 0, 0, 0, 0, 0}, d = 0, sv = 0;
+  if (j < p.N && kb < p.nblk) {
+    const uint32_t start = (uint32_t)((int64_t)r * p.ldb + (int64_t)kb0 * VBPB);
+    const int byte = (int)(start & 3u) + bl * VBPB;
+    const uint32_t* src = &raw[r * SEGW + (byte >> 2)];
+    const int sh = (byte & 3) * 8;
+    constexpr int NWM = (VBPB + 3) / 4 + 1;
+    uint32_t m[NWM];
+#pragma unroll
+    for (int k = 0; k < NWM; ++k) m[k] = __builtin_amdgcn_alignbit(src[k + 1], src[k], sh);
+    d = m[0] & 0xffffu;
+    if constexpr (VBPB == 36) sv = m[0] >> 16;
+    unroll<8>([&](auto K) { q[K] = get32<VQS + 4 * K>(m); });
+  }
+  unsigned char* ch = ws + (int64_t)z * L.b_slice + ((int64_t)(j / F6_TJ) * L.nsteps + kb / F6_KB) * F6_B_BYTES;
+  store_b_fp6(ch, kb % F6_KB, (int)(j % F6_TJ), q, d, sv);
+}
+
 // ---------------------------------------------------------------- GEMM
 template <int N_>
 __device__ __forceinline__ void f6_wait_vm() {   // s_waitcnt vmcnt(N) (lgkmcnt untouched)
@@ -865,10 +961,13 @@ hipError_t launch_fp6_t(const GemvArgs& p, const void* prepA, void* ws, hipStrea
         hipLaunchKernelGGL(kone, dim3((unsigned)(rgroups * nb_all), (unsigned)(p.ne12 * p.ne13)), dim3(PREP_NT), 0, s,
                            p, wsB);
     };
-    if (p.b_f32)
+    if (p.b_f32) {
       prep(prep_b_fp6<T, PREP_NB, true>, prep_b_fp6<T, 1, true>);
-    else
-      prep(prep_b_fp6<T, PREP_NB, false>, prep_b_fp6<T, 1, false>);
+    } else {
+      const int nbg = (nb_all + PB_NB - 1) / PB_NB, rg = (L.njt * F6_TJ + PB_ROWS - 1) / PB_ROWS;
+      hipLaunchKernelGGL(prep_b_fp6_tile<T>, dim3((unsigned)(rg * nbg), (unsigned)(p.ne12 * p.ne13)), dim3(PB_NT), 0,
+                         s, p, wsB);
+    }
   }
   const F6Plan plan = f6_plan(p, L);
   const int nsplit = plan.nsplit;

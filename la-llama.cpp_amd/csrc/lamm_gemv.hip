@@ -1240,9 +1240,9 @@ int rpw_waves(const GemvArgs& p) {
   // fewer rows than one per wave of 256 sixteen-wave workgroups (a row slab of a sharded
   // weight, bench.py --gpus N): smaller workgroups spread the rows over more CUs
   if (rows < 4096) return rows >= 2048 ? 8 : 4;
-  // waves per workgroup by rows per launch (profiles/r02/ab_gemv_waves.json, interleaved A/B):
-  // q8 rows 4096 x 4096 16 waves 4.17 us (4: 4.53), 11008 16, 22016 8; F32 rows 4096 16, more 8
-  return rows <= (p.b_f32 ? 4096 : 12288) ? 16 : 8;
+  // 8 waves: with the slim prologue (round 3) the 512-workgroup grid beats 256 x 16 waves on
+  // config 2 (probe clones R8 3.74-3.89 vs R16 3.99-4.07 us, profiles/r03/gemv_probe_*.json)
+  return 8;
 }
 
 hipError_t launch_gemv(int type, const GemvArgs& p, hipStream_t s) {

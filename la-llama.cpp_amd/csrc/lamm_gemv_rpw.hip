@@ -38,10 +38,19 @@ __global__ __launch_bounds__(64 * WAVES) void gemv_rpw_kernel(GemvArgs p) {
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int z = blockIdx.y, i12 = z % p.ne12, i13 = z / p.ne12;
-  const unsigned char* Az = p.A + (int64_t)(i12 / p.r2) * p.sa2 + (int64_t)(i13 / p.r3) * p.sa3;
-  const unsigned char* Bz = p.B + (int64_t)i12 * p.sb2 + (int64_t)i13 * p.sb3;
-  float* Cz = p.C + (int64_t)i12 * p.sc2 + (int64_t)i13 * p.sc3;
+  // The prologue is on the critical path of a ~4 us launch: the first loads wait for every
+  // instruction before them, so nothing here divides unless the launch has several slices
+  // (round 2's prologue -- four runtime divisions, ~220 instructions before the first load --
+  // cost ~0.5 us per config-2 call, profiles/r03/gemv_probe_*.json: lib vs R16)
+  const unsigned char* Az = p.A;
+  const unsigned char* Bz = p.B;
+  float* Cz = p.C;
+  if (gridDim.y > 1) {
+    const int z = blockIdx.y, i12 = z % p.ne12, i13 = z / p.ne12;
+    Az += (int64_t)(i12 / p.r2) * p.sa2 + (int64_t)(i13 / p.r3) * p.sa3;
+    Bz += (int64_t)i12 * p.sb2 + (int64_t)i13 * p.sb3;
+    Cz += (int64_t)i12 * p.sc2 + (int64_t)i13 * p.sc3;
+  }
   const int ncols = p.N < NC ? p.N : NC;
   const uint32_t row_bytes = (uint32_t)((nb * F::BPB + 3) & ~3);
   const int stride = gridDim.x * WAVES;
@@ -146,7 +155,8 @@ __global__ __launch_bounds__(64 * WAVES) void gemv_rpw_kernel(GemvArgs p) {
     __syncthreads();
   } else {
     // straight-line (no branch between them), so the activation loads stay ahead of the row's
-    // HBM stream and waiting for them does not wait for A; out-of-range loads read zeros
+    // HBM stream and waiting for them does not wait for A; out-of-range loads read zeros (a
+    // branch around them lets the compiler pull the decode in front of the A loads)
     st.template load<NC>(p, rb, t0);
     __builtin_amdgcn_sched_barrier(0);   // keep the activation loads first in the vmcnt order
     issue(row < p.M ? row : 0, wa0);

@@ -423,12 +423,14 @@ struct WeightEntry {
 };
 
 uint64_t fingerprint(const unsigned char* p, size_t pitch, size_t row_bytes, int64_t rows) {
-  // FNV-1a over 64 sampled 8-byte windows spread over the slice, plus the shape.
+  // FNV-1a over 16 sampled 8-byte windows spread over the slice, plus the shape (each window is a
+  // host cache miss on every decode call: 64 of them cost ~1.5 us of a ~20 us call,
+  // profiles/r02/ab_zero_copy_spin.txt "weights lookup")
   uint64_t h = 1469598103934665603ull ^ (row_bytes * 31 + (uint64_t)rows);
   const size_t total = (size_t)(rows - 1) * pitch + row_bytes;
   const size_t win = total < 8 ? total : 8;
-  for (int s = 0; s < 64; ++s) {
-    const size_t pos = (size_t)((double)(total - win) * s / 63.0);
+  for (int s = 0; s < 16; ++s) {
+    const size_t pos = (size_t)((double)(total - win) * s / 15.0);
     uint64_t v = 0;
     memcpy(&v, p + pos, win);
     for (int b = 0; b < 8; ++b) { h ^= (v >> (8 * b)) & 0xff; h *= 1099511628211ull; }

@@ -128,8 +128,9 @@ struct ActStage {
 
   template <int NC>
   __device__ __forceinline__ void load(const GemvArgs& p, __amdgpu_buffer_rsrc_t rb, int it) {
+    static_assert(NC <= 2, "column by comparison, not division");
     const int ncols = p.N < NC ? p.N : NC;
-    const int j = it / p.nblk, b = it % p.nblk;
+    const int j = NC > 1 && it >= p.nblk ? 1 : 0, b = it - j * p.nblk;
     const bool ok = j < ncols && it < NC * p.nblk;
     if constexpr (BF32) {
       off = ok ? (uint32_t)(j * p.ldb + (int64_t)b * 128) : 0x7ffffff0u;
@@ -191,9 +192,10 @@ struct ActStageL {
 
   template <int NC>
   __device__ __forceinline__ void load(const GemvArgs& p, __amdgpu_buffer_rsrc_t rb, int t) {
+    static_assert(NC <= 2, "column by comparison, not division");
     const int ncols = p.N < NC ? p.N : NC;
     const int it = t / L, part = t % L;
-    const int j = it / p.nblk, b = it % p.nblk;
+    const int j = NC > 1 && it >= p.nblk ? 1 : 0, b = it - j * p.nblk;
     const bool ok = j < ncols && it < NC * p.nblk;
     load_words<NV, 0>(rb, ok ? (uint32_t)(j * p.ldb + (int64_t)b * 128 + 4 * NV * part) : 0x7ffffff0u, w);
   }

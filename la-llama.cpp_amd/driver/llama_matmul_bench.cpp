@@ -347,6 +347,7 @@ struct ShardOpts {
   int rank = -1;            // >= 0: one rank per process
   std::string comm_id;      // hex (2 * LAMM_COMM_ID_BYTES digits) or "auto" (world 1 only)
   std::string dump;
+  std::string dump_q;       // the first projection's gathered output (identical inputs at any G)
 };
 
 int run_sharded(const ShardOpts& o, int type, int out_type, int N, int iters, int layers, bool stationary, bool tall) {
@@ -482,10 +483,31 @@ int run_sharded(const ShardOpts& o, int type, int out_type, int N, int iters, in
     fprintf(stderr, "llama-matmul-bench: non-finite logits\n");
     return 1;
   }
-  if (!o.dump.empty()) {
-    FILE* f = fopen(o.dump.c_str(), "wb");
-    if (!f || fwrite(lg.data(), 4, lg.size(), f) != lg.size()) { fprintf(stderr, "llama-matmul-bench: --dump failed\n"); return 1; }
-    fclose(f);
+  auto dump = [](const std::string& path, const std::vector<float>& v) {
+    FILE* f = fopen(path.c_str(), "wb");
+    const bool ok = f && fwrite(v.data(), 4, v.size(), f) == v.size();
+    if (f) fclose(f);
+    if (!ok) fprintf(stderr, "llama-matmul-bench: writing %s failed\n", path.c_str());
+    return ok;
+  };
+  if (!o.dump.empty() && !dump(o.dump, lg)) return 1;
+  if (!o.dump_q.empty()) {   // layer 0's q|k|v (tall) or q projection, from the input every G shares
+    std::vector<float> x((size_t)N * H);
+    for (size_t j = 0; j < x.size(); ++j) x[j] = std::sin(0.37f * (float)j);
+    for (Rank& r : R) {
+      hip_ok(hipSetDevice(r.dev), "hipSetDevice");
+      hip_ok(hipMemcpy(r.d, x.data(), x.size() * 4, hipMemcpyHostToDevice), "upload x");
+    }
+    project(R, comm, N, [&](Rank& r) -> const Tensor& { return r.wq[0]; }, [](Rank& r) -> Act& { return r.a4096; },
+            [](Rank& r) { return r.q; });
+    for (Rank& r : R) {
+      hip_ok(hipSetDevice(r.dev), "hipSetDevice");
+      hip_ok(hipStreamSynchronize(r.s), "first projection");
+    }
+    std::vector<float> q((size_t)N * R[0].wq[0].Mfull);
+    hip_ok(hipSetDevice(R[0].dev), "hipSetDevice");
+    hip_ok(hipMemcpy(q.data(), R[0].q, q.size() * 4, hipMemcpyDeviceToHost), "download q");
+    if (!dump(o.dump_q, q)) return 1;
   }
   const int projections = (tall ? 4 : 7) * layers + 1;
   printf("step %.3f ms  |  %.1f tok/s  |  weight stream %.1f GB/s (whole model)  |  %d matmuls + %d all-gathers per rank "
@@ -540,6 +562,7 @@ int main(int argc, char** argv) {
     else if (a == "--comm-id") so.comm_id = next();
     else if (a == "--device") so.devices = {atoi(next())};
     else if (a == "--dump") so.dump = next();
+    else if (a == "--dump-q") so.dump_q = next();
     else {
       fprintf(stderr, "usage: %s [-d q4_0] [-n tokens] [-i replays] [-l layers] [--no-graph] [-s] [--output-type q6_k] "
                       "[--unfused] [--batch-proj] [--concurrent] [--shard G [--devices 0,1,..]] "
@@ -552,7 +575,7 @@ int main(int argc, char** argv) {
     fprintf(stderr, "llama-matmul-bench: no gfx950 device (%s)\n", lamm_hip_last_error());
     return 1;
   }
-  if (so.rank >= 0 || shard > 0 || !so.devices.empty() || !so.dump.empty()) {   // the row-sharded form
+  if (so.rank >= 0 || shard > 0 || !so.devices.empty() || !so.dump.empty() || !so.dump_q.empty()) {   // the row-sharded form
     if (so.rank >= 0) {
       if (so.world < 1 || so.rank >= so.world || so.comm_id.empty()) {
         fprintf(stderr, "llama-matmul-bench: --rank needs --world > rank and --comm-id\n");

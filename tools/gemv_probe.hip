@@ -532,6 +532,56 @@ __global__ __launch_bounds__(64 * WAVES) void kF(const unsigned char* A, const u
   if (t < WAVES) C[row0 + t] = part[2 * t] + part[2 * t + 1];
 }
 
+// L: the WG's W rows pulled into LDS by LDS-DMA in WG-contiguous 1 KiB pieces (wave w issues
+// pieces w, w + W, ...: the access order of the fastest read floor, rw<W>x<W>), then lane l of
+// wave w reads row w's blocks l, l + 64 back from LDS (dword reads + realignment) -- the same
+// block arithmetic as R
+template <int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void kL(const unsigned char* A, const unsigned char* B, float* C) {
+  __shared__ Act S;
+  __shared__ __attribute__((aligned(16))) uint32_t rows[WAVES * ROW / 4 + 16];
+  constexpr int PIECES = (WAVES * ROW + 1023) / 1024, PPW = (PIECES + WAVES - 1) / WAVES;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), t = threadIdx.x;
+  const int row0 = blockIdx.x * WAVES;
+  const auto rb = make_rsrc(B, BROW);
+  const auto ra = make_rsrc(A + (size_t)row0 * ROW, ROW * WAVES);
+  uint32_t bw[10];
+  if (t < NB) stage_load(rb, t, bw);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int k = 0; k < PPW; ++k) {
+    const int m = k * WAVES + w;   // wave-uniform
+    if (m < PIECES) {
+      auto* d = (__attribute__((address_space(3))) void*)(reinterpret_cast<unsigned char*>(rows) + m * 1024);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, d, 16, lane * 16, m * 1024, 0, 2);
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  if (t < NB) stage_store(S, t, bw);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  float acc = 0.f;
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int b = lane + 64 * it;
+    const int byte = w * ROW + b * 18;
+    const uint32_t* src = &rows[byte >> 2];
+    uint32_t wa[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) wa[k] = src[k];
+    const int sh = (byte & 3) * 8;
+    uint32_t m[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) m[k] = __builtin_amdgcn_alignbit(wa[k + 1], wa[k], sh);
+    uint32_t qs[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) qs[k] = __builtin_amdgcn_alignbit(m[k + 1], m[k], 16);
+    acc = blockdot(qs, m[0], S.q0[b], S.q1[b], S.d[b], S.sb[b], acc);
+  }
+  acc = wave_sum(acc);
+  if (lane == 0) C[row0 + w] = acc;
+}
+
 __global__ void kEmpty(float* C) {
   if (threadIdx.x == 1023) C[0] = 1.f;
 }
@@ -666,13 +716,15 @@ int main(int argc, char** argv) {
   RK("R16", 16, 0, true);
   RK("R8", 8, 0, true);
   RK("R4", 4, 0, true);
-  RK("R8-gather", 8, 0, true, 2);
-  RK("R8-aux0", 8, 0, true, 0, 0);
   RK("R8-nostore", 8, 1, false);
   RK("R8-nocompute", 8, 4, false);
   RK("R8-nocompute-nostore", 8, 5, false);
   RK("R8-nostage", 8, 32, false);
   RK("R8-nostage-nostore", 8, 33, false);
+#define LK(name, W) run(name, [&](const unsigned char* a) { kL<W><<<M / W, 64 * W, 0, s>>>(a, dB, dC); }, true)
+  LK("L8", 8);
+  LK("L4", 4);
+  LK("L16", 16);
 #define FK(name, W, S2) run(name, [&](const unsigned char* a) { kF<W, S2><<<M / W, 64 * W, 0, s>>>(a, dB, dC); }, true)
   FK("F8", 8, 0);
   FK("F8-s2", 8, 1);
@@ -683,10 +735,6 @@ int main(int argc, char** argv) {
   RW("rw4x4", 4, 4);
   RW("rw8x8", 8, 8);
   RW("rw16x16", 16, 16);
-  RW("rw4x8", 4, 8);
-  RW("rw8x4", 8, 4);
-  RW("rw4x2", 4, 2);
-  RW("rw2x2", 2, 2);
   run("rd8", [&](const unsigned char* a) { kReadR<8, 0><<<M / 8, 512, 0, s>>>(a, dC); }, false);
   run("rd8-blocks", [&](const unsigned char* a) { kReadR<8, 1><<<M / 8, 512, 0, s>>>(a, dC); }, false);
   run("rd4", [&](const unsigned char* a) { kReadR<4, 0><<<M / 4, 256, 0, s>>>(a, dC); }, false);

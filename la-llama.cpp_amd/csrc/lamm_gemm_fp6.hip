@@ -835,6 +835,220 @@ __global__ __launch_bounds__((F6Waves<WJ, SI, SJ, KG>::NT)) void gemm_fp6_kernel
   if (t == 0) __hip_atomic_store(&tile_ctr[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// K-group plan, A through VGPRs (the default for grids of < 256 big tiles, config 3).
+// The workgroup's 128 x 64 output tile, 8 waves = 4 K-groups x 2 row halves, as
+// gemm_fp6_kernel<.., 2, 2, 2, 4>, but only the activation planes (shared by a group's two waves)
+// go through LDS-DMA; every wave loads ITS 64 weight rows straight into VGPRs (a 1 KiB coalesced
+// load per plane and block: lane l = row l), and one v_permlane32_swap per dword turns it into the
+// two 32-row fragments the MFMA wants (rows 0-31 in both half-waves, rows 32-63 in both).  The LDS
+// path moved ~66 GB/s per CU, plain loads ~114 (tools/gemm_stream_probe.hip,
+// profiles/r03/gemm_stream_probe_1.json): half the operand bytes leave the slower path.
+// Stages: KG K-steps of activation planes (32 KiB), NB stages; the weight loads of a stage go out
+// with its DMA pieces, D = NB - 1 stages ahead, so one vmcnt wait covers both.
+template <int T>
+__global__ __launch_bounds__(512) void gemm_fp6_kg_kernel(GemvArgs p, const unsigned char* wsA,
+                                                          const unsigned char* wsB) {
+  using F = F6<T>;
+  constexpr bool AFF = F::AFF;
+  constexpr int KG = 4, TI = 128, TJ = 64, NW = 8, WJ = 2, UPB = 2 * WJ, NU = UPB * F6_KB;
+  constexpr int B_SUB = 2 * F6_KB * 2 * TJ * 16;   // 8 KiB: one K-step's activation planes
+  constexpr int STAGE = KG * B_SUB, NB = 3, D = NB - 1;
+  constexpr int PPW = STAGE / F6_PIECE / NW;       // DMA pieces per wave per stage (4)
+  constexpr int AL = 2 * F6_KB;                    // weight loads per wave per K-step (planes x blocks)
+  static_assert(D == 2, "the stage loop is unrolled by the weight ring depth");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const F6Layout L = F6Layout::of(p);
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int lr = lane & 31, h = lane >> 5;
+  const int g = w / 2, wi = w % 2;
+  const int nsi = (p.M + TI - 1) / TI, nsj = (p.N + TJ - 1) / TJ;
+  int ti, tj, z;
+  {   // XCD-aware tile order (gemm_fp6_kernel)
+    const int ntile = nsi * nsj * p.ne12 * p.ne13;
+    const int id = blockIdx.x, x = id & 7, k = id >> 3, q = ntile >> 3, rmd = ntile & 7;
+    const int wv = x < rmd ? x * (q + 1) + k : rmd * (q + 1) + (x - rmd) * q + k;
+    const int per = nsi * nsj;
+    z = wv / per;
+    const int ws_ = wv % per, ib = ws_ / (8 * nsj), rem = ws_ % (8 * nsj);
+    const int width = min(8, nsi - ib * 8);
+    tj = rem / width;
+    ti = ib * 8 + rem % width;
+  }
+  const int it = ti / 2, jt = tj / 2, ri0 = (ti % 2) * TI, rj0 = (tj % 2) * TJ;
+  const int i12 = z % p.ne12, i13 = z / p.ne12;
+  const int ne02 = p.ne12 / p.r2, a = (i12 / p.r2) + (i13 / p.r3) * ne02;
+  const unsigned char* wa = wsA + (int64_t)a * L.a_slice + (int64_t)it * L.nsteps * F6_A_BYTES;
+  const unsigned char* wb = wsB + (int64_t)z * L.b_slice + (int64_t)jt * L.nsteps * F6_B_BYTES;
+  const int nsteps = L.nsteps;
+  const int ns = (nsteps + KG - 1) / KG;   // stages
+  const auto ra = make_rsrc(wa, (uint32_t)(nsteps * F6_A_BYTES));
+  const auto rb = make_rsrc(wb, (uint32_t)(nsteps * F6_B_BYTES));
+
+  // stage ss: this wave's PPW activation pieces (K-group kg = pc / 8 of the stage, piece pc % 8 of
+  // that K-step's planes) and its own weight rows of K-step KG ss + g, into ring slot `slot`
+  u32x4 wt[D][AL];
+  auto issue = [&](int ss, auto slot_c) {
+    constexpr int slot = decltype(slot_c)::value;
+    unsigned char* dst = smem + (ss % NB) * STAGE;
+#pragma unroll
+    for (int k = 0; k < PPW; ++k) {
+      const int pc = k * NW + w, kg = pc / (B_SUB / F6_PIECE), q = pc % (B_SUB / F6_PIECE);
+      const int ks = min(KG * ss + kg, nsteps - 1);
+      const int plane = q / (TJ / 64), part_ = q % (TJ / 64);
+      auto* d = (__attribute__((address_space(3))) void*)(dst + pc * F6_PIECE);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, d, 16, lane * 16,
+                                               ks * F6_B_BYTES + (plane * F6_TJ + rj0 + 64 * part_) * 16, 0, 0);
+    }
+    const int ks = min(KG * ss + g, nsteps - 1);
+#pragma unroll
+    for (int k = 0; k < AL; ++k)   // k = plane * KB + block: rows ri0 + 64 wi + lane
+      wt[slot][k] = __builtin_amdgcn_raw_buffer_load_b128(ra, ks * F6_A_BYTES + ((k * F6_TI) + ri0 + 64 * wi + lane) * 16,
+                                                          0, 0);
+  };
+
+  const int sc_a = h ? SCALE_LO : SCALE_HI;
+  f32x16 acc[WJ][2];
+#pragma unroll
+  for (int x = 0; x < WJ; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[x][y][e] = 0.f;
+  const f32x16 fz = {};
+  issue(0, std::integral_constant<int, 0>{});
+  if (ns > 1) issue(1, std::integral_constant<int, 1>{});
+  F6Frag fb[2][WJ], fa[2][2];
+  F6Res rr[2];
+  bool pend = false;
+
+  auto stage = [&](int ss, auto slot_c) {
+    constexpr int slot = decltype(slot_c)::value;
+    // stage ss's pieces and this wave's weight rows landed: the younger stage's ops may fly
+    if (ss + 1 < ns) f6_wait_vm<PPW + AL>();
+    else f6_wait_vm<0>();
+    f6_barrier();   // stage ss visible to all waves; stage ss - 1 no longer read
+    // weights of K-step KG ss + g -> fragments: v_permlane32_swap(X, X) = (rows 0-31 | rows 0-31,
+    // rows 32-63 | rows 32-63)
+#pragma unroll
+    for (int b = 0; b < F6_KB; ++b)
+#pragma unroll
+      for (int pl = 0; pl < 2; ++pl) {
+        const u32x4 v = wt[slot][pl * F6_KB + b];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const auto sw = __builtin_amdgcn_permlane32_swap(v[e], v[e], false, false);
+          fa[b][0].v[4 * pl + e] = (int)sw[0];
+          fa[b][1].v[4 * pl + e] = (int)sw[1];
+        }
+      }
+    if (ss + D < ns) issue(ss + D, slot_c);   // (this slot's registers are now in fa)
+    const int ks = KG * ss + g;
+    if (ks >= nsteps) return;                 // this group's K-step is past the end (wave-uniform)
+    const unsigned char* sB = smem + (ss % NB) * STAGE + g * B_SUB;
+    auto ldB = [&](int b, int x) {
+      const int r = 32 * x + lr;
+      const int o0 = (((0 * F6_KB + b) * 2 + h) * TJ + r) * 16, o1 = (((1 * F6_KB + b) * 2 + h) * TJ + r) * 16;
+      f6_load(fb[b & 1][x], sB + o0, sB + o1);
+    };
+    auto mfmas = [&](int n, F6Res& R) {
+      const F6Frag& fB = fb[(n / UPB) & 1][(n / 2) % WJ];
+      const F6Frag& fA = fa[(n / UPB) & 1][n & 1];
+      R.s = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fB.v, fA.v, fz, 2, 2, 0, sc_a, 0, SCALE_W);
+      R.pr = __builtin_amdgcn_mfma_f32_32x32x8f16(f6_dq<AFF>(fB), f6_dq<AFF>(fA), fz, 0, 0, 0);
+    };
+    auto epi = [&](int n, const F6Res& R) {
+      f32x16& c = acc[(n / 2) % WJ][n & 1];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) c[e] = __builtin_fmaf(R.s[e], R.pr[e], c[e]);
+    };
+    uint32_t msA[2][2] = {{0, 0}, {0, 0}}, msB[WJ][2] = {};   // q4_1: m_a / s_b per block
+    auto keep_ms = [&](int b) {
+      if constexpr (AFF) {
+#pragma unroll
+        for (int y = 0; y < 2; ++y) msA[y][b >> 1] |= ((uint32_t)fa[b & 1][y].v[7] & 0xffffu) << (16 * (b & 1));
+#pragma unroll
+        for (int x = 0; x < WJ; ++x) msB[x][b >> 1] |= ((uint32_t)fb[b & 1][x].v[7] & 0xffffu) << (16 * (b & 1));
+      }
+    };
+    ldB(0, 0);
+    ldB(0, 1);
+    if (pend) {   // the previous stage's last unit, under this stage's first LDS reads
+      __builtin_amdgcn_sched_barrier(0);
+      epi(NU - 1, rr[(NU - 1) % 2]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    mfmas(0, rr[0]);
+    unroll<NU>([&](auto NN) {
+      constexpr int n = NN;
+      if constexpr (n % UPB == UPB - 1) keep_ms(n / UPB);
+      if constexpr (n == 1) { ldB(1, 0); ldB(1, 1); }   // the next block's activation fragments
+      if constexpr (n + 1 < NU) mfmas(n + 1, rr[(n + 1) % 2]);
+      __builtin_amdgcn_sched_barrier(0);
+      if (n != NU - 1) epi(n, rr[n % 2]);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    pend = true;
+    if constexpr (AFF) {   // sum_b m_a * s_b: rank-KB per K-step, both k halves carry it (x2 like P)
+#pragma unroll
+      for (int x = 0; x < WJ; ++x) {
+        const half4 sf = __builtin_bit_cast(half4, uint2{msB[x][0], msB[x][1]});
+#pragma unroll
+        for (int y = 0; y < 2; ++y) {
+          const half4 mf = __builtin_bit_cast(half4, uint2{msA[y][0], msA[y][1]});
+          acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x8f16(sf, mf, acc[x][y], 0, 0, 0);
+        }
+      }
+    }
+  };
+  for (int ss = 0; ss < ns; ss += D) {
+    stage(ss, std::integral_constant<int, 0>{});
+    if (ss + 1 < ns) stage(ss + 1, std::integral_constant<int, 1>{});
+  }
+  if (pend) {
+    f32x16& c = acc[((NU - 1) / 2) % WJ][(NU - 1) & 1];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) c[e] = __builtin_fmaf(rr[(NU - 1) % 2].s[e], rr[(NU - 1) % 2].pr[e], c[e]);
+  }
+  // K-group epilogue (gemm_fp6_kernel's): partial tiles parked in LDS, rows split over all waves,
+  // summed in group order, 512-byte non-temporal runs of C
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(smem);
+  constexpr int PI = TI + 8, RPW = TJ / NW;
+#pragma unroll
+  for (int x = 0; x < WJ; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int i = 64 * wi + 32 * y + lr, j = 32 * x + (e & 3) + 8 * (e >> 2) + 4 * h;
+        red[(g * TJ + j) * PI + i] = acc[x][y][e];
+      }
+  __syncthreads();
+  float* C = p.C + (int64_t)i12 * p.sc2 + (int64_t)i13 * p.sc3;
+  const int64_t i = (int64_t)ti * TI + 2 * lane;
+  const bool pair = i + 1 < p.M && (p.ldc & 1) == 0 && ((uintptr_t)C & 7) == 0;
+#pragma unroll
+  for (int q = 0; q < RPW; ++q) {
+    const int jl = w * RPW + q;
+    const int64_t j = (int64_t)tj * TJ + jl;
+    f32x2 v = *reinterpret_cast<const f32x2*>(&red[jl * PI + 2 * lane]);
+#pragma unroll
+    for (int g_ = 1; g_ < KG; ++g_) v += *reinterpret_cast<const f32x2*>(&red[(g_ * TJ + jl) * PI + 2 * lane]);
+    v *= 0.5f;
+    if (j < p.N) {
+      float* c = C + j * p.ldc + i;
+      if (pair) {
+        __builtin_nontemporal_store(v, reinterpret_cast<f32x2*>(c));
+      } else {
+        if (i < p.M) c[0] = v[0];
+        if (i + 1 < p.M) c[1] = v[1];
+      }
+    }
+  }
+}
+
 // C[z][j][i] = sum_{s < nsplit} part[s][z][j][i], in split order; V4: 4 consecutive i per
 // thread (M, ldc and the C slice strides multiples of 4, so every float4 is aligned)
 template <bool V4>
@@ -990,6 +1204,13 @@ hipError_t launch_fp6_t(const GemvArgs& p, const void* prepA, void* ws, hipStrea
 #ifdef LAMM_AB_VARIANTS
   const char* ev = getenv("LAMM_GEMM_VARIANT");
 #endif
+  if (plan.sub == 1 && knobs().fp6_av) {
+    constexpr size_t lds = (size_t)4 * 64 * (128 + 8) * 4;   // the epilogue's parked tiles (> 3 x 32 KiB stages)
+    set_max_lds((const void*)gemm_fp6_kg_kernel<T>, (int)lds);
+    hipLaunchKernelGGL(gemm_fp6_kg_kernel<T>, dim3((unsigned)plan.grid), dim3(512), lds, s, p, kA,
+                       static_cast<const unsigned char*>(wsB));
+    return hipGetLastError();
+  }
   if (plan.sub == 1) {
     using WK = F6Waves<2, 2, 2, 4>;
 #ifdef LAMM_AB_VARIANTS

@@ -22,6 +22,23 @@
 namespace lamm {
 namespace {
 
+// Completion signal (LAMM_HIP_KERNEL_SIGNAL=1, see GemvArgs): every workgroup releases its C
+// stores to system scope before it counts itself in; the last one to arrive acquires the others'
+// releases and only then stores the flag the host spins on (a relaxed counter alone
+// let the host see the flag before other workgroups' C reached host memory).
+__device__ __forceinline__ void signal_done(const GemvArgs& p) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's C stores have completed
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence_system();
+    if (atomicAdd(p.done_ctr, 1u) == gridDim.x * gridDim.y - 1) {
+      __threadfence_system();
+      __hip_atomic_store(p.done_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(p.flag, p.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
 // One wave per row: the row's loads for ITER blocks per lane (K <= ITER * 2048) go out at once;
 // each wave also issues its NEXT row's loads before computing the current one (rows strided by
 // the grid), so a persistent grid keeps HBM busy across rows.
@@ -179,15 +196,99 @@ __global__ __launch_bounds__(64 * WAVES) void gemv_rpw_kernel(GemvArgs p) {
     compute(row, wa1);
     row = next;
   }
-  if (p.flag) {   // completion signal: the last workgroup to finish tells the host (see GemvArgs)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's C stores have completed
-    __syncthreads();
-    if (threadIdx.x == 0 && atomicAdd(p.done_ctr, 1u) == gridDim.x * gridDim.y - 1) {
-      __hip_atomic_store(p.done_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __threadfence_system();
-      __hip_atomic_store(p.flag, p.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+  if (p.flag) signal_done(p);
+}
+
+// Single-column decode with K a multiple of 2048 (nb = 64 ITER blocks; config 2, every
+// Llama-7B projection but ffn_down): the workgroup's WAVES rows as ONE flat list of
+// WAVES * nb blocks, wave w's instruction k taking blocks (k WAVES + w) 64 + lane -- so the
+// workgroup's first loads cover contiguous bytes (the fastest read order on this chip:
+// profiles/r03/gemv_probe_4.json rw8x8 2.75 us vs 3.41 row by row) -- each 64-block run lies in
+// one row; a wave reduces each run (fixed DPP order), the runs of a row are summed in LDS in
+// run order (deterministic), one store per row.  Rows past M load zeros and store nothing.
+template <int T, int WAVES, bool BF32, int ITER>
+__global__ __launch_bounds__(64 * WAVES) void gemv_flat_kernel(GemvArgs p) {
+  using F = RFmt<T>;
+  constexpr int NWA = (F::BPB + 3) / 4 + 1;
+  constexpr int NB = 64 * ITER;
+  __shared__ u32x4 sq0[NB], sq1[NB];
+  __shared__ float sbd[NB], sbs[NB];
+  __shared__ float part[WAVES * ITER];
+  const int lane = threadIdx.x & 63, t0 = threadIdx.x;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const unsigned char* Az = p.A;
+  const unsigned char* Bz = p.B;
+  float* Cz = p.C;
+  if (gridDim.y > 1) {
+    const int z = blockIdx.y, i12 = z % p.ne12, i13 = z / p.ne12;
+    Az += (int64_t)(i12 / p.r2) * p.sa2 + (int64_t)(i13 / p.r3) * p.sa3;
+    Bz += (int64_t)i12 * p.sb2 + (int64_t)i13 * p.sb3;
+    Cz += (int64_t)i12 * p.sc2 + (int64_t)i13 * p.sc3;
   }
+  const int row0 = blockIdx.x * WAVES;
+  const int nrows = p.M - row0 < WAVES ? p.M - row0 : WAVES;
+  // A resource over this workgroup's rows (pitch lda, rows of NB blocks)
+  const auto ra = make_rsrc(Az + (int64_t)row0 * p.lda, (uint32_t)((nrows - 1) * p.lda + ((NB * F::BPB + 3) & ~3)));
+  const auto rb = act_rsrc<T, 1, BF32>(p, Bz);
+  uint32_t wa[ITER][NWA];
+  auto issue = [&]() {
+#pragma unroll
+    for (int k = 0; k < ITER; ++k) {
+      const int m = k * WAVES + w, r = m / ITER, bi = (m % ITER) * 64 + lane;   // wave-uniform run m
+      const uint32_t off = r < nrows ? (uint32_t)(r * p.lda + ((bi * F::BPB) & ~3)) : 0x7ffffff0u;
+      load_words<NWA, 2>(ra, off, wa[k]);
+    }
+  };
+  if constexpr (BF32) {   // F32 rows: four lanes per block, one pass (4 NB <= 64 WAVES)
+    static_assert(4 * NB <= 64 * WAVES, "one staging pass");
+    ActStageL<T, 4> sl;
+    sl.template load<1>(p, rb, t0);
+    __builtin_amdgcn_sched_barrier(0);
+    issue();
+    __builtin_amdgcn_sched_barrier(0);
+    if (t0 < 4 * NB) sl.store(t0, sq0, sq1, sbd, sbs);
+  } else {
+    static_assert(NB <= 64 * WAVES, "one staging pass");
+    ActStage<T, false> st;
+    st.template load<1>(p, rb, t0);        // straight-line; out-of-range loads read zeros
+    __builtin_amdgcn_sched_barrier(0);
+    issue();
+    __builtin_amdgcn_sched_barrier(0);
+    if (t0 < NB) st.store(t0, sq0, sq1, sbd, sbs);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < ITER; ++k) {
+    const int m = k * WAVES + w, bi = (m % ITER) * 64 + lane;
+    uint32_t mm[NWA - 1];
+    realign(wa[k], mm, (int)((uint32_t)(bi * F::BPB) & 3u));
+    uint32_t q[8];
+    float da, ma;
+    unpack_a<T>(mm, q, da, ma);
+    const u32x4 b0 = sq0[bi], b1 = sq1[bi];
+    const float db = sbd[bi], bsv = sbs[bi];
+    int sdot = 0;
+    sdot = dot4(q[0], b0[0], sdot); sdot = dot4(q[1], b0[1], sdot); sdot = dot4(q[2], b0[2], sdot);
+    sdot = dot4(q[3], b0[3], sdot); sdot = dot4(q[4], b1[0], sdot); sdot = dot4(q[5], b1[1], sdot);
+    sdot = dot4(q[6], b1[2], sdot); sdot = dot4(q[7], b1[3], sdot);
+    if constexpr (T == kQ4_0) sdot -= 8 * __builtin_bit_cast(int, bsv);
+    if constexpr (T == kQ5_0) sdot -= 16 * __builtin_bit_cast(int, bsv);
+    float acc;
+    if constexpr (T == kQ4_1 || T == kQ5_1)
+      acc = __builtin_fmaf(da * db, (float)sdot, ma * bsv);
+    else
+      acc = da * db * (float)sdot;
+    acc = wave_sum(acc);
+    if (lane == 0) part[m] = acc;
+  }
+  __syncthreads();
+  if (t0 < nrows) {
+    float c = part[t0 * ITER];
+#pragma unroll
+    for (int k = 1; k < ITER; ++k) c += part[t0 * ITER + k];
+    Cz[row0 + t0] = c;
+  }
+  if (p.flag) signal_done(p);
 }
 
 template <int T, int NC, int WAVES, bool BF32, int ITER>
@@ -212,6 +313,17 @@ hipError_t launch_rpw_k(const GemvArgs& p, hipStream_t s) {
 template <int T, int NC>
 hipError_t launch_rpw_nc(const GemvArgs& p, hipStream_t s, int waves) {
   const bool bf = p.b_f32 != 0;
+  // one column, K = 4096 (128 blocks): the flat-run kernel, 8 waves
+  if constexpr (NC == 1) {
+    if (p.nblk == 128 && waves == 8 && !knobs().gemv_laneb) {
+      const dim3 g((unsigned)((p.M + 7) / 8), (unsigned)(p.ne12 * p.ne13));
+      if (bf)
+        hipLaunchKernelGGL((gemv_flat_kernel<T, 8, true, 2>), g, dim3(512), 0, s, p);
+      else
+        hipLaunchKernelGGL((gemv_flat_kernel<T, 8, false, 2>), g, dim3(512), 0, s, p);
+      return hipGetLastError();
+    }
+  }
   if (p.nblk <= 128) {
     if (waves >= 16) return bf ? launch_rpw_k<T, NC, 16, true, 2>(p, s) : launch_rpw_k<T, NC, 16, false, 2>(p, s);
     if (waves >= 8) return bf ? launch_rpw_k<T, NC, 8, true, 2>(p, s) : launch_rpw_k<T, NC, 8, false, 2>(p, s);

@@ -269,18 +269,21 @@ def test_gemm_fp6_split_k(t, split, monkeypatch):
 FP6_KG_SHAPES = [(300, 140, 4096 + 64), (257, 129, 96), (33, 17, 1024), (130, 9, 8192 + 512), (64, 64, 64)]
 
 
-@pytest.mark.parametrize("form", ["1", "2"])
+@pytest.mark.parametrize("form", ["1", "1lds", "2"])
 @pytest.mark.parametrize("t", FP6_TYPES, ids=[ol.NAMES[t] for t in FP6_TYPES])
 @pytest.mark.parametrize("shape", FP6_KG_SHAPES, ids=[f"{m}x{n}x{k}" for m, n, k in FP6_KG_SHAPES])
 def test_gemm_fp6_k_groups(t, shape, form, monkeypatch):
     """fp6 engine on 128x64 workgroup tiles whose waves split K into groups summed through LDS
-    (LAMM_FP6_SUB=1: 4 groups of 64x64 waves, 2: 2 groups of 32x64 waves; automatic for grids
+    (LAMM_FP6_SUB=1: 4 groups of 64x64 waves, weights straight into VGPRs; "1lds": the same with
+    LAMM_FP6_AV=0, weights through LDS-DMA too; 2: 2 groups of 32x64 waves; automatic for grids
     of < 256 big tiles): K-step counts that leave groups with nothing in the last stage (65,
     2, 136 K-steps), tiles cut by M / N, C with a padded pitch."""
     monkeypatch.setenv("LAMM_GEMM_PATH", "fp6")
-    monkeypatch.setenv("LAMM_FP6_SUB", form)
+    monkeypatch.setenv("LAMM_FP6_SUB", form[0])
+    if form == "1lds":
+        monkeypatch.setenv("LAMM_FP6_AV", "0")
     M, N, K = shape
-    A_q, B_q = random_case(t, M, N, K, seed=M + N + K + int(form))
+    A_q, B_q = random_case(t, M, N, K, seed=M + N + K + int(form[0]))
     c, raw = gpu_mul_mat(t, A_q, B_q, M, N, K, ldc=M + 3)
     ref = ORACLE.mul_mat(t, M, N, K, A_q, B_q)
     assert rel_err(c, ref, absdot(t, A_q, B_q, M, N, K)).max() < TOL

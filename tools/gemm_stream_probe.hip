@@ -35,9 +35,13 @@ constexpr int CHUNK = 8192;                        // bytes per (tile, K-step), 
 constexpr size_t A_BYTES = (size_t)NIT * NSTEP * CHUNK, B_BYTES = (size_t)NJT * NSTEP * CHUNK;
 constexpr int KG = 4, NW = 8;
 
-__device__ __forceinline__ void tile_of(int& it, int& jt) {
+__device__ __forceinline__ void tile_of(int& it, int& jt, int mode) {
   // XCD-aware order of the real kernel: one XCD's 32 workgroups = 8 i-tiles x 4 j-tiles
+  // mode 1: every workgroup streams tile (0, 0) (L2-resident after the first touch);
+  // mode 2: the workgroups of an XCD share one tile, XCDs differ (a per-XCD working set of 1 tile)
   const int id = blockIdx.x, x = id & 7, k = id >> 3, q = 256 >> 3;
+  if (mode == 1) { it = jt = 0; return; }
+  if (mode == 2) { it = x; jt = 0; return; }
   const int wv = x * q + k, per = NIT * NJT;
   const int ws_ = wv % per, ib = ws_ / (8 * NJT), rem = ws_ % (8 * NJT);
   jt = rem / 8;
@@ -45,11 +49,11 @@ __device__ __forceinline__ void tile_of(int& it, int& jt) {
 }
 
 template <int NBUF>
-__global__ __launch_bounds__(512) void k_dma(const unsigned char* A, const unsigned char* B, unsigned* out) {
+__global__ __launch_bounds__(512) void k_dma(const unsigned char* A, const unsigned char* B, unsigned* out, int mode) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int STAGE = KG * 2 * CHUNK;   // 64 KiB
   int it, jt;
-  tile_of(it, jt);
+  tile_of(it, jt, mode);
   const int t = threadIdx.x, lane = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6);
   const auto ra = make_rsrc(A + (size_t)it * NSTEP * CHUNK, NSTEP * CHUNK);
   const auto rb = make_rsrc(B + (size_t)jt * NSTEP * CHUNK, NSTEP * CHUNK);
@@ -90,9 +94,9 @@ __global__ __launch_bounds__(512) void k_dma(const unsigned char* A, const unsig
 }
 
 template <int D>
-__global__ __launch_bounds__(512) void k_vgpr(const unsigned char* A, const unsigned char* B, unsigned* out) {
+__global__ __launch_bounds__(512) void k_vgpr(const unsigned char* A, const unsigned char* B, unsigned* out, int mode) {
   int it, jt;
-  tile_of(it, jt);
+  tile_of(it, jt, mode);
   const int t = threadIdx.x, lane = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int g = w / 2, wi = w % 2;
   const auto ra = make_rsrc(A + (size_t)it * NSTEP * CHUNK, NSTEP * CHUNK);
@@ -172,14 +176,20 @@ int main() {
     first = false;
     fflush(stdout);
   };
-  {
-    constexpr int lds = 2 * 65536;
-    CK(hipFuncSetAttribute((const void*)k_dma<2>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-    report("dma2", time_graph([&] { k_dma<2><<<256, 512, lds, s>>>(A, B, out); }));
+  constexpr int lds = 2 * 65536;
+  CK(hipFuncSetAttribute((const void*)k_dma<2>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+  const char* mname[3] = {"", "-same", "-xcd"};
+  for (int mode = 0; mode < 3; ++mode) {
+    char n[32];
+    snprintf(n, sizeof n, "dma2%s", mname[mode]);
+    report(n, time_graph([&] { k_dma<2><<<256, 512, lds, s>>>(A, B, out, mode); }));
+    snprintf(n, sizeof n, "vgpr2%s", mname[mode]);
+    report(n, time_graph([&] { k_vgpr<2><<<256, 512, 0, s>>>(A, B, out, mode); }));
+    if (mode == 0) {
+      report("vgpr3", time_graph([&] { k_vgpr<3><<<256, 512, 0, s>>>(A, B, out, 0); }));
+      report("vgpr4", time_graph([&] { k_vgpr<4><<<256, 512, 0, s>>>(A, B, out, 0); }));
+    }
   }
-  report("vgpr2", time_graph([&] { k_vgpr<2><<<256, 512, 0, s>>>(A, B, out); }));
-  report("vgpr3", time_graph([&] { k_vgpr<3><<<256, 512, 0, s>>>(A, B, out); }));
-  report("vgpr4", time_graph([&] { k_vgpr<4><<<256, 512, 0, s>>>(A, B, out); }));
   printf(", \"bytes_per_cu\": %.0f}\n", per_cu);
   return 0;
 }

@@ -396,14 +396,15 @@ def llama_step_sharded(ctx, fmt):
     projection's output, the whole step one hipGraph per process).  Returns rank 0's view with the
     step time maxed over ranks."""
     exe = os.path.join(ROOT, "la-llama.cpp_amd", "llama-matmul-bench")
-    uid = [ctx.la.comm_unique_id().hex() if ctx.rank == 0 else None]
-    if ctx.world > 1:
-        ctx.dist.broadcast_object_list(uid, src=0)
     out = {"note": f"weight rows sharded over {ctx.world} GPU(s), one process per GPU, RCCL all-gather after every "
                    "projection (hipGraph per process); synthetic weights, weight matmuls only"}
     for name, argv in (("decode_n1_batch_proj", ["-n", "1", "-i", "50", "--batch-proj"]),
                        ("prefill_n512", ["-n", "512", "-i", "5", "-s", "--batch-proj"])):
         res = {}
+        # a fresh RCCL unique id per communicator: an id's bootstrap root serves ONE init
+        uid = [ctx.la.comm_unique_id().hex() if ctx.rank == 0 else None]
+        if ctx.world > 1:
+            ctx.dist.broadcast_object_list(uid, src=0)
         try:
             r = subprocess.run([exe, "-d", fmt, "--rank", str(ctx.rank), "--world", str(ctx.world), "--comm-id", uid[0],
                                 "--device", str(ctx.device)] + argv, capture_output=True, text=True, timeout=300)

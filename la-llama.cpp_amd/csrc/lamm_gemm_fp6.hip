@@ -835,27 +835,29 @@ __global__ __launch_bounds__((F6Waves<WJ, SI, SJ, KG>::NT)) void gemm_fp6_kernel
   if (t == 0) __hip_atomic_store(&tile_ctr[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// K-group plan, A through VGPRs (the default for grids of < 256 big tiles, config 3).
-// The workgroup's 128 x 64 output tile, 8 waves = 4 K-groups x 2 row halves, as
-// gemm_fp6_kernel<.., 2, 2, 2, 4>, but only the activation planes (shared by a group's two waves)
-// go through LDS-DMA; every wave loads ITS 64 weight rows straight into VGPRs (a 1 KiB coalesced
-// load per plane and block: lane l = row l), and one v_permlane32_swap per dword turns it into the
-// two 32-row fragments the MFMA wants (rows 0-31 in both half-waves, rows 32-63 in both).  The LDS
-// path moved ~66 GB/s per CU, plain loads ~114 (tools/gemm_stream_probe.hip,
-// profiles/r03/gemm_stream_probe_1.json): half the operand bytes leave the slower path.
-// Stages: KG K-steps of activation planes (32 KiB), NB stages; the weight loads of a stage go out
-// with its DMA pieces, D = NB - 1 stages ahead, so one vmcnt wait covers both.
-template <int T>
-__global__ __launch_bounds__(512) void gemm_fp6_kg_kernel(GemvArgs p, const unsigned char* wsA,
+// K-group plan without workgroup barriers in the main loop.  The workgroup's 128 x 64 tile and
+// waves as gemm_fp6_kernel<.., 2, 2, 2, 4> (4 K-groups x 2 row halves), but every wave streams its
+// own blocks:
+//   weights   : its 64 rows by LDS-DMA into a ring of its OWN (P x 2 KiB) -- only this wave writes
+//               and reads it, so its vmcnt is the only synchronisation -- read back by ds_read
+//               with both half-waves on the same rows (the MFMA wants each weight row in both
+//               K halves; LDS serves the duplicate addresses, no cross-lane VALU)
+//   activations: the group's 64 rows straight into VGPRs in fragment order (lane (r, h) = row r,
+//               hi / lo plane h; the group's second wave hits L1)
+// P blocks in flight per wave.  A fragment's six code dwords and its {d, m / s} pair are separate
+// operands (scale MFMA / f16 MFMA), assembled from the two 16-byte planes at use.
+// AB (ablations, tools/prep_probe.hip only): 1 loads only; 2 compute only (no loads after the first
+// P blocks); 3 compute only with half the FMAs; 4 compute only, one FMA per unit.
+template <int T, int P, int AB = 0>
+__global__ __launch_bounds__(512) void gemm_fp6_kv_kernel(GemvArgs p, const unsigned char* wsA,
                                                           const unsigned char* wsB) {
   using F = F6<T>;
   constexpr bool AFF = F::AFF;
-  constexpr int KG = 4, TI = 128, TJ = 64, NW = 8, WJ = 2, UPB = 2 * WJ, NU = UPB * F6_KB;
-  constexpr int B_SUB = 2 * F6_KB * 2 * TJ * 16;   // 8 KiB: one K-step's activation planes
-  constexpr int STAGE = KG * B_SUB, NB = 3, D = NB - 1;
-  constexpr int PPW = STAGE / F6_PIECE / NW;       // DMA pieces per wave per stage (4)
-  constexpr int AL = 2 * F6_KB;                    // weight loads per wave per K-step (planes x blocks)
-  static_assert(D == 2, "the stage loop is unrolled by the weight ring depth");
+  constexpr int KG = 4, TI = 128, TJ = 64, NW = 8, WJ = 2, UPB = 2 * WJ;
+  constexpr int LPB = 2 + 2 * WJ;   // vmem ops per block: 2 weight DMA pieces, WJ x 2 activation loads
+  constexpr int RING = P * 2 * F6_PIECE;   // bytes of a wave's weight ring
+  static_assert(P >= 2 && P <= 6, "blocks in flight");
+  static_assert(NW * RING <= 4 * 64 * (128 + 8) * 4, "the rings live under the epilogue's LDS");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const F6Layout L = F6Layout::of(p);
   const int t = threadIdx.x, lane = t & 63;
@@ -881,30 +883,32 @@ __global__ __launch_bounds__(512) void gemm_fp6_kg_kernel(GemvArgs p, const unsi
   const unsigned char* wa = wsA + (int64_t)a * L.a_slice + (int64_t)it * L.nsteps * F6_A_BYTES;
   const unsigned char* wb = wsB + (int64_t)z * L.b_slice + (int64_t)jt * L.nsteps * F6_B_BYTES;
   const int nsteps = L.nsteps;
-  const int ns = (nsteps + KG - 1) / KG;   // stages
+  const int nbw = nsteps > g ? (nsteps - g + KG - 1) / KG * F6_KB : 0;   // this wave's blocks
   const auto ra = make_rsrc(wa, (uint32_t)(nsteps * F6_A_BYTES));
   const auto rb = make_rsrc(wb, (uint32_t)(nsteps * F6_B_BYTES));
+  const int a0 = (ri0 + 64 * wi) * 16;                         // f6_aoff(0, 0, first row)
+  const uint32_t b0 = (uint32_t)(h * F6_TJ + rj0 + lr) * 16;   // f6_boff(0, 0, h, row)
+  unsigned char* ring = smem + w * RING;
 
-  // stage ss: this wave's PPW activation pieces (K-group kg = pc / 8 of the stage, piece pc % 8 of
-  // that K-step's planes) and its own weight rows of K-step KG ss + g, into ring slot `slot`
-  u32x4 wt[D][AL];
-  auto issue = [&](int ss, auto slot_c) {
-    constexpr int slot = decltype(slot_c)::value;
-    unsigned char* dst = smem + (ss % NB) * STAGE;
+  u32x4 rb_[P][WJ][2];   // activation ring: sub-tile x, plane
+  // block u of this wave (K-step g + KG (u / KB), block u % KB) into ring slot S; past the end the
+  // last block is fetched again (unused) so every slot's wait count stays the same
+  auto issue = [&](int u, auto S_) {
+    constexpr int S = decltype(S_)::value;
+    const int uu = min(u, nbw - 1);
+    const int ks = g + KG * (uu / F6_KB), b = uu % F6_KB;
+    const int ka = ks * F6_A_BYTES, kb = ks * F6_B_BYTES;
 #pragma unroll
-    for (int k = 0; k < PPW; ++k) {
-      const int pc = k * NW + w, kg = pc / (B_SUB / F6_PIECE), q = pc % (B_SUB / F6_PIECE);
-      const int ks = min(KG * ss + kg, nsteps - 1);
-      const int plane = q / (TJ / 64), part_ = q % (TJ / 64);
-      auto* d = (__attribute__((address_space(3))) void*)(dst + pc * F6_PIECE);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, d, 16, lane * 16,
-                                               ks * F6_B_BYTES + (plane * F6_TJ + rj0 + 64 * part_) * 16, 0, 0);
+    for (int pl = 0; pl < 2; ++pl) {
+      auto* d = (__attribute__((address_space(3))) void*)(ring + (S * 2 + pl) * F6_PIECE);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, d, 16, lane * 16, ka + a0 + (pl * F6_KB + b) * F6_TI * 16, 0, 0);
     }
-    const int ks = min(KG * ss + g, nsteps - 1);
 #pragma unroll
-    for (int k = 0; k < AL; ++k)   // k = plane * KB + block: rows ri0 + 64 wi + lane
-      wt[slot][k] = __builtin_amdgcn_raw_buffer_load_b128(ra, ks * F6_A_BYTES + ((k * F6_TI) + ri0 + 64 * wi + lane) * 16,
-                                                          0, 0);
+    for (int x = 0; x < WJ; ++x)
+#pragma unroll
+      for (int pl = 0; pl < 2; ++pl)
+        rb_[S][x][pl] = __builtin_amdgcn_raw_buffer_load_b128(
+            rb, b0 + (uint32_t)((((pl * F6_KB + b) * 2) * F6_TJ + 32 * x) * 16), kb, 0);
   };
 
   const int sc_a = h ? SCALE_LO : SCALE_HI;
@@ -916,102 +920,150 @@ __global__ __launch_bounds__(512) void gemm_fp6_kg_kernel(GemvArgs p, const unsi
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[x][y][e] = 0.f;
   const f32x16 fz = {};
-  issue(0, std::integral_constant<int, 0>{});
-  if (ns > 1) issue(1, std::integral_constant<int, 1>{});
-  F6Frag fb[2][WJ], fa[2][2];
   F6Res rr[2];
   bool pend = false;
+  uint32_t msA[2] = {0, 0}, msB[WJ] = {};   // q4_1: the K-step's m_a / s_b (16 bits per block)
+  // a fragment's operands from its two 16-byte planes: the scale MFMA's six code dwords, the f16
+  // MFMA's {d, 0, 0, 0} (q4_1: {d, m} -> {d, 0, 0, 0} too)
+  auto codes = [](const u32x4& p0, const u32x4& p1) {
+    return i32x8{(int)p0[0], (int)p0[1], (int)p0[2], (int)p0[3], (int)p1[0], (int)p1[1], 0, 0};
+  };
+  auto dq = [](const u32x4& p1) {
+    if constexpr (AFF) return __builtin_bit_cast(half4, uint2{p1[2], 0u});
+    else return __builtin_bit_cast(half4, uint2{p1[2], p1[3]});
+  };
 
-  auto stage = [&](int ss, auto slot_c) {
-    constexpr int slot = decltype(slot_c)::value;
-    // stage ss's pieces and this wave's weight rows landed: the younger stage's ops may fly
-    if (ss + 1 < ns) f6_wait_vm<PPW + AL>();
-    else f6_wait_vm<0>();
-    f6_barrier();   // stage ss visible to all waves; stage ss - 1 no longer read
-    // weights of K-step KG ss + g -> fragments: v_permlane32_swap(X, X) = (rows 0-31 | rows 0-31,
-    // rows 32-63 | rows 32-63)
+  // a block's weight fragments from its ring slot: per sub-tile y (rows 32 y + lr in both half-waves)
+  // the scale MFMA's six code dwords and the f16 MFMA's {d, m} pair
+  struct WFrag { i32x8 c[2]; i32x2 d[2]; };
+  const int lo = (32 * 0 + lr) * 16;
+  auto wread = [&](int slot, WFrag& f) {
+    const unsigned char* r0 = ring + slot * 2 * F6_PIECE;
 #pragma unroll
-    for (int b = 0; b < F6_KB; ++b)
-#pragma unroll
-      for (int pl = 0; pl < 2; ++pl) {
-        const u32x4 v = wt[slot][pl * F6_KB + b];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const auto sw = __builtin_amdgcn_permlane32_swap(v[e], v[e], false, false);
-          fa[b][0].v[4 * pl + e] = (int)sw[0];
-          fa[b][1].v[4 * pl + e] = (int)sw[1];
-        }
-      }
-    if (ss + D < ns) issue(ss + D, slot_c);   // (this slot's registers are now in fa)
-    const int ks = KG * ss + g;
-    if (ks >= nsteps) return;                 // this group's K-step is past the end (wave-uniform)
-    const unsigned char* sB = smem + (ss % NB) * STAGE + g * B_SUB;
-    auto ldB = [&](int b, int x) {
-      const int r = 32 * x + lr;
-      const int o0 = (((0 * F6_KB + b) * 2 + h) * TJ + r) * 16, o1 = (((1 * F6_KB + b) * 2 + h) * TJ + r) * 16;
-      f6_load(fb[b & 1][x], sB + o0, sB + o1);
-    };
-    auto mfmas = [&](int n, F6Res& R) {
-      const F6Frag& fB = fb[(n / UPB) & 1][(n / 2) % WJ];
-      const F6Frag& fA = fa[(n / UPB) & 1][n & 1];
-      R.s = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fB.v, fA.v, fz, 2, 2, 0, sc_a, 0, SCALE_W);
-      R.pr = __builtin_amdgcn_mfma_f32_32x32x8f16(f6_dq<AFF>(fB), f6_dq<AFF>(fA), fz, 0, 0, 0);
-    };
-    auto epi = [&](int n, const F6Res& R) {
-      f32x16& c = acc[(n / 2) % WJ][n & 1];
-#pragma unroll
-      for (int e = 0; e < 16; ++e) c[e] = __builtin_fmaf(R.s[e], R.pr[e], c[e]);
-    };
-    uint32_t msA[2][2] = {{0, 0}, {0, 0}}, msB[WJ][2] = {};   // q4_1: m_a / s_b per block
-    auto keep_ms = [&](int b) {
-      if constexpr (AFF) {
-#pragma unroll
-        for (int y = 0; y < 2; ++y) msA[y][b >> 1] |= ((uint32_t)fa[b & 1][y].v[7] & 0xffffu) << (16 * (b & 1));
-#pragma unroll
-        for (int x = 0; x < WJ; ++x) msB[x][b >> 1] |= ((uint32_t)fb[b & 1][x].v[7] & 0xffffu) << (16 * (b & 1));
-      }
-    };
-    ldB(0, 0);
-    ldB(0, 1);
-    if (pend) {   // the previous stage's last unit, under this stage's first LDS reads
-      __builtin_amdgcn_sched_barrier(0);
-      epi(NU - 1, rr[(NU - 1) % 2]);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    mfmas(0, rr[0]);
-    unroll<NU>([&](auto NN) {
-      constexpr int n = NN;
-      if constexpr (n % UPB == UPB - 1) keep_ms(n / UPB);
-      if constexpr (n == 1) { ldB(1, 0); ldB(1, 1); }   // the next block's activation fragments
-      if constexpr (n + 1 < NU) mfmas(n + 1, rr[(n + 1) % 2]);
-      __builtin_amdgcn_sched_barrier(0);
-      if (n != NU - 1) epi(n, rr[n % 2]);
-      __builtin_amdgcn_sched_barrier(0);
-    });
-    pend = true;
-    if constexpr (AFF) {   // sum_b m_a * s_b: rank-KB per K-step, both k halves carry it (x2 like P)
-#pragma unroll
-      for (int x = 0; x < WJ; ++x) {
-        const half4 sf = __builtin_bit_cast(half4, uint2{msB[x][0], msB[x][1]});
-#pragma unroll
-        for (int y = 0; y < 2; ++y) {
-          const half4 mf = __builtin_bit_cast(half4, uint2{msA[y][0], msA[y][1]});
-          acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x8f16(sf, mf, acc[x][y], 0, 0, 0);
-        }
-      }
+    for (int y = 0; y < 2; ++y) {
+      const int o = lo + 32 * y * 16;
+      const i32x4 q0 = *reinterpret_cast<const i32x4*>(r0 + o);
+      const i32x4 q1 = *reinterpret_cast<const i32x4*>(r0 + F6_PIECE + o);
+      f.d[y] = i32x2{q1[2], q1[3]};
+      f.c[y] = i32x8{q0[0], q0[1], q0[2], q0[3], q1[0], q1[1], 0, 0};
     }
   };
-  for (int ss = 0; ss < ns; ss += D) {
-    stage(ss, std::integral_constant<int, 0>{});
-    if (ss + 1 < ns) stage(ss + 1, std::integral_constant<int, 1>{});
+  WFrag wc;   // the current block's weight fragments (read during the block before)
+
+  int sink = 0;
+  auto block = [&](int u, auto S_) {
+    constexpr int S = decltype(S_)::value;
+    constexpr int SN = (S + 1) % P;
+    f6_wait_vm<LPB * (P - 1)>();   // block u's activations landed; the P - 1 younger may fly
+    if constexpr (AB == 1) {
+#pragma unroll
+      for (int x = 0; x < WJ; ++x) sink ^= (int)(rb_[S][x][0][0] ^ rb_[S][x][1][3]);
+      sink ^= *(const int*)(ring + S * 2 * F6_PIECE + lane * 4);
+      issue(u + P, S_);
+      return;
+    }
+    if constexpr (AB >= 2) {
+#pragma unroll
+      for (int x = 0; x < WJ; ++x) asm volatile("" : "+v"(rb_[S][x][0]), "+v"(rb_[S][x][1]));
+    }
+    WFrag wn;   // the next block's, read half-way through this one
+    // unit n: S = the exact block dots (scale MFMA), P = 2 d_b d_a (f16 MFMA), then acc += S * P.
+    // Issue order per unit: S(n+1), half of unit n's FMAs, P(n+1), the other half -- each MFMA's 32
+    // cycles in the matrix pipe covered by 8 FMAs (32 issue cycles) of the unit before
+    auto mfma_s = [&](int n, F6Res& R) {
+      const int x = (n / 2) % WJ, y = n & 1;
+      R.s = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(codes(rb_[S][x][0], rb_[S][x][1]), wc.c[y], fz, 2, 2, 0,
+                                                            sc_a, 0, SCALE_W);
+    };
+    auto mfma_p = [&](int n, F6Res& R) {
+      const int x = (n / 2) % WJ, y = n & 1;
+      const half4 da = AFF ? __builtin_bit_cast(half4, i32x2{wc.d[y][0], 0}) : __builtin_bit_cast(half4, wc.d[y]);
+      R.pr = __builtin_amdgcn_mfma_f32_32x32x8f16(dq(rb_[S][x][1]), da, fz, 0, 0, 0);
+    };
+    auto epi = [&](int n, const F6Res& R, int half) {
+      f32x16& c = acc[(n / 2) % WJ][n & 1];
+      if constexpr (AB == 4) {
+        if (half == 0) c[0] = __builtin_fmaf(R.s[0], R.pr[0], c[0]);
+        return;
+      }
+      if (AB == 3 && half == 1) return;
+#pragma unroll
+      for (int e = 8 * half; e < 8 * half + 8; ++e) c[e] = __builtin_fmaf(R.s[e], R.pr[e], c[e]);
+    };
+    auto sb = [] { __builtin_amdgcn_sched_barrier(0); };
+    sb();
+    mfma_s(0, rr[0]);
+    sb();
+    if (pend) epi(UPB - 1, rr[(UPB - 1) % 2], 0);   // the previous block's last unit
+    sb();
+    mfma_p(0, rr[0]);
+    sb();
+    if (pend) epi(UPB - 1, rr[(UPB - 1) % 2], 1);
+    sb();
+    unroll<UPB - 1>([&](auto NN) {
+      constexpr int n = NN;
+      if constexpr (n == 1) {   // the next block's weights: its DMA pieces landed (the oldest vmem ops
+        // but this block's activation loads are older still -- all landed at the top)
+        if constexpr (AB < 2) f6_wait_vm<LPB * (P - 2) + 2 * WJ>();
+        wread(SN, wn);
+        sb();
+      }
+      mfma_s(n + 1, rr[(n + 1) % 2]);
+      sb();
+      epi(n, rr[n % 2], 0);
+      sb();
+      mfma_p(n + 1, rr[(n + 1) % 2]);
+      sb();
+      epi(n, rr[n % 2], 1);
+      sb();
+    });
+    pend = true;
+    if constexpr (AFF) {   // sum_b m_a s_b per K-step: rank-KB, both k halves carry it (x2 like P)
+      const int bk = u % F6_KB;
+#pragma unroll
+      for (int y = 0; y < 2; ++y) msA[y] |= ((uint32_t)wc.d[y][1] & 0xffffu) << (16 * bk);
+#pragma unroll
+      for (int x = 0; x < WJ; ++x) msB[x] |= (rb_[S][x][1][3] & 0xffffu) << (16 * bk);
+      if (bk == F6_KB - 1) {
+#pragma unroll
+        for (int x = 0; x < WJ; ++x) {
+          const half4 sf = __builtin_bit_cast(half4, uint2{msB[x], 0u});
+#pragma unroll
+          for (int y = 0; y < 2; ++y) {
+            const half4 mf = __builtin_bit_cast(half4, uint2{msA[y], 0u});
+            acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x8f16(sf, mf, acc[x][y], 0, 0, 0);
+          }
+          msB[x] = 0;
+        }
+        msA[0] = msA[1] = 0;
+      }
+    }
+    sb();
+    // this slot's registers were read by the MFMAs above and its LDS by the ds_reads they waited
+    // for: refill it P blocks ahead
+    if constexpr (AB < 2) issue(u + P, S_);
+    wc = wn;
+  };
+  if (nbw > 0) {
+    // whole rounds of the ring without branches (the wait-count pass stays exact), then the
+    // remaining nbw % P blocks (a multiple of KB = 2)
+    unroll<P>([&](auto K) { issue(K, K); });
+    f6_wait_vm<LPB * (P - 1) + 2 * WJ>();   // block 0's weight pieces
+    wread(0, wc);
+    int u0 = 0;
+    for (; u0 + P <= nbw; u0 += P) unroll<P>([&](auto K) { block(u0 + K, K); });
+    unroll<P - 1>([&](auto K) {
+      if (u0 + (int)K < nbw) block(u0 + K, K);
+    });
   }
   if (pend) {
-    f32x16& c = acc[((NU - 1) / 2) % WJ][(NU - 1) & 1];
+    f32x16& c = acc[((UPB - 1) / 2) % WJ][(UPB - 1) & 1];
 #pragma unroll
-    for (int e = 0; e < 16; ++e) c[e] = __builtin_fmaf(rr[(NU - 1) % 2].s[e], rr[(NU - 1) % 2].pr[e], c[e]);
+    for (int e = 0; e < 16; ++e) c[e] = __builtin_fmaf(rr[(UPB - 1) % 2].s[e], rr[(UPB - 1) % 2].pr[e], c[e]);
   }
-  // K-group epilogue (gemm_fp6_kernel's): partial tiles parked in LDS, rows split over all waves,
-  // summed in group order, 512-byte non-temporal runs of C
+  if constexpr (AB == 1)
+    if (sink == 0x9e3779b9) acc[0][0][0] = 1.f;
+  // K-group epilogue (gemm_fp6_kernel's), over the rings: every wave past its last ring read
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   float* red = reinterpret_cast<float*>(smem);
@@ -1204,11 +1256,11 @@ hipError_t launch_fp6_t(const GemvArgs& p, const void* prepA, void* ws, hipStrea
 #ifdef LAMM_AB_VARIANTS
   const char* ev = getenv("LAMM_GEMM_VARIANT");
 #endif
-  if (plan.sub == 1 && knobs().fp6_av) {
-    constexpr size_t lds = (size_t)4 * 64 * (128 + 8) * 4;   // the epilogue's parked tiles (> 3 x 32 KiB stages)
-    set_max_lds((const void*)gemm_fp6_kg_kernel<T>, (int)lds);
-    hipLaunchKernelGGL(gemm_fp6_kg_kernel<T>, dim3((unsigned)plan.grid), dim3(512), lds, s, p, kA,
-                       static_cast<const unsigned char*>(wsB));
+  if (plan.sub == 1 && knobs().fp6_av) {   // LAMM_FP6_AV=0: the LDS-staged form below
+    constexpr size_t lds = (size_t)4 * 64 * (128 + 8) * 4;   // the epilogue's parked tiles
+    auto kern = gemm_fp6_kv_kernel<T, F6<T>::AFF ? 2 : 3>;   // more in flight spills
+    set_max_lds((const void*)kern, (int)lds);
+    hipLaunchKernelGGL(kern, dim3((unsigned)plan.grid), dim3(512), lds, s, p, kA, static_cast<const unsigned char*>(wsB));
     return hipGetLastError();
   }
   if (plan.sub == 1) {

@@ -274,8 +274,9 @@ FP6_KG_SHAPES = [(300, 140, 4096 + 64), (257, 129, 96), (33, 17, 1024), (130, 9,
 @pytest.mark.parametrize("shape", FP6_KG_SHAPES, ids=[f"{m}x{n}x{k}" for m, n, k in FP6_KG_SHAPES])
 def test_gemm_fp6_k_groups(t, shape, form, monkeypatch):
     """fp6 engine on 128x64 workgroup tiles whose waves split K into groups summed through LDS
-    (LAMM_FP6_SUB=1: 4 groups of 64x64 waves, weights straight into VGPRs; "1lds": the same with
-    LAMM_FP6_AV=0, weights through LDS-DMA too; 2: 2 groups of 32x64 waves; automatic for grids
+    (LAMM_FP6_SUB=1: 4 groups of 64x64 waves streaming their own blocks, no barriers -- weights by
+    LDS-DMA into per-wave rings, activations into VGPRs; "1lds": LAMM_FP6_AV=0, the barrier-staged
+    LDS form; 2: 2 groups of 32x64 waves; automatic for grids
     of < 256 big tiles): K-step counts that leave groups with nothing in the last stage (65,
     2, 136 K-steps), tiles cut by M / N, C with a padded pitch."""
     monkeypatch.setenv("LAMM_GEMM_PATH", "fp6")

@@ -206,7 +206,9 @@ __global__ __launch_bounds__(64 * WAVES) void gemv_rpw_kernel(GemvArgs p) {
 // profiles/r03/gemv_probe_4.json rw8x8 2.75 us vs 3.41 row by row) -- each 64-block run lies in
 // one row; a wave reduces each run (fixed DPP order), the runs of a row are summed in LDS in
 // run order (deterministic), one store per row.  Rows past M load zeros and store nothing.
-template <int T, int WAVES, bool BF32, int ITER>
+// SL: more than one slice (the slice offsets; a one-slice launch reads no gridDim.y, does no
+// divisions).  Rows past M: their offsets lie past the A resource's range and read zeros.
+template <int T, int WAVES, bool BF32, int ITER, bool SL>
 __global__ __launch_bounds__(64 * WAVES) void gemv_flat_kernel(GemvArgs p) {
   using F = RFmt<T>;
   constexpr int NWA = (F::BPB + 3) / 4 + 1;
@@ -219,7 +221,7 @@ __global__ __launch_bounds__(64 * WAVES) void gemv_flat_kernel(GemvArgs p) {
   const unsigned char* Az = p.A;
   const unsigned char* Bz = p.B;
   float* Cz = p.C;
-  if (gridDim.y > 1) {
+  if constexpr (SL) {
     const int z = blockIdx.y, i12 = z % p.ne12, i13 = z / p.ne12;
     Az += (int64_t)(i12 / p.r2) * p.sa2 + (int64_t)(i13 / p.r3) * p.sa3;
     Bz += (int64_t)i12 * p.sb2 + (int64_t)i13 * p.sb3;
@@ -227,18 +229,18 @@ __global__ __launch_bounds__(64 * WAVES) void gemv_flat_kernel(GemvArgs p) {
   }
   const int row0 = blockIdx.x * WAVES;
   const int nrows = p.M - row0 < WAVES ? p.M - row0 : WAVES;
-  // A resource over this workgroup's rows (pitch lda, rows of NB blocks)
-  const auto ra = make_rsrc(Az + (int64_t)row0 * p.lda, (uint32_t)((nrows - 1) * p.lda + ((NB * F::BPB + 3) & ~3)));
-  const auto rb = act_rsrc<T, 1, BF32>(p, Bz);
+  const uint32_t lda = (uint32_t)p.lda;   // < 2^16 here: nb = 64 ITER blocks
+  // A resource over this workgroup's rows, ending at its last row's last block byte
+  const auto ra = make_rsrc(Az + (int64_t)row0 * p.lda, (uint32_t)(nrows - 1) * lda + ((NB * F::BPB + 3) & ~3));
   uint32_t wa[ITER][NWA];
   auto issue = [&]() {
 #pragma unroll
     for (int k = 0; k < ITER; ++k) {
       const int m = k * WAVES + w, r = m / ITER, bi = (m % ITER) * 64 + lane;   // wave-uniform run m
-      const uint32_t off = r < nrows ? (uint32_t)(r * p.lda + ((bi * F::BPB) & ~3)) : 0x7ffffff0u;
-      load_words<NWA, 2>(ra, off, wa[k]);
+      load_words<NWA, 2>(ra, (uint32_t)r * lda + ((uint32_t)(bi * F::BPB) & ~3u), wa[k]);
     }
   };
+  const auto rb = make_rsrc(Bz, BF32 ? (uint32_t)p.K * 4 : (uint32_t)(NB * F::VBPB + 3) & ~3u);
   if constexpr (BF32) {   // F32 rows: four lanes per block, one pass (4 NB <= 64 WAVES)
     static_assert(4 * NB <= 64 * WAVES, "one staging pass");
     ActStageL<T, 4> sl;
@@ -317,10 +319,11 @@ hipError_t launch_rpw_nc(const GemvArgs& p, hipStream_t s, int waves) {
   if constexpr (NC == 1) {
     if (p.nblk == 128 && waves == 8 && !knobs().gemv_laneb) {
       const dim3 g((unsigned)((p.M + 7) / 8), (unsigned)(p.ne12 * p.ne13));
-      if (bf)
-        hipLaunchKernelGGL((gemv_flat_kernel<T, 8, true, 2>), g, dim3(512), 0, s, p);
-      else
-        hipLaunchKernelGGL((gemv_flat_kernel<T, 8, false, 2>), g, dim3(512), 0, s, p);
+      const bool sl = g.y > 1;
+      if (bf && sl) hipLaunchKernelGGL((gemv_flat_kernel<T, 8, true, 2, true>), g, dim3(512), 0, s, p);
+      else if (bf) hipLaunchKernelGGL((gemv_flat_kernel<T, 8, true, 2, false>), g, dim3(512), 0, s, p);
+      else if (sl) hipLaunchKernelGGL((gemv_flat_kernel<T, 8, false, 2, true>), g, dim3(512), 0, s, p);
+      else hipLaunchKernelGGL((gemv_flat_kernel<T, 8, false, 2, false>), g, dim3(512), 0, s, p);
       return hipGetLastError();
     }
   }

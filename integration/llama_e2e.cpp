@@ -7,7 +7,12 @@
 // computes a matmul.
 //
 //   llama_e2e [-m model.gguf] [--layers L] [--regen] [-t threads] [-p n_prompt] [-n n_gen]
-//             [-r reps] [--logits out.bin] [--write-only] [--seed S]
+//             [-r reps] [--logits out.bin] [--write-only] [--seed S] [--force t0,t1,...]
+//
+// --force: teacher forcing -- generation step k feeds token t_k instead of the previous step's
+// argmax (the parity runs feed the reference's own greedy tokens to every build, so each logits
+// row is computed from the same context on both sides); "argmax" in the JSON is each logits
+// row's own argmax either way.
 //
 // The model is a Llama-2-7B-shaped GGUF (n_embd 4096, n_ff 11008, 32 heads, n_vocab 32000,
 // `--layers` blocks, default 32) with synthetic weights, written by write_model() below when
@@ -252,6 +257,7 @@ int main(int argc, char** argv) {
   int n_layer = 32, threads = 16, n_prompt = 512, n_gen = 128, reps = 1;
   uint64_t seed = 1;
   bool regen = false, write_only = false;
+  std::vector<llama_token> forced;
   for (int i = 1; i < argc; ++i) {
     const std::string a = argv[i];
     auto next = [&]() -> const char* {
@@ -269,6 +275,15 @@ int main(int argc, char** argv) {
     else if (a == "--regen") regen = true;
     else if (a == "--write-only") write_only = true;
     else if (a == "--dump") g_dump_dir = next();
+    else if (a == "--force") {
+      for (const char* c = next(); *c;) {
+        char* end = nullptr;
+        const long v = strtol(c, &end, 10);
+        if (end == c) break;
+        forced.push_back((llama_token)v);
+        c = *end == ',' ? end + 1 : end;
+      }
+    }
     else { fprintf(stderr, "unknown argument %s\n", a.c_str()); return 2; }
   }
   double t_write = 0;
@@ -308,7 +323,7 @@ int main(int argc, char** argv) {
   for (auto& tok : prompt) tok = (llama_token)(1 + splitmix(s) % (uint64_t)(n_vocab - 1));
 
   std::vector<float> logits_out;
-  std::vector<int> gen_tokens;
+  std::vector<int> gen_tokens, row_argmax;
   auto run = [&](bool record, double* pp_ms, double* tg_ms) -> bool {
     llama_kv_cache_clear(ctx);
     llama_batch b = llama_batch_init(n_prompt, 0, 1);
@@ -328,8 +343,10 @@ int main(int argc, char** argv) {
     const float* lg = llama_get_logits_ith(ctx, n_prompt - 1);
     if (record) logits_out.insert(logits_out.end(), lg, lg + n_vocab);
     llama_token tok = argmax(lg, n_vocab);
+    if (record) row_argmax.push_back(tok);
     llama_batch g = llama_batch_init(1, 0, 1);
     for (int k = 0; k < n_gen; ++k) {
+      if (k < (int)forced.size()) tok = forced[k];
       if (record) gen_tokens.push_back(tok);
       g.token[0] = tok;
       g.pos[0] = n_prompt + k;
@@ -341,6 +358,7 @@ int main(int argc, char** argv) {
       const float* l2 = llama_get_logits_ith(ctx, 0);
       if (record) logits_out.insert(logits_out.end(), l2, l2 + n_vocab);
       tok = argmax(l2, n_vocab);
+      if (record) row_argmax.push_back(tok);
     }
     const double t2 = now_ms();
     llama_batch_free(g);
@@ -372,7 +390,9 @@ int main(int argc, char** argv) {
          n_layer, threads, n_prompt, n_gen, reps, pp_med, tg_med, n_prompt / (pp_med * 1e-3),
          n_gen > 0 ? n_gen / (tg_med * 1e-3) : 0.0, t_load, t_write);
   for (size_t i = 0; i < gen_tokens.size(); ++i) printf("%s%d", i ? ", " : "", gen_tokens[i]);
-  printf("]}\n");
+  printf("], \"argmax\": [");
+  for (size_t i = 0; i < row_argmax.size(); ++i) printf("%s%d", i ? ", " : "", row_argmax[i]);
+  printf("], \"forced\": %s}\n", forced.empty() ? "false" : "true");
   fflush(stdout);
   llama_free(ctx);
   llama_free_model(m);

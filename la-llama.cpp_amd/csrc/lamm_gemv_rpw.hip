@@ -208,8 +208,13 @@ __global__ __launch_bounds__(64 * WAVES) void gemv_rpw_kernel(GemvArgs p) {
 // run order (deterministic), one store per row.  Rows past M load zeros and store nothing.
 // SL: more than one slice (the slice offsets; a one-slice launch reads no gridDim.y, does no
 // divisions).  Rows past M: their offsets lie past the A resource's range and read zeros.
-template <int T, int WAVES, bool BF32, int ITER, bool SL>
-__global__ __launch_bounds__(64 * WAVES) void gemv_flat_kernel(GemvArgs p) {
+// The body, on plain values: the slice offsets (SL) and the completion signal (gemv_flat_kernel's
+// SIG) stay outside it, so a one-slice launch without a signal reads nothing but its five scalar
+// arguments (gemv_flat1_kernel: preloaded into SGPRs, no kernarg load before the first A load and
+// none after the last one).
+template <int T, int WAVES, bool BF32, int ITER>
+__device__ __forceinline__ void flat_body(const unsigned char* Az, uint32_t lda, const unsigned char* Bz, float* Cz,
+                                          int M) {
   using F = RFmt<T>;
   constexpr int NWA = (F::BPB + 3) / 4 + 1;
   constexpr int NB = 64 * ITER;
@@ -218,20 +223,10 @@ __global__ __launch_bounds__(64 * WAVES) void gemv_flat_kernel(GemvArgs p) {
   __shared__ float part[WAVES * ITER];
   const int lane = threadIdx.x & 63, t0 = threadIdx.x;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const unsigned char* Az = p.A;
-  const unsigned char* Bz = p.B;
-  float* Cz = p.C;
-  if constexpr (SL) {
-    const int z = blockIdx.y, i12 = z % p.ne12, i13 = z / p.ne12;
-    Az += (int64_t)(i12 / p.r2) * p.sa2 + (int64_t)(i13 / p.r3) * p.sa3;
-    Bz += (int64_t)i12 * p.sb2 + (int64_t)i13 * p.sb3;
-    Cz += (int64_t)i12 * p.sc2 + (int64_t)i13 * p.sc3;
-  }
   const int row0 = blockIdx.x * WAVES;
-  const int nrows = p.M - row0 < WAVES ? p.M - row0 : WAVES;
-  const uint32_t lda = (uint32_t)p.lda;   // < 2^16 here: nb = 64 ITER blocks
+  const int nrows = M - row0 < WAVES ? M - row0 : WAVES;
   // A resource over this workgroup's rows, ending at its last row's last block byte
-  const auto ra = make_rsrc(Az + (int64_t)row0 * p.lda, (uint32_t)(nrows - 1) * lda + ((NB * F::BPB + 3) & ~3));
+  const auto ra = make_rsrc(Az + (int64_t)row0 * lda, (uint32_t)(nrows - 1) * lda + ((NB * F::BPB + 3) & ~3));
   uint32_t wa[ITER][NWA];
   auto issue = [&]() {
 #pragma unroll
@@ -240,7 +235,10 @@ __global__ __launch_bounds__(64 * WAVES) void gemv_flat_kernel(GemvArgs p) {
       load_words<NWA, 2>(ra, (uint32_t)r * lda + ((uint32_t)(bi * F::BPB) & ~3u), wa[k]);
     }
   };
-  const auto rb = make_rsrc(Bz, BF32 ? (uint32_t)p.K * 4 : (uint32_t)(NB * F::VBPB + 3) & ~3u);
+  const auto rb = make_rsrc(Bz, BF32 ? (uint32_t)(NB * 32 * 4) : (uint32_t)(NB * F::VBPB + 3) & ~3u);
+  GemvArgs p{};   // what the staging reads of it: one column of nb blocks at B
+  p.N = 1;
+  p.nblk = NB;
   if constexpr (BF32) {   // F32 rows: four lanes per block, one pass (4 NB <= 64 WAVES)
     static_assert(4 * NB <= 64 * WAVES, "one staging pass");
     ActStageL<T, 4> sl;
@@ -290,7 +288,29 @@ __global__ __launch_bounds__(64 * WAVES) void gemv_flat_kernel(GemvArgs p) {
     for (int k = 1; k < ITER; ++k) c += part[t0 * ITER + k];
     Cz[row0 + t0] = c;
   }
-  if (p.flag) signal_done(p);
+}
+
+// SL: more than one slice; SIG: the launch carries the boundary's completion signal
+template <int T, int WAVES, bool BF32, int ITER, bool SL, bool SIG>
+__global__ __launch_bounds__(64 * WAVES) void gemv_flat_kernel(GemvArgs p) {
+  const unsigned char* Az = p.A;
+  const unsigned char* Bz = p.B;
+  float* Cz = p.C;
+  if constexpr (SL) {
+    const int z = blockIdx.y, i12 = z % p.ne12, i13 = z / p.ne12;
+    Az += (int64_t)(i12 / p.r2) * p.sa2 + (int64_t)(i13 / p.r3) * p.sa3;
+    Bz += (int64_t)i12 * p.sb2 + (int64_t)i13 * p.sb3;
+    Cz += (int64_t)i12 * p.sc2 + (int64_t)i13 * p.sc3;
+  }
+  flat_body<T, WAVES, BF32, ITER>(Az, (uint32_t)p.lda, Bz, Cz, p.M);   // lda < 2^16 here: nb = 64 ITER
+  if constexpr (SIG) signal_done(p);
+}
+
+// One slice, no signal (BASELINE config 2 as bench.py and the device API launch it)
+template <int T, bool BF32>
+__global__ __launch_bounds__(512) void gemv_flat1_kernel(const unsigned char* A, const unsigned char* B, float* C,
+                                                         uint32_t lda, int M) {
+  flat_body<T, 8, BF32, 2>(A, lda, B, C, M);
 }
 
 template <int T, int NC, int WAVES, bool BF32, int ITER>
@@ -319,11 +339,26 @@ hipError_t launch_rpw_nc(const GemvArgs& p, hipStream_t s, int waves) {
   if constexpr (NC == 1) {
     if (p.nblk == 128 && waves == 8 && !knobs().gemv_laneb) {
       const dim3 g((unsigned)((p.M + 7) / 8), (unsigned)(p.ne12 * p.ne13));
-      const bool sl = g.y > 1;
-      if (bf && sl) hipLaunchKernelGGL((gemv_flat_kernel<T, 8, true, 2, true>), g, dim3(512), 0, s, p);
-      else if (bf) hipLaunchKernelGGL((gemv_flat_kernel<T, 8, true, 2, false>), g, dim3(512), 0, s, p);
-      else if (sl) hipLaunchKernelGGL((gemv_flat_kernel<T, 8, false, 2, true>), g, dim3(512), 0, s, p);
-      else hipLaunchKernelGGL((gemv_flat_kernel<T, 8, false, 2, false>), g, dim3(512), 0, s, p);
+      const bool sl = g.y > 1, sig = p.flag != nullptr;
+      if (!sl && !sig) {
+        const uint32_t lda = (uint32_t)p.lda;
+        if (bf) hipLaunchKernelGGL((gemv_flat1_kernel<T, true>), g, dim3(512), 0, s, p.A, p.B, p.C, lda, p.M);
+        else hipLaunchKernelGGL((gemv_flat1_kernel<T, false>), g, dim3(512), 0, s, p.A, p.B, p.C, lda, p.M);
+        return hipGetLastError();
+      }
+      auto go = [&](auto bfc, auto slc, auto sgc) {
+        hipLaunchKernelGGL((gemv_flat_kernel<T, 8, decltype(bfc)::value, 2, decltype(slc)::value, decltype(sgc)::value>),
+                           g, dim3(512), 0, s, p);
+      };
+      using t_ = std::true_type;
+      using f_ = std::false_type;
+      if (bf) {
+        if (sl) sig ? go(t_{}, t_{}, t_{}) : go(t_{}, t_{}, f_{});
+        else go(t_{}, f_{}, t_{});
+      } else {
+        if (sl) sig ? go(f_{}, t_{}, t_{}) : go(f_{}, t_{}, f_{});
+        else go(f_{}, f_{}, t_{});
+      }
       return hipGetLastError();
     }
   }

@@ -697,6 +697,12 @@ class Runtime {
     return hbuf_[which];
   }
   void* pinned_dev(int which) const { return hdev_[which]; }
+  // the staging buffer (grown to `bytes`) has one address on every device: what zero-copy over
+  // several devices needs (ROCm maps pinned host memory at its host address)
+  bool pinned_shared(int which, size_t bytes) {
+    pinned(which, bytes);
+    return hdev_[which] == static_cast<void*>(hbuf_[which]);
+  }
 
   void clear() {
     for (Dev& d : devs)
@@ -910,8 +916,10 @@ extern "C" void lamm_mul_mat(const struct ggml_compute_params* vparams, struct g
   const size_t x_row = act == kCpuInit ? b_row : (size_t)ldx * sizeof(float);
   const size_t x_bytes = x_row * (size_t)(N * nslices);
   const size_t c_bytes = (size_t)M * N * nslices * sizeof(float);
-  const bool zc_in = G == 1 && zero_copy(x_bytes, true) && act != kGpuQuant;
-  const bool zc_out = G == 1 && zero_copy(c_bytes, false);
+  // zero-copy on several devices too: every device reads the one pinned activation buffer and
+  // writes its own rows of the one pinned C (mapped pinned memory has one address on every device)
+  const bool zc_in = zero_copy(x_bytes, true) && act != kGpuQuant && (G == 1 || rt.pinned_shared(0, x_bytes));
+  const bool zc_out = zero_copy(c_bytes, false) && (G == 1 || rt.pinned_shared(1, c_bytes));
   const unsigned char* x_host = nullptr;   // the bytes every device uploads (or reads in place)
   auto gather_f32 = [&](unsigned char* out) {   // F32 src1 rows (any strides) -> [slice][N][ldx]
     for (int64_t i13 = 0; i13 < ne13; ++i13)
@@ -999,13 +1007,16 @@ extern "C" void lamm_mul_mat(const struct ggml_compute_params* vparams, struct g
     }
     const bool b_f32 = act == kFused || (act == kGpuQuant && (vdt == kQ8_0 || vdt == kQ8_1));
     const size_t b_pitch = b_f32 ? x_row : b_row;
-    const size_t c_slice = (size_t)rows * N * sizeof(float);
-    float* dC = zc_out ? static_cast<float*>((rt.pinned(1, c_bytes), rt.pinned_dev(1)))
+    // C: zero-copy = this device's rows [r0, r0 + rows) of the pinned [slice][N][M] image; else a
+    // dense [slice][N][rows] scratch copied into dst below
+    const int64_t ldc = zc_out ? M : rows;
+    const size_t c_slice = (size_t)ldc * N * sizeof(float);
+    float* dC = zc_out ? static_cast<float*>((rt.pinned(1, c_bytes), rt.pinned_dev(1))) + r0
                        : static_cast<float*>(d.scratch(1, c_slice * (size_t)nslices + 64));
 
     lamm_matrix A{a_dev, t0, (int)rows, (int)kb, a_pitch / (int64_t)block_bytes(t0)};
     lamm_matrix B = b_f32 ? lamm_matrix{dB, kF32, (int)ne00, (int)N, ldx} : lamm_matrix{dB, vdt, (int)kb, (int)N, (int64_t)kb};
-    lamm_matrix C{dC, kF32, (int)rows, (int)N, rows};
+    lamm_matrix C{dC, kF32, (int)rows, (int)N, ldc};
     lamm_batch bt{ne02, ne03, ne12, ne13, a_s2, a_s3,
                   b_pitch * (size_t)N, b_pitch * (size_t)(N * ne12), c_slice, c_slice * (size_t)ne12};
     // prefill calls on the fp6 / super-block engines reuse the weights' packed form

@@ -445,9 +445,10 @@ struct CallStats {
   const char* name;
   uint64_t calls = 0;
   double us = 0;
-  double phase_us[4] = {0, 0, 0, 0};   // fingerprint + lookup, enqueue (copies + launches), sync, C to dst
+  double phase_us[7] = {0, 0, 0, 0, 0, 0, 0};
 };
-const char* kPhase[4] = {"weights lookup", "enqueue", "device sync", "C to dst"};
+constexpr int kPhases = 7;
+const char* kPhase[kPhases] = {"host staging", "src0", "B up", "launch", "C down", "device sync", "C to dst"};
 CallStats g_stats[4] = {{"weights N<=8"}, {"weights N>8"}, {"views N<=8"}, {"views N>8"}};
 bool stats_on() { return knobs().stats; }
 void print_stats() {
@@ -456,7 +457,7 @@ void print_stats() {
     {
       fprintf(stderr, "lamm_hip stats: %-13s %8llu calls %12.1f us total %8.2f us/call  (", c.name,
               (unsigned long long)c.calls, c.us, c.us / (double)c.calls);
-      for (int k = 0; k < 4; ++k) fprintf(stderr, "%s%s %.2f", k ? ", " : "", kPhase[k], c.phase_us[k] / c.calls);
+      for (int k = 0; k < kPhases; ++k) fprintf(stderr, "%s%s %.2f", k ? ", " : "", kPhase[k], c.phase_us[k] / c.calls);
       fprintf(stderr, ")\n");
     }
 }
@@ -542,8 +543,10 @@ Transient upload_transient(Dev& d, const ggml::tensor* src0, size_t row_bytes) {
   const size_t span = (size_t)(ne1 - 1) * nb1 + (size_t)(ne2 - 1) * nb2 + (size_t)(ne3 - 1) * nb3 + row_bytes;
   const size_t payload = row_bytes * (size_t)(ne1 * ne2 * ne3);
   const bool stacked = nb2 == nb1 * (size_t)ne1 && nb3 == nb2 * (size_t)ne2;
-  if (!stacked && nb1 % 16 == 0 && nb2 % 16 == 0 && nb3 % 16 == 0 && nb1 % bpb == 0 && nb1 >= row_bytes &&
-      span <= 2 * payload) {
+  // the whole span in one linear copy, host strides kept (the K view: heads interleaved; the
+  // transposed V view: rows of n_kv cells at an n_ctx pitch) -- a 2D copy from pageable memory
+  // goes row by row
+  if (nb1 % 16 == 0 && nb2 % 16 == 0 && nb3 % 16 == 0 && nb1 % bpb == 0 && nb1 >= row_bytes && span <= 2 * payload) {
     void* dev = d.scratch(3, span + 64);
     HIPCHK(hipMemcpyAsync(dev, host, span, hipMemcpyHostToDevice, d.stream));
     return Transient{dev, (int64_t)nb1, nb2, nb3};
@@ -972,19 +975,27 @@ extern "C" void lamm_mul_mat(const struct ggml_compute_params* vparams, struct g
       a_s2 = tr.s2;
       a_s3 = tr.s3;
     }
+    stat.phase(1);
     // activations on (or mapped into) the device
     void* dB;
     if (zc_in) {
       dB = rt.pinned_dev(0);
     } else if (act == kFused || act == kGpuQuant) {
       float* dX = static_cast<float*>(d.scratch(2, x_bytes + 64));
-      for (int64_t i13 = 0; i13 < ne13; ++i13)
-        for (int64_t i12 = 0; i12 < ne12; ++i12) {
-          const unsigned char* x =
-              static_cast<const unsigned char*>(src1->data) + i12 * src1->nb[2] + i13 * src1->nb[3];
-          HIPCHK(hipMemcpy2DAsync(dX + (i13 * ne12 + i12) * N * ldx, (size_t)ldx * sizeof(float), x, src1->nb[1],
-                                  (size_t)ne00 * sizeof(float), (size_t)N, hipMemcpyHostToDevice, s));
-        }
+      const bool dense = ldx == ne00 && src1->nb[1] == (size_t)ne00 * sizeof(float) &&
+                         src1->nb[2] == src1->nb[1] * (size_t)N && src1->nb[3] == src1->nb[2] * (size_t)ne12;
+      if (dense) {   // one linear copy (HIP's 2D path moves pageable rows one by one)
+        HIPCHK(hipMemcpyAsync(dX, src1->data, x_bytes, hipMemcpyHostToDevice, s));
+      } else {
+        for (int64_t i13 = 0; i13 < ne13; ++i13)
+          for (int64_t i12 = 0; i12 < ne12; ++i12) {
+            const unsigned char* x =
+                static_cast<const unsigned char*>(src1->data) + i12 * src1->nb[2] + i13 * src1->nb[3];
+            HIPCHK(hipMemcpy2DAsync(dX + (i13 * ne12 + i12) * N * ldx, (size_t)ldx * sizeof(float), x, src1->nb[1],
+                                    (size_t)ne00 * sizeof(float), (size_t)N, hipMemcpyHostToDevice, s));
+          }
+      }
+      stat.phase(2);
       dB = dX;
       // q8_0 / q8_1 activations are quantized by the library inside the kernels that read them;
       // q8_K / f16 ones here
@@ -1042,22 +1053,30 @@ extern "C" void lamm_mul_mat(const struct ggml_compute_params* vparams, struct g
       fprintf(stderr, "lamm_hip: lamm_hip_matmul_batched failed (%d): %s\n", rc, g_err.c_str());
       std::abort();
     }
+    stat.phase(3);
     if (!zc_out) {   // this device's rows straight into dst
-      for (int64_t i13 = 0; i13 < ne13; ++i13)
-        for (int64_t i12 = 0; i12 < ne12; ++i12) {
-          unsigned char* c_host =
-              static_cast<unsigned char*>(dst->data) + i12 * dst->nb[2] + i13 * dst->nb[3] + r0 * sizeof(float);
-          HIPCHK(hipMemcpy2DAsync(c_host, dst->nb[1], dC + (i13 * ne12 + i12) * rows * N, (size_t)rows * sizeof(float),
-                                  (size_t)rows * sizeof(float), N, hipMemcpyDeviceToHost, s));
-        }
+      const bool dense = rows == M && dst->nb[1] == (size_t)M * sizeof(float) &&
+                         dst->nb[2] == dst->nb[1] * (size_t)N && dst->nb[3] == dst->nb[2] * (size_t)ne12;
+      if (dense) {
+        HIPCHK(hipMemcpyAsync(dst->data, dC, c_bytes, hipMemcpyDeviceToHost, s));
+      } else {
+        for (int64_t i13 = 0; i13 < ne13; ++i13)
+          for (int64_t i12 = 0; i12 < ne12; ++i12) {
+            unsigned char* c_host =
+                static_cast<unsigned char*>(dst->data) + i12 * dst->nb[2] + i13 * dst->nb[3] + r0 * sizeof(float);
+            HIPCHK(hipMemcpy2DAsync(c_host, dst->nb[1], dC + (i13 * ne12 + i12) * rows * N,
+                                    (size_t)rows * sizeof(float), (size_t)rows * sizeof(float), N,
+                                    hipMemcpyDeviceToHost, s));
+          }
+      }
     }
+    stat.phase(4);
   }
-  stat.phase(1);
   for (int g = 0; g < G; ++g) {
     HIPCHK(hipSetDevice(rt.devs[g].id));
     wait_device(rt.devs[g]);
   }
-  stat.phase(2);
+  stat.phase(5);
   if (zc_out) {
     const unsigned char* hC = rt.pinned(1, c_bytes);
     const size_t c_slice = (size_t)M * N * sizeof(float);
@@ -1069,7 +1088,7 @@ extern "C" void lamm_mul_mat(const struct ggml_compute_params* vparams, struct g
           memcpy(c_host + j * dst->nb[1], src + (size_t)j * M * sizeof(float), M * sizeof(float));
       }
   }
-  stat.phase(3);
+  stat.phase(6);
 }
 
 extern "C" void lamm_hip_cache_clear(void) {

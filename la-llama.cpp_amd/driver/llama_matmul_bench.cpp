@@ -39,6 +39,11 @@
 // GEMV, which quantizes them while staging (bit-exact with the separate quantizer), and prefill
 // steps (N > 8) to the GEMMs, which quantize them in their activation prep;
 // --unfused runs the separate lamm_hip_quantize launches instead.
+// --ctx P (single GPU, -n 1): a decode step with the attention matmuls too -- per layer the token's
+// K row / V column appended to a device-resident F16 KV cache of P cells, KQ and KQV over all P
+// cells as batched F16 GEMVs (32 heads per launch), the F32 -> F16 conversions of their src1
+// (ggml's INIT) on the GPU: every mul_mat of a llama.cpp decode step, with nothing crossing
+// PCIe.  Softmax / RoPE / norms are llama.cpp ops outside the hook and stay out.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -151,6 +156,11 @@ struct Model {
   std::vector<Tensor> wq, wk, wv, wo, w1, w3, w2, out;
   Act a4096, b4096, c4096, a11008;
   float *q, *k, *v, *o, *g, *u, *d, *logits;
+  // --ctx P: the attention matmuls over a device-resident F16 KV cache of P cells per layer
+  int ctx = 0;
+  std::vector<void*> kc, vt;   // per layer: K [head][P][128], V transposed [head][128][P] (b2430)
+  void *qh = nullptr, *probs = nullptr, *vrow = nullptr;
+  float *scores = nullptr, *kqv = nullptr;
 };
 
 bool g_fused = true;   // decode (N <= 8): F32 activations straight into the GEMV (INIT fused)
@@ -184,6 +194,36 @@ void matmul(const Tensor& w, const Act& a, float* C, int N, hipStream_t s) {
   }
 }
 
+// Decode attention of layer l on the device (N = 1, the token at cache cell P - 1): what
+// llm_build_kqv sends to the mul_mat hook (LC/llama.cpp:5322-5372) with the KV cache resident on
+// the GPU instead of in host memory -- this token's K row and V column appended to the F16 cache
+// (the ggml_cpy of k_cur / v_cur, LC/llama.cpp:5252-5270), q to F16 (ggml's INIT of the F16
+// matmul), KQ = K . q per head, then KQV = V^T . p per head.  Scale, mask and softmax between
+// the two are llama.cpp ops, not mul_mats: the scores go to KQV as its src1 unchanged.
+void attention(Model& m, int l, hipStream_t s) {
+  constexpr int NH = 32, D = 128, F16 = 1;
+  const int P = m.ctx;
+  const bool tall = m.wq[l].slices == 3;   // --batch-proj: q | k | v in one output
+  const float* k = tall ? m.q + NH * D : m.k;
+  const float* v = tall ? m.q + 2 * NH * D : m.v;
+  lamm_ok(lamm_hip_quantize(F16, 0, k, D, (char*)m.kc[l] + (size_t)(P - 1) * D * 2, (int64_t)P * D, D, NH, s),
+          "K append");
+  // V^T column P - 1: the row converted once, then scattered at the cache's row pitch (a strided
+  // device copy; ggml's cpy into the transposed view)
+  lamm_ok(lamm_hip_quantize(F16, 0, v, NH * D, m.vrow, NH * D, NH * D, 1, s), "V -> f16");
+  hip_ok(hipMemcpy2DAsync((char*)m.vt[l] + (size_t)(P - 1) * 2, (size_t)P * 2, m.vrow, 2, 2, NH * D,
+                          hipMemcpyDeviceToDevice, s),
+         "V append");
+  lamm_ok(lamm_hip_quantize(F16, 0, m.q, D, m.qh, D, D, NH, s), "q -> f16");
+  const lamm_matrix A{m.kc[l], F16, P, D, D}, B{m.qh, F16, D, 1, D}, C{m.scores, 0, P, 1, P};
+  const lamm_batch bt{NH, 1, NH, 1, (size_t)P * D * 2, 0, (size_t)D * 2, 0, (size_t)P * 4, 0};
+  lamm_ok(lamm_hip_matmul_batched(&A, &B, &C, &bt, s), "KQ");
+  lamm_ok(lamm_hip_quantize(F16, 0, m.scores, P, m.probs, P, P, NH, s), "kq -> f16");
+  const lamm_matrix A2{m.vt[l], F16, D, P, P}, B2{m.probs, F16, P, 1, P}, C2{m.kqv, 0, D, 1, D};
+  const lamm_batch bt2{NH, 1, NH, 1, (size_t)D * P * 2, 0, (size_t)P * 2, 0, (size_t)D * 4, 0};
+  lamm_ok(lamm_hip_matmul_batched(&A2, &B2, &C2, &bt2, s), "KQV");
+}
+
 // one token step: the mul_mat nodes of build_llama in graph order
 void step(Model& m, int layers, hipStream_t s) {
   const int N = m.N;
@@ -206,7 +246,8 @@ void step(Model& m, int layers, hipStream_t s) {
         matmul(m.wv[l], m.a4096, m.v, N, s);
       }
     }
-    quantize(m.wo[l].type, m.b4096, N, s);           // kqv_out (here: the q projection) -> wo
+    if (m.ctx > 0) attention(m, l, s);               // kqv_out -> wo
+    quantize(m.wo[l].type, m.b4096, N, s);           // kqv_out (without --ctx: the q projection) -> wo
     matmul(m.wo[l], m.b4096, m.o, N, s);
     quantize(m.w1[l].type, m.c4096, N, s);           // ffn_norm output (here: wo's) -> gate / up
     if (m.side[0] && m.w1[l].slices == 1) {          // ffn_up on a forked stream
@@ -527,7 +568,7 @@ int run_sharded(const ShardOpts& o, int type, int out_type, int N, int iters, in
 }  // namespace
 
 int main(int argc, char** argv) {
-  int type = 2, N = 1, iters = 20, layers = 32, out_type = 14;
+  int type = 2, N = 1, iters = 20, layers = 32, out_type = 14, ctx = 0;
   bool graph = true, stationary = false, batch_proj = false, concurrent = false;
   ShardOpts so;
   int shard = 0;
@@ -563,10 +604,11 @@ int main(int argc, char** argv) {
     else if (a == "--device") so.devices = {atoi(next())};
     else if (a == "--dump") so.dump = next();
     else if (a == "--dump-q") so.dump_q = next();
+    else if (a == "--ctx") ctx = atoi(next());
     else {
       fprintf(stderr, "usage: %s [-d q4_0] [-n tokens] [-i replays] [-l layers] [--no-graph] [-s] [--output-type q6_k] "
                       "[--unfused] [--batch-proj] [--concurrent] [--shard G [--devices 0,1,..]] "
-                      "[--rank r --world w --comm-id HEX|auto [--device d]] [--dump FILE]\n",
+                      "[--rank r --world w --comm-id HEX|auto [--device d]] [--dump FILE] [--ctx P]\n",
               argv[0]);
       return 1;
     }
@@ -593,7 +635,15 @@ int main(int argc, char** argv) {
       fprintf(stderr, "llama-matmul-bench: the sharded form is graph-captured, without --concurrent\n");
       return 1;
     }
+    if (ctx > 0) {
+      fprintf(stderr, "llama-matmul-bench: --ctx runs in the single-GPU form\n");
+      return 1;
+    }
     return run_sharded(so, type, out_type, N, iters, layers, stationary, batch_proj);
+  }
+  if (ctx > 0 && (N != 1 || ctx % 8 || concurrent)) {
+    fprintf(stderr, "llama-matmul-bench: --ctx P needs -n 1, P a multiple of 8, no --concurrent\n");
+    return 1;
   }
   constexpr int H = 4096, F = 11008, V = 32000;
   hipStream_t s;
@@ -647,7 +697,34 @@ int main(int argc, char** argv) {
     hip_ok(hipMemcpy(m.d, h.data(), h.size() * 4, hipMemcpyHostToDevice), "upload x");
   }
   mk_act(m.a4096, H, m.d);    // layer input = previous layer's ffn_down output
-  mk_act(m.b4096, H, m.q);
+  m.ctx = ctx;
+  size_t kv_bytes = 0;
+  if (ctx > 0) {   // the F16 KV cache (random contents), q / scores / probs / kqv buffers
+    const size_t cell = (size_t)H * 2;   // one token's K row (or V column) over all heads, bytes
+    float* r = nullptr;
+    hip_ok(hipMalloc(&r, (size_t)ctx * H * 4), "hipMalloc");
+    {
+      std::vector<float> h((size_t)ctx * H);
+      for (size_t i = 0; i < h.size(); ++i) h[i] = std::sin(0.011f * (float)i) * 0.5f;
+      hip_ok(hipMemcpy(r, h.data(), h.size() * 4, hipMemcpyHostToDevice), "upload kv");
+    }
+    for (int l = 0; l < layers; ++l)
+      for (auto* v : {&m.kc, &m.vt}) {
+        void* p = nullptr;
+        hip_ok(hipMalloc(&p, cell * ctx + 256), "hipMalloc(kv)");
+        lamm_ok(lamm_hip_quantize(1, 0, r, H, p, H, H, ctx, s), "kv init");
+        v->push_back(p);
+      }
+    hip_ok(hipStreamSynchronize(s), "kv init");
+    hip_ok(hipFree(r), "hipFree");
+    kv_bytes = 2 * cell * ctx * layers;
+    hip_ok(hipMalloc(&m.qh, (size_t)H * 2 + 256), "hipMalloc");
+    hip_ok(hipMalloc(&m.vrow, (size_t)H * 2 + 256), "hipMalloc");
+    hip_ok(hipMalloc(&m.scores, (size_t)32 * ctx * 4 + 256), "hipMalloc");
+    hip_ok(hipMalloc(&m.probs, (size_t)32 * ctx * 2 + 256), "hipMalloc");
+    mk_out(m.kqv, H);
+  }
+  mk_act(m.b4096, H, ctx > 0 ? m.kqv : m.q);
   mk_act(m.c4096, H, m.o);
   mk_act(m.a11008, F, batch_proj ? m.g + (size_t)N * F : m.u);   // the up projection's output
 
@@ -691,15 +768,16 @@ int main(int argc, char** argv) {
     fprintf(stderr, "llama-matmul-bench: non-finite logits\n");
     return 1;
   }
-  const int launches = (batch_proj ? 4 : 7) * layers + 1;
+  const int launches = (batch_proj ? 4 : 7) * layers + 1 + (ctx > 0 ? 7 * layers : 0);
   printf("step %.3f ms  |  %.1f tok/s  |  weight stream %.1f GB/s  |  %.1f TFLOP/s  |  %d matmul launches + %d quantizations per step  |  logits |sum| %.4g\n",
          t * 1e3, N / t, wbytes / t / 1e9, 2.0 * params * N / t / 1e12, launches,
          fused(type, N) ? 1 : 4 * layers + 1, cs);
   printf("{\"tool\": \"llama-matmul-bench\", \"layers\": %d, \"tokens_per_step\": %d, \"ms_per_step\": %.4f, \"tok_per_s\": %.2f, "
          "\"weight_GBps\": %.1f, \"TFLOPs\": %.2f, \"graph\": %s, \"stationary\": %s, \"type\": \"%s\", "
-         "\"mode\": \"%s\", \"launches\": %d}\n",
+         "\"mode\": \"%s\", \"launches\": %d, \"ctx\": %d, \"kv_cache_GB\": %.3f, \"bytes_GBps\": %.1f}\n",
          layers, N, t * 1e3, N / t, wbytes / t / 1e9, 2.0 * params * N / t / 1e12, graph ? "true" : "false",
          stationary ? "true" : "false", type_name(type),
-         batch_proj ? "batch-proj" : concurrent ? "concurrent" : "separate", launches);
+         batch_proj ? "batch-proj" : concurrent ? "concurrent" : "separate", launches, ctx, kv_bytes / 1e9,
+         (wbytes + kv_bytes) / t / 1e9);
   return 0;
 }

@@ -74,6 +74,32 @@ int main() {
     CK(hipHostFree(pin));
     CK(hipFree(d));
   }
+  // 2D copies from / to pageable memory, as the boundary issues them: 512 rows x 16 KiB with the
+  // pitch equal to the width (a dense F32 activation / C block), and 4096 rows x 1 KiB at a
+  // 1280-byte pitch (b2430's transposed V-cache view at n_kv = 512, n_ctx = 640); "lin" = the
+  // same bytes as one linear copy of the whole span
+  struct R2 { const char* name; size_t rows, width, pitch; };
+  const R2 shapes[] = {{"dense_512x16K", 512, 16384, 16384}, {"vview_4096x1K_p1280", 4096, 1024, 1280}};
+  for (const R2& r : shapes) {
+    const size_t span = r.rows * r.pitch;
+    void* d;
+    CK(hipMalloc(&d, span));
+    std::vector<unsigned char> page(span + 4096, 1);
+    unsigned char* h = page.data();
+    printf(", \"h2d_2d_%s\": %.1f", r.name, med([&] {
+             CK(hipMemcpy2DAsync(d, r.pitch, h, r.pitch, r.width, r.rows, hipMemcpyHostToDevice, s));
+             CK(hipStreamSynchronize(s));
+           }));
+    printf(", \"d2h_2d_%s\": %.1f", r.name, med([&] {
+             CK(hipMemcpy2DAsync(h, r.pitch, d, r.pitch, r.width, r.rows, hipMemcpyDeviceToHost, s));
+             CK(hipStreamSynchronize(s));
+           }));
+    printf(", \"h2d_lin_%s\": %.1f", r.name, med([&] {
+             CK(hipMemcpyAsync(d, h, span, hipMemcpyHostToDevice, s));
+             CK(hipStreamSynchronize(s));
+           }));
+    CK(hipFree(d));
+  }
   printf("}\n");
   return 0;
 }

@@ -512,13 +512,16 @@ def llama_e2e(devices, n_prompt=512, n_gen=128, threads=16, exe=None, extra_env=
 def llama_step(fmt):
     """The model's weight matmuls through the device API, hipGraph-replayed (llama-matmul-bench)."""
     exe = os.path.join(ROOT, "la-llama.cpp_amd", "llama-matmul-bench")
-    res = {"note": "weight matmuls only (no attention/norms), synthetic weights, hipGraph replay: the ceiling "
-                   "without the ggml boundary's host round trips"}
+    res = {"note": "weight matmuls (and with ctx512 the attention matmuls; no softmax / norms / RoPE), "
+                   "synthetic weights, hipGraph replay: the ceiling without the ggml boundary's host round trips"}
     # decode_n1: llama.cpp's 7 projection tensors per layer, one launch each; decode_n1_batch_proj:
     # q|k|v and gate|up stored as one tensor each (4 launches per layer, a GPU-native layout)
     for name, argv in (("decode_n1", ["-n", "1", "-i", "50"]),
                        ("decode_n1_batch_proj", ["-n", "1", "-i", "50", "--batch-proj"]),
-                       ("prefill_n512", ["-n", "512", "-i", "5", "-s"])):
+                       ("prefill_n512", ["-n", "512", "-i", "5", "-s"]),
+                       # every mul_mat of a decode step incl. KQ / KQV over a device-resident F16 KV
+                       # cache of 512 cells per layer (the fully-GPU decode step, SURVEY §8f row 4)
+                       ("decode_n1_batch_proj_ctx512", ["-n", "1", "-i", "50", "--batch-proj", "--ctx", "512"])):
         try:
             r = subprocess.run([exe, "-d", fmt] + argv, capture_output=True, text=True, timeout=180)
             line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -685,7 +688,10 @@ def main():
                            "weights device-resident after a warm-up pass; reference published (3A6000, 4 threads, "
                            "README.md:684,710): prompt 8.27 tok/s, text-gen 4.69 tok/s",
                    "devices": devs or [ctx.device],
-                   "t16": llama_e2e(devs, threads=min(16, host_cores()[0]))}
+                   "t16": llama_e2e(devs, threads=min(16, host_cores()[0])),
+                   # the GPU build leaves ggml fewer CPU ops: 8 pool threads spin less against the
+                   # boundary's thread (short-context decode 69 -> 97 tok/s, profiles/r03/boundary/)
+                   "t8": llama_e2e(devs, threads=min(8, host_cores()[0]))}
             if world == 1:
                 extras["llama7b_matmul_step"] = llama_step(fmt)
             extras["llama7b_e2e"] = e2e

@@ -595,7 +595,7 @@ def main():
                          "algorithmic_bytes_per_launch") == g["slab_bytes"] else None,
                      "traffic_source": f"profiles/traffic_{fmt}_gemv_single.json (rocprofv3 --pmc FETCH_SIZE x2 + "
                                        "WRITE_SIZE, per launch)",
-                     "kernel": "lamm::gemv_rpw_kernel (csrc/lamm_gemv_rpw.hip)",
+                     "kernel": "lamm::gemv_flat1_kernel (csrc/lamm_gemv_rpw.hip; gemv_rpw_kernel for other shapes)",
                      "per_launch_us": round(g["kern"] * 1e6, 3),
                      "algorithmic_bytes_per_launch": g["slab_bytes"]},
     }

@@ -43,7 +43,8 @@
 // K row / V column appended to a device-resident F16 KV cache of P cells, KQ and KQV over all P
 // cells as batched F16 GEMVs (32 heads per launch), the F32 -> F16 conversions of their src1
 // (ggml's INIT) on the GPU: every mul_mat of a llama.cpp decode step, with nothing crossing
-// PCIe.  Softmax / RoPE / norms are llama.cpp ops outside the hook and stay out.
+// PCIe.  Softmax / RoPE / norms are llama.cpp ops outside the hook and stay out.  --check
+// recomputes the last layer's attention on the host from the device buffers after the replays.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -222,6 +223,68 @@ void attention(Model& m, int l, hipStream_t s) {
   const lamm_matrix A2{m.vt[l], F16, D, P, P}, B2{m.probs, F16, P, 1, P}, C2{m.kqv, 0, D, 1, D};
   const lamm_batch bt2{NH, 1, NH, 1, (size_t)D * P * 2, 0, (size_t)P * 2, 0, (size_t)D * 4, 0};
   lamm_ok(lamm_hip_matmul_batched(&A2, &B2, &C2, &bt2, s), "KQV");
+}
+
+// --check: the last layer's attention of the last replay recomputed on the host from the device
+// buffers it used -- the appended K row / V column equal this token's k / v in F16, every score is
+// K . q and every kqv value V^T . p (F16 products summed in double), within 1e-3 of sum |a b|
+bool check_attention(const Model& m, int l) {
+  constexpr int NH = 32, D = 128, H = NH * D;
+  const int P = m.ctx;
+  auto down = [](const void* src, size_t bytes) {
+    std::vector<unsigned char> v(bytes);
+    hip_ok(hipMemcpy(v.data(), src, bytes, hipMemcpyDeviceToHost), "download (check)");
+    return v;
+  };
+  auto h2f = [](const unsigned char* p) {
+    _Float16 h;
+    memcpy(&h, p, 2);
+    return (double)h;
+  };
+  const bool tall = m.wq[l].slices == 3;
+  const auto kc = down(m.kc[l], (size_t)H * P * 2), vt = down(m.vt[l], (size_t)H * P * 2);
+  const auto qh = down(m.qh, (size_t)H * 2), pr = down(m.probs, (size_t)NH * P * 2);
+  const auto sc = down(m.scores, (size_t)NH * P * 4), kqv = down(m.kqv, (size_t)H * 4);
+  const auto kv = down(tall ? m.q + H : m.k, (size_t)H * 4), vv = down(tall ? m.q + 2 * H : m.v, (size_t)H * 4);
+  const auto qf = down(m.q, (size_t)H * 4);
+  auto f32 = [](const std::vector<unsigned char>& v, size_t i) {
+    float f;
+    memcpy(&f, &v[4 * i], 4);
+    return f;
+  };
+  double worst = 0;
+  int bad_cells = 0;
+  for (int h = 0; h < NH; ++h) {
+    for (int d = 0; d < D; ++d) {   // the appended cell and q, as F16 of this token's values
+      const size_t i = (size_t)h * D + d;
+      bad_cells += h2f(&kc[(((size_t)h * P + P - 1) * D + d) * 2]) != (double)(_Float16)f32(kv, i);
+      bad_cells += h2f(&vt[(((size_t)h * D + d) * P + P - 1) * 2]) != (double)(_Float16)f32(vv, i);
+      bad_cells += h2f(&qh[i * 2]) != (double)(_Float16)f32(qf, i);
+    }
+    for (int p = 0; p < P; ++p) {   // KQ
+      double s = 0, a = 0;
+      for (int d = 0; d < D; ++d) {
+        const double x = h2f(&kc[(((size_t)h * P + p) * D + d) * 2]) * h2f(&qh[((size_t)h * D + d) * 2]);
+        s += x;
+        a += std::fabs(x);
+      }
+      worst = std::max(worst, std::fabs(f32(sc, (size_t)h * P + p) - s) / (a + 1e-30));
+      bad_cells += h2f(&pr[((size_t)h * P + p) * 2]) != (double)(_Float16)f32(sc, (size_t)h * P + p);
+    }
+    for (int d = 0; d < D; ++d) {   // KQV
+      double s = 0, a = 0;
+      for (int p = 0; p < P; ++p) {
+        const double x = h2f(&vt[(((size_t)h * D + d) * P + p) * 2]) * h2f(&pr[((size_t)h * P + p) * 2]);
+        s += x;
+        a += std::fabs(x);
+      }
+      worst = std::max(worst, std::fabs(f32(kqv, (size_t)h * D + d) - s) / (a + 1e-30));
+    }
+  }
+  const bool ok = bad_cells == 0 && worst < 1e-3;
+  printf("attention check (layer %d, %d cells): %s, max rel err %.3e, F16 conversions off %d\n", l, P,
+         ok ? "ok" : "FAILED", worst, bad_cells);
+  return ok;
 }
 
 // one token step: the mul_mat nodes of build_llama in graph order
@@ -569,7 +632,7 @@ int run_sharded(const ShardOpts& o, int type, int out_type, int N, int iters, in
 
 int main(int argc, char** argv) {
   int type = 2, N = 1, iters = 20, layers = 32, out_type = 14, ctx = 0;
-  bool graph = true, stationary = false, batch_proj = false, concurrent = false;
+  bool graph = true, stationary = false, batch_proj = false, concurrent = false, check = false;
   ShardOpts so;
   int shard = 0;
   for (int i = 1; i < argc; ++i) {
@@ -605,10 +668,11 @@ int main(int argc, char** argv) {
     else if (a == "--dump") so.dump = next();
     else if (a == "--dump-q") so.dump_q = next();
     else if (a == "--ctx") ctx = atoi(next());
+    else if (a == "--check") check = true;
     else {
       fprintf(stderr, "usage: %s [-d q4_0] [-n tokens] [-i replays] [-l layers] [--no-graph] [-s] [--output-type q6_k] "
                       "[--unfused] [--batch-proj] [--concurrent] [--shard G [--devices 0,1,..]] "
-                      "[--rank r --world w --comm-id HEX|auto [--device d]] [--dump FILE] [--ctx P]\n",
+                      "[--rank r --world w --comm-id HEX|auto [--device d]] [--dump FILE] [--ctx P [--check]]\n",
               argv[0]);
       return 1;
     }
@@ -768,6 +832,7 @@ int main(int argc, char** argv) {
     fprintf(stderr, "llama-matmul-bench: non-finite logits\n");
     return 1;
   }
+  if (ctx > 0 && check && !check_attention(m, layers - 1)) return 1;
   const int launches = (batch_proj ? 4 : 7) * layers + 1 + (ctx > 0 ? 7 * layers : 0);
   printf("step %.3f ms  |  %.1f tok/s  |  weight stream %.1f GB/s  |  %.1f TFLOP/s  |  %d matmul launches + %d quantizations per step  |  logits |sum| %.4g\n",
          t * 1e3, N / t, wbytes / t / 1e9, 2.0 * params * N / t / 1e12, launches,

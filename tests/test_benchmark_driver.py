@@ -142,3 +142,17 @@ def test_llama_bench_sharded_prefill(tmp_path):
     _, l2 = _llama_logits(tmp_path, "p2", ["--shard", "2", "-n", "16"])
     assert np.isfinite(l2).all()
     assert np.abs(l2 - l1).max() <= 0.2 * np.abs(l1).max()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("args", [["--batch-proj", "--ctx", "64"], ["--ctx", "200"]], ids=["batch-proj-ctx64", "ctx200"])
+def test_llama_bench_decode_attention(args):
+    """The fully-GPU decode step (SURVEY §8f row 4 through the device API): per layer this token's
+    K row and V column appended to a device-resident F16 KV cache, KQ and KQV as batched F16 GEMVs
+    over every cell.  --check recomputes the last layer's attention on the host from the device
+    buffers: the appended cells and the F16 conversions bit for bit, every score and kqv value
+    within 1e-3 of sum |a b| (the north-star tolerance)."""
+    r = subprocess.run([LLAMA, "-l", "2", "-i", "3", "-n", "1", "--check", *args], capture_output=True, text=True,
+                       timeout=180)
+    assert r.returncode == 0, r.stdout[-1500:] + r.stderr[-1500:]
+    assert "attention check" in r.stdout and ": ok," in r.stdout, r.stdout[-800:]

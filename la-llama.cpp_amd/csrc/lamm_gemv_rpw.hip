@@ -199,25 +199,26 @@ __global__ __launch_bounds__(64 * WAVES) void gemv_rpw_kernel(GemvArgs p) {
   if (p.flag) signal_done(p);
 }
 
-// Single-column decode with K a multiple of 2048 (nb = 64 ITER blocks; config 2, every
-// Llama-7B projection but ffn_down): the workgroup's WAVES rows as ONE flat list of
-// WAVES * nb blocks, wave w's instruction k taking blocks (k WAVES + w) 64 + lane -- so the
-// workgroup's first loads cover contiguous bytes (the fastest read order on this chip:
-// profiles/r03/gemv_probe_4.json rw8x8 2.75 us vs 3.41 row by row) -- each 64-block run lies in
-// one row; a wave reduces each run (fixed DPP order), the runs of a row are summed in LDS in
-// run order (deterministic), one store per row.  Rows past M load zeros and store nothing.
-// SL: more than one slice (the slice offsets; a one-slice launch reads no gridDim.y, does no
-// divisions).  Rows past M: their offsets lie past the A resource's range and read zeros.
-// The body, on plain values: the slice offsets (SL) and the completion signal (gemv_flat_kernel's
-// SIG) stay outside it, so a one-slice launch without a signal reads nothing but its five scalar
+// Single-column decode, 64 (ITER - 1) < nblk <= 64 ITER blocks per row (ITER = 2, K = 4096: config
+// 2 and every Llama-7B projection but ffn_down -- a 6-run instance for ffn_down's K = 11008 measured
+// no faster than gemv_rpw_kernel in the decode step, profiles/r03/decode_step/): the workgroup's WAVES
+// rows as ONE flat list of WAVES * ITER runs of 64 blocks, wave w's load k taking run
+// m = k WAVES + w (row m / ITER, blocks (m % ITER) 64 + lane) -- so the workgroup's first loads
+// cover contiguous bytes (the fastest read order on this chip: profiles/r03/gemv_probe_4.json
+// rw8x8 2.75 us vs 3.41 row by row) -- each run lies in one row; a wave reduces each run (fixed
+// DPP order), the runs of a row are summed in LDS in run order (deterministic), one store per
+// row.  Blocks past nblk (the last run of a ragged row) and rows past M load zeros and store
+// nothing.
+// The body takes plain values: the slice offsets (SL) and the completion signal (gemv_flat_kernel's
+// SIG) stay outside it, so a one-slice launch without a signal reads nothing but its scalar
 // arguments (gemv_flat1_kernel: preloaded into SGPRs, no kernarg load before the first A load and
 // none after the last one).
 template <int T, int WAVES, bool BF32, int ITER>
 __device__ __forceinline__ void flat_body(const unsigned char* Az, uint32_t lda, const unsigned char* Bz, float* Cz,
-                                          int M) {
+                                          int M, int nblk) {
   using F = RFmt<T>;
   constexpr int NWA = (F::BPB + 3) / 4 + 1;
-  constexpr int NB = 64 * ITER;
+  constexpr int NB = 64 * ITER, NT = 64 * WAVES;
   __shared__ u32x4 sq0[NB], sq1[NB];
   __shared__ float sbd[NB], sbs[NB];
   __shared__ float part[WAVES * ITER];
@@ -226,29 +227,31 @@ __device__ __forceinline__ void flat_body(const unsigned char* Az, uint32_t lda,
   const int row0 = blockIdx.x * WAVES;
   const int nrows = M - row0 < WAVES ? M - row0 : WAVES;
   // A resource over this workgroup's rows, ending at its last row's last block byte
-  const auto ra = make_rsrc(Az + (int64_t)row0 * lda, (uint32_t)(nrows - 1) * lda + ((NB * F::BPB + 3) & ~3));
+  const auto ra = make_rsrc(Az + (int64_t)row0 * lda, (uint32_t)(nrows - 1) * lda + ((nblk * F::BPB + 3) & ~3));
   uint32_t wa[ITER][NWA];
   auto issue = [&]() {
 #pragma unroll
     for (int k = 0; k < ITER; ++k) {
       const int m = k * WAVES + w, r = m / ITER, bi = (m % ITER) * 64 + lane;   // wave-uniform run m
-      load_words<NWA, 2>(ra, (uint32_t)r * lda + ((uint32_t)(bi * F::BPB) & ~3u), wa[k]);
+      const uint32_t off = bi < nblk ? (uint32_t)r * lda + ((uint32_t)(bi * F::BPB) & ~3u) : 0x7ffffff0u;
+      load_words<NWA, 2>(ra, off, wa[k]);
     }
   };
-  const auto rb = make_rsrc(Bz, BF32 ? (uint32_t)(NB * 32 * 4) : (uint32_t)(NB * F::VBPB + 3) & ~3u);
-  GemvArgs p{};   // what the staging reads of it: one column of nb blocks at B
+  const auto rb = make_rsrc(Bz, BF32 ? (uint32_t)nblk * 128 : (uint32_t)(nblk * F::VBPB + 3) & ~3u);
+  GemvArgs p{};   // what the staging reads of it: one column of nblk blocks at B
   p.N = 1;
-  p.nblk = NB;
-  if constexpr (BF32) {   // F32 rows: four lanes per block, one pass (4 NB <= 64 WAVES)
-    static_assert(4 * NB <= 64 * WAVES, "one staging pass");
-    ActStageL<T, 4> sl;
+  p.nblk = nblk;
+  if constexpr (BF32) {   // F32 rows: four (or two) lanes per block, one pass
+    constexpr int LB = 4 * NB <= NT ? 4 : 2;
+    static_assert(LB * NB <= NT, "one staging pass");
+    ActStageL<T, LB> sl;
     sl.template load<1>(p, rb, t0);
     __builtin_amdgcn_sched_barrier(0);
     issue();
     __builtin_amdgcn_sched_barrier(0);
-    if (t0 < 4 * NB) sl.store(t0, sq0, sq1, sbd, sbs);
+    if (t0 < LB * NB) sl.store(t0, sq0, sq1, sbd, sbs);
   } else {
-    static_assert(NB <= 64 * WAVES, "one staging pass");
+    static_assert(NB <= NT, "one staging pass");
     ActStage<T, false> st;
     st.template load<1>(p, rb, t0);        // straight-line; out-of-range loads read zeros
     __builtin_amdgcn_sched_barrier(0);
@@ -264,7 +267,7 @@ __device__ __forceinline__ void flat_body(const unsigned char* Az, uint32_t lda,
     realign(wa[k], mm, (int)((uint32_t)(bi * F::BPB) & 3u));
     uint32_t q[8];
     float da, ma;
-    unpack_a<T>(mm, q, da, ma);
+    unpack_a<T>(mm, q, da, ma);   // blocks past nblk: all-zero bytes -> d = 0, no contribution
     const u32x4 b0 = sq0[bi], b1 = sq1[bi];
     const float db = sbd[bi], bsv = sbs[bi];
     int sdot = 0;
@@ -302,15 +305,99 @@ __global__ __launch_bounds__(64 * WAVES) void gemv_flat_kernel(GemvArgs p) {
     Bz += (int64_t)i12 * p.sb2 + (int64_t)i13 * p.sb3;
     Cz += (int64_t)i12 * p.sc2 + (int64_t)i13 * p.sc3;
   }
-  flat_body<T, WAVES, BF32, ITER>(Az, (uint32_t)p.lda, Bz, Cz, p.M);   // lda < 2^16 here: nb = 64 ITER
+  flat_body<T, WAVES, BF32, ITER>(Az, (uint32_t)p.lda, Bz, Cz, p.M, p.nblk);   // lda < 2^16: nb <= 64 ITER
   if constexpr (SIG) signal_done(p);
 }
 
-// One slice, no signal (BASELINE config 2 as bench.py and the device API launch it)
+// One slice, no signal, K = 4096 (BASELINE config 2 as bench.py and the device API launch it)
 template <int T, bool BF32>
 __global__ __launch_bounds__(512) void gemv_flat1_kernel(const unsigned char* A, const unsigned char* B, float* C,
                                                          uint32_t lda, int M) {
-  flat_body<T, 8, BF32, 2>(A, lda, B, C, M);
+  flat_body<T, 8, BF32, 2>(A, lda, B, C, M, 128);
+}
+
+// q2_K x q8_K, one column, K <= 12288 (the reference's Q2_K kernel, src/lamm_kernel_q2_k.hpp,
+// whose block dot is LC/ggml-quants.c ggml_vec_dot_q2_K_q8_K): one wave per row, lane l on
+// super-block 16 c + l / 4 (c < ITER) and its quarter qq = l % 4 = sub-blocks 4 qq .. 4 qq + 3 --
+// 32 bytes of qs read at two shifts, its 4 scale bytes, the super-block's d / dmin; the activation
+// row staged once per workgroup in LDS (q8_K: d, 256 quants, 16 bsums; 80 dwords per super-block
+// so a quarter's 64 quants are four aligned ds_read_b128).  A super-block's four quarters meet in
+// their quad by DPP on the integer sums (exact), then d_b d_a isum - d_b dmin summs once per
+// super-block as in the reference; the wave's super-blocks reduce in a fixed DPP order.
+template <int ITER>
+__global__ __launch_bounds__(512) void gemv_q2k_kernel(const unsigned char* A, int64_t lda, const unsigned char* B,
+                                                       float* C, int M, int nsb) {
+  constexpr int WAVES = 8, NSB = 16 * ITER, SBW = 80, SDW = NSB * 73, PASS = (SDW + 64 * WAVES - 1) / (64 * WAVES);
+  __shared__ __attribute__((aligned(16))) uint32_t act[NSB * SBW];
+  const int lane = threadIdx.x & 63, t0 = threadIdx.x, qq = lane & 3;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int row = blockIdx.x * WAVES + w;
+  const auto rb = make_rsrc(B, (uint32_t)nsb * 292);
+  uint32_t sv[PASS];
+#pragma unroll
+  for (int k = 0; k < PASS; ++k) {
+    const int idx = t0 + 64 * WAVES * k;
+    sv[k] = bload4(rb, idx < SDW ? (uint32_t)idx * 4 : 0x7ffffff0u);   // past the row: zeros
+  }
+  __builtin_amdgcn_sched_barrier(0);   // the activation loads first in the vmcnt order
+  const auto ra = make_rsrc(A + (int64_t)(row < M ? row : 0) * lda, (uint32_t)nsb * 84);
+  u32x4 qa[ITER][2];
+  uint32_t sc[ITER], dd[ITER];
+#pragma unroll
+  for (int c = 0; c < ITER; ++c) {
+    const int sb = 16 * c + (lane >> 2);
+    const uint32_t base = sb < nsb ? (uint32_t)sb * 84 : 0x7fff0000u;
+    const uint32_t qo = base + 16 + 32 * (qq >> 1);
+    qa[c][0] = __builtin_amdgcn_raw_buffer_load_b128(ra, qo, 0, 2);
+    qa[c][1] = __builtin_amdgcn_raw_buffer_load_b128(ra, qo + 16, 0, 2);
+    sc[c] = __builtin_amdgcn_raw_buffer_load_b32(ra, base + 4 * qq, 0, 2);
+    dd[c] = __builtin_amdgcn_raw_buffer_load_b32(ra, base + 80, 0, 2);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int k = 0; k < PASS; ++k) {   // dword k of a 73-dword super-block: d -> 0, quants / bsums -> 3 + k
+    const int idx = t0 + 64 * WAVES * k;
+    if (idx < SDW) {
+      const int sb = idx / 73, kk = idx % 73;
+      act[sb * SBW + (kk ? 3 + kk : 0)] = sv[k];
+    }
+  }
+  __syncthreads();
+  float acc = 0.f;
+#pragma unroll
+  for (int c = 0; c < ITER; ++c) {
+    const int sb = 16 * c + (lane >> 2);
+    const uint32_t* a = &act[sb * SBW];
+    u32x4 b[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) b[i] = *reinterpret_cast<const u32x4*>(a + 4 + 16 * qq + 4 * i);
+    const uint2 bsw = *reinterpret_cast<const uint2*>(a + 68 + 2 * qq);   // bsums 4qq .. 4qq + 3 (int16)
+    const float yd = __builtin_bit_cast(float, a[0]);
+    int isum = 0, summs = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {   // sub-block s = 4 qq + i: half i & 1 of the qs run, shift 2 jj
+      const int sh = 2 * (2 * (qq & 1) + (i >> 1));
+      const int scv = (int)((sc[c] >> (8 * i)) & 0xffu);
+      int part = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) part = dot4((qa[c][i & 1][k] >> sh) & 0x03030303u, b[i][k], part);
+      const uint32_t bw = i < 2 ? bsw.x : bsw.y;
+      const int bsum = (int)(int16_t)((bw >> (16 * (i & 1))) & 0xffffu);
+      isum += (scv & 0xf) * part;
+      summs += bsum * (scv >> 4);
+    }
+    // the quad's four quarters of one super-block (integer: exact)
+    isum += __builtin_amdgcn_update_dpp(0, isum, 0xB1, 0xF, 0xF, false);
+    isum += __builtin_amdgcn_update_dpp(0, isum, 0x4E, 0xF, 0xF, false);
+    summs += __builtin_amdgcn_update_dpp(0, summs, 0xB1, 0xF, 0xF, false);
+    summs += __builtin_amdgcn_update_dpp(0, summs, 0x4E, 0xF, 0xF, false);
+    if (qq == 0 && sb < nsb) {
+      const float da = h2f(dd[c] & 0xffffu), dm = h2f(dd[c] >> 16);
+      acc += (yd * da) * (float)isum - (yd * dm) * (float)summs;
+    }
+  }
+  acc = wave_sum(acc);
+  if (lane == 0 && row < M) C[row] = acc;
 }
 
 template <int T, int NC, int WAVES, bool BF32, int ITER>
@@ -379,6 +466,18 @@ hipError_t launch_rpw_t(const GemvArgs& p, hipStream_t s, int waves) {
 }
 
 }  // namespace
+
+bool gemv_q2k_supported(const GemvArgs& p) {
+  return p.N == 1 && p.ne12 * p.ne13 == 1 && p.nblk <= 48 && p.flag == nullptr && p.b_f32 == 0;
+}
+
+hipError_t launch_gemv_q2k(const GemvArgs& p, hipStream_t s) {
+  const dim3 g((unsigned)((p.M + 7) / 8));
+  if (p.nblk <= 16) hipLaunchKernelGGL(gemv_q2k_kernel<1>, g, dim3(512), 0, s, p.A, p.lda, p.B, p.C, p.M, p.nblk);
+  else if (p.nblk <= 32) hipLaunchKernelGGL(gemv_q2k_kernel<2>, g, dim3(512), 0, s, p.A, p.lda, p.B, p.C, p.M, p.nblk);
+  else hipLaunchKernelGGL(gemv_q2k_kernel<3>, g, dim3(512), 0, s, p.A, p.lda, p.B, p.C, p.M, p.nblk);
+  return hipGetLastError();
+}
 
 bool gemv_rpw_supported(int type, const GemvArgs& p) {
   return p.N <= 2 && p.nblk <= 6 * 64 &&

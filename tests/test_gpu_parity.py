@@ -863,7 +863,7 @@ def test_config3_four_slice_batched_launch():
 # ---------------------------------------------------------------- row-per-wave decode GEMV
 RPW_TYPES = [ol.Q4_0, ol.Q4_1, ol.Q5_0, ol.Q5_1, ol.Q8_0]
 RPW_SHAPES = [(1, 1, 32), (5, 1, 96), (67, 2, 512), (130, 1, 4096), (33, 2, 4096 + 256), (9, 1, 11008),
-              (257, 1, 8192 + 32)]
+              (257, 1, 8192 + 32), (133, 1, 10272), (70, 1, 12288), (4096, 1, 11008)]
 
 
 @pytest.mark.parametrize("rows", ["4", "8", "16"])
@@ -871,8 +871,9 @@ RPW_SHAPES = [(1, 1, 32), (5, 1, 96), (67, 2, 512), (130, 1, 4096), (33, 2, 4096
 @pytest.mark.parametrize("shape", RPW_SHAPES, ids=[f"{m}x{n}x{k}" for m, n, k in RPW_SHAPES])
 def test_gemv_row_per_wave(t, shape, rows, monkeypatch):
     """lamm_gemv_rpw.hip (LAMM_GEMV_RPW = waves per workgroup, 8 at most past K = 4096): ragged
-    M / K, one and two columns,
-    q8 activations and F32 activations (INIT fused, must equal quantize + matmul)."""
+    M / K, one and two columns, q8 activations and F32 activations (INIT fused, must equal
+    quantize + matmul).  One column, K = 4096 and 8 waves: the flat kernel (2 runs of 64 blocks per
+    row)."""
     monkeypatch.setenv("LAMM_GEMV_RPW", rows)
     M, N, K = shape
     A_q, B_q = random_case(t, M, N, K, seed=M * 7 + K + int(rows))
@@ -980,3 +981,22 @@ def test_config1_f32_512_cube():
     ref = ORACLE.mul_mat(ol.F32, M, N, K, a.view(np.uint8), b.view(np.uint8))
     absd = np.abs(b.astype(np.float64)) @ np.abs(a.astype(np.float64)).T
     assert rel_err(c, ref, absd).max() < TOL
+
+
+# ---------------------------------------------------------------- q2_K single-column decode
+Q2K_SHAPES = [(1, 256), (9, 4096), (133, 4352), (64, 8192), (37, 11008), (4096, 4096), (70, 12288)]
+
+
+@pytest.mark.parametrize("shape", Q2K_SHAPES, ids=[f"{m}x1x{k}" for m, k in Q2K_SHAPES])
+def test_gemv_q2k_row_per_wave(shape):
+    """lamm_gemv_rpw.hip's q2_K kernel (one column, up to 48 super-blocks per row): lanes on
+    quarter super-blocks, the quarters' integer sums combined in the quad (exact), one float
+    epilogue per super-block as the reference's ggml_vec_dot_q2_K_q8_K; ragged M, K from one to 48
+    super-blocks, against the oracle."""
+    M, K = shape
+    rng = np.random.default_rng(M * 31 + K)
+    A_q = ol.random_kq_blocks(ol.Q2_K, M, K, rng)
+    B_q = ORACLE.quantize(ol.Q8_K, rng.standard_normal((1, K), dtype=np.float32))
+    c, _ = gpu_mul_mat(ol.Q2_K, A_q, B_q, M, 1, K)
+    ref = ORACLE.mul_mat(ol.Q2_K, M, 1, K, A_q, B_q)
+    assert rel_err(c, ref, absdot(ol.Q2_K, A_q, B_q, M, 1, K)).max() < TOL

@@ -100,6 +100,46 @@ int main() {
            }));
     CK(hipFree(d));
   }
+  // Overlap of the two directions, as a pipelined prefill call would use them: 8 MiB up from one
+  // pageable buffer and 8 MiB down into another, one after the other on one stream ("seq"), on two
+  // streams issued back to back ("2s"), and in 4 chunks alternating between the streams ("4c")
+  {
+    const size_t n = (size_t)8 << 20, nc = n / 4;
+    void *du, *dd;
+    CK(hipMalloc(&du, n));
+    CK(hipMalloc(&dd, n));
+    std::vector<unsigned char> up(n + 4096, 1), dn(n + 4096, 2);
+    hipStream_t s2;
+    CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+    printf(", \"updown_seq\": %.1f", med([&] {
+             CK(hipMemcpyAsync(du, up.data(), n, hipMemcpyHostToDevice, s));
+             CK(hipMemcpyAsync(dn.data(), dd, n, hipMemcpyDeviceToHost, s));
+             CK(hipStreamSynchronize(s));
+           }));
+    printf(", \"updown_2s\": %.1f", med([&] {
+             CK(hipMemcpyAsync(du, up.data(), n, hipMemcpyHostToDevice, s));
+             CK(hipMemcpyAsync(dn.data(), dd, n, hipMemcpyDeviceToHost, s2));
+             CK(hipStreamSynchronize(s));
+             CK(hipStreamSynchronize(s2));
+           }));
+    printf(", \"updown_4c\": %.1f", med([&] {
+             for (int c = 0; c < 4; ++c) {
+               CK(hipMemcpyAsync((char*)du + c * nc, up.data() + c * nc, nc, hipMemcpyHostToDevice, s));
+               CK(hipMemcpyAsync(dn.data() + c * nc, (char*)dd + c * nc, nc, hipMemcpyDeviceToHost, s2));
+             }
+             CK(hipStreamSynchronize(s));
+             CK(hipStreamSynchronize(s2));
+           }));
+    // the host-side cost of issuing the 8 MiB pageable upload alone (does the call return before
+    // the bytes have moved?)
+    printf(", \"h2d_issue_only\": %.1f", med([&] {
+             CK(hipMemcpyAsync(du, up.data(), n, hipMemcpyHostToDevice, s));
+           }));
+    CK(hipStreamSynchronize(s));
+    CK(hipStreamDestroy(s2));
+    CK(hipFree(du));
+    CK(hipFree(dd));
+  }
   printf("}\n");
   return 0;
 }

@@ -136,6 +136,52 @@ int main() {
              CK(hipMemcpyAsync(du, up.data(), n, hipMemcpyHostToDevice, s));
            }));
     CK(hipStreamSynchronize(s));
+    // the same with both host buffers registered: for the whole run ("reg"), or around each call
+    // ("regpc": register, move, unregister -- what a boundary call could do with ggml's buffers)
+    CK(hipHostRegister(up.data(), n, hipHostRegisterDefault));
+    CK(hipHostRegister(dn.data(), n, hipHostRegisterDefault));
+    printf(", \"updown_reg_seq\": %.1f", med([&] {
+             CK(hipMemcpyAsync(du, up.data(), n, hipMemcpyHostToDevice, s));
+             CK(hipMemcpyAsync(dn.data(), dd, n, hipMemcpyDeviceToHost, s));
+             CK(hipStreamSynchronize(s));
+           }));
+    printf(", \"updown_reg_2s\": %.1f", med([&] {
+             CK(hipMemcpyAsync(du, up.data(), n, hipMemcpyHostToDevice, s));
+             CK(hipMemcpyAsync(dn.data(), dd, n, hipMemcpyDeviceToHost, s2));
+             CK(hipStreamSynchronize(s));
+             CK(hipStreamSynchronize(s2));
+           }));
+    printf(", \"updown_reg_4c\": %.1f", med([&] {
+             for (int c = 0; c < 4; ++c) {
+               CK(hipMemcpyAsync((char*)du + c * nc, up.data() + c * nc, nc, hipMemcpyHostToDevice, s));
+               CK(hipMemcpyAsync(dn.data() + c * nc, (char*)dd + c * nc, nc, hipMemcpyDeviceToHost, s2));
+             }
+             CK(hipStreamSynchronize(s));
+             CK(hipStreamSynchronize(s2));
+           }));
+    printf(", \"h2d_reg_issue_only\": %.1f", med([&] {
+             CK(hipMemcpyAsync(du, up.data(), n, hipMemcpyHostToDevice, s));
+           }));
+    CK(hipStreamSynchronize(s));
+    CK(hipHostUnregister(up.data()));
+    CK(hipHostUnregister(dn.data()));
+    printf(", \"updown_regpc_2s\": %.1f", med([&] {
+             CK(hipHostRegister(up.data(), n, hipHostRegisterDefault));
+             CK(hipHostRegister(dn.data(), n, hipHostRegisterDefault));
+             CK(hipMemcpyAsync(du, up.data(), n, hipMemcpyHostToDevice, s));
+             CK(hipMemcpyAsync(dn.data(), dd, n, hipMemcpyDeviceToHost, s2));
+             CK(hipStreamSynchronize(s));
+             CK(hipStreamSynchronize(s2));
+             CK(hipHostUnregister(up.data()));
+             CK(hipHostUnregister(dn.data()));
+           }));
+    // registering a range that overlaps a registered one (two tensors sharing a page)
+    CK(hipHostRegister(up.data(), n / 2 + 100, hipHostRegisterDefault));
+    const hipError_t eo = hipHostRegister(up.data() + n / 2, n / 2, hipHostRegisterDefault);
+    printf(", \"overlapping_register\": \"%s\"", hipGetErrorString(eo));
+    if (eo == hipSuccess) CK(hipHostUnregister(up.data() + n / 2));
+    (void)hipGetLastError();
+    CK(hipHostUnregister(up.data()));
     CK(hipStreamDestroy(s2));
     CK(hipFree(du));
     CK(hipFree(dd));

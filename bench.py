@@ -544,7 +544,7 @@ def read_traffic(tag):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=200)   # 200 x ~4 us: the graph replay's start-up amortized
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--fmt", default="q4_0")
     ap.add_argument("--M", type=int, default=4096)

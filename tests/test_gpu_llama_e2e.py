@@ -63,10 +63,13 @@ def ref_spread(model2, cpu_ref, tmp_path_factory):
     return spread
 
 
-@pytest.mark.parametrize("mode", ["default", "views_on_gpu", "cpu_init"])
+@pytest.mark.parametrize("mode", ["default", "views_on_gpu", "cpu_init", "two_devices"])
 def test_llama_logits_match_reference(model2, cpu_ref, ref_spread, mode, tmp_path):
+    """two_devices: every weight's rows split over two devices (LAMM_HIP_DEVICES, rehearsed on one
+    GPU listed twice; decode calls zero-copy on both), as bench.py runs config 5 on N GPUs."""
     env = {"default": {}, "views_on_gpu": {"LAMM_HIP_VIEWS": "1"},
-           "cpu_init": {"LAMM_HIP_GPU_QUANT": "0", "LAMM_HIP_VIEWS": "0"}}[mode]
+           "cpu_init": {"LAMM_HIP_GPU_QUANT": "0", "LAMM_HIP_VIEWS": "0"},
+           "two_devices": {"LAMM_HIP_DEVICES": "0,0"}}[mode]
     ref, lref = cpu_ref
     got, lgot = _run(HIP, model2, str(tmp_path / "l.bin"), env)
     assert got["n_layer"] == 2 and lgot.shape == lref.shape == (9, 32000)

@@ -1246,8 +1246,10 @@ int rpw_waves(const GemvArgs& p) {
 }
 
 hipError_t launch_gemv(int type, const GemvArgs& p, hipStream_t s) {
-  // q2_K single columns: the row-per-wave kernel (LAMM_GEMV_VARIANT != 0 keeps the wave-group ones)
-  if (type == kQ2_K && gemv_q2k_supported(p) && knobs().gemv_variant == 0) return launch_gemv_q2k(p, s);
+  // q2_K / q4_K / q5_K single columns: the row-per-wave kernel (LAMM_GEMV_RPW=0 or a
+  // LAMM_GEMV_VARIANT keep the wave-group ones)
+  if (gemv_kq_supported(type, p) && knobs().gemv_variant == 0 && knobs().gemv_rpw != 0)
+    return launch_gemv_kq(type, p, s);
   if (gemv_rpw_supported(type, p)) {
     const int w = rpw_waves(p);
     if (w > 0) return launch_gemv_rpw(type, p, s, w);

@@ -316,18 +316,30 @@ __global__ __launch_bounds__(512) void gemv_flat1_kernel(const unsigned char* A,
   flat_body<T, 8, BF32, 2>(A, lda, B, C, M, 128);
 }
 
-// q2_K x q8_K, one column, K <= 12288 (the reference's Q2_K kernel, src/lamm_kernel_q2_k.hpp,
-// whose block dot is LC/ggml-quants.c ggml_vec_dot_q2_K_q8_K): one wave per row, lane l on
-// super-block 16 c + l / 4 (c < ITER) and its quarter qq = l % 4 = sub-blocks 4 qq .. 4 qq + 3 --
-// 32 bytes of qs read at two shifts, its 4 scale bytes, the super-block's d / dmin; the activation
-// row staged once per workgroup in LDS (q8_K: d, 256 quants, 16 bsums; 80 dwords per super-block
-// so a quarter's 64 quants are four aligned ds_read_b128).  A super-block's four quarters meet in
-// their quad by DPP on the integer sums (exact), then d_b d_a isum - d_b dmin summs once per
-// super-block as in the reference; the wave's super-blocks reduce in a fixed DPP order.
-template <int ITER>
-__global__ __launch_bounds__(512) void gemv_q2k_kernel(const unsigned char* A, int64_t lda, const unsigned char* B,
-                                                       float* C, int M, int nsb) {
+// The k-quant formats against q8_K, one column, K <= 12288 (the reference's Q2_K kernel,
+// src/lamm_kernel_q2_k.hpp, whose block dot is LC/ggml-quants.c ggml_vec_dot_q2_K_q8_K; q4_K /
+// q5_K, SURVEY §8f: ggml_vec_dot_q4_K_q8_K / _q5_K_q8_K): one wave per row, lane l on super-block
+// 16 c + l / 4 (c < ITER) and its quarter qq = l % 4 = 64 consecutive elements; the activation row
+// staged once per workgroup in LDS (q8_K: d, 256 quants, 16 bsums; 80 dwords per super-block so a
+// quarter's 64 quants are four aligned ds_read_b128).  A super-block's four quarters meet in their
+// quad by DPP on the integer sums (exact), then the reference's
+//   d_b (d_a sum_s sc_s sum q b - dmin sum_s mn_s bsums_s)
+// runs once per super-block; the wave's super-blocks reduce in a fixed DPP order.  Per quarter:
+//   q2_K: sub-blocks 4qq..4qq+3 (16 elements each): 32 bytes of qs read at two shifts, 4 scale
+//         bytes (4-bit scale | 4-bit min), d / dmin
+//   q4_K: sub-blocks 2qq, 2qq+1 (32 elements each): 32 bytes of qs (low / high nibbles), the
+//         6-bit scales / mins of both (LC/ggml-quants.c's utmp shuffle), d / dmin
+//   q5_K: as q4_K, plus bit sb of qh[l] as the 5th bit
+template <int T> struct KQ;
+template <> struct KQ<kQ2_K> { static constexpr int BPB = 84; };
+template <> struct KQ<kQ4_K> { static constexpr int BPB = 144; };
+template <> struct KQ<kQ5_K> { static constexpr int BPB = 176; };
+
+template <int T, int ITER>
+__global__ __launch_bounds__(512) void gemv_kq_kernel(const unsigned char* A, int64_t lda, const unsigned char* B,
+                                                      float* C, int M, int nsb) {
   constexpr int WAVES = 8, NSB = 16 * ITER, SBW = 80, SDW = NSB * 73, PASS = (SDW + 64 * WAVES - 1) / (64 * WAVES);
+  constexpr int BPB = KQ<T>::BPB;
   __shared__ __attribute__((aligned(16))) uint32_t act[NSB * SBW];
   const int lane = threadIdx.x & 63, t0 = threadIdx.x, qq = lane & 3;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -340,18 +352,30 @@ __global__ __launch_bounds__(512) void gemv_q2k_kernel(const unsigned char* A, i
     sv[k] = bload4(rb, idx < SDW ? (uint32_t)idx * 4 : 0x7ffffff0u);   // past the row: zeros
   }
   __builtin_amdgcn_sched_barrier(0);   // the activation loads first in the vmcnt order
-  const auto ra = make_rsrc(A + (int64_t)(row < M ? row : 0) * lda, (uint32_t)nsb * 84);
-  u32x4 qa[ITER][2];
-  uint32_t sc[ITER], dd[ITER];
+  const auto ra = make_rsrc(A + (int64_t)(row < M ? row : 0) * lda, (uint32_t)nsb * BPB);
+  // this lane's bytes of each of its super-blocks: qs (32 B), the header, and for q5_K qh (32 B)
+  u32x4 qa[ITER][2], hd[ITER], qh[ITER][2];
+  uint32_t sc[ITER];
 #pragma unroll
   for (int c = 0; c < ITER; ++c) {
     const int sb = 16 * c + (lane >> 2);
-    const uint32_t base = sb < nsb ? (uint32_t)sb * 84 : 0x7fff0000u;
-    const uint32_t qo = base + 16 + 32 * (qq >> 1);
-    qa[c][0] = __builtin_amdgcn_raw_buffer_load_b128(ra, qo, 0, 2);
-    qa[c][1] = __builtin_amdgcn_raw_buffer_load_b128(ra, qo + 16, 0, 2);
-    sc[c] = __builtin_amdgcn_raw_buffer_load_b32(ra, base + 4 * qq, 0, 2);
-    dd[c] = __builtin_amdgcn_raw_buffer_load_b32(ra, base + 80, 0, 2);
+    const uint32_t base = sb < nsb ? (uint32_t)sb * BPB : 0x7fff0000u;
+    if constexpr (T == kQ2_K) {
+      const uint32_t qo = base + 16 + 32 * (qq >> 1);
+      qa[c][0] = __builtin_amdgcn_raw_buffer_load_b128(ra, qo, 0, 2);
+      qa[c][1] = __builtin_amdgcn_raw_buffer_load_b128(ra, qo + 16, 0, 2);
+      sc[c] = __builtin_amdgcn_raw_buffer_load_b32(ra, base + 4 * qq, 0, 2);
+      hd[c][0] = __builtin_amdgcn_raw_buffer_load_b32(ra, base + 80, 0, 2);   // d | dmin
+    } else {
+      constexpr int QS = T == kQ5_K ? 48 : 16;
+      hd[c] = __builtin_amdgcn_raw_buffer_load_b128(ra, base, 0, 2);   // d | dmin, scales[12]
+      qa[c][0] = __builtin_amdgcn_raw_buffer_load_b128(ra, base + QS + 32 * qq, 0, 2);
+      qa[c][1] = __builtin_amdgcn_raw_buffer_load_b128(ra, base + QS + 32 * qq + 16, 0, 2);
+      if constexpr (T == kQ5_K) {
+        qh[c][0] = __builtin_amdgcn_raw_buffer_load_b128(ra, base + 16, 0, 2);
+        qh[c][1] = __builtin_amdgcn_raw_buffer_load_b128(ra, base + 32, 0, 2);
+      }
+    }
   }
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -372,19 +396,47 @@ __global__ __launch_bounds__(512) void gemv_q2k_kernel(const unsigned char* A, i
 #pragma unroll
     for (int i = 0; i < 4; ++i) b[i] = *reinterpret_cast<const u32x4*>(a + 4 + 16 * qq + 4 * i);
     const uint2 bsw = *reinterpret_cast<const uint2*>(a + 68 + 2 * qq);   // bsums 4qq .. 4qq + 3 (int16)
+    auto bsum = [&](int i) { return (int)(int16_t)(((i < 2 ? bsw.x : bsw.y) >> (16 * (i & 1))) & 0xffffu); };
     const float yd = __builtin_bit_cast(float, a[0]);
     int isum = 0, summs = 0;
+    uint32_t dd;
+    if constexpr (T == kQ2_K) {
+      dd = hd[c][0];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {   // sub-block s = 4 qq + i: half i & 1 of the qs run, shift 2 jj
-      const int sh = 2 * (2 * (qq & 1) + (i >> 1));
-      const int scv = (int)((sc[c] >> (8 * i)) & 0xffu);
-      int part = 0;
+      for (int i = 0; i < 4; ++i) {   // sub-block s = 4 qq + i: half i & 1 of the qs run, shift 2 jj
+        const int sh = 2 * (2 * (qq & 1) + (i >> 1));
+        const int scv = (int)((sc[c] >> (8 * i)) & 0xffu);
+        int part = 0;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) part = dot4((qa[c][i & 1][k] >> sh) & 0x03030303u, b[i][k], part);
-      const uint32_t bw = i < 2 ? bsw.x : bsw.y;
-      const int bsum = (int)(int16_t)((bw >> (16 * (i & 1))) & 0xffffu);
-      isum += (scv & 0xf) * part;
-      summs += bsum * (scv >> 4);
+        for (int k = 0; k < 4; ++k) part = dot4((qa[c][i & 1][k] >> sh) & 0x03030303u, b[i][k], part);
+        isum += (scv & 0xf) * part;
+        summs += bsum(i) * (scv >> 4);
+      }
+    } else {
+      dd = hd[c][0];
+      // the 6-bit scales / mins of the 8 sub-blocks (LC/ggml-quants.c:7324-7330's utmp shuffle),
+      // then this quarter's two: sub-blocks 2 qq, 2 qq + 1
+      uint32_t u0 = hd[c][1], u1 = hd[c][2], u2 = hd[c][3];
+      const uint32_t u3 = ((u2 >> 4) & 0x0f0f0f0fu) | (((u1 >> 6) & 0x03030303u) << 4);
+      const uint32_t uaux = u1 & 0x3f3f3f3fu;
+      u1 = (u2 & 0x0f0f0f0fu) | (((u0 >> 6) & 0x03030303u) << 4);
+      u2 = uaux;
+      u0 &= 0x3f3f3f3fu;
+      const uint32_t scw = qq < 2 ? u0 : u1, mnw = qq < 2 ? u2 : u3;
+      const int sh = 16 * (qq & 1);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {   // sub-block 2 qq + h: nibble h of the 32 qs bytes
+        const int scv = (int)((scw >> (sh + 8 * h)) & 0xffu), mnv = (int)((mnw >> (sh + 8 * h)) & 0xffu);
+        int part = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          uint32_t q = (qa[c][k >> 2][k & 3] >> (4 * h)) & 0x0f0f0f0fu;
+          if constexpr (T == kQ5_K) q |= ((qh[c][k >> 2][k & 3] >> (2 * qq + h)) & 0x01010101u) << 4;
+          part = dot4(q, b[2 * h + (k >> 2)][k & 3], part);
+        }
+        isum += scv * part;
+        summs += mnv * (bsum(2 * h) + bsum(2 * h + 1));
+      }
     }
     // the quad's four quarters of one super-block (integer: exact)
     isum += __builtin_amdgcn_update_dpp(0, isum, 0xB1, 0xF, 0xF, false);
@@ -392,7 +444,7 @@ __global__ __launch_bounds__(512) void gemv_q2k_kernel(const unsigned char* A, i
     summs += __builtin_amdgcn_update_dpp(0, summs, 0xB1, 0xF, 0xF, false);
     summs += __builtin_amdgcn_update_dpp(0, summs, 0x4E, 0xF, 0xF, false);
     if (qq == 0 && sb < nsb) {
-      const float da = h2f(dd[c] & 0xffffu), dm = h2f(dd[c] >> 16);
+      const float da = h2f(dd & 0xffffu), dm = h2f(dd >> 16);
       acc += (yd * da) * (float)isum - (yd * dm) * (float)summs;
     }
   }
@@ -467,15 +519,25 @@ hipError_t launch_rpw_t(const GemvArgs& p, hipStream_t s, int waves) {
 
 }  // namespace
 
-bool gemv_q2k_supported(const GemvArgs& p) {
-  return p.N == 1 && p.ne12 * p.ne13 == 1 && p.nblk <= 48 && p.flag == nullptr && p.b_f32 == 0;
+bool gemv_kq_supported(int type, const GemvArgs& p) {
+  return (type == kQ2_K || type == kQ4_K || type == kQ5_K) && p.N == 1 && p.ne12 * p.ne13 == 1 && p.nblk <= 48 &&
+         p.flag == nullptr && p.b_f32 == 0;
 }
 
-hipError_t launch_gemv_q2k(const GemvArgs& p, hipStream_t s) {
+hipError_t launch_gemv_kq(int type, const GemvArgs& p, hipStream_t s) {
   const dim3 g((unsigned)((p.M + 7) / 8));
-  if (p.nblk <= 16) hipLaunchKernelGGL(gemv_q2k_kernel<1>, g, dim3(512), 0, s, p.A, p.lda, p.B, p.C, p.M, p.nblk);
-  else if (p.nblk <= 32) hipLaunchKernelGGL(gemv_q2k_kernel<2>, g, dim3(512), 0, s, p.A, p.lda, p.B, p.C, p.M, p.nblk);
-  else hipLaunchKernelGGL(gemv_q2k_kernel<3>, g, dim3(512), 0, s, p.A, p.lda, p.B, p.C, p.M, p.nblk);
+  auto go = [&](auto tc) {
+    constexpr int T = decltype(tc)::value;
+    if (p.nblk <= 16) hipLaunchKernelGGL((gemv_kq_kernel<T, 1>), g, dim3(512), 0, s, p.A, p.lda, p.B, p.C, p.M, p.nblk);
+    else if (p.nblk <= 32) hipLaunchKernelGGL((gemv_kq_kernel<T, 2>), g, dim3(512), 0, s, p.A, p.lda, p.B, p.C, p.M, p.nblk);
+    else hipLaunchKernelGGL((gemv_kq_kernel<T, 3>), g, dim3(512), 0, s, p.A, p.lda, p.B, p.C, p.M, p.nblk);
+  };
+  switch (type) {
+    case kQ2_K: go(std::integral_constant<int, kQ2_K>{}); break;
+    case kQ4_K: go(std::integral_constant<int, kQ4_K>{}); break;
+    case kQ5_K: go(std::integral_constant<int, kQ5_K>{}); break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 

@@ -34,9 +34,10 @@ hipError_t launch_gemv(int type, const GemvArgs& p, hipStream_t s);
 bool gemv_rpw_supported(int type, const GemvArgs& p);
 int rpw_waves(const GemvArgs& p);   // 0: the wave-group kernels (lamm_gemv.hip) take the call
 hipError_t launch_gemv_rpw(int type, const GemvArgs& p, hipStream_t s, int waves);
-// q2_K single-column decode GEMV (lamm_gemv_rpw.hip): one slice, K <= 12288, q8_K activations
-bool gemv_q2k_supported(const GemvArgs& p);
-hipError_t launch_gemv_q2k(const GemvArgs& p, hipStream_t s);
+// q2_K / q4_K / q5_K single-column decode GEMV (lamm_gemv_rpw.hip): one slice, K <= 12288, q8_K
+// activations
+bool gemv_kq_supported(int type, const GemvArgs& p);
+hipError_t launch_gemv_kq(int type, const GemvArgs& p, hipStream_t s);
 size_t gemv_lds_bytes(int type, int nc);
 hipError_t launch_gemv_dense(int type, const GemvArgs& p, hipStream_t s);   // F32 / F16 rows
 // q4_K / q5_K / q6_K prefill GEMM (lamm_gemm_kq.hip); B rows (q8_K) 4-byte aligned

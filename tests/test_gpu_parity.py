@@ -987,16 +987,17 @@ def test_config1_f32_512_cube():
 Q2K_SHAPES = [(1, 256), (9, 4096), (133, 4352), (64, 8192), (37, 11008), (4096, 4096), (70, 12288)]
 
 
+@pytest.mark.parametrize("t", [ol.Q2_K, ol.Q4_K, ol.Q5_K], ids=["q2_k", "q4_k", "q5_k"])
 @pytest.mark.parametrize("shape", Q2K_SHAPES, ids=[f"{m}x1x{k}" for m, k in Q2K_SHAPES])
-def test_gemv_q2k_row_per_wave(shape):
-    """lamm_gemv_rpw.hip's q2_K kernel (one column, up to 48 super-blocks per row): lanes on
+def test_gemv_kq_row_per_wave(t, shape):
+    """lamm_gemv_rpw.hip's k-quant kernel (one column, up to 48 super-blocks per row): lanes on
     quarter super-blocks, the quarters' integer sums combined in the quad (exact), one float
-    epilogue per super-block as the reference's ggml_vec_dot_q2_K_q8_K; ragged M, K from one to 48
-    super-blocks, against the oracle."""
+    epilogue per super-block as the reference's ggml_vec_dot_q{2,4,5}_K_q8_K; ragged M, K from one
+    to 48 super-blocks, against the oracle."""
     M, K = shape
-    rng = np.random.default_rng(M * 31 + K)
-    A_q = ol.random_kq_blocks(ol.Q2_K, M, K, rng)
+    rng = np.random.default_rng(M * 31 + K + t)
+    A_q = ol.random_kq_blocks(t, M, K, rng)
     B_q = ORACLE.quantize(ol.Q8_K, rng.standard_normal((1, K), dtype=np.float32))
-    c, _ = gpu_mul_mat(ol.Q2_K, A_q, B_q, M, 1, K)
-    ref = ORACLE.mul_mat(ol.Q2_K, M, 1, K, A_q, B_q)
-    assert rel_err(c, ref, absdot(ol.Q2_K, A_q, B_q, M, 1, K)).max() < TOL
+    c, _ = gpu_mul_mat(t, A_q, B_q, M, 1, K)
+    ref = ORACLE.mul_mat(t, M, 1, K, A_q, B_q)
+    assert rel_err(c, ref, absdot(t, A_q, B_q, M, 1, K)).max() < TOL

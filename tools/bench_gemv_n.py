@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
-"""GEMV (decode) timing vs the number of activation rows N = 1..8 per weight format:
-algorithmic bytes (A + B + C) / kernel time, weights > MALL per launch.  One JSON line."""
+"""Single-call decode GEMV per weight format (config 2's measurement: ONE M x 1 x K GEMV per step,
+the steps rotating over weight copies > the 256 MiB MALL, the kernel alone over 1000
+graph-replayed launches): algorithmic bytes (A + B + C) / per-launch time.  One JSON line.
+usage: python tools/bench_gemv_n.py [fmt,fmt,...] [M] [K]"""
 import json
 import os
 import sys
@@ -15,16 +17,15 @@ import bench  # noqa: E402
 
 
 def main():
-    fmts = (sys.argv[1] if len(sys.argv) > 1 else "q4_0,q8_0,q4_k,q6_k,f16").split(",")
-    M = K = 4096
-    out = {}
+    fmts = (sys.argv[1] if len(sys.argv) > 1 else "q4_0,q4_k,q5_k,q6_k,f16").split(",")
+    M = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
+    K = int(sys.argv[3]) if len(sys.argv) > 3 else 4096
+    ctx = bench.Ctx(torch, la)
+    out = {"M": M, "K": K}
     for f in fmts:
-        out[f] = {}
-        for N in [int(n) for n in os.environ.get("NS", "1,2,4,8").split(",")]:
-            u = bench.gemv_bytes(la, f, M, K, N)
-            sl = max(4, -(-int(1.15 * bench.MALL_BYTES) // u))
-            _, _, kk = bench.run_case(torch, la, None, f, M, N, K, sl, 10, 2, 1)
-            out[f][N] = {"GBs": round(sl * u / kk / 1e9, 1), "us_per_slice": round(kk / sl * 1e6, 3)}
+        g = bench.config2_gemv(ctx, f, M, K, 50, 5)
+        out[f] = {"us": round(g["kern"] * 1e6, 3), "GBs": round(g["slab_bytes"] / g["kern"] / 1e9, 1),
+                  "frac": round(g["slab_bytes"] / g["kern"] / 1e9 / bench.HBM_PEAK_GBS, 4)}
     print(json.dumps(out), flush=True)
 
 

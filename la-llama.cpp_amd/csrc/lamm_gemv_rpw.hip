@@ -519,9 +519,14 @@ hipError_t launch_rpw_t(const GemvArgs& p, hipStream_t s, int waves) {
 
 }  // namespace
 
+// Up to which row count the row-per-wave form beats the wave-group kernels (single calls, K = 4096,
+// profiles/r03/gemv_kq/): q2_K / q4_K faster at 4096 and 11008 rows, slower at 32000 (the
+// wave-group stream wins once the grid is long); q5_K (each lane also reads the whole 32-byte qh)
+// faster at 4096 only.
 bool gemv_kq_supported(int type, const GemvArgs& p) {
+  const int max_rows = type == kQ5_K ? 6144 : 16384;
   return (type == kQ2_K || type == kQ4_K || type == kQ5_K) && p.N == 1 && p.ne12 * p.ne13 == 1 && p.nblk <= 48 &&
-         p.flag == nullptr && p.b_f32 == 0;
+         p.M <= max_rows && p.flag == nullptr && p.b_f32 == 0;
 }
 
 hipError_t launch_gemv_kq(int type, const GemvArgs& p, hipStream_t s) {

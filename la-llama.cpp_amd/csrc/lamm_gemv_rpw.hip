@@ -352,7 +352,7 @@ __global__ __launch_bounds__(512) void gemv_kq_kernel(const unsigned char* A, in
     sv[k] = bload4(rb, idx < SDW ? (uint32_t)idx * 4 : 0x7ffffff0u);   // past the row: zeros
   }
   __builtin_amdgcn_sched_barrier(0);   // the activation loads first in the vmcnt order
-  const auto ra = make_rsrc(A + (int64_t)(row < M ? row : 0) * lda, (uint32_t)nsb * BPB);
+  const auto ra = make_rsrc(A + (int64_t)(row < M ? row : 0) * lda, ((uint32_t)nsb * BPB + 3) & ~3u);
   // this lane's bytes of each of its super-blocks: qs (32 B), the header, and for q5_K qh (32 B)
   u32x4 qa[ITER][2], hd[ITER], qh[ITER][2];
   uint32_t sc[ITER];

@@ -72,6 +72,9 @@ constexpr int SCALE_W = 130, SCALE_HI = 134, SCALE_LO = 130;   // E8M0: 2^(s-127
 // profiles/r02/ab_c_nt/ab_ct_nt.txt).  0: cached stores (A/B build, tools/ab_ct_nt.sh).
 #define F6_CT_NT 1
 #endif
+#ifndef F6_KV_ORDER
+#define F6_KV_ORDER 0   // gemm_fp6_kv_kernel's issue order per unit (probe builds only, see block())
+#endif
 #ifndef F6_PD
 #define F6_PD 1   // MFMA pipeline depth: unit n+PD's MFMAs are issued before unit n's FMAs (2: no gain, +20 VGPRs)
 #endif
@@ -991,15 +994,21 @@ __global__ __launch_bounds__(512) void gemm_fp6_kv_kernel(GemvArgs p, const unsi
       for (int e = 8 * half; e < 8 * half + 8; ++e) c[e] = __builtin_fmaf(R.s[e], R.pr[e], c[e]);
     };
     auto sb = [] { __builtin_amdgcn_sched_barrier(0); };
+    // issue order of one unit step (F6_KV_ORDER, probe builds): 0 S, E/2, P, E/2 (production);
+    // 1 P, E/2, S, E/2; 2 S, P, E
+    auto unit = [&](auto do_s, auto do_p, auto do_e0, auto do_e1) {
+      if constexpr (F6_KV_ORDER == 1) {
+        do_p(); sb(); do_e0(); sb(); do_s(); sb(); do_e1(); sb();
+      } else if constexpr (F6_KV_ORDER == 2) {
+        do_s(); sb(); do_p(); sb(); do_e0(); sb(); do_e1(); sb();
+      } else {
+        do_s(); sb(); do_e0(); sb(); do_p(); sb(); do_e1(); sb();
+      }
+    };
     sb();
-    mfma_s(0, rr[0]);
-    sb();
-    if (pend) epi(UPB - 1, rr[(UPB - 1) % 2], 0);   // the previous block's last unit
-    sb();
-    mfma_p(0, rr[0]);
-    sb();
-    if (pend) epi(UPB - 1, rr[(UPB - 1) % 2], 1);
-    sb();
+    unit([&] { mfma_s(0, rr[0]); }, [&] { mfma_p(0, rr[0]); },
+         [&] { if (pend) epi(UPB - 1, rr[(UPB - 1) % 2], 0); },   // the previous block's last unit
+         [&] { if (pend) epi(UPB - 1, rr[(UPB - 1) % 2], 1); });
     unroll<UPB - 1>([&](auto NN) {
       constexpr int n = NN;
       if constexpr (n == 1) {   // the next block's weights: its DMA pieces landed (the oldest vmem ops
@@ -1008,14 +1017,8 @@ __global__ __launch_bounds__(512) void gemm_fp6_kv_kernel(GemvArgs p, const unsi
         wread(SN, wn);
         sb();
       }
-      mfma_s(n + 1, rr[(n + 1) % 2]);
-      sb();
-      epi(n, rr[n % 2], 0);
-      sb();
-      mfma_p(n + 1, rr[(n + 1) % 2]);
-      sb();
-      epi(n, rr[n % 2], 1);
-      sb();
+      unit([&] { mfma_s(n + 1, rr[(n + 1) % 2]); }, [&] { mfma_p(n + 1, rr[(n + 1) % 2]); },
+           [&] { epi(n, rr[n % 2], 0); }, [&] { epi(n, rr[n % 2], 1); });
     });
     pend = true;
     if constexpr (AFF) {   // sum_b m_a s_b per K-step: rank-KB, both k halves carry it (x2 like P)

@@ -73,7 +73,11 @@ template <int CTRL>
 __device__ __forceinline__ float dpp_get(float x) {
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
 }
+// No contraction: the first add must not fuse with the caller's product (hipcc contracts across the
+// inlined call, so the same per-lane product would sum differently in two kernels -- a row's value
+// would depend on the kernel its launch picks, tests/test_gpu_parity.py::test_gemv_row_slab_invariance).
 __device__ __forceinline__ float wave_sum(float x) {
+#pragma clang fp contract(off)
   x += dpp_get<0xB1>(x);    // quad_perm [1,0,3,2]
   x += dpp_get<0x4E>(x);    // quad_perm [2,3,0,1]
   x += dpp_get<0x141>(x);   // row_half_mirror

@@ -88,13 +88,20 @@ __global__ __launch_bounds__(64 * WAVES) void gemv_rpw_kernel(GemvArgs p) {
   constexpr bool LANEB = LB && !BF32 && NC == 1 && ITER == 2;
   uint32_t lq[ITER][8];
   float ld[ITER], ls[ITER];
+  // ITER = 2 (64 < nblk <= 128): each 64-block run reduces on its own and the two run sums add in
+  // run order -- gemv_flat_kernel's order, so a row's value does not depend on which of the two
+  // kernels the launch's row count picks (a sharded weight's 1024-row slab vs the whole 4096)
+  constexpr int NR = ITER == 2 ? 2 : 1;
   auto compute = [&](int64_t row, const uint32_t (&wa)[ITER][NWA]) {
-    float acc[NC];
+    float accr[NR][NC];
 #pragma unroll
-    for (int j = 0; j < NC; ++j) acc[j] = 0.f;
+    for (int r = 0; r < NR; ++r)
+#pragma unroll
+      for (int j = 0; j < NC; ++j) accr[r][j] = 0.f;
 #pragma unroll
     for (int it = 0; it < ITER; ++it) {
       const int b = lane + 64 * it;
+      float (&acc)[NC] = accr[NR == 2 ? it : 0];
       if (b < nb) {
         uint32_t m[NWA - 1];
         realign(wa[it], m, (int)((uint32_t)(b * F::BPB) & 3u));
@@ -128,8 +135,12 @@ __global__ __launch_bounds__(64 * WAVES) void gemv_rpw_kernel(GemvArgs p) {
         }
       }
     }
+    float acc[NC];
 #pragma unroll
-    for (int j = 0; j < NC; ++j) acc[j] = wave_sum(acc[j]);   // 64-lane reduction, fixed order
+    for (int j = 0; j < NC; ++j) {
+      acc[j] = wave_sum(accr[0][j]);   // 64-lane reduction, fixed order
+      if constexpr (NR == 2) acc[j] += wave_sum(accr[1][j]);
+    }
     if (lane == 0) {
 #pragma unroll
       for (int j = 0; j < NC; ++j)

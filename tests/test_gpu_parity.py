@@ -917,6 +917,25 @@ def test_gemv_row_per_wave_batched_broadcast(monkeypatch):
         assert rel_err(c[z], ref, absdot(t, As[z // 2], Bs[z], M, N, K)).max() < TOL, z
 
 
+@pytest.mark.parametrize("t", RPW_TYPES, ids=[ol.NAMES[t] for t in RPW_TYPES])
+def test_gemv_row_slab_invariance(t):
+    """A row's value does not depend on the launch it is in: the 4096 x 4096 decode GEMV (flat
+    kernel, 8 waves) against row slabs of it as `bench.py --gpus N` shards them (2048 rows: flat;
+    1024 / 512 / 1000: the row-per-wave kernel with 4 waves) and one column against the same
+    column inside a two-column call -- bit-identical, as the multi-GPU gather check requires."""
+    M, K = 4096, 4096
+    A_q, B_q = random_case(t, M, 2, K, seed=9100 + t)
+    rows_q = np.ascontiguousarray(A_q).reshape(M, -1)
+    b1 = np.ascontiguousarray(B_q).reshape(2, -1)[:1]
+    full, _ = gpu_mul_mat(t, rows_q, b1, M, 1, K)
+    full = np.asarray(full).reshape(-1)
+    for r0, rows in ((0, 2048), (2048, 1024), (3584, 512), (1000, 1000)):
+        slab, _ = gpu_mul_mat(t, np.ascontiguousarray(rows_q[r0:r0 + rows]), b1, rows, 1, K)
+        np.testing.assert_array_equal(np.asarray(slab).reshape(-1), full[r0:r0 + rows], err_msg=f"rows {r0}+{rows}")
+    two, _ = gpu_mul_mat(t, rows_q, B_q, M, 2, K)
+    np.testing.assert_array_equal(np.asarray(two).reshape(2, M)[0], full)
+
+
 # ---------------------------------------------------------------- BASELINE config 4, full size
 CONFIG4_TYPES = [ol.Q4_1, ol.Q5_0, ol.Q5_1, ol.Q8_0, ol.Q2_K]   # src/la-benchmark-matmult.cpp:26-36
 _CONFIG4_CACHE = {}

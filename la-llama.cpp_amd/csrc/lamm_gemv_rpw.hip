@@ -182,14 +182,19 @@ __global__ __launch_bounds__(64 * WAVES) void gemv_rpw_kernel(GemvArgs p) {
       stage(std::integral_constant<int, 2>{});
     __syncthreads();
   } else {
-    // straight-line (no branch between them), so the activation loads stay ahead of the row's
-    // HBM stream and waiting for them does not wait for A; out-of-range loads read zeros (a
-    // branch around them lets the compiler pull the decode in front of the A loads)
-    st.template load<NC>(p, rb, t0);
+    // the activation loads ahead of the row's HBM stream (the sched barriers keep them first in
+    // the vmcnt order and the decode behind the A loads), issued only by the waves that hold a
+    // block: a scalar branch -- letting every wave issue them with out-of-range offsets (zeros)
+    // cost 0.16 us per config-2 launch (tools/gemv_probe.hip G8 vs G8-allstage,
+    // profiles/r03/gemv_probe_11.json)
+    if (wave * 64 < nact) st.template load<NC>(p, rb, t0);
     __builtin_amdgcn_sched_barrier(0);   // keep the activation loads first in the vmcnt order
     issue(row < p.M ? row : 0, wa0);
     __builtin_amdgcn_sched_barrier(0);
-    if (t0 < nact) st.store(t0, sq0, sq1, sbd, sbs);
+    if (t0 < nact) {
+      st.pin();
+      st.store(t0, sq0, sq1, sbd, sbs);
+    }
     for (int it = t0 + blockDim.x; it < nact; it += blockDim.x) {
       st.template load<NC>(p, rb, it);
       st.store(it, sq0, sq1, sbd, sbs);
@@ -264,11 +269,14 @@ __device__ __forceinline__ void flat_body(const unsigned char* Az, uint32_t lda,
   } else {
     static_assert(NB <= NT, "one staging pass");
     ActStage<T, false> st;
-    st.template load<1>(p, rb, t0);        // straight-line; out-of-range loads read zeros
+    if (w * 64 < NB) st.template load<1>(p, rb, t0);   // the two waves that hold a block (scalar branch)
     __builtin_amdgcn_sched_barrier(0);
     issue();
     __builtin_amdgcn_sched_barrier(0);
-    if (t0 < NB) st.store(t0, sq0, sq1, sbd, sbs);
+    if (t0 < NB) {
+      st.pin();
+      st.store(t0, sq0, sq1, sbd, sbs);
+    }
   }
   __syncthreads();
 #pragma unroll

@@ -141,6 +141,14 @@ struct ActStage {
     }
   }
 
+  // the loaded words as an opaque definition here: the decode cannot be hoisted above this point
+  // (behind a branch around the loads the compiler otherwise moves it -- and its wait for the
+  // activation -- in front of the row's A loads)
+  __device__ __forceinline__ void pin() {
+#pragma unroll
+    for (int i = 0; i < NW; ++i) asm volatile("" : "+v"(w[i]));
+  }
+
   __device__ __forceinline__ void store(int it, u32x4* q0, u32x4* q1, float* bd, float* bs) const {
     uint32_t q[8];
     float d, sx;

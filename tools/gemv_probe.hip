@@ -532,6 +532,91 @@ __global__ __launch_bounds__(64 * WAVES) void kF(const unsigned char* A, const u
   if (t < WAVES) C[row0 + t] = part[2 * t] + part[2 * t + 1];
 }
 
+// G: kF's flat order (WAVES even, so a wave's two runs are the same half of a row and lane l meets
+// ONE activation block, (w % 2) 64 + l) with ablations.  FL 1: no C store; 2: the lane's activation
+// block loaded and decoded in its own registers (no LDS staging, no staging barrier); 4: no
+// activation at all (constant block: the staging's cost); 8: XCD-aware row groups (workgroup b runs
+// on XCD b % 8; group (b % 8) G/8 + b / 8, so the groups one XCD runs are consecutive and each
+// 128-byte line of C is written from ONE L2); 16: every thread issues the staging loads
+template <int WAVES, int FL>
+__global__ __launch_bounds__(64 * WAVES) void kG(const unsigned char* A, const unsigned char* B, float* C) {
+  static_assert(WAVES % 2 == 0, "a wave's runs share one half");
+  __shared__ Act S;
+  __shared__ float part[2 * WAVES];
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), t = threadIdx.x;
+  const int bid = (FL & 8) ? (int)(blockIdx.x & 7) * (int)(gridDim.x >> 3) + (int)(blockIdx.x >> 3) : (int)blockIdx.x;
+  const int row0 = bid * WAVES;
+  const auto rb = make_rsrc(B, BROW);
+  const auto ra = make_rsrc(A + (size_t)row0 * ROW, ROW * WAVES);
+  const int bl = (w & 1) * 64 + lane;   // this lane's block in both its runs
+  uint32_t bw[10];
+  if constexpr (FL & 2) {
+    stage_load(rb, bl, bw);
+  } else if constexpr (FL & 16) {
+    stage_load(rb, t < NB ? t : 0x3fffff, bw);   // every thread, out-of-range ones read zeros (as flat1)
+  } else if constexpr (!(FL & 4)) {
+    if (t < NB) stage_load(rb, t, bw);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  uint32_t wa[2][6];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int m = k * WAVES + w;
+    const uint32_t off = (uint32_t)((m >> 1) * ROW + bl * 18) & ~3u;
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, 2);
+    const auto u = __builtin_amdgcn_raw_buffer_load_b64(ra, off + 16, 0, 2);
+    wa[k][0] = v[0]; wa[k][1] = v[1]; wa[k][2] = v[2]; wa[k][3] = v[3];
+    wa[k][4] = (uint32_t)u[0]; wa[k][5] = (uint32_t)u[1];
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  u32x4 b0, b1;
+  float db;
+  int sb;
+  if constexpr (FL & 2) {
+    uint32_t q[8];
+    act_decode(bl, bw, q, db, sb);
+    b0 = u32x4{q[0], q[1], q[2], q[3]};
+    b1 = u32x4{q[4], q[5], q[6], q[7]};
+  } else if constexpr (FL & 4) {
+    b0 = u32x4{1u, 2u, 3u, 4u};
+    b1 = u32x4{5u, 6u, 7u, 8u};
+    db = 0.5f;
+    sb = 3;
+  } else {
+    if (t < NB) stage_store(S, t, bw);
+    __syncthreads();
+    b0 = S.q0[bl];
+    b1 = S.q1[bl];
+    db = S.d[bl];
+    sb = S.sb[bl];
+  }
+  const int sh = ((bl * 18) & 3) * 8;
+  float acc[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    uint32_t m[5];
+#pragma unroll
+    for (int q = 0; q < 5; ++q) m[q] = __builtin_amdgcn_alignbit(wa[k][q + 1], wa[k][q], sh);
+    uint32_t qs[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) qs[q] = __builtin_amdgcn_alignbit(m[q + 1], m[q], 16);
+    acc[k] = wave_sum(blockdot(qs, m[0], b0, b1, db, sb, 0.f));
+  }
+  if (lane == 0) {
+    part[w] = acc[0];
+    part[WAVES + w] = acc[1];
+  }
+  __syncthreads();
+  if (t < WAVES) {
+    const float c = part[2 * t] + part[2 * t + 1];
+    if constexpr (FL & 1) {
+      if (c == 1234567.f) C[row0 + t] = c;
+    } else {
+      C[row0 + t] = c;
+    }
+  }
+}
+
 // L: the WG's W rows pulled into LDS by LDS-DMA in WG-contiguous 1 KiB pieces (wave w issues
 // pieces w, w + W, ...: the access order of the fastest read floor, rw<W>x<W>), then lane l of
 // wave w reads row w's blocks l, l + 64 back from LDS (dword reads + realignment) -- the same
@@ -731,6 +816,21 @@ int main(int argc, char** argv) {
   FK("F4", 4, 0);
   FK("F16", 16, 0);
   FK("F16-s2", 16, 1);
+#define GK(name, W, FL, full) run(name, [&](const unsigned char* a) { kG<W, FL><<<M / W, 64 * W, 0, s>>>(a, dB, dC); }, full)
+  GK("G8", 8, 0, true);
+  GK("G8-lane", 8, 2, true);
+  GK("G8-noact", 8, 4, false);
+  GK("G8-nostore", 8, 1, false);
+  GK("G8-lane-nostore", 8, 3, false);
+  GK("G8-noact-nostore", 8, 5, false);
+  GK("G8-allstage", 8, 16, true);
+  GK("G8-xcd", 8, 8, true);
+  GK("G8-xcd-nostore", 8, 9, false);
+  GK("G8-xcd-noact", 8, 12, false);
+  GK("G4-xcd", 4, 8, true);
+  GK("G16-xcd", 16, 8, true);
+  GK("G4-lane", 4, 2, true);
+  GK("G16-lane", 16, 2, true);
 #define RW(name, W, R) run(name, [&](const unsigned char* a) { kReadW<W, R><<<M / R, 64 * W, 0, s>>>(a, dC); }, false)
   RW("rw4x4", 4, 4);
   RW("rw8x8", 8, 8);

@@ -231,7 +231,7 @@ __global__ __launch_bounds__(64 * WAVES) void gemv_rpw_kernel(GemvArgs p) {
 // none after the last one).
 template <int T, int WAVES, bool BF32, int ITER>
 __device__ __forceinline__ void flat_body(const unsigned char* Az, uint32_t lda, const unsigned char* Bz, float* Cz,
-                                          int M, int nblk) {
+                                          int M, int nblk, int group) {
   using F = RFmt<T>;
   constexpr int NWA = (F::BPB + 3) / 4 + 1;
   constexpr int NB = 64 * ITER, NT = 64 * WAVES;
@@ -240,7 +240,7 @@ __device__ __forceinline__ void flat_body(const unsigned char* Az, uint32_t lda,
   __shared__ float part[WAVES * ITER];
   const int lane = threadIdx.x & 63, t0 = threadIdx.x;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int row0 = blockIdx.x * WAVES;
+  const int row0 = group * WAVES;
   const int nrows = M - row0 < WAVES ? M - row0 : WAVES;
   // A resource over this workgroup's rows, ending at its last row's last block byte
   const auto ra = make_rsrc(Az + (int64_t)row0 * lda, (uint32_t)(nrows - 1) * lda + ((nblk * F::BPB + 3) & ~3));
@@ -324,7 +324,7 @@ __global__ __launch_bounds__(64 * WAVES) void gemv_flat_kernel(GemvArgs p) {
     Bz += (int64_t)i12 * p.sb2 + (int64_t)i13 * p.sb3;
     Cz += (int64_t)i12 * p.sc2 + (int64_t)i13 * p.sc3;
   }
-  flat_body<T, WAVES, BF32, ITER>(Az, (uint32_t)p.lda, Bz, Cz, p.M, p.nblk);   // lda < 2^16: nb <= 64 ITER
+  flat_body<T, WAVES, BF32, ITER>(Az, (uint32_t)p.lda, Bz, Cz, p.M, p.nblk, blockIdx.x);   // lda < 2^16: nb <= 64 ITER
   if constexpr (SIG) signal_done(p);
 }
 
@@ -332,7 +332,12 @@ __global__ __launch_bounds__(64 * WAVES) void gemv_flat_kernel(GemvArgs p) {
 template <int T, bool BF32>
 __global__ __launch_bounds__(512) void gemv_flat1_kernel(const unsigned char* A, const unsigned char* B, float* C,
                                                          uint32_t lda, int M) {
-  flat_body<T, 8, BF32, 2>(A, lda, B, C, M, 128);
+  // XCD-aware row groups: workgroup b runs on XCD b % 8 (round-robin dispatch); give each XCD a
+  // contiguous range of groups, so its rows' C lines are written from one L2 (probe G8-xcd vs G8,
+  // profiles/r03/gemv_probe_12/13.json)
+  const int n = gridDim.x, x = blockIdx.x & 7, k = blockIdx.x >> 3, q = n >> 3, r = n & 7;
+  const int group = x < r ? x * (q + 1) + k : r * (q + 1) + (x - r) * q + k;
+  flat_body<T, 8, BF32, 2>(A, lda, B, C, M, 128, group);
 }
 
 // The k-quant formats against q8_K, one column, K <= 12288 (the reference's Q2_K kernel,

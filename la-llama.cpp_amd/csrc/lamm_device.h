@@ -14,6 +14,8 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x2 __attribute__((ext_vector_type(2)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 __device__ __forceinline__ float h2f(uint32_t h16) {
@@ -34,6 +36,21 @@ __device__ __forceinline__ uint32_t bload4(__amdgpu_buffer_rsrc_t r, uint32_t of
 }
 __device__ __forceinline__ uint16_t bload2(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __builtin_amdgcn_raw_buffer_load_b16(r, off, 0, 0);
+}
+
+// Write-through vector stores (sc0 sc1): a short launch's results go straight past L2 instead of
+// waiting in it, dirty, for the end-of-kernel write-back.  tools/write_probe.hip
+// (profiles/r03/write_probe.json): 4 MB written by a 1024-workgroup pass 2.13 us per launch with
+// plain stores, 1.85 us with sc0 sc1 (2 MB 1.99 -> 1.68, 8 MB 2.87 -> 2.52).
+constexpr int kAuxWriteThrough = 1 | 16;   // sc0 | sc1
+__device__ __forceinline__ void bstore4_wt(__amdgpu_buffer_rsrc_t r, uint32_t off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, off, 0, kAuxWriteThrough);
+}
+__device__ __forceinline__ void bstore8_wt(__amdgpu_buffer_rsrc_t r, uint32_t off, f32x2 v) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, off, 0, kAuxWriteThrough);
+}
+__device__ __forceinline__ void bstore16_wt(__amdgpu_buffer_rsrc_t r, uint32_t off, u32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kAuxWriteThrough);
 }
 
 // dword starting at byte offset O of a register-resident byte string (O compile-time).

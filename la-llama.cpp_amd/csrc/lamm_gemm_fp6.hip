@@ -334,8 +334,11 @@ __device__ __forceinline__ void pack_fp6_bytes(const uint32_t (&c)[8], uint32_t 
   o[5] = (t[6] >> 16) | (t[7] << 8);
 }
 
-// one activation block (32 int8 quants as 8 dwords, fp16 d / s bits) -> its hi / lo fragments
-__device__ __forceinline__ void store_b_fp6(unsigned char* ch, int b, int r, const uint32_t (&q)[8], uint32_t d,
+// one activation block (32 int8 quants as 8 dwords, fp16 d / s bits) -> its hi / lo fragments, at
+// byte offset `ch` of the slice's workspace `ws` (write-through: the planes are read by the next
+// launch, not this one -- nothing of them should wait dirty in L2 for the end-of-kernel write-back)
+template <class Put>
+__device__ __forceinline__ void store_b_fp6(Put&& put, int b, int r, const uint32_t (&q)[8], uint32_t d,
                                             uint32_t sv) {
   uint32_t hi[8], lo[8];
 #pragma unroll
@@ -348,10 +351,10 @@ __device__ __forceinline__ void store_b_fp6(unsigned char* ch, int b, int r, con
   uint32_t oh[6], ol[6];
   pack_fp6_bytes(hi, oh);
   pack_fp6_bytes(lo, ol);
-  *(u32x4*)(ch + f6_boff(0, b, 0, r)) = u32x4{oh[0], oh[1], oh[2], oh[3]};
-  *(u32x4*)(ch + f6_boff(1, b, 0, r)) = u32x4{oh[4], oh[5], d, sv};
-  *(u32x4*)(ch + f6_boff(0, b, 1, r)) = u32x4{ol[0], ol[1], ol[2], ol[3]};
-  *(u32x4*)(ch + f6_boff(1, b, 1, r)) = u32x4{ol[4], ol[5], d, sv};
+  put(f6_boff(0, b, 0, r), u32x4{oh[0], oh[1], oh[2], oh[3]});
+  put(f6_boff(1, b, 0, r), u32x4{oh[4], oh[5], d, sv});
+  put(f6_boff(0, b, 1, r), u32x4{ol[0], ol[1], ol[2], ol[3]});
+  put(f6_boff(1, b, 1, r), u32x4{ol[4], ol[5], d, sv});
 }
 
 template <int T>
@@ -400,8 +403,14 @@ __global__ __launch_bounds__(PB_NT) void prep_b_fp6_tile(GemvArgs p, unsigned ch
     if constexpr (VBPB == 36) sv = m[0] >> 16;
     unroll<8>([&](auto K) { q[K] = get32<VQS + 4 * K>(m); });
   }
-  unsigned char* ch = ws + (int64_t)z * L.b_slice + ((int64_t)(j / F6_TJ) * L.nsteps + kb / F6_KB) * F6_B_BYTES;
-  store_b_fp6(ch, kb % F6_KB, (int)(j % F6_TJ), q, d, sv);
+  unsigned char* wz = ws + (int64_t)z * L.b_slice;
+  const int64_t ch = ((int64_t)(j / F6_TJ) * L.nsteps + kb / F6_KB) * F6_B_BYTES;
+  if (L.b_slice <= 0x7fffffff) {   // write-through buffer stores from a wave-uniform base
+    const auto wr = make_rsrc(wz, (uint32_t)L.b_slice);
+    store_b_fp6([&](int o, u32x4 v) { bstore16_wt(wr, (uint32_t)(ch + o), v); }, kb % F6_KB, (int)(j % F6_TJ), q, d, sv);
+  } else {
+    store_b_fp6([&](int o, u32x4 v) { *(u32x4*)(wz + ch + o) = v; }, kb % F6_KB, (int)(j % F6_TJ), q, d, sv);
+  }
 }
 
 // ---------------------------------------------------------------- GEMM
@@ -1084,6 +1093,9 @@ __global__ __launch_bounds__(512) void gemm_fp6_kv_kernel(GemvArgs p, const unsi
   float* C = p.C + (int64_t)i12 * p.sc2 + (int64_t)i13 * p.sc3;
   const int64_t i = (int64_t)ti * TI + 2 * lane;
   const bool pair = i + 1 < p.M && (p.ldc & 1) == 0 && ((uintptr_t)C & 7) == 0;
+  // the tile's C rows through a write-through resource from the tile's first row (wave-uniform)
+  const bool wt = (int64_t)TJ * p.ldc * 4 < 0x7fffffff;
+  const auto cr = make_rsrc(C + (int64_t)tj * TJ * p.ldc, wt ? (uint32_t)(TJ * p.ldc * 4) : 0u);
 #pragma unroll
   for (int q = 0; q < RPW; ++q) {
     const int jl = w * RPW + q;
@@ -1094,7 +1106,9 @@ __global__ __launch_bounds__(512) void gemm_fp6_kv_kernel(GemvArgs p, const unsi
     v *= 0.5f;
     if (j < p.N) {
       float* c = C + j * p.ldc + i;
-      if (pair) {
+      if (pair && wt) {
+        bstore8_wt(cr, (uint32_t)((jl * p.ldc + i) * 4), v);
+      } else if (pair) {
         __builtin_nontemporal_store(v, reinterpret_cast<f32x2*>(c));
       } else {
         if (i < p.M) c[0] = v[0];

@@ -308,7 +308,7 @@ __device__ __forceinline__ void flat_body(const unsigned char* Az, uint32_t lda,
     float c = part[t0 * ITER];
 #pragma unroll
     for (int k = 1; k < ITER; ++k) c += part[t0 * ITER + k];
-    Cz[row0 + t0] = c;
+    Cz[row0 + t0] = c;   // (a write-through store here measured no faster, profiles/r03/write_through/)
   }
 }
 

@@ -316,7 +316,10 @@ __global__ __launch_bounds__(PREP_NT) void prep_b_fp6(GemvArgs p, unsigned char*
 // full_run_6/kernel_stats_bench.csv).  Codes by SWAR, 4 per dword:
 //   lo = q & 15 (e2m3 code n/8 = n for 0 <= n <= 15)
 //   hi = u < 8 ? u : 48 - u, u = q >> 4 as a nibble (sign | |h| for h = floor(q / 16) in [-8, 7])
-constexpr int PB_ROWS = 32, PB_NB = 8, PB_NT = 256;
+#ifndef F6_PB_NB
+#define F6_PB_NB 8   // blocks per row of a prep workgroup (A/B builds: 4, 2 -- more, smaller workgroups)
+#endif
+constexpr int PB_ROWS = 32, PB_NB = F6_PB_NB, PB_NT = PB_ROWS * PB_NB;
 
 // 32 six-bit codes held as bytes (code e = byte e % 4 of c[e / 4]) -> the 192-bit fragment
 __device__ __forceinline__ void pack_fp6_bytes(const uint32_t (&c)[8], uint32_t (&o)[6]) {

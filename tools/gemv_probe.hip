@@ -884,6 +884,12 @@ int main(int argc, char** argv) {
 #define XK(name, W) run(name, [&](const unsigned char* a) { kX<W><<<M / W, 64 * W, 0, s>>>(a, dB, dC); }, true)
   run("read", [&](const unsigned char* a) { kRead<<<M / 4, 256, 0, s>>>(a, dC); }, false);
   run("empty", [&](const unsigned char*) { kEmpty<<<1024, 256, 0, s>>>(dC); }, false);
+  run("empty-256x256", [&](const unsigned char*) { kEmpty<<<256, 256, 0, s>>>(dC); }, false);
+  run("empty-512x256", [&](const unsigned char*) { kEmpty<<<512, 256, 0, s>>>(dC); }, false);
+  run("empty-256x512", [&](const unsigned char*) { kEmpty<<<256, 512, 0, s>>>(dC); }, false);
+  run("empty-512x512", [&](const unsigned char*) { kEmpty<<<512, 512, 0, s>>>(dC); }, false);
+  run("empty-2048x256", [&](const unsigned char*) { kEmpty<<<2048, 256, 0, s>>>(dC); }, false);
+  run("empty-256x64", [&](const unsigned char*) { kEmpty<<<256, 64, 0, s>>>(dC); }, false);
   printf(", \"bytes\": %.0f}\n", bytes);
   return 0;
 }

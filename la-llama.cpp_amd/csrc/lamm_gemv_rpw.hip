@@ -78,7 +78,7 @@ __global__ __launch_bounds__(64 * WAVES) void gemv_rpw_kernel(GemvArgs p) {
     for (int it = 0; it < ITER; ++it) {
       const int b = lane + 64 * it;
       const uint32_t off = b < nb ? (uint32_t)(b * F::BPB) & ~3u : 0x7ffffff0u;
-      load_words<NWA, 2>(ra, off, wa[it]);   // non-temporal: A is read once
+      load_block_words<F::BPB, 2>(ra, off, wa[it]);   // non-temporal: A is read once
     }
   };
   // LANEB (q8 activations, one column, K <= 4096): each lane holds the two activation blocks its
@@ -250,7 +250,7 @@ __device__ __forceinline__ void flat_body(const unsigned char* Az, uint32_t lda,
     for (int k = 0; k < ITER; ++k) {
       const int m = k * WAVES + w, r = m / ITER, bi = (m % ITER) * 64 + lane;   // wave-uniform run m
       const uint32_t off = bi < nblk ? (uint32_t)r * lda + ((uint32_t)(bi * F::BPB) & ~3u) : 0x7ffffff0u;
-      load_words<NWA, 2>(ra, off, wa[k]);
+      load_block_words<F::BPB, 2>(ra, off, wa[k]);
     }
   };
   const auto rb = make_rsrc(Bz, BF32 ? (uint32_t)nblk * 128 : (uint32_t)(nblk * F::VBPB + 3) & ~3u);

@@ -37,6 +37,25 @@ __device__ __forceinline__ void load_words(__amdgpu_buffer_rsrc_t r, uint32_t of
   }
 }
 
+// One weight block's dwords from the dword below its start, into NWA = (BPB + 3) / 4 + 1 words (the
+// realignment's input).  Every block size is even, so a block starts at a shift of 0 or 2 bytes
+// (always 0 when BPB % 4 == 0): ceil((BPB + 2) / 4) dwords hold it, one fewer than NWA -- q4_0
+// 20 bytes (b128 + b32) instead of 24 (b128 + b64).  The spare word is 0; realign never needs its
+// bytes (config 2 probe: G8-n5 vs G8, profiles/r03/gemv_probe_15.json; library A/B
+// profiles/r03/block_words/: q4_0 3.65 -> 3.61 us, q8_0 5.85 -> 5.76, decode step -1.3 %).  q5_0
+// (22 bytes) keeps b128 + b64 + b32: its 6-dword form measured 4.01 -> 4.11 us.
+template <int BPB>
+constexpr int block_dwords() { return BPB % 4 == 0 ? BPB / 4 : BPB == 22 ? (BPB + 3) / 4 + 1 : (BPB + 2 + 3) / 4; }
+template <int BPB, int AUX, int NWA>
+__device__ __forceinline__ void load_block_words(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t (&w)[NWA]) {
+  constexpr int NL = block_dwords<BPB>();
+  static_assert(NL <= NWA, "fits the realignment input");
+  uint32_t t[NL];
+  load_words<NL, AUX>(r, off, t);
+#pragma unroll
+  for (int k = 0; k < NWA; ++k) w[k] = k < NL ? t[k] : 0u;
+}
+
 // bytes [sh, sh + 4*(NW-1)) of w as NW-1 dwords (sh in {0, 1, 2, 3} bytes)
 template <int NW>
 __device__ __forceinline__ void realign(const uint32_t (&w)[NW], uint32_t (&m)[NW - 1], int sh) {

@@ -565,9 +565,14 @@ __global__ __launch_bounds__(64 * WAVES) void kG(const unsigned char* A, const u
     const int m = k * WAVES + w;
     const uint32_t off = (uint32_t)((m >> 1) * ROW + bl * 18) & ~3u;
     const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, 2);
-    const auto u = __builtin_amdgcn_raw_buffer_load_b64(ra, off + 16, 0, 2);
     wa[k][0] = v[0]; wa[k][1] = v[1]; wa[k][2] = v[2]; wa[k][3] = v[3];
-    wa[k][4] = (uint32_t)u[0]; wa[k][5] = (uint32_t)u[1];
+    if constexpr (FL & 512) {   // 20 bytes: an 18-byte block at a 0 / 2 byte shift needs no 6th dword
+      wa[k][4] = __builtin_amdgcn_raw_buffer_load_b32(ra, off + 16, 0, 2);
+      wa[k][5] = 0;
+    } else {
+      const auto u = __builtin_amdgcn_raw_buffer_load_b64(ra, off + 16, 0, 2);
+      wa[k][4] = (uint32_t)u[0]; wa[k][5] = (uint32_t)u[1];
+    }
   }
   __builtin_amdgcn_sched_barrier(0);
   u32x4 b0, b1;
@@ -863,6 +868,8 @@ int main(int argc, char** argv) {
   GK("G8-loadsonly", 8, 64, false);
   GK("G8-loadsonly-noact", 8, 68, false);
   GK("G8-oneline", 8, 128, false);
+  GK("G8-n5", 8, 512, true);
+  GK("G8-n5-xcd", 8, 520, true);
   GK("G8-ticket", 8, 256, true);
   GK("G8-ticket-xcd", 8, 264, true);
   GK("G8-xcd", 8, 8, true);

@@ -50,6 +50,7 @@ template <int BPB, int AUX, int NWA>
 __device__ __forceinline__ void load_block_words(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t (&w)[NWA]) {
   constexpr int NL = block_dwords<BPB>();
   static_assert(NL <= NWA, "fits the realignment input");
+  static_assert(BPB % 2 == 0 && 4 * NL >= BPB + (BPB % 4 ? 2 : 0), "covers the block at its largest shift");
   uint32_t t[NL];
   load_words<NL, AUX>(r, off, t);
 #pragma unroll

@@ -415,8 +415,11 @@ def llama_step_sharded(ctx, fmt):
         ms = res.get("ms_per_step", float("inf"))
         (ms_max,) = ctx.max(ms)
         if "error" not in res:
-            res["ms_per_step_max_over_ranks"] = round(ms_max, 4)
-            res["tok_per_s"] = round(res["tokens_per_step"] / (ms_max * 1e-3), 2)
+            if ms_max != ms_max or ms_max == float("inf"):   # another rank failed
+                res["error"] = "a rank failed: no step time from every rank"
+            else:
+                res["ms_per_step_max_over_ranks"] = round(ms_max, 4)
+                res["tok_per_s"] = round(res["tokens_per_step"] / (ms_max * 1e-3), 2)
         out[name] = res
     return out
 

@@ -134,6 +134,14 @@ int lamm_hip_matmul_weights(const lamm_weights *W, const lamm_matrix *B, const l
 size_t lamm_hip_weights_bytes(const lamm_weights *W);
 void lamm_hip_weights_destroy(lamm_weights *W);
 
+/* Which engine lamm_hip_matmul* (stationary = 0) or lamm_hip_matmul_weights (stationary = 1)
+ * runs an M x N x K call of weight type `type` over `slices` A slices on, under the current
+ * LAMM_* switches: "gemv" (decode GEMV), "gemv-groups" (GEMV launches of 8 columns), "dense"
+ * (F32 / F16 GEMM), "superblock" (k-quant GEMM), "fp6" (block-scaled fp6 MFMA GEMM), "i8"
+ * (MFMA-i8 GEMM); "" for an unsupported type or shape.  b_f32: B holds F32 rows (q8_0 / q8_1
+ * activation types).  Host-only: no device is touched. */
+const char *lamm_hip_engine(int type, int64_t M, int N, int K, int slices, int stationary, int b_f32);
+
 const char *lamm_hip_last_error(void);
 int lamm_hip_device_count(void);
 /* Provenance: hash (sha256, 16 hex digits) of the sources this library was built from. */

@@ -265,14 +265,24 @@ extern "C" int lamm_hip_allgather_rows(lamm_comm* c, const float* const* slabs, 
     // the caller's next matmul on stream k overwrites C[k] / gbuf[k] (without that
     // wait a reader of the previous contents could race it)
     if (c->packed.empty()) {
-      c->packed.resize(nl);
-      c->done.resize(nl);
-      for (int i = 0; i < nl; ++i) {
+      // created into locals and handed to the communicator only once all exist (a
+      // failure half-way used to leave null handles that later calls recorded and destroyed)
+      std::vector<hipEvent_t> packed(nl, nullptr), done(nl, nullptr);
+      bool made = true;
+      for (int i = 0; i < nl && made; ++i) {
         (void)hipSetDevice(c->devices[i]);
-        if (hipEventCreateWithFlags(&c->packed[i], hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&c->done[i], hipEventDisableTiming) != hipSuccess)
-          return cfail(LAMM_ERR_HIP, "hipEventCreate");
+        made = hipEventCreateWithFlags(&packed[i], hipEventDisableTiming) == hipSuccess &&
+               hipEventCreateWithFlags(&done[i], hipEventDisableTiming) == hipSuccess;
       }
+      if (!made) {
+        for (int i = 0; i < nl; ++i) {
+          if (packed[i]) (void)hipEventDestroy(packed[i]);
+          if (done[i]) (void)hipEventDestroy(done[i]);
+        }
+        return cfail(LAMM_ERR_HIP, "hipEventCreate");
+      }
+      c->packed.swap(packed);
+      c->done.swap(done);
     }
     auto ok = [](hipError_t e) { return e == hipSuccess; };
     for (int i = 0; i < nl; ++i) {

@@ -181,11 +181,24 @@ GemvArgs weight_args(const lamm_matrix* A, int64_t ne02, int64_t ne03, size_t nb
 // LAMM_GEMV_MAX_N=n overrides (A/B).
 int gemv_max_n(int type) {
   int n = 8;
-  if (knobs().gemv_max_n > 0) n = knobs().gemv_max_n;
+  if (knobs().gemv_max_n >= 0) n = knobs().gemv_max_n;
   else if (type == kQ2_K) n = 5;
   else if (type == kQ4_K) n = 6;
   else if (type == kQ5_K || type == kQ6_K || type == kF16) n = 4;
   return n < 1 ? 1 : (n > 8 ? 8 : n);
+}
+
+// Which engine lamm_hip_matmul* runs a call on (lamm_hip_engine reports the same choice to
+// callers and tests).  stationary: the weights' packed prefill form is resident (lamm_weights);
+// b_al4: B and its slice strides are 4-byte aligned (the super-block GEMM reads q8_K as dwords).
+enum Engine { kEngGemv, kEngDense, kEngKq, kEngFp6, kEngI8, kEngGemvGroups };
+Engine pick_engine(int type, const GemvArgs& p, bool stationary, bool b_al4) {
+  if (p.N <= gemv_max_n(type) || (p.b_f32 && p.N <= 8)) return kEngGemv;
+  if (gemm_dense_supported(type) && knobs().dense_gemm) return kEngDense;
+  if (gemm_kq_supported(type) && knobs().kq_gemm && b_al4) return kEngKq;
+  if (gemm_fp6_supported(type) && gemm_path(p, stationary) == 0) return kEngFp6;
+  if (gemm_supported(type) && gemm_args_ok(type, p)) return kEngI8;
+  return kEngGemvGroups;
 }
 
 // A completion signal the ggml boundary asks of the next matmul on this thread (decode calls):
@@ -253,46 +266,56 @@ int matmul_impl(const lamm_matrix* A, const lamm_matrix* B, const lamm_matrix* C
   p.sc3 = (int64_t)(bt.nbc3 / 4);
   p.b_f32 = b_f32 ? 1 : 0;
   hipError_t e;
-  if (N <= gemv_max_n(A->type) || (b_f32 && N <= 8)) {
-    if (done && gemv_rpw_supported(A->type, p) && rpw_waves(p) > 0) {
-      p.done_ctr = done->ctr;
-      p.flag = done->flag;
-      p.seq = done->seq;
-      done->signaled = true;
+  const bool b_al4 = (ldb & 3) == 0 && ((uintptr_t)B->data & 3) == 0 && (bt.nbb2 & 3) == 0 && (bt.nbb3 & 3) == 0;
+  switch (pick_engine(A->type, p, W && W->packed, b_al4)) {
+    case kEngGemv:
+      if (done && gemv_rpw_supported(A->type, p) && rpw_waves(p) > 0) {
+        p.done_ctr = done->ctr;
+        p.flag = done->flag;
+        p.seq = done->seq;
+        done->signaled = true;
+      }
+      e = launch_gemv(A->type, p, s);
+      break;
+    case kEngDense: {
+      const size_t wsb = gemm_dense_workspace_bytes(A->type, p);
+      void* ws = nullptr;
+      if (wsb && !(ws = workspace(wsb, s))) return fail(LAMM_ERR_HIP, "workspace allocation of %zu bytes failed", wsb);
+      e = launch_gemm_dense(A->type, p, ws, s);
+      break;
     }
-    e = launch_gemv(A->type, p, s);
-  } else if (gemm_dense_supported(A->type) && knobs().dense_gemm) {
-    const size_t wsb = gemm_dense_workspace_bytes(A->type, p);
-    void* ws = nullptr;
-    if (wsb && !(ws = workspace(wsb, s))) return fail(LAMM_ERR_HIP, "workspace allocation of %zu bytes failed", wsb);
-    e = launch_gemm_dense(A->type, p, ws, s);
-  } else if (gemm_kq_supported(A->type) && knobs().kq_gemm && (ldb & 3) == 0 &&
-             ((uintptr_t)B->data & 3) == 0 && (bt.nbb2 & 3) == 0 && (bt.nbb3 & 3) == 0) {
-    const void* prepA = W ? W->packed : nullptr;
-    const size_t wsb = gemm_kq_workspace_bytes(A->type, p, prepA != nullptr);
-    void* ws = workspace(wsb, s);
-    if (!ws) return fail(LAMM_ERR_HIP, "workspace allocation of %zu bytes failed", wsb);
-    e = launch_gemm_kq(A->type, p, prepA, ws, s);
-  } else if (gemm_fp6_supported(A->type) && gemm_path(p, W && W->packed) == 0) {
-    const void* prepA = W ? W->packed : nullptr;
-    const size_t wsb = gemm_fp6_workspace_bytes(A->type, p, prepA != nullptr);
-    void* ws = workspace(wsb, s);
-    if (!ws) return fail(LAMM_ERR_HIP, "workspace allocation of %zu bytes failed", wsb);
-    e = launch_gemm_fp6(A->type, p, prepA, ws, s);
-  } else if (gemm_supported(A->type) && gemm_args_ok(A->type, p)) {
-    void* ws = nullptr;
-    const size_t wsb = gemm_workspace_bytes(A->type, p);
-    if (wsb && !(ws = workspace(wsb, s))) return fail(LAMM_ERR_HIP, "workspace allocation of %zu bytes failed", wsb);
-    e = launch_gemm(A->type, p, ws, s);
-  } else {
-    e = hipSuccess;
-    for (int j0 = 0; j0 < N && e == hipSuccess; j0 += 8) {
-      GemvArgs q = p;
-      q.B = p.B + (int64_t)j0 * ldb;
-      q.C = p.C + (int64_t)j0 * p.ldc;
-      q.N = N - j0 < 8 ? N - j0 : 8;
-      e = launch_gemv(A->type, q, s);
+    case kEngKq: {
+      const void* prepA = W ? W->packed : nullptr;
+      const size_t wsb = gemm_kq_workspace_bytes(A->type, p, prepA != nullptr);
+      void* ws = workspace(wsb, s);
+      if (!ws) return fail(LAMM_ERR_HIP, "workspace allocation of %zu bytes failed", wsb);
+      e = launch_gemm_kq(A->type, p, prepA, ws, s);
+      break;
     }
+    case kEngFp6: {
+      const void* prepA = W ? W->packed : nullptr;
+      const size_t wsb = gemm_fp6_workspace_bytes(A->type, p, prepA != nullptr);
+      void* ws = workspace(wsb, s);
+      if (!ws) return fail(LAMM_ERR_HIP, "workspace allocation of %zu bytes failed", wsb);
+      e = launch_gemm_fp6(A->type, p, prepA, ws, s);
+      break;
+    }
+    case kEngI8: {
+      void* ws = nullptr;
+      const size_t wsb = gemm_workspace_bytes(A->type, p);
+      if (wsb && !(ws = workspace(wsb, s))) return fail(LAMM_ERR_HIP, "workspace allocation of %zu bytes failed", wsb);
+      e = launch_gemm(A->type, p, ws, s);
+      break;
+    }
+    default:   // kEngGemvGroups: GEMV launches of 8 columns
+      e = hipSuccess;
+      for (int j0 = 0; j0 < N && e == hipSuccess; j0 += 8) {
+        GemvArgs q = p;
+        q.B = p.B + (int64_t)j0 * ldb;
+        q.C = p.C + (int64_t)j0 * p.ldc;
+        q.N = N - j0 < 8 ? N - j0 : 8;
+        e = launch_gemv(A->type, q, s);
+      }
   }
   if (e != hipSuccess) return fail(LAMM_ERR_HIP, "kernel launch: %s", hipGetErrorString(e));
   return LAMM_OK;
@@ -303,6 +326,18 @@ int matmul_impl(const lamm_matrix* A, const lamm_matrix* B, const lamm_matrix* C
 extern "C" int lamm_hip_matmul_batched(const lamm_matrix* A, const lamm_matrix* B, const lamm_matrix* C,
                                        const lamm_batch* batch, void* hip_stream) {
   return matmul_impl(A, B, C, batch, hip_stream, nullptr);
+}
+
+extern "C" const char* lamm_hip_engine(int type, int64_t M, int N, int K, int slices, int stationary, int b_f32) {
+  static const char* const names[] = {"gemv", "dense", "superblock", "fp6", "i8", "gemv-groups"};
+  if (!is_weight_type(type) || M < 1 || N < 1 || K < 1 || slices < 1 || K % block_elems(type)) return "";
+  const int kb = K / block_elems(type);
+  GemvArgs p{nullptr, (int64_t)kb * (int64_t)block_bytes(type), nullptr, 0, nullptr, M, (int)M, N, K, kb};
+  p.ne12 = slices;
+  p.r2 = 1;
+  p.b_f32 = b_f32 && (vec_dot_type(type) == kQ8_0 || vec_dot_type(type) == kQ8_1) ? 1 : 0;
+  const bool packs = gemm_fp6_supported(type) || gemm_kq_supported(type);
+  return names[pick_engine(type, p, stationary && packs, true)];
 }
 
 extern "C" int lamm_hip_weights_create(const lamm_matrix* A, int64_t ne02, int64_t ne03, size_t nba2, size_t nba3,
@@ -919,10 +954,13 @@ extern "C" void lamm_mul_mat(const struct ggml_compute_params* vparams, struct g
   const size_t x_row = act == kCpuInit ? b_row : (size_t)ldx * sizeof(float);
   const size_t x_bytes = x_row * (size_t)(N * nslices);
   const size_t c_bytes = (size_t)M * N * nslices * sizeof(float);
-  // zero-copy on several devices too: every device reads the one pinned activation buffer and
-  // writes its own rows of the one pinned C (mapped pinned memory has one address on every device)
-  const bool zc_in = zero_copy(x_bytes, true) && act != kGpuQuant && (G == 1 || rt.pinned_shared(0, x_bytes));
-  const bool zc_out = zero_copy(c_bytes, false) && (G == 1 || rt.pinned_shared(1, c_bytes));
+  // zero copy on several devices (LAMM_HIP_ZERO_COPY_SPLIT=1): every device reads the one pinned
+  // activation buffer and writes its own rows of the one pinned C (mapped pinned memory has one
+  // address on every device).  Off by default: it has only run with one GPU listed several times,
+  // and with N > 1 and M not a multiple of 16 two devices' rows of C can share a host cache line
+  const bool zc_split = G == 1 || knobs().zero_copy_split;
+  const bool zc_in = zc_split && zero_copy(x_bytes, true) && act != kGpuQuant && (G == 1 || rt.pinned_shared(0, x_bytes));
+  const bool zc_out = zc_split && zero_copy(c_bytes, false) && (G == 1 || rt.pinned_shared(1, c_bytes));
   const unsigned char* x_host = nullptr;   // the bytes every device uploads (or reads in place)
   auto gather_f32 = [&](unsigned char* out) {   // F32 src1 rows (any strides) -> [slice][N][ldx]
     for (int64_t i13 = 0; i13 < ne13; ++i13)

@@ -29,7 +29,7 @@ Knobs* read_env() {
     if (!strcmp(e, "i8") || !strcmp(e, "1")) k->gemm_path = 1;
     if (!strcmp(e, "fp6") || !strcmp(e, "0")) k->gemm_path = 0;
   }
-  k->gemv_max_n = env_int("LAMM_GEMV_MAX_N", 0);
+  k->gemv_max_n = env_int("LAMM_GEMV_MAX_N", -1);
   k->dense_gemm = !env_off("LAMM_DENSE_GEMM");
   k->kq_gemm = !env_off("LAMM_KQ_GEMM");
   k->fp6_split = env_int("LAMM_FP6_SPLIT", 0);
@@ -59,6 +59,7 @@ Knobs* read_env() {
   k->kernel_signal = env_on("LAMM_HIP_KERNEL_SIGNAL");
   const char* zc = getenv("LAMM_HIP_ZERO_COPY");
   k->zero_copy = !k->pinned || (zc && zc[0] == '0') ? 0 : zc && !strcmp(zc, "in") ? 1 : zc && !strcmp(zc, "out") ? 2 : 3;
+  k->zero_copy_split = env_on("LAMM_HIP_ZERO_COPY_SPLIT");
   return k;
 }
 

@@ -9,7 +9,8 @@ namespace lamm {
 struct Knobs {
   // ---- operator API: engine and plan selection
   int gemm_path = -1;          // LAMM_GEMM_PATH: fp6|0 / i8|1 forces the q4_0/q4_1/q5_0 prefill engine
-  int gemv_max_n = 0;          // LAMM_GEMV_MAX_N: widest N on the decode GEMV (0: per-type default)
+  int gemv_max_n = -1;         // LAMM_GEMV_MAX_N: widest N on the decode GEMV (-1 unset: per-type default;
+                               // 0 and 1 both mean N = 1 only, the floor)
   bool dense_gemm = true;      // LAMM_DENSE_GEMM=0: F32/F16 prefill on the grouped GEMV instead
   bool kq_gemm = true;         // LAMM_KQ_GEMM=0: k-quant prefill on the grouped GEMV / i8 engine
   int fp6_split = 0;           // LAMM_FP6_SPLIT=n: split-K plan with n splits
@@ -38,6 +39,7 @@ struct Knobs {
   bool spin = true;            // LAMM_HIP_SPIN=0: hipStreamSynchronize instead of the flag spin
   bool kernel_signal = false;  // LAMM_HIP_KERNEL_SIGNAL=1: the GEMV writes the completion flag
   int zero_copy = 3;           // LAMM_HIP_ZERO_COPY: 0 off, 1 in, 2 out, 3 both
+  bool zero_copy_split = false;  // LAMM_HIP_ZERO_COPY_SPLIT=1: zero copy also when rows split over devices
 };
 
 // The current switches (read from the environment at the first call).

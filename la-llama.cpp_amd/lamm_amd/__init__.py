@@ -115,6 +115,9 @@ lib.lamm_blck_size.restype = ctypes.c_int
 lib.lamm_type_size.restype = ctypes.c_size_t
 lib.lamm_vec_dot_type.restype = ctypes.c_int
 lib.lamm_hip_build_id.restype = ctypes.c_char_p
+lib.lamm_hip_engine.restype = ctypes.c_char_p
+lib.lamm_hip_engine.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                ctypes.c_int]
 lib.lamm_hip_shard_rows.restype = None
 lib.lamm_hip_shard_rows.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                     ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]
@@ -301,42 +304,13 @@ def quantize_torch(vtype, x, y, flavour=1, stream=None):
            "lamm_hip_quantize")
 
 
-def gemm_engine(fmt, M, N, K, slices=1, stationary=False):
-    """Which prefill engine lamm_hip_matmul* picks for N > 8 (mirrors gemm_path() in
-    csrc/lamm_hip.cpp): "fp6" (q4_0/q4_1/q5_0 when its 256x128 tiles fill >= 256 CUs -- or,
-    for stationary weights (la.Weights), its 128x64 K-group tiles or tiles x K-splits do), "i8"
-    (K-split on small grids)
-    otherwise; LAMM_GEMM_PATH overrides."""
+def gemm_engine(fmt, M, N, K, slices=1, stationary=False, b_f32=False):
+    """Which engine lamm_hip_matmul* (or, stationary, lamm_hip_matmul_weights) runs the call on,
+    as the library decides it under the current LAMM_* switches (lamm_hip_engine): "gemv",
+    "gemv-groups", "dense", "superblock", "fp6" or "i8"."""
     t = BY_NAME[fmt] if isinstance(fmt, str) else fmt
-    env_n = os.environ.get("LAMM_GEMV_MAX_N")   # gemv_max_n() in csrc/lamm_hip.cpp
-    max_n = int(env_n) if env_n else {Q2_K: 5, Q4_K: 6, Q5_K: 4, Q6_K: 4, F16: 4}.get(t, 8)
-    if N <= max(1, min(8, max_n)):
-        return "gemv"
-    if t in (F32, F16):
-        return "dense"          # lamm_gemm_dense.hip (LAMM_DENSE_GEMM=0: grouped GEMV)
-    if t in (Q2_K, Q4_K, Q5_K, Q6_K):
-        return "superblock"     # lamm_gemm_kq.hip (LAMM_KQ_GEMM=0: q2_K i8 / grouped GEMV)
-    if t not in (Q4_0, Q4_1, Q5_0):
-        return "i8"
-    env = os.environ.get("LAMM_GEMM_PATH")
-    if env in ("i8", "1"):
-        return "i8"
-    if env in ("fp6", "0"):
-        return "fp6"
-    tiles = -(-M // 256) * -(-N // 128) * slices
-    nsteps = -(-(K // 32) // 2)
-    split = int(os.environ.get("LAMM_FP6_SPLIT", "0") or 0)
-    sub = int(os.environ.get("LAMM_FP6_SUB", "-1") or -1)
-    subt = -(-M // 128) * -(-N // 64) * slices   # f6_plan(): 128x64 tiles with K-groups
-    if split <= 0 and sub != 0 and (sub > 0 or (tiles < 256 and subt >= 256)):
-        grid = subt
-    else:
-        if split <= 0:   # f6_nsplit_for(): double until 256 workgroups, >= 8 K-steps per split, <= 16
-            split = 1
-            while tiles * split < 256 and split < 16 and nsteps // (2 * split) >= 8:
-                split *= 2
-        grid = tiles * max(1, min(split, nsteps))
-    return "fp6" if (grid if stationary else tiles) >= 256 else "i8"
+    _sync_env()
+    return lib.lamm_hip_engine(t, M, N, K, slices, int(bool(stationary)), int(bool(b_f32))).decode()
 
 
 COMM_ID_BYTES = 128

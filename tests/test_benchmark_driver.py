@@ -105,7 +105,7 @@ def _llama_logits(tmp_path, name, args):
 def test_llama_bench_sharded_decode_bitexact(tmp_path, tall):
     """Config 5 as north_star states it: every weight's rows sharded over the ranks
     (lamm_hip_shard_rows) with lamm_hip_allgather_rows after every projection, the whole step one
-    hipGraph.  Rehearsed on one GPU: 2 and 3 local ranks on device 0 (the loopback exchange,
+    hipGraph.  Rehearsed on one GPU: 2, 3 and 8 local ranks on device 0 (the loopback exchange,
     event-ordered) and the RCCL path with one rank (--rank 0 --world 1): the decode step's logits
     must equal the one-rank run bit for bit (each output row is computed by the same kernel the
     same way whichever rank owns it)."""
@@ -113,7 +113,7 @@ def test_llama_bench_sharded_decode_bitexact(tmp_path, tall):
     extra = ["-n", "1"] + (["--batch-proj"] if tall else [])
     d1, l1 = _llama_logits(tmp_path, "g1", ["--shard", "1"] + extra)
     assert d1["world"] == 1 and np.isfinite(l1).all() and np.abs(l1).sum() > 0
-    for G in (2, 3):
+    for G in (2, 3, 8):
         dg, lg = _llama_logits(tmp_path, f"g{G}", ["--shard", str(G)] + extra)
         assert dg["world"] == G and dg["allgathers"] == d1["allgathers"]
         np.testing.assert_array_equal(lg.view(np.uint32), l1.view(np.uint32), err_msg=f"{G} ranks")

@@ -242,17 +242,20 @@ def test_views_bypass_weight_cache(monkeypatch):
 
 
 @pytest.mark.parametrize("quant", ["cpu_init", "gpu"])
+@pytest.mark.parametrize("zc_split", ["0", "1"])
 @pytest.mark.parametrize("devices", ["0,0", "0,0,0"])
 @pytest.mark.parametrize("t,M,N,K", [(ol.Q4_0, 4096, 1, 4096), (ol.Q4_0, 1000, 20, 512), (ol.Q8_0, 77, 3, 256),
                                      (ol.Q2_K, 300, 9, 512)])
-def test_boundary_rows_split_over_devices(devices, t, M, N, K, quant, monkeypatch):
+def test_boundary_rows_split_over_devices(devices, t, M, N, K, quant, zc_split, monkeypatch):
     """LAMM_HIP_DEVICES: the weight's rows split over the listed devices, each writing its rows
-    of C into dst (host consumes C): decode-sized calls zero-copy on every device (one
-    pinned activation buffer read by all, each device's rows of one pinned C), larger ones by
-    device copies.  Rehearsed with one device listed several times (separate streams and
+    of C into dst (host consumes C) by device copies, or with zc_split = "1" decode-sized
+    calls zero-copy on every device (one pinned activation buffer read by all, each device's rows
+    of one pinned C).  Rehearsed with one device listed several times (separate streams and
     caches, the same slab bookkeeping as real devices); the result must be bit-identical to the
     same slabs computed one by one, and match the oracle within the parity tolerance.  quant:
-    ggml's CPU INIT (q8 rows) or the boundary's default (F32 rows quantized on the GPU)."""
+    ggml's CPU INIT (q8 rows) or the boundary's default (F32 rows quantized on the GPU).
+    zc_split: device copies (default) or zero copy on every device (LAMM_HIP_ZERO_COPY_SPLIT=1)."""
+    monkeypatch.setenv("LAMM_HIP_ZERO_COPY_SPLIT", zc_split)
     if quant == "cpu_init":
         monkeypatch.setenv("LAMM_HIP_GPU_QUANT", "0")
     else:

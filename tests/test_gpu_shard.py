@@ -149,3 +149,51 @@ def test_rccl_allgather_across_devices():
         np.testing.assert_array_equal(c, Cs[0])
     assert np.abs(Cs[0] - ref).max() <= 1e-3 * np.abs(ref).max()
     comm.close()
+
+
+PREFILL = [(4096, 4096), (11008, 4096), (4096, 11008)]   # Llama-7B q/k/v/o, gate/up, down
+
+
+@pytest.mark.parametrize("N", [16, 512])
+@pytest.mark.parametrize("MK", PREFILL, ids=[f"{m}x{k}" for m, k in PREFILL])
+def test_sharded_prefill_slabs_match_whole(MK, N):
+    """Config 5's sharded prefill, node by node: every rank's slab GEMM
+    (stationary weights, rows [r0, r0 + rows) of lamm_hip_shard_rows at llama-matmul-bench's
+    16-row granularity, 2 and 8 ranks) against the same rows of the one-GPU call, from identical
+    inputs, at the north-star tolerance |c - c_whole| <= 1e-3 sum |a b| per element.  A slab may
+    run another tile plan (another fp32 summation order of the exact block dots) than the whole
+    weight, so this is a tolerance, not bits; the whole call is pinned to the oracle on sampled
+    rows."""
+    M, K = MK
+    t = ol.Q4_0
+    A_q, B_q = _case(t, M, N, K, seed=M + N + K)
+    arow = ORACLE.row_bytes(t, K)
+    assert arow % 16 == 0
+    A = torch.from_numpy(np.concatenate([A_q, np.zeros(64, np.uint8)])).cuda()
+    B = torch.from_numpy(B_q.copy()).cuda()
+    W = la.Weights(t, A, M, K)
+    C = torch.full((N * M,), float("nan"), dtype=torch.float32, device="cuda")
+    W.matmul_torch(B, C, N)
+    torch.cuda.synchronize()
+    whole = C.cpu().numpy().reshape(N, M)
+    W.close()
+    Ad = ORACLE.dequantize(t, A_q, M, K).astype(np.float64)
+    Bd = ORACLE.dequantize(la.vec_dot_type(t), B_q, N, K).astype(np.float64)
+    absdot = np.abs(Bd) @ np.abs(Ad).T
+    rows_s = [0, 1, M // 2, M - 1]
+    ref = ORACLE.mul_mat(t, len(rows_s), N, K, A_q.reshape(M, arow)[rows_s].reshape(-1), B_q)
+    assert rel_err(whole[:, rows_s], ref, absdot[:, rows_s]).max() < TOL
+    worst = 0.0
+    for world in (2, 8):
+        for r in range(world):
+            r0, rows = la.shard_rows(M, world, r, 16)
+            Ws = la.Weights(t, A[r0 * arow:], rows, K)
+            slab = torch.full((rows * N,), float("nan"), dtype=torch.float32, device="cuda")
+            Ws.matmul_torch(B, slab, N)
+            torch.cuda.synchronize()
+            got = slab.cpu().numpy().reshape(N, rows)
+            Ws.close()
+            err = rel_err(got, whole[:, r0:r0 + rows], absdot[:, r0:r0 + rows]).max()
+            assert err < TOL, f"world {world} rank {r}: {err}"
+            worst = max(worst, float(err))
+    print(f"sharded prefill q4_0 {M}x{N}x{K}: worst slab vs whole {worst:.2e} of sum |a b|")

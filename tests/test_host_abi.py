@@ -174,3 +174,38 @@ def test_no_getenv_on_launch_paths():
                 depth -= 1
             elif "getenv(" in ln:
                 assert depth > 0, f"{f}: getenv outside the variant build: {ln.strip()}"
+
+
+def test_engine_choice(monkeypatch):
+    """lamm_hip_engine reports the dispatch lamm_hip_matmul* makes (host logic, no device): the
+    decode GEMV up to each type's widest N, then the prefill engines; LAMM_GEMV_MAX_N overrides
+    the per-type width, with 0 and 1 both meaning N = 1 only ('0' had silently
+    become 'unset' in the library while the binding read it as 1)."""
+    for k in ("LAMM_GEMV_MAX_N", "LAMM_GEMM_PATH", "LAMM_FP6_SPLIT", "LAMM_FP6_SUB", "LAMM_DENSE_GEMM", "LAMM_KQ_GEMM"):
+        monkeypatch.delenv(k, raising=False)
+    e = la.gemm_engine
+    assert e("q4_0", 4096, 1, 4096) == "gemv" and e("q4_0", 4096, 8, 4096) == "gemv"
+    assert e("q2_k", 4096, 5, 4096) == "gemv" and e("q2_k", 4096, 6, 4096) == "superblock"
+    assert e("q6_k", 4096, 4, 4096) == "gemv" and e("q6_k", 4096, 5, 4096) == "superblock"
+    assert e("f16", 4096, 5, 4096) == "dense" and e("f32", 512, 512, 512) == "dense"
+    # BASELINE config 3: the fp6 engine's 128x64 K-group tiles fill the chip with stationary weights
+    assert e("q4_0", 4096, 512, 4096, stationary=True) == "fp6"
+    assert e("q5_1", 4096, 512, 4096, stationary=True) == "i8"
+    assert e("q8_0", 4096, 512, 4096) == "i8"
+    assert e("q4_0", 4096, 9, 4096) in ("fp6", "i8")
+    assert e("q5_0", 4096, 512, 4096, b_f32=True) == e("q5_0", 4096, 512, 4096)
+    assert e("q4_0", 4096, 8, 4096, b_f32=True) == "gemv"
+    assert e(11, 4096, 1, 4096) == "" and e("q4_0", 4096, 1, 100) == ""
+    monkeypatch.setenv("LAMM_GEMV_MAX_N", "0")
+    assert e("q4_0", 4096, 1, 4096) == "gemv" and e("q4_0", 4096, 2, 4096) != "gemv"
+    monkeypatch.setenv("LAMM_GEMV_MAX_N", "1")
+    assert e("q4_0", 4096, 2, 4096) != "gemv"
+    # F32 activations stay on the fused GEMV up to 8 columns whatever the override
+    assert e("q4_0", 4096, 8, 4096, b_f32=True) == "gemv"
+    monkeypatch.setenv("LAMM_GEMV_MAX_N", "4")
+    assert e("q4_0", 4096, 4, 4096) == "gemv" and e("q4_0", 4096, 5, 4096) != "gemv"
+    monkeypatch.delenv("LAMM_GEMV_MAX_N")
+    monkeypatch.setenv("LAMM_GEMM_PATH", "i8")
+    assert e("q4_0", 4096, 512, 4096, stationary=True) == "i8"
+    monkeypatch.setenv("LAMM_GEMM_PATH", "fp6")
+    assert e("q4_0", 4096, 64, 4096) == "fp6"

@@ -201,24 +201,63 @@ def time_steps(ctx, step, steps, warmup, graph=True):
             log("graph capture failed, eager steps:", str(e)[:200])
             g = None
             torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ctx.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    with torch.cuda.stream(st):
-        e0.record(st)
+    def run():
         if g is not None:
             g.replay()
         else:
             for s in range(steps):
                 step(warmup + s)
+
+    # the timed region: nothing but the K steps between the barrier + synchronize brackets (the
+    # events of the second pass cost host calls of their own: profiles/r04/roofline/)
+    with torch.cuda.stream(st):
+        ctx.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        run()
+        torch.cuda.synchronize()
+        ctx.barrier()
+        wall = time.perf_counter() - t0
+        # the same K steps again, timed by HIP events on the stream they run on
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        run()
         e1.record(st)
     torch.cuda.synchronize()
-    ctx.barrier()
-    wall = time.perf_counter() - t0
     ev = e0.elapsed_time(e1) / 1e3
     wmax, emax = ctx.max(wall / steps, ev / steps)
     return wmax, emax, g is not None
+
+
+_STEPS_LIB = None
+
+
+def isolated_launches(la, mats, R, Bm, Cm, n):
+    """median device time (s) of n lamm_hip_matmul launches, each isolated (tools/steps_loop.hip);
+    None when the helper is not built"""
+    global _STEPS_LIB
+    import ctypes
+    path = os.path.join(ROOT, "tools", "libsteps_loop.so")
+    if _STEPS_LIB is None:
+        if not os.path.exists(path):
+            return None
+        _STEPS_LIB = ctypes.CDLL(path)
+        _STEPS_LIB.lamm_steps_isolated.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(la.Matrix),
+                                                   ctypes.POINTER(la.Matrix), ctypes.c_int, ctypes.c_int,
+                                                   ctypes.c_void_p, ctypes.POINTER(ctypes.c_float)]
+    import torch
+    arr = (la.Matrix * R)(*mats)
+    out = (ctypes.c_float * n)()
+    st = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    rc = _STEPS_LIB.lamm_steps_isolated(ctypes.cast(arr, ctypes.c_void_p), R, ctypes.byref(Bm), ctypes.byref(Cm), 0, n,
+                                        ctypes.c_void_p(st.cuda_stream), out)
+    torch.cuda.synchronize()
+    if rc != 0:
+        log("lamm_steps_isolated failed:", rc)
+        return None
+    v = sorted(out)
+    return v[n // 2] * 1e-6
 
 
 def config2_gemv(ctx, fmt, M, K, steps, warmup):
@@ -278,11 +317,19 @@ def config2_gemv(ctx, fmt, M, K, steps, warmup):
         a = A[(last % R) * slab_bytes:(last % R + 1) * slab_bytes].view(M, arow)
         sample.update(A=a[sample["rows"]].cpu().numpy(), B=B[:la.row_bytes(vt, K)].cpu().numpy(),
                       C=gathered[sample["rows"]].cpu().numpy())
-    # the rank's kernel alone (no collective): roofline numerator.  1000 launches per graph: the
-    # replay's own start-up (~20-30 us before the first kernel runs) spread over 50 launches of a
-    # ~4 us kernel added ~0.6 us to every launch (profiles/r02/ab_gemv_waves.json: 4.17 us at 200)
-    _, kern, _ = time_steps(ctx, gemv, max(steps, 1000), 3)
-    res = dict(per_step=per_step, ev_step=ev_step, kern=kern, graphed=graphed, R=R, rows=rows,
+    # the rank's kernel alone (no collective): the roofline's per-launch time.  Each launch timed
+    # on its own by HIP events, the stream held until the events and the launch are all enqueued
+    # (tools/steps_loop.hip lamm_steps_isolated): the device's time for one dispatch with nothing
+    # queued behind it -- the duration rocprofv3's kernel trace reports for the same dispatch
+    # (back-to-back launches overlap a dispatch's start with the previous one's tail, and under the
+    # tracer are stretched by its own per-dispatch cost instead)
+    iso = isolated_launches(la, mats, R, Bm, Cm, 300)
+    if iso is not None:
+        kern, kern_method = iso, "median of 300 isolated launches, HIP events around each (lamm_steps_isolated)"
+    else:
+        _, kern, _ = time_steps(ctx, gemv, max(steps, 1000), 3)
+        kern_method = "HIP events over 1000 back-to-back hipGraph-replayed launches on their stream"
+    res = dict(per_step=per_step, ev_step=ev_step, kern=kern, kern_method=kern_method, graphed=graphed, R=R, rows=rows,
                slab_bytes=slab_bytes + la.row_bytes(vt, K) + 4 * rows, gather_check=check, sample=sample)
     del A, B, C
     torch.cuda.empty_cache()
@@ -534,8 +581,11 @@ def llama_step(fmt):
     return res
 
 
-def read_traffic(tag):
-    p = os.path.join(ROOT, "profiles", f"traffic_{tag}.json")
+def read_profile(kind, tag):
+    """A committed per-launch measurement of config 2's kernel (profiles/<kind>_<tag>.json): the
+    PMC traffic (tools/pmc_traffic_flat1.py) or the kernel tracer's paced durations
+    (tools/kt_roofline.py), both written by tools/roofline_trace.sh."""
+    p = os.path.join(ROOT, "profiles", f"{kind}_{tag}.json")
     if os.path.exists(p):
         try:
             return json.load(open(p))
@@ -575,7 +625,9 @@ def main():
     g = config2_gemv(ctx, fmt, M, K, args.steps, args.warmup)
     value = unit / g["per_step"] / 1e9
     achieved = g["slab_bytes"] / g["kern"] / 1e9
-    traffic = read_traffic(f"{fmt}_gemv_single")
+    traffic = read_profile("traffic", f"{fmt}_gemv_single")
+    trace = read_profile("roofline", f"{fmt}_gemv_single")
+    kname = "gemv_flat1_kernel" if la.gemm_engine(fmt, g["rows"], 1, K) == "gemv" and K == 4096 else None
     out = {
         "metric": "Q4_0xQ8_0 GEMM effective GFLOPS @ K=4096; achieved HBM GB/s (GEMV)",
         "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -595,13 +647,24 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic.get("bytes_per_launch") if traffic and traffic.get(
-                         "algorithmic_bytes_per_launch") == g["slab_bytes"] else None,
-                     "traffic_source": f"profiles/traffic_{fmt}_gemv_single.json (rocprofv3 --pmc FETCH_SIZE x2 + "
-                                       "WRITE_SIZE, per launch)",
+                         "algorithmic_bytes_per_launch") == g["slab_bytes"] and traffic.get("kernel") == kname
+                     else None,
+                     "traffic_source": f"profiles/traffic_{fmt}_gemv_single.json (rocprofv3 --pmc FETCH_SIZE + "
+                                       "WRITE_SIZE passes of tools/pmc_flat1.py, FETCH calibrated on a 312 MB launch "
+                                       "of the same body, per launch)",
                      "kernel": "lamm::gemv_flat1_kernel (csrc/lamm_gemv_rpw.hip; gemv_rpw_kernel for other shapes)",
                      "per_launch_us": round(g["kern"] * 1e6, 3),
+                     "per_launch_method": g["kern_method"],
                      "algorithmic_bytes_per_launch": g["slab_bytes"]},
     }
+    if trace and kname and trace.get("algorithmic_bytes_per_launch") == g["slab_bytes"]:
+        # the kernel tracer's own durations of the same kernel, launched one at a time (the tracer
+        # stretches back-to-back dispatches by its own per-dispatch cost)
+        tm = trace["duration_us"]["median"]
+        out["roofline"]["rocprof_paced"] = {
+            "file": f"profiles/roofline_{fmt}_gemv_single.json", "median_us": tm,
+            "frac_at_median": round(g["slab_bytes"] / (tm * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+            "events_over_trace": round(g["kern"] * 1e6 / tm, 4)}
     if g["gather_check"] is not None:
         out["config"]["gather_check"] = g["gather_check"]
     samples = {"gemv_config2": g["sample"]}

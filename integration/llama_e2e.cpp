@@ -8,6 +8,7 @@
 //
 //   llama_e2e [-m model.gguf] [--layers L] [--regen] [-t threads] [-p n_prompt] [-n n_gen]
 //             [-r reps] [--logits out.bin] [--write-only] [--seed S] [--force t0,t1,...]
+//             [--dump DIR] [--dump-mm DIR]
 //
 // --force: teacher forcing -- generation step k feeds token t_k instead of the previous step's
 // argmax (the parity runs feed the reference's own greedy tokens to every build, so each logits
@@ -250,6 +251,72 @@ bool dump_cb(struct ggml_tensor* t, bool ask, void*) {
   return true;
 }
 
+// --dump-mm DIR: the MUL_MAT nodes of block 0, the last block and the output projection, in the
+// warm-up pass's prefill and its first decode step, with their operands as ggml hands them to the
+// mul_mat (src0: the weight blocks or the F16 KV-cache view; src1: the F32 activations; dst) -- so
+// a test can recompute every node with the oracle from exactly the node's own inputs.  Every
+// operand is written row by row ((ne1, ne2, ne3) rows of ne0 elements, the view strides resolved);
+// a weight is written once and referenced by later nodes.  DIR/index.jsonl lists the nodes.
+std::string g_mm_dir;
+bool g_mm_on = false;
+int g_mm_idx = 0, g_mm_layers = 0;
+const char* g_mm_phase = "prefill";
+
+bool mm_selected(const struct ggml_tensor* t) {
+  if (t->op != GGML_OP_MUL_MAT || !t->src[0] || !t->src[1]) return false;
+  const std::string n = t->src[0]->name;
+  if (n == "output.weight") return true;
+  for (int l : {0, g_mm_layers - 1}) {
+    const std::string L = std::to_string(l);
+    if (n.rfind("blk." + L + ".", 0) == 0 || n == "k-" + L || n == "v-" + L) return true;
+  }
+  return false;
+}
+
+void write_rows(const struct ggml_tensor* t, const std::string& path) {
+  FILE* f = fopen(path.c_str(), "wb");
+  if (!f) { perror(path.c_str()); return; }
+  const size_t rb = ggml_row_size(t->type, t->ne[0]);
+  for (int64_t i3 = 0; i3 < t->ne[3]; ++i3)
+    for (int64_t i2 = 0; i2 < t->ne[2]; ++i2)
+      for (int64_t i1 = 0; i1 < t->ne[1]; ++i1)
+        fwrite(static_cast<const char*>(t->data) + i1 * t->nb[1] + i2 * t->nb[2] + i3 * t->nb[3], 1, rb, f);
+  fclose(f);
+}
+
+std::string ne_json(const struct ggml_tensor* t) {
+  char b[160];
+  snprintf(b, sizeof b, "[%lld, %lld, %lld, %lld]", (long long)t->ne[0], (long long)t->ne[1], (long long)t->ne[2],
+           (long long)t->ne[3]);
+  return b;
+}
+
+bool mm_cb(struct ggml_tensor* t, bool ask, void*) {
+  if (ask) return g_mm_on && mm_selected(t);
+  if (!g_mm_on || !mm_selected(t)) return true;
+  const struct ggml_tensor* a = t->src[0];
+  const struct ggml_tensor* b = t->src[1];
+  const int idx = g_mm_idx++;
+  const bool weight = a->view_src == nullptr && a->op == GGML_OP_NONE;
+  std::string a_file = weight ? std::string("w_") + a->name + ".bin" : std::to_string(idx) + "_src0.bin";
+  for (auto& c : a_file)
+    if (c == '/' || c == ' ') c = '_';
+  FILE* probe = weight ? fopen((g_mm_dir + "/" + a_file).c_str(), "rb") : nullptr;
+  if (probe) fclose(probe);
+  else write_rows(a, g_mm_dir + "/" + a_file);
+  write_rows(b, g_mm_dir + "/" + std::to_string(idx) + "_src1.bin");
+  write_rows(t, g_mm_dir + "/" + std::to_string(idx) + "_dst.bin");
+  FILE* ix = fopen((g_mm_dir + "/index.jsonl").c_str(), "ab");
+  if (ix) {
+    fprintf(ix, "{\"idx\": %d, \"phase\": \"%s\", \"name\": \"%s\", \"src0\": \"%s\", \"src0_file\": \"%s\", "
+                "\"type0\": %d, \"ne0\": %s, \"type1\": %d, \"ne1\": %s, \"ne\": %s, \"weight\": %s}\n",
+            idx, g_mm_phase, t->name, a->name, a_file.c_str(), (int)a->type, ne_json(a).c_str(), (int)b->type,
+            ne_json(b).c_str(), ne_json(t).c_str(), weight ? "true" : "false");
+    fclose(ix);
+  }
+  return true;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -275,6 +342,7 @@ int main(int argc, char** argv) {
     else if (a == "--regen") regen = true;
     else if (a == "--write-only") write_only = true;
     else if (a == "--dump") g_dump_dir = next();
+    else if (a == "--dump-mm") g_mm_dir = next();
     else if (a == "--force") {
       for (const char* c = next(); *c;) {
         char* end = nullptr;
@@ -309,6 +377,9 @@ int main(int argc, char** argv) {
   if (!g_dump_dir.empty()) {
     cp.cb_eval = dump_cb;
     g_dump_on = true;
+  } else if (!g_mm_dir.empty()) {
+    cp.cb_eval = mm_cb;
+    g_mm_on = true;
   }
   llama_context* ctx = llama_new_context_with_model(m, cp);
   if (!ctx) { fprintf(stderr, "llama_e2e: cannot create context\n"); return 1; }
@@ -317,6 +388,7 @@ int main(int argc, char** argv) {
     char buf[32] = {0};
     if (llama_model_meta_val_str(m, "llama.block_count", buf, sizeof buf) > 0) n_layer = atoi(buf);
   }
+  g_mm_layers = n_layer;
 
   std::vector<llama_token> prompt(n_prompt);
   uint64_t s = seed * 7919;
@@ -339,6 +411,7 @@ int main(int argc, char** argv) {
     if (llama_decode(ctx, b) != 0) { fprintf(stderr, "llama_decode (prompt) failed\n"); return false; }
     const double t1 = now_ms();
     g_dump_on = false;
+    g_mm_phase = "decode";   // --dump-mm: the first decode step too, then off
     llama_batch_free(b);
     const float* lg = llama_get_logits_ith(ctx, n_prompt - 1);
     if (record) logits_out.insert(logits_out.end(), lg, lg + n_vocab);
@@ -355,6 +428,7 @@ int main(int argc, char** argv) {
       g.logits[0] = 1;
       g.n_tokens = 1;
       if (llama_decode(ctx, g) != 0) { fprintf(stderr, "llama_decode (gen) failed\n"); return false; }
+      g_mm_on = false;
       const float* l2 = llama_get_logits_ith(ctx, 0);
       if (record) logits_out.insert(logits_out.end(), l2, l2 + n_vocab);
       tok = argmax(l2, n_vocab);

@@ -619,3 +619,89 @@ void lo_mul_mat(int type, int M, int N, int K, const void *A, size_t lda_bytes,
       C[(size_t)j * ldc + i] = lo_vec_dot(type, K, (const uint8_t *)A + (size_t)i * lda_bytes,
                                           (const uint8_t *)B + (size_t)j * ldb_bytes);
 }
+
+/* --------------------------------------------------------- the AVX2 float order
+ * The reference's CPU path on x86 (the lamm opt-3 AVX2 kernels, src/lamm_kernel_q*.hpp
+ * lamm_simd_block_kernel / lamm_simd_kernel with src/lamm_simd_avx2.h; for q6_K, which lamm
+ * declines, ggml's AVX2 ggml_vec_dot_q6_K_q8_K, LC/ggml-quants.c:8305-8385) keeps EIGHT fp32
+ * accumulators per output -- one per 32-bit lane of an __m256 -- and for every block / super-block
+ * adds d * (float)X_l into lane l with a fused multiply-add (_mm256_fmadd_ps), where X_l is the
+ * exact int32 sum of the 4 products (block formats: elements 4l..4l+3, through
+ * mul_sum_i8_pairs_float / mul_sum_us8_pairs_float) or of the scaled group sums (q6_K: positions
+ * 4l..4l+3 of each of the 8 32-element groups) that land in lane l, and d = fp32(d_a) * fp32(d_b)
+ * rounded once.  The lanes then meet in reduce_sum's tree (src/lamm_simd_avx2.h:117-127, the same
+ * as hsum_float_8): ((a0 + a4) + (a2 + a6)) + ((a1 + a5) + (a3 + a7)).  q4_1 / q5_1 add
+ * sum_k fp32(m_a) * fp32(s_b) (a separate fp32 sum, :lamm_kernel_q4_1.hpp) after the tree; f32
+ * keeps element 8i + l in lane l (src/lamm_kernel_f32.hpp).
+ * q8_0 is not restated here: lamm's AVX2 q8_0 kernel treats the weight quants as unsigned
+ * (mul_sum_us8_pairs_float, SURVEY §8a defect 2), so its output is not the product. */
+static float tree8(const float *a) {
+  const float x0 = a[0] + a[4], x1 = a[1] + a[5], x2 = a[2] + a[6], x3 = a[3] + a[7];
+  return (x0 + x2) + (x1 + x3);
+}
+
+/* quant e (0..31) of a 32-element block, with the format's offset (q4_0: q - 8, q5_0: q - 16) */
+static int blk_q(int type, const uint8_t *a, int e) {
+  const int j = e & 15, hi = e >= 16;
+  switch (type) {
+  case LO_Q4_0: return (hi ? a[2 + j] >> 4 : a[2 + j] & 0xF) - 8;
+  case LO_Q4_1: return hi ? a[4 + j] >> 4 : a[4 + j] & 0xF;
+  case LO_Q5_0: case LO_Q5_1: {
+    const int qs = type == LO_Q5_0 ? 6 : 8;
+    uint32_t qh; memcpy(&qh, a + (type == LO_Q5_0 ? 2 : 4), 4);
+    const int q = (hi ? a[qs + j] >> 4 : a[qs + j] & 0xF) | (((qh >> e) & 1) << 4);
+    return type == LO_Q5_0 ? q - 16 : q;
+  }
+  default: return 0;
+  }
+}
+
+float lo_vec_dot_avx(int type, int k, const void *va, const void *vb) {
+  const uint8_t *a = (const uint8_t *)va, *b = (const uint8_t *)vb;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (type == LO_F32) {
+    const float *x = (const float *)va, *y = (const float *)vb;
+    for (int i = 0; i < k; i += 8)
+      for (int l = 0; l < 8; ++l) acc[l] = fmaf(x[i + l], y[i + l], acc[l]);
+    return tree8(acc);
+  }
+  const size_t ab = lo_block_bytes(type), bb = lo_block_bytes(lo_vec_dot_type(type));
+  if (type == LO_Q6_K) {
+    for (int i = 0; i < k / 256; ++i, a += ab, b += bb) {
+      float yd; memcpy(&yd, b, 4);
+      const int8_t *q8 = (const int8_t *)(b + 4);
+      const float d = yd * H2F(rd16(a + 208));
+      int32_t X[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (int h = 0; h < 8; ++h)          /* 32-element group h = 4 j + g: elements 32 h .. */
+        for (int e = 0; e < 32; ++e) {
+          const int y = 32 * h + e;
+          X[e / 4] += (int8_t)a[192 + y / 16] * (q6_value(a, y) * q8[y]);
+        }
+      for (int l = 0; l < 8; ++l) acc[l] = fmaf(d, (float)X[l], acc[l]);
+    }
+    return tree8(acc);
+  }
+  if (type != LO_Q4_0 && type != LO_Q4_1 && type != LO_Q5_0 && type != LO_Q5_1) return 0.0f;
+  const int aff = type == LO_Q4_1 || type == LO_Q5_1;
+  const int8_t *bq;
+  float summs = 0.0f;
+  for (int i = 0; i < k / 32; ++i, a += ab, b += bb) {
+    bq = (const int8_t *)(b + (aff ? 4 : 2));
+    const float d = H2F(rd16(a)) * H2F(rd16(b));
+    for (int l = 0; l < 8; ++l) {
+      int X = 0;
+      for (int e = 4 * l; e < 4 * l + 4; ++e) X += blk_q(type, a, e) * bq[e];
+      acc[l] = fmaf(d, (float)X, acc[l]);
+    }
+    if (aff) summs += H2F(rd16(a + 2)) * H2F(rd16(b + 2));
+  }
+  return tree8(acc) + summs;
+}
+
+void lo_mul_mat_avx(int type, int M, int N, int K, const void *A, size_t lda_bytes,
+                    const void *B, size_t ldb_bytes, float *C, size_t ldc) {
+  for (int j = 0; j < N; j++)
+    for (int i = 0; i < M; i++)
+      C[(size_t)j * ldc + i] = lo_vec_dot_avx(type, K, (const uint8_t *)A + (size_t)i * lda_bytes,
+                                              (const uint8_t *)B + (size_t)j * ldb_bytes);
+}

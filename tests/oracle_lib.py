@@ -63,6 +63,7 @@ class Oracle:
         L.lo_mul_mat.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                  ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t,
                                  ctypes.c_void_p, ctypes.c_size_t]
+        L.lo_mul_mat_avx.argtypes = L.lo_mul_mat.argtypes
         L.lo_fp32_to_fp16.restype = ctypes.c_uint16
         L.lo_fp32_to_fp16.argtypes = [ctypes.c_float]
         L.lo_fp16_to_fp32.restype = ctypes.c_float
@@ -106,4 +107,15 @@ class Oracle:
         C = np.zeros((N, M), dtype=np.float32)
         self.L.lo_mul_mat(t, M, N, K, A.ctypes.data, self.row_bytes(t, K), B.ctypes.data,
                           self.row_bytes(vt, K), C.ctypes.data, M)
+        return C
+
+    def mul_mat_avx(self, t, M, N, K, A, B):
+        """C[N][M] in the reference's x86 float order (lo_vec_dot_avx: the lamm opt-3 AVX2
+        kernels' eight FMA lanes and their reduction tree; ggml's AVX2 q6_K)."""
+        A = np.ascontiguousarray(A, dtype=np.uint8)
+        B = np.ascontiguousarray(B, dtype=np.uint8)
+        vt = self.vec_dot_type(t)
+        C = np.zeros((N, M), dtype=np.float32)
+        self.L.lo_mul_mat_avx(t, M, N, K, A.ctypes.data, self.row_bytes(t, K), B.ctypes.data,
+                              self.row_bytes(vt, K), C.ctypes.data, M)
         return C

@@ -148,3 +148,34 @@ def test_llama_32_layers_vs_reference(model32, tmp_path):
           f"top-2 gaps of the flipped rows {[round(float(gap[i]), 4) for i in flips_gpu]}")
     assert float(err_rows.max()) <= 1.5 * spread + 1e-4
     assert all(gap[i] <= 0.15 for i in flips_gpu)
+
+
+KINDS = {"wq", "wk", "wv", "wo", "w1", "w2", "w3", "KQ", "KQV"}
+
+
+@pytest.mark.parametrize("views", ["default", "views_on_gpu"])
+def test_llama_32_layers_matmul_nodes_vs_oracle(model32, tmp_path, views):
+    """Every kind of mul_mat llama.cpp-b2430's graph sends through the boundary (llama.cpp:5708-5830:
+    wq, wk, wv, wo, w1 = ffn_gate, w2 = ffn_down, w3 = ffn_up, KQ, KQV), in block 0 and the last
+    block of the 32-layer model, plus the Q6_K output.weight, in the prefill (GEMM engines, GPU F16
+    attention on the KV-cache views) and in a decode step (GEMVs): the HIP build dumps each node's
+    operands and result (llama_e2e --dump-mm) and the oracle recomputes the node from exactly those
+    operands.  Bar: the north-star 1e-3 of max(|c|, sum |a b|) per element (observed ~1e-7).
+    views_on_gpu: the decode step's attention matmuls on the GPU too (LAMM_HIP_VIEWS=1; by default
+    ggml keeps them)."""
+    import llama_nodes as ln
+    d = tmp_path / "mm"
+    d.mkdir()
+    env = dict(os.environ, **({"LAMM_HIP_VIEWS": "1"} if views == "views_on_gpu" else {}))
+    r = subprocess.run([HIP, "-m", model32, "-t", "16", "-p", "32", "-n", "1", "--dump-mm", str(d)],
+                       capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    res = ln.check_nodes(str(d), workers=12)
+    for phase, layer, kind, name, shape, err in res:
+        print(f"{phase:8s} layer {layer:3d} {kind:6s} {name:16s} M,N,K,slices={shape}: {err:.2e}")
+    assert all(err < 1e-3 for *_, err in res), [x for x in res if x[-1] >= 1e-3]
+    seen = {(p, l, k) for p, l, k, *_ in res}
+    for phase in ("prefill", "decode"):
+        assert (phase, -1, "output") in seen
+        for layer in (0, 31):
+            assert {k for p, l, k in seen if p == phase and l == layer} == KINDS, (phase, layer)

@@ -66,6 +66,29 @@ def test_oracle_vs_reference_avx_paths_within_tolerance(path):
         assert err.max() < 1e-5
 
 
+AVX_ORDER = ("f32", "q4_0", "q4_1", "q5_0", "q5_1", "q6_k")
+
+
+@pytest.mark.parametrize("path", [p for p in FIXTURES if _ids([p])[0].rsplit("_", 1)[0] in AVX_ORDER],
+                         ids=_ids([p for p in FIXTURES if _ids([p])[0].rsplit("_", 1)[0] in AVX_ORDER]))
+def test_avx_order_matches_lamm3_bit_exact(path):
+    """lo_mul_mat_avx restates the reference's x86 float order (the lamm opt-3 AVX2 kernels'
+    eight FMA lanes + reduce_sum's tree; ggml's AVX2 q6_K for the format lamm declines): bit for
+    bit the reference's own lamm3 output on every row it computed (rows >= 4 (M // 4) are SURVEY
+    §8a defect 1's unwritten tail).  This is the order the boundary's reference-order kernels
+    (csrc/lamm_ref.hip) reproduce on the GPU."""
+    z = load_fixture(path)
+    t, M, N, K = int(z["type"]), int(z["M"]), int(z["N"]), int(z["K"])
+    if t == ol.F32:
+        a, b = load_inputs(M, N, K)
+        A, B = a.view(np.uint8).reshape(-1), b.view(np.uint8).reshape(-1)
+    else:
+        A, B = z["A_q"], z["B_avx"]
+    c = ORACLE.mul_mat_avx(t, M, N, K, A, B)
+    done = M if t in ol.KQ_TYPES else 4 * (M // 4)   # q6_K is ggml's own loop: every row
+    assert np.array_equal(c[:, :done].view(np.uint32), z["C_lamm3"][:, :done].view(np.uint32))
+
+
 def test_fp16_round_trip_exhaustive():
     L = ORACLE.L
     for h in range(0, 0x10000, 7):

@@ -106,6 +106,17 @@ typedef struct lamm_batch {
 int lamm_hip_matmul_batched(const lamm_matrix *A, const lamm_matrix *B, const lamm_matrix *C,
                             const lamm_batch *batch, void *hip_stream);
 
+/* lamm_hip_matmul_batched with flags.  LAMM_ORDER_REFERENCE: compute every output in the
+ * reference's own x86 float order -- the lamm opt-3 AVX2 kernels' eight fp32 FMA lanes per output
+ * and reduce_sum's tree (src/lamm_kernel_q4_0.hpp:59-128, src/lamm_simd_avx2.h:117-127), ggml's
+ * AVX2 ggml_vec_dot_q6_K_q8_K for q6_K (LC/ggml-quants.c:8305-8385) -- so C is bit-identical to
+ * the reference's CPU build on the same blocks (VALU kernels, slower than the default engines).
+ * Supported: q4_0 / q5_0 with q8_0 B, q4_1 / q5_1 with q8_1 B, q6_K with q8_K B (quantized B
+ * only); others return LAMM_ERR_TYPE.  The ggml boundary uses it by default (LAMM_HIP_ORDER). */
+#define LAMM_ORDER_REFERENCE 1
+int lamm_hip_matmul_ex(const lamm_matrix *A, const lamm_matrix *B, const lamm_matrix *C,
+                       const lamm_batch *batch, int flags, void *hip_stream);
+
 /* Activation quantizer on device (ggml INIT phase, LC/ggml.c:10865-10887, run on
  * the GPU): x[N][K] f32 (row j at x + j*ldx floats) -> y, N rows of `vec_type`
  * blocks (row j at y + j*ldy blocks).  flavour 0 = *_reference rounding

@@ -358,6 +358,7 @@ template <int T> struct KQ;
 template <> struct KQ<kQ2_K> { static constexpr int BPB = 84; };
 template <> struct KQ<kQ4_K> { static constexpr int BPB = 144; };
 template <> struct KQ<kQ5_K> { static constexpr int BPB = 176; };
+template <> struct KQ<kQ6_K> { static constexpr int BPB = 210; };
 
 template <int T, int ITER>
 __global__ __launch_bounds__(512) void gemv_kq_kernel(const unsigned char* A, int64_t lda, const unsigned char* B,
@@ -377,14 +378,38 @@ __global__ __launch_bounds__(512) void gemv_kq_kernel(const unsigned char* A, in
   }
   __builtin_amdgcn_sched_barrier(0);   // the activation loads first in the vmcnt order
   const auto ra = make_rsrc(A + (int64_t)(row < M ? row : 0) * lda, ((uint32_t)nsb * BPB + 3) & ~3u);
-  // this lane's bytes of each of its super-blocks: qs (32 B), the header, and for q5_K qh (32 B)
+  // this lane's bytes of each of its super-blocks: qs (32 B), the header, and for q5_K qh (32 B);
+  // q6_K: ql (2 x 16 B) and qh (16 B) of its 64 elements, 2-byte aligned (210-byte super-blocks)
   u32x4 qa[ITER][2], hd[ITER], qh[ITER][2];
-  uint32_t sc[ITER];
+  uint32_t sc[ITER], sc6[ITER][2];
 #pragma unroll
   for (int c = 0; c < ITER; ++c) {
     const int sb = 16 * c + (lane >> 2);
     const uint32_t base = sb < nsb ? (uint32_t)sb * BPB : 0x7fff0000u;
-    if constexpr (T == kQ2_K) {
+    if constexpr (T == kQ6_K) {
+      // quarter qq = (half j, 16-element column t): elements 128 j + 32 g + 16 t + i (g < 4, i < 16):
+      // ql[64 j + 16 t ..] (g = 0, 2: low / high nibbles), ql[64 j + 32 + 16 t ..] (g = 1, 3),
+      // qh[32 j + 16 t ..] (bits 2 g), scales sc[8 j + 2 g + t], d at 208
+      const int j = qq >> 1, t = qq & 1;
+      const uint32_t b4 = base & ~3u;
+      const int shb = (int)(base & 3u) * 8;
+      auto chunk16 = [&](uint32_t o) {   // 16 bytes at base + o (o a multiple of 4)
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(ra, b4 + o, 0, 2);
+        const uint32_t w4 = __builtin_amdgcn_raw_buffer_load_b32(ra, b4 + o + 16, 0, 2);
+        return u32x4{__builtin_amdgcn_alignbit(v[1], v[0], shb), __builtin_amdgcn_alignbit(v[2], v[1], shb),
+                     __builtin_amdgcn_alignbit(v[3], v[2], shb), __builtin_amdgcn_alignbit(w4, v[3], shb)};
+      };
+      qa[c][0] = chunk16(64 * j + 16 * t);
+      qa[c][1] = chunk16(64 * j + 32 + 16 * t);
+      qh[c][0] = chunk16(128 + 32 * j + 16 * t);
+      // scales 8 j .. 8 j + 7 and d (bytes 192 + 8 j .., 208): three dwords from the dword below
+      const uint32_t s0 = __builtin_amdgcn_raw_buffer_load_b32(ra, b4 + 192 + 8 * j, 0, 2);
+      const uint32_t s1 = __builtin_amdgcn_raw_buffer_load_b32(ra, b4 + 196 + 8 * j, 0, 2);
+      const uint32_t s2 = __builtin_amdgcn_raw_buffer_load_b32(ra, b4 + 200 + 8 * j, 0, 2);
+      sc6[c][0] = __builtin_amdgcn_alignbit(s1, s0, shb);
+      sc6[c][1] = __builtin_amdgcn_alignbit(s2, s1, shb);
+      hd[c][0] = __builtin_amdgcn_raw_buffer_load_b32(ra, b4 + 208, 0, 2);   // d = bits [shb, shb + 16)
+    } else if constexpr (T == kQ2_K) {
       const uint32_t qo = base + 16 + 32 * (qq >> 1);
       qa[c][0] = __builtin_amdgcn_raw_buffer_load_b128(ra, qo, 0, 2);
       qa[c][1] = __builtin_amdgcn_raw_buffer_load_b128(ra, qo + 16, 0, 2);
@@ -424,7 +449,30 @@ __global__ __launch_bounds__(512) void gemv_kq_kernel(const unsigned char* A, in
     const float yd = __builtin_bit_cast(float, a[0]);
     int isum = 0, summs = 0;
     uint32_t dd;
-    if constexpr (T == kQ2_K) {
+    if constexpr (T == kQ6_K) {
+      // (q - 32) b = q b - 32 b: the sum of b per 16 elements is the q8_K bsum of that group
+      const int j = qq >> 1, t = qq & 1;
+      dd = (hd[c][0] >> (((uint32_t)(16 * c + (lane >> 2)) * 210u & 3u) * 8)) & 0xffffu;
+      const u32x4 bj[4] = {*reinterpret_cast<const u32x4*>(a + 4 + 32 * j + 4 * t),
+                           *reinterpret_cast<const u32x4*>(a + 4 + 32 * j + 8 + 4 * t),
+                           *reinterpret_cast<const u32x4*>(a + 4 + 32 * j + 16 + 4 * t),
+                           *reinterpret_cast<const u32x4*>(a + 4 + 32 * j + 24 + 4 * t)};
+      const uint32_t* bs = a + 68;   // 16 int16 bsums, two per dword
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        int part = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t lo = (qa[c][g & 1][k] >> (g >= 2 ? 4 : 0)) & 0x0f0f0f0fu;
+          const uint32_t q = lo | (((qh[c][0][k] >> (2 * g)) & 0x03030303u) << 4);
+          part = dot4(q, bj[g][k], part);
+        }
+        const int bi = 8 * j + 2 * g + t;
+        const int bsum = (int)(int16_t)((bs[bi >> 1] >> (16 * (bi & 1))) & 0xffffu);
+        const int scv = (int)(int8_t)((sc6[c][g >> 1] >> (8 * (2 * (g & 1) + t))) & 0xffu);
+        isum += scv * (part - 32 * bsum);
+      }
+    } else if constexpr (T == kQ2_K) {
       dd = hd[c][0];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {   // sub-block s = 4 qq + i: half i & 1 of the qs run, shift 2 jj
@@ -468,8 +516,12 @@ __global__ __launch_bounds__(512) void gemv_kq_kernel(const unsigned char* A, in
     summs += __builtin_amdgcn_update_dpp(0, summs, 0xB1, 0xF, 0xF, false);
     summs += __builtin_amdgcn_update_dpp(0, summs, 0x4E, 0xF, 0xF, false);
     if (qq == 0 && sb < nsb) {
-      const float da = h2f(dd & 0xffffu), dm = h2f(dd >> 16);
-      acc += (yd * da) * (float)isum - (yd * dm) * (float)summs;
+      if constexpr (T == kQ6_K) {
+        acc += (yd * h2f(dd)) * (float)isum;
+      } else {
+        const float da = h2f(dd & 0xffffu), dm = h2f(dd >> 16);
+        acc += (yd * da) * (float)isum - (yd * dm) * (float)summs;
+      }
     }
   }
   acc = wave_sum(acc);
@@ -548,9 +600,10 @@ hipError_t launch_rpw_t(const GemvArgs& p, hipStream_t s, int waves) {
 // wave-group stream wins once the grid is long); q5_K (each lane also reads the whole 32-byte qh)
 // faster at 4096 only.
 bool gemv_kq_supported(int type, const GemvArgs& p) {
-  const int max_rows = type == kQ5_K ? 6144 : 16384;
-  return (type == kQ2_K || type == kQ4_K || type == kQ5_K) && p.N == 1 && p.ne12 * p.ne13 == 1 && p.nblk <= 48 &&
-         p.M <= max_rows && p.flag == nullptr && p.b_f32 == 0;
+  // q6_K: every row count (a Q4_0 model's 32000-row output.weight, llama.cpp:11731-11742)
+  const int max_rows = type == kQ6_K ? (1 << 30) : type == kQ5_K ? 6144 : 16384;
+  return (type == kQ2_K || type == kQ4_K || type == kQ5_K || type == kQ6_K) && p.N == 1 && p.ne12 * p.ne13 == 1 &&
+         p.nblk <= 48 && p.M <= max_rows && p.flag == nullptr && p.b_f32 == 0;
 }
 
 hipError_t launch_gemv_kq(int type, const GemvArgs& p, hipStream_t s) {
@@ -565,6 +618,7 @@ hipError_t launch_gemv_kq(int type, const GemvArgs& p, hipStream_t s) {
     case kQ2_K: go(std::integral_constant<int, kQ2_K>{}); break;
     case kQ4_K: go(std::integral_constant<int, kQ4_K>{}); break;
     case kQ5_K: go(std::integral_constant<int, kQ5_K>{}); break;
+    case kQ6_K: go(std::integral_constant<int, kQ6_K>{}); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

@@ -213,7 +213,7 @@ struct Completion {
 thread_local Completion* g_completion = nullptr;
 
 int matmul_impl(const lamm_matrix* A, const lamm_matrix* B, const lamm_matrix* C, const lamm_batch* batch,
-                void* hip_stream, const lamm_weights* W) {
+                void* hip_stream, const lamm_weights* W, int flags = 0) {
   Completion* done = g_completion;
   g_completion = nullptr;
   if (!A || !B || !C) return fail(LAMM_ERR_SHAPE, "null matrix");
@@ -266,6 +266,13 @@ int matmul_impl(const lamm_matrix* A, const lamm_matrix* B, const lamm_matrix* C
   p.sc3 = (int64_t)(bt.nbc3 / 4);
   p.b_f32 = b_f32 ? 1 : 0;
   hipError_t e;
+  if (flags & LAMM_ORDER_REFERENCE) {   // the reference's x86 float order (lamm_ref.hip), bit for bit
+    if (!ref_order_supported(A->type, B->type))
+      return fail(LAMM_ERR_TYPE, "no reference-order kernel for A type %d with B type %d", A->type, B->type);
+    e = launch_ref(A->type, p, s);
+    if (e != hipSuccess) return fail(LAMM_ERR_HIP, "kernel launch: %s", hipGetErrorString(e));
+    return LAMM_OK;
+  }
   const bool b_al4 = (ldb & 3) == 0 && ((uintptr_t)B->data & 3) == 0 && (bt.nbb2 & 3) == 0 && (bt.nbb3 & 3) == 0;
   switch (pick_engine(A->type, p, W && W->packed, b_al4)) {
     case kEngGemv:
@@ -399,6 +406,11 @@ extern "C" void lamm_hip_weights_destroy(lamm_weights* W) {
 extern "C" int lamm_hip_matmul(const lamm_matrix* A, const lamm_matrix* B, const lamm_matrix* C,
                                void* hip_stream) {
   return lamm_hip_matmul_batched(A, B, C, nullptr, hip_stream);
+}
+
+extern "C" int lamm_hip_matmul_ex(const lamm_matrix* A, const lamm_matrix* B, const lamm_matrix* C,
+                                  const lamm_batch* batch, int flags, void* hip_stream) {
+  return matmul_impl(A, B, C, batch, hip_stream, nullptr, flags);
 }
 
 extern "C" int lamm_hip_quantize(int vec_type, int flavour, const float* x, int64_t ldx, void* y,
@@ -803,10 +815,21 @@ constexpr int64_t kViewMinRows = 8;
 bool views_accepted(const ggml::tensor* src0, const ggml::tensor* src1) {
   if (is_weight(src0)) return true;
   if (knobs().views >= 0) return knobs().views == 1;
+  // in the reference's float order the F16 views stay with ggml (no reference-order F16 kernel:
+  // the reference's own routing, LAMM_HIP_VIEWS=1 takes them anyway)
+  if (knobs().ref_order) return false;
   return src1->ne[1] >= kViewMinRows;
 }
 
 bool extra_types_enabled() { return knobs().extra_types; }
+
+// The boundary computes in the reference's own x86 float order (lamm_ref.hip: the lamm opt-3 AVX2
+// lanes; ggml's AVX2 q6_K) for every format that has that kernel, so llama.cpp through the hook
+// produces the bits the reference's CPU build produces.  LAMM_HIP_ORDER=fast: the
+// fast engines (exact block dots, another fp32 summation order).
+bool boundary_ref_order(const ggml::tensor* src0) {
+  return knobs().ref_order && ref_order_supported(src0->type, vec_dot_type(src0->type));
+}
 
 // How an F32 src1 reaches the kernels (ggml's INIT phase quantizes it on thread 0, serially:
 // LC/ggml.c:10865-10887).  Whenever the GPU takes it over, the hook claims the INIT phase too
@@ -829,7 +852,10 @@ ActMode act_mode(const ggml::tensor* src0, const ggml::tensor* src1) {
   if (!f32_rows) return kCpuInit;
   const int gq = knobs().gpu_quant;
   if (gq == 0) return kCpuInit;
-  if (knobs().fused && gq != 1 && (vdt == kQ8_0 || vdt == kQ8_1) && src1->ne[1] <= 8 && is_weight(src0))
+  // the reference-order kernels take quantized rows: ggml's own INIT for decode-sized calls, the GPU
+  // quantizer (the same AVX2-flavour bytes) from 8 rows up
+  if (knobs().fused && gq != 1 && (vdt == kQ8_0 || vdt == kQ8_1) && src1->ne[1] <= 8 && is_weight(src0) &&
+      !boundary_ref_order(src0))
     return kFused;
   const int64_t rows = src1->ne[1] * src1->ne[2] * src1->ne[3];
   if (gq != 1 && rows < 8) return kCpuInit;
@@ -937,6 +963,7 @@ extern "C" void lamm_mul_mat(const struct ggml_compute_params* vparams, struct g
   const size_t b_row = (size_t)kb * block_bytes(vdt);           // ggml_row_size(vdt, ne10)
   const bool use_wdata = src1->type != vdt;
   const ActMode act = use_wdata ? act_mode(src0, src1) : kCpuInit;
+  const bool ref = boundary_ref_order(src0);
   const int64_t M = ne01, N = ne11, nslices = ne12 * ne13;
 
   Runtime& rt = Runtime::get();
@@ -1037,7 +1064,7 @@ extern "C" void lamm_mul_mat(const struct ggml_compute_params* vparams, struct g
       dB = dX;
       // q8_0 / q8_1 activations are quantized by the library inside the kernels that read them;
       // q8_K / f16 ones here
-      if (act == kGpuQuant && vdt != kQ8_0 && vdt != kQ8_1) {
+      if (act == kGpuQuant && (ref || (vdt != kQ8_0 && vdt != kQ8_1))) {
         void* dq = d.scratch(0, b_row * (size_t)(N * nslices) + 64);
         const int qrc = lamm_hip_quantize(vdt, /*AVX2 flavour*/ 1, dX, ldx, dq, kb, (int)ne00, (int)(N * nslices), s);
         if (qrc != LAMM_OK) {
@@ -1054,7 +1081,7 @@ extern "C" void lamm_mul_mat(const struct ggml_compute_params* vparams, struct g
       HIPCHK(hipMemcpy2DAsync(dB, b_row, src1->data, src1->nb[1], b_row, (size_t)(N * nslices), hipMemcpyHostToDevice,
                               s));
     }
-    const bool b_f32 = act == kFused || (act == kGpuQuant && (vdt == kQ8_0 || vdt == kQ8_1));
+    const bool b_f32 = act == kFused || (act == kGpuQuant && !ref && (vdt == kQ8_0 || vdt == kQ8_1));
     const size_t b_pitch = b_f32 ? x_row : b_row;
     // C: zero-copy = this device's rows [r0, r0 + rows) of the pinned [slice][N][M] image; else a
     // dense [slice][N][rows] scratch copied into dst below
@@ -1075,7 +1102,7 @@ extern "C" void lamm_mul_mat(const struct ggml_compute_params* vparams, struct g
     pa.ne13 = (int)ne13;
     pa.r2 = (int)(ne12 / ne02);
     pa.r3 = (int)(ne13 / ne03);
-    const bool stationary = weight && N > gemv_max_n(t0) && (!b_f32 || N > 8) &&
+    const bool stationary = !ref && weight && N > gemv_max_n(t0) && (!b_f32 || N > 8) &&
                             ((gemm_fp6_supported(t0) && gemm_path(pa, true) == 0) ||
                              (gemm_kq_supported(t0) && knobs().kq_gemm));
     Completion comp{d.done_ctr, d.flag_dev, 0, false};
@@ -1084,7 +1111,7 @@ extern "C" void lamm_mul_mat(const struct ggml_compute_params* vparams, struct g
       g_completion = &comp;
     }
     const int rc = stationary ? lamm_hip_matmul_weights(rt.prepared(d, *w, A, ne02, ne03), &B, &C, &bt, s)
-                              : lamm_hip_matmul_batched(&A, &B, &C, &bt, s);
+                              : lamm_hip_matmul_ex(&A, &B, &C, &bt, ref ? LAMM_ORDER_REFERENCE : 0, s);
     g_completion = nullptr;
     d.pending = comp.signaled ? comp.seq : 0;
     if (rc != LAMM_OK) {

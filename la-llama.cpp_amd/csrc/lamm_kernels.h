@@ -67,6 +67,11 @@ void set_max_lds(const void* kernel, int bytes);
 // completion flag (lamm_signal.hip): stores seq into *flag_dev after everything queued on s
 hipError_t launch_signal(unsigned* flag_dev, unsigned seq, hipStream_t s);
 
+// mul_mat in the reference's x86 float order, bit for bit (lamm_ref.hip): q4_0 / q5_0 x q8_0,
+// q4_1 / q5_1 x q8_1, q6_K x q8_K; any N, batch slices
+bool ref_order_supported(int type, int btype);
+hipError_t launch_ref(int type, const GemvArgs& p, hipStream_t s);
+
 hipError_t launch_gemm(int type, const GemvArgs& p, void* workspace, hipStream_t s);
 size_t gemm_workspace_bytes(int type, const GemvArgs& p);   // device scratch launch_gemm needs
 bool gemm_supported(int type);

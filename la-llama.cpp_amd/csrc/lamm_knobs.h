@@ -39,7 +39,9 @@ struct Knobs {
   bool spin = true;            // LAMM_HIP_SPIN=0: hipStreamSynchronize instead of the flag spin
   bool kernel_signal = false;  // LAMM_HIP_KERNEL_SIGNAL=1: the GEMV writes the completion flag
   int zero_copy = 3;           // LAMM_HIP_ZERO_COPY: 0 off, 1 in, 2 out, 3 both
-  bool zero_copy_split = false;  // LAMM_HIP_ZERO_COPY_SPLIT=1: zero copy also when rows split over devices
+  bool zero_copy_split = false;
+  bool ref_order = true;       // LAMM_HIP_ORDER=fast: the boundary runs the fast engines instead of the
+                               // reference's float order (lamm_ref.hip) for the formats that have both  // LAMM_HIP_ZERO_COPY_SPLIT=1: zero copy also when rows split over devices
 };
 
 // The current switches (read from the environment at the first call).

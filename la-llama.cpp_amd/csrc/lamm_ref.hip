@@ -1,0 +1,297 @@
+// lamm_ref.hip -- mul_mat in the reference's own x86 float order, bit for bit.
+//
+// The reference's CPU path (the lamm opt-3 AVX2 kernels, src/lamm_kernel_q*.hpp
+// lamm_simd_block_kernel with src/lamm_simd_avx2.h; for q6_K, which lamm declines, ggml's AVX2
+// ggml_vec_dot_q6_K_q8_K, LC/ggml-quants.c:8305-8385) computes every output with EIGHT fp32
+// accumulators -- the lanes of one __m256 -- and per block (super-block for q6_K):
+//     acc_l = fma(d, (float)X_l, acc_l),   l = 0..7
+// with d = fp32(d_a) * fp32(d_b) rounded once and X_l the exact int32 sum of what lands in lane l:
+//     q4_0 / q4_1 / q5_0 / q5_1 : elements 4l .. 4l+3 of the 32-element block
+//                                 (mul_sum_i8_pairs_float / mul_sum_us8_pairs_float)
+//     q6_K                      : positions 4l .. 4l+3 of each of the 8 32-element groups h,
+//                                 times the group half's int8 scale sc[2h + (l >= 4)]
+// then the fixed tree ((a0+a4) + (a2+a6)) + ((a1+a5) + (a3+a7)) (reduce_sum / hsum_float_8);
+// q4_1 / q5_1 add the separate fp32 sum of fp32(m_a) * fp32(s_b) after it.  oracle/lamm_oracle.c
+// lo_vec_dot_avx restates this and is pinned bit-exact to the reference's own lamm3 output
+// (tests/test_oracle_golden.py::test_avx_order_matches_lamm3_bit_exact).
+//
+// The ggml boundary runs its calls here by default (LAMM_HIP_ORDER=reference), so
+// llama.cpp through the boundary computes the same bits as the reference's CPU build; the device
+// API keeps the fast engines (lamm_hip_matmul) and offers this order as lamm_hip_matmul_ex(...,
+// LAMM_ORDER_REFERENCE, ...).
+//
+// Layout: a workgroup owns 16 / 32 rows x NCOL columns (1, 2, 4 or 8 by N); thread (row r, lane l)
+// runs the NCOL column chains of lane l for row r (the A quads it decodes are shared by the columns).
+// Per chunk of K both operands come through LDS: the rows' raw block bytes by coalesced 16-byte
+// loads (the 2-byte aligned blocks read back with a realignment), the activation columns as quads
+// laid out [column][lane][unit].  The quants are turned into signed bytes (q - 8,
+// q - 16, q - 32) so each X_l is one v_dot4 -- integer, exact, any order.
+#include "lamm_device.h"
+#include "lamm_kernels.h"
+
+namespace lamm {
+namespace {
+
+constexpr int RR = 32;           // rows per workgroup (16 for decode calls: launch_ref)
+
+template <int T> struct RefFmt;
+// BPB: A block bytes; QS / QH / M: byte offsets of the quants, the 5th bits, m (-1: none);
+// OFF: the signed-byte offset of the quants (their unsigned maximum + 1, halved); UE: elements per unit
+template <> struct RefFmt<kQ4_0> { static constexpr int BPB = 18, QS = 2, QH = -1, M = -1, OFF = 8, UE = 32, VB = 34; };
+template <> struct RefFmt<kQ4_1> { static constexpr int BPB = 20, QS = 4, QH = -1, M = 2, OFF = 0, UE = 32, VB = 36; };
+template <> struct RefFmt<kQ5_0> { static constexpr int BPB = 22, QS = 6, QH = 2, M = -1, OFF = 16, UE = 32, VB = 34; };
+template <> struct RefFmt<kQ5_1> { static constexpr int BPB = 24, QS = 8, QH = 4, M = 2, OFF = 0, UE = 32, VB = 36; };
+template <> struct RefFmt<kQ6_K> { static constexpr int BPB = 210, QS = 0, QH = 128, M = -1, OFF = 32, UE = 256, VB = 292; };
+
+// units of K per LDS chunk, and the dwords of quads one (column, lane, unit) holds
+template <int T> constexpr int ref_kch() { return RefFmt<T>::UE == 256 ? 8 : 64; }
+template <int T> constexpr int ref_qw() { return RefFmt<T>::UE / 32; }   // groups per lane: 1 or 8
+
+// unsigned quant bytes (0 .. 2 OFF - 1) -> signed (q - OFF), bytewise: flip the top bit of the
+// field, then copy it into the bits above (the multiply stays inside each byte)
+template <int OFF>
+__device__ __forceinline__ uint32_t to_signed(uint32_t q) {
+  if constexpr (OFF == 0) {
+    return q;
+  } else {
+    constexpr uint32_t top = (uint32_t)OFF * 0x01010101u;                  // the field's top bit per byte
+    constexpr uint32_t ext = (uint32_t)(0x100 - 2 * OFF) / (uint32_t)OFF;   // top bit * ext = the bits above it
+    const uint32_t t = q ^ top;
+    return t | ((t & top) * ext);
+  }
+}
+
+// one dword at a 2-byte aligned byte offset of an LDS row image
+__device__ __forceinline__ uint32_t lds32(const uint32_t* row, int byte) {
+  const int i = byte >> 2;
+  return __builtin_amdgcn_alignbit(row[i + 1], row[i], (byte & 3) * 8);
+}
+
+template <int T, int RR, int NCOL, bool ONE_SLICE>
+__global__ __launch_bounds__(RR * 8) void ref_kernel(GemvArgs p) {
+  using F = RefFmt<T>;
+  constexpr int NT = RR * 8;
+  constexpr int KCH = ref_kch<T>(), QW = ref_qw<T>();
+  constexpr int U = QW == 1 ? 4 : 1;                 // units per batch of LDS reads
+  constexpr bool AFF = F::M >= 0;
+  constexpr bool KQ = F::UE == 256;
+  constexpr int SEG = KCH * F::BPB;                  // bytes of a row's chunk (a multiple of 16)
+  constexpr int SEGW = SEG / 4 + 1;                  // dwords per LDS row (+1: realignment reads)
+  static_assert(SEG % 16 == 0, "chunks start 16-byte aligned");
+  __shared__ __attribute__((aligned(16))) uint32_t sa[RR * SEGW];               // A rows, raw bytes
+  __shared__ __attribute__((aligned(16))) uint32_t sq[NCOL * 8 * KCH * QW];   // [col][lane][unit][group]
+  __shared__ __attribute__((aligned(16))) float sd[NCOL * KCH];               // d_b     [col][unit]
+  __shared__ __attribute__((aligned(16))) float ss[AFF ? NCOL * KCH : 1];     // s_b (q8_1)
+
+  const unsigned char* Az = p.A;
+  const unsigned char* Bz = p.B;
+  float* Cz = p.C;
+  if constexpr (!ONE_SLICE) {
+    const int z = blockIdx.z, i12 = z % p.ne12, i13 = z / p.ne12;
+    Az += (int64_t)(i12 / p.r2) * p.sa2 + (int64_t)(i13 / p.r3) * p.sa3;
+    Bz += (int64_t)i12 * p.sb2 + (int64_t)i13 * p.sb3;
+    Cz += (int64_t)i12 * p.sc2 + (int64_t)i13 * p.sc3;
+  }
+  const int t = threadIdx.x, l = t & 7, rloc = t >> 3;
+  const int row0 = blockIdx.x * RR, row = row0 + rloc;
+  const int nrows = p.M - row0 < RR ? p.M - row0 : RR;
+  const int n0 = blockIdx.y * NCOL;
+  const int ncols = p.N - n0 < NCOL ? p.N - n0 : NCOL;
+  const int nunits = p.nblk;
+  // A: the workgroup's rows, from its first row to its last row's last byte (wave-uniform base)
+  const auto ra = make_rsrc(Az + (int64_t)row0 * p.lda,
+                            (uint32_t)(((int64_t)(nrows - 1) * p.lda + (int64_t)nunits * F::BPB + 3) & ~int64_t(3)));
+  const int64_t bbytes = (int64_t)(ncols - 1) * p.ldb + (int64_t)nunits * F::VB;
+  const auto rb = make_rsrc(Bz + (int64_t)n0 * p.ldb, (uint32_t)((bbytes + 3) & ~int64_t(3)));
+
+  // the reference's lane l of each column's __m256 accumulator: one fp32 chain per column here
+  // (the 8 lanes of a row sit in 8 threads)
+  float chain[NCOL], summs[AFF ? NCOL : 1];
+#pragma unroll
+  for (int c = 0; c < NCOL; ++c) {
+    chain[c] = 0.f;
+    if constexpr (AFF) summs[c] = 0.f;
+  }
+  const uint32_t* arow = &sa[rloc * SEGW];
+
+  for (int u0 = 0; u0 < nunits; u0 += KCH) {
+    const int nu = nunits - u0 < KCH ? nunits - u0 : KCH;
+    // ---- stage the A chunk: each row's bytes [u0 BPB, (u0 + KCH) BPB) as coalesced 16-byte loads
+    for (int it = t; it < RR * (SEG / 16); it += NT) {
+      const int r = it / (SEG / 16), o = it % (SEG / 16);
+      const uint32_t off = r < nrows ? (uint32_t)((int64_t)r * p.lda + (int64_t)u0 * F::BPB) + 16 * o : 0x7ffffff0u;
+      const u32x4 v = bload16(ra, off);   // past the rows / the row's end: zeros (never summed)
+      uint32_t* dst = &sa[r * SEGW + 4 * o];
+      dst[0] = v[0]; dst[1] = v[1]; dst[2] = v[2]; dst[3] = v[3];
+    }
+    // ---- stage the activation chunk: columns n0 .. n0 + NCOL, units u0 .. u0 + nu
+    if constexpr (!KQ) {
+      for (int it = t; it < NCOL * KCH; it += NT) {
+        const int c = it / KCH, k = it % KCH;
+        const bool ok = c < ncols && k < nu;
+        const uint32_t off = (uint32_t)((int64_t)c * p.ldb + (int64_t)(u0 + k) * F::VB);
+        uint32_t w[10];
+        const uint32_t base = ok ? (off & ~3u) : 0x7ffffff0u;
+#pragma unroll
+        for (int i = 0; i < 10; ++i) w[i] = bload4(rb, base + 4 * i);
+        const int sh = (int)(off & 3u) * 8;
+        uint32_t m[9];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) m[i] = __builtin_amdgcn_alignbit(w[i + 1], w[i], sh);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {   // quad q = quants 4q .. 4q+3 (q8_0: from byte 2; q8_1: d, s, then byte 4)
+          const uint32_t v = AFF ? m[1 + q] : __builtin_amdgcn_alignbit(m[q + 1], m[q], 16);
+          sq[((c * 8 + q) * KCH + k) * QW] = ok ? v : 0u;
+        }
+        sd[c * KCH + k] = ok ? h2f(m[0] & 0xffffu) : 0.f;
+        if constexpr (AFF) ss[c * KCH + k] = ok ? h2f(m[0] >> 16) : 0.f;
+      }
+    } else {
+      // q8_K super-block: float d, 256 quants, bsums; 4 threads per (column, unit), 16 quads each
+      for (int it = t; it < NCOL * KCH * 4; it += NT) {
+        const int item = it >> 2, part = it & 3, c = item / KCH, k = item % KCH;
+        const bool ok = c < ncols && k < nu;
+        const uint32_t base = ok ? (uint32_t)((int64_t)c * p.ldb + (int64_t)(u0 + k) * F::VB) : 0x7ffffff0u;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {   // past the range (base 0x7ffffff0): zeros
+          const u32x4 v = bload16(rb, base + 4 + 64 * part + 16 * i);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int qd = 16 * part + 4 * i + e, h = qd >> 3, ln = qd & 7;   // position 4 qd = 32 h + 4 ln
+            sq[((c * 8 + ln) * KCH + k) * QW + h] = v[e];
+          }
+        }
+        if (part == 0) sd[c * KCH + k] = ok ? __builtin_bit_cast(float, bload4(rb, base)) : 0.f;
+      }
+    }
+    __syncthreads();
+    // ---- the chains: units u0 .. u0 + nu, this thread's lane l, its row, every column
+    if (row < p.M) {
+      for (int k0 = 0; k0 < nu; k0 += U) {
+        uint32_t aq[U][QW];
+        int sc[U][QW];
+        float da[U], ma[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int ub = (k0 + u) * F::BPB;   // this unit's bytes in the row's LDS image
+          da[u] = h2f(lds32(arow, ub + (KQ ? 208 : 0)) & 0xffffu);
+          ma[u] = AFF ? h2f(lds32(arow, ub + (AFF ? F::M : 0)) & 0xffffu) : 0.f;
+          if constexpr (!KQ) {
+            const uint32_t qw = lds32(arow, ub + F::QS + 4 * (l & 3));
+            uint32_t q = l < 4 ? qw & 0x0f0f0f0fu : (qw >> 4) & 0x0f0f0f0fu;
+            if constexpr (F::QH >= 0) {
+              const uint32_t qh = lds32(arow, ub + (F::QH >= 0 ? F::QH : 0));
+              q |= spread4_hi((qh >> (4 * l)) & 0xfu);
+            }
+            aq[u][0] = to_signed<F::OFF>(q);
+            sc[u][0] = 1;
+          } else {
+            const uint32_t sc0 = lds32(arow, ub + 192), sc1 = lds32(arow, ub + 196);
+            const uint32_t sc2 = lds32(arow, ub + 200), sc3 = lds32(arow, ub + 204);
+            const uint32_t scw[4] = {sc0, sc1, sc2, sc3};
+#pragma unroll
+            for (int h = 0; h < 8; ++h) {   // group h = 4 j + g: ql[64 j + 32 (g & 1) + 4 l], qh[32 j + 4 l] >> 2 g
+              const int j = h >> 2, g = h & 3;
+              const uint32_t ql = lds32(arow, ub + F::QS + 64 * j + 32 * (g & 1) + 4 * l);
+              const uint32_t qh = lds32(arow, ub + F::QH + 32 * j + 4 * l);
+              const uint32_t q = ((g < 2 ? ql : ql >> 4) & 0x0f0f0f0fu) | (((qh >> (2 * g)) & 0x03030303u) << 4);
+              aq[u][h] = to_signed<F::OFF>(q);
+              const int si = 2 * h + (l < 4 ? 0 : 1);   // scale byte 2h + (l >= 4)
+              sc[u][h] = (int)(int8_t)((scw[si >> 2] >> (8 * (si & 3))) & 0xffu);
+            }
+          }
+        }
+#pragma unroll
+        for (int c = 0; c < NCOL; ++c) {
+          uint32_t bq[U][QW];
+          float db[U], sb[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+#pragma unroll
+            for (int h = 0; h < QW; ++h) bq[u][h] = sq[((c * 8 + l) * KCH + k0 + u) * QW + h];
+            db[u] = sd[c * KCH + k0 + u];
+            sb[u] = AFF ? ss[c * KCH + k0 + u] : 0.f;
+          }
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            if (k0 + u >= nu) break;   // (uniform)
+            int X = 0;
+#pragma unroll
+            for (int h = 0; h < QW; ++h) {
+              const int d4 = dot4(aq[u][h], bq[u][h], 0);
+              X = KQ ? X + sc[u][h] * d4 : d4;
+            }
+            // d = fp32(d_a) * fp32(d_b) rounded once (q6_K: y.d * fp32(x.d)), then one fused step
+            float d = KQ ? db[u] * da[u] : da[u] * db[u];
+            asm volatile("" : "+v"(d));   // a separate rounding of the product: never contracted into the fma
+            chain[c] = __builtin_fmaf(d, (float)X, chain[c]);
+            if constexpr (AFF) {
+              float pm = ma[u] * sb[u];
+              asm volatile("" : "+v"(pm));
+              summs[c] = summs[c] + pm;
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  // ---- the tree over the row's 8 lanes: ((a0 + a4) + (a2 + a6)) + ((a1 + a5) + (a3 + a7))
+#pragma unroll
+  for (int c = 0; c < NCOL; ++c) {
+    float v = chain[c];
+    {
+#pragma clang fp contract(off)
+      v = v + __shfl_down(v, 4, 8);   // lanes 0..3: a_l + a_{l+4}
+      v = v + __shfl_down(v, 2, 8);   // lanes 0, 1: x_l + x_{l+2}
+      v = v + __shfl_down(v, 1, 8);   // lane 0: (x0 + x2) + (x1 + x3)
+      if constexpr (AFF) v = v + summs[c];
+    }
+    if (l == 0 && row < p.M && c < ncols) Cz[(int64_t)(n0 + c) * p.ldc + row] = v;
+  }
+}
+
+}  // namespace
+
+bool ref_order_supported(int type, int btype) {
+  switch (type) {
+    case kQ4_0: case kQ5_0: return btype == kQ8_0;
+    case kQ4_1: case kQ5_1: return btype == kQ8_1;
+    case kQ6_K: return btype == kQ8_K;
+    default: return false;
+  }
+}
+
+hipError_t launch_ref(int type, const GemvArgs& p, hipStream_t s) {
+  const int slices = p.ne12 * p.ne13;
+  // columns per workgroup: the N of a decode call (1, 2, 4), else 8
+  const int nc = p.N <= 1 ? 1 : p.N <= 2 ? 2 : p.N <= 4 ? 4 : 8;
+  const dim3 g((unsigned)((p.M + RR - 1) / RR), (unsigned)((p.N + nc - 1) / nc), (unsigned)slices);
+  auto go = [&](auto tc) {
+    constexpr int T = decltype(tc)::value;
+    auto go2 = [&](auto ncc) {
+      constexpr int NC = decltype(ncc)::value;
+      // 16 rows per workgroup for one or two columns (a decode GEMV: twice the workgroups) and for
+      // q6_K (8 super-blocks of 32 rows would not fit the 64 KiB of static LDS), else 32
+      constexpr int R = NC <= 2 || RefFmt<T>::UE == 256 ? 16 : 32;
+      const dim3 gr((unsigned)((p.M + R - 1) / R), g.y, g.z);
+      if (slices == 1) hipLaunchKernelGGL((ref_kernel<T, R, NC, true>), gr, dim3(R * 8), 0, s, p);
+      else hipLaunchKernelGGL((ref_kernel<T, R, NC, false>), gr, dim3(R * 8), 0, s, p);
+    };
+    if (nc == 1) go2(std::integral_constant<int, 1>{});
+    else if (nc == 2) go2(std::integral_constant<int, 2>{});
+    else if (nc == 4) go2(std::integral_constant<int, 4>{});
+    else go2(std::integral_constant<int, 8>{});
+  };
+  switch (type) {
+    case kQ4_0: go(std::integral_constant<int, kQ4_0>{}); break;
+    case kQ4_1: go(std::integral_constant<int, kQ4_1>{}); break;
+    case kQ5_0: go(std::integral_constant<int, kQ5_0>{}); break;
+    case kQ5_1: go(std::integral_constant<int, kQ5_1>{}); break;
+    case kQ6_K: go(std::integral_constant<int, kQ6_K>{}); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace lamm

@@ -94,6 +94,9 @@ lib.lamm_mul_mat.argtypes = [ctypes.POINTER(GgmlComputeParams), ctypes.POINTER(G
 lib.lamm_get_opt_level.restype = ctypes.c_int
 lib.lamm_hip_matmul.restype = ctypes.c_int
 lib.lamm_hip_matmul.argtypes = [ctypes.POINTER(Matrix)] * 3 + [ctypes.c_void_p]
+lib.lamm_hip_matmul_ex.restype = ctypes.c_int
+lib.lamm_hip_matmul_ex.argtypes = [ctypes.POINTER(Matrix)] * 3 + [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+ORDER_REFERENCE = 1   # LAMM_ORDER_REFERENCE: the reference's x86 float order, bit for bit (lamm_ref.hip)
 lib.lamm_hip_matmul_batched.restype = ctypes.c_int
 lib.lamm_hip_matmul_batched.argtypes = [ctypes.POINTER(Matrix)] * 3 + [ctypes.POINTER(Batch), ctypes.c_void_p]
 lib.lamm_hip_quantize.restype = ctypes.c_int
@@ -218,17 +221,26 @@ def matmul(A, B, C, stream=0):
            "lamm_hip_matmul")
 
 
+def matmul_ex(A, B, C, batch=None, flags=0, stream=0):
+    """lamm_hip_matmul_ex: flags = ORDER_REFERENCE computes in the reference's x86 float order."""
+    _sync_env()
+    _check(lib.lamm_hip_matmul_ex(ctypes.byref(A), ctypes.byref(B), ctypes.byref(C),
+                                  ctypes.byref(batch) if batch is not None else None, flags, ctypes.c_void_p(stream)),
+           "lamm_hip_matmul_ex")
+
+
 def matmul_batched(A, B, C, batch, stream=0):
     _sync_env()
     _check(lib.lamm_hip_matmul_batched(ctypes.byref(A), ctypes.byref(B), ctypes.byref(C), ctypes.byref(batch),
                                        ctypes.c_void_p(stream)), "lamm_hip_matmul_batched")
 
 
-def mul_mat_torch(wtype, a, b, c, M, N, K, lda=None, ldb=None, ldc=None, stream=None, batch=None):
+def mul_mat_torch(wtype, a, b, c, M, N, K, lda=None, ldb=None, ldc=None, stream=None, batch=None, flags=0):
     """C[j*ldc+i] = A_i . B_j for torch device tensors (uint8 blocks for A/B, f32 C).
 
     lda/ldb in blocks (default: packed rows), ldc in floats (default M).
-    Runs on ``stream`` (default: torch's current stream)."""
+    Runs on ``stream`` (default: torch's current stream).  flags: ORDER_REFERENCE for the
+    reference's float order (lamm_hip_matmul_ex)."""
     import torch
     vt = vec_dot_type(wtype)
     kb = K // blck_size(wtype)
@@ -237,7 +249,9 @@ def mul_mat_torch(wtype, a, b, c, M, N, K, lda=None, ldb=None, ldc=None, stream=
     A = Matrix(a.data_ptr(), wtype, M, kb, lda if lda is not None else kb)
     B = Matrix(b.data_ptr(), vt, kb, N, ldb if ldb is not None else kb)
     C = Matrix(c.data_ptr(), F32, M, N, ldc if ldc is not None else M)
-    if batch is None:
+    if flags:
+        matmul_ex(A, B, C, batch, flags, stream)
+    elif batch is None:
         matmul(A, B, C, stream)
     else:
         matmul_batched(A, B, C, batch, stream)

@@ -30,6 +30,7 @@
 
 #include <float.h>
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 /* ---------------------------------------------------------------- fp16 */
@@ -698,8 +699,57 @@ float lo_vec_dot_avx(int type, int k, const void *va, const void *vb) {
   return tree8(acc) + summs;
 }
 
+/* the same order as lo_vec_dot_avx, with each A row's quants decoded once for all N columns */
+static void row_avx(int type, int N, int K, const uint8_t *a, const uint8_t *B, size_t ldb_bytes, float *C,
+                    size_t ldc, int8_t *av) {
+  const size_t ab = lo_block_bytes(type), bb = lo_block_bytes(lo_vec_dot_type(type));
+  if (type == LO_Q6_K) {
+    for (int e = 0; e < K; ++e) av[e] = (int8_t)q6_value(a + (size_t)(e / 256) * ab, e % 256);
+    for (int j = 0; j < N; ++j) {
+      const uint8_t *b = B + (size_t)j * ldb_bytes;
+      float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (int i = 0; i < K / 256; ++i) {
+        const uint8_t *x = a + (size_t)i * ab, *y = b + (size_t)i * bb;
+        float yd; memcpy(&yd, y, 4);
+        const int8_t *q8 = (const int8_t *)(y + 4), *v = av + 256 * i;
+        const float d = yd * H2F(rd16(x + 208));
+        int32_t X[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int e = 0; e < 256; ++e) X[(e % 32) / 4] += (int8_t)x[192 + e / 16] * (v[e] * q8[e]);
+        for (int l = 0; l < 8; ++l) acc[l] = fmaf(d, (float)X[l], acc[l]);
+      }
+      C[(size_t)j * ldc] = tree8(acc);
+    }
+    return;
+  }
+  const int aff = type == LO_Q4_1 || type == LO_Q5_1;
+  for (int e = 0; e < K; ++e) av[e] = (int8_t)blk_q(type, a + (size_t)(e / 32) * ab, e % 32);
+  for (int j = 0; j < N; ++j) {
+    const uint8_t *b = B + (size_t)j * ldb_bytes;
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, summs = 0.0f;
+    for (int i = 0; i < K / 32; ++i) {
+      const uint8_t *x = a + (size_t)i * ab, *y = b + (size_t)i * bb;
+      const int8_t *bq = (const int8_t *)(y + (aff ? 4 : 2)), *v = av + 32 * i;
+      const float d = H2F(rd16(x)) * H2F(rd16(y));
+      for (int l = 0; l < 8; ++l) {
+        const int X = v[4 * l] * bq[4 * l] + v[4 * l + 1] * bq[4 * l + 1] + v[4 * l + 2] * bq[4 * l + 2] +
+                      v[4 * l + 3] * bq[4 * l + 3];
+        acc[l] = fmaf(d, (float)X, acc[l]);
+      }
+      if (aff) summs += H2F(rd16(x + 2)) * H2F(rd16(y + 2));
+    }
+    C[(size_t)j * ldc] = tree8(acc) + summs;
+  }
+}
+
 void lo_mul_mat_avx(int type, int M, int N, int K, const void *A, size_t lda_bytes,
                     const void *B, size_t ldb_bytes, float *C, size_t ldc) {
+  if (type == LO_Q6_K || type == LO_Q4_0 || type == LO_Q4_1 || type == LO_Q5_0 || type == LO_Q5_1) {
+    int8_t *av = (int8_t *)malloc((size_t)K);
+    for (int i = 0; i < M; i++)
+      row_avx(type, N, K, (const uint8_t *)A + (size_t)i * lda_bytes, (const uint8_t *)B, ldb_bytes, C + i, ldc, av);
+    free(av);
+    return;
+  }
   for (int j = 0; j < N; j++)
     for (int i = 0; i < M; i++)
       C[(size_t)j * ldc + i] = lo_vec_dot_avx(type, K, (const uint8_t *)A + (size_t)i * lda_bytes,

@@ -40,7 +40,12 @@ def layer_of(src0):
     return int(src0.split(".")[1])
 
 
+AVX_TYPES = (ol.Q4_0, ol.Q4_1, ol.Q5_0, ol.Q5_1, ol.Q6_K)   # lo_mul_mat_avx: the reference's x86 order
+
+
 def check_node(d, ent):
+    """(worst |c - c_ref| / max(|c_ref|, sum |a b|) against the oracle's scalar order, whether c is
+    bit-identical to the reference's x86 float order -- None for types without that restatement)"""
     t0, t1 = ent["type0"], ent["type1"]
     K, M, ne02, ne03 = ent["ne0"]
     _, N, ne12, ne13 = ent["ne1"]
@@ -53,6 +58,7 @@ def check_node(d, ent):
     assert t1 == ol.F32
     flavour = ol.QUANT_AVX if vt in (ol.Q8_0, ol.Q8_1) else ol.QUANT_REF
     worst = 0.0
+    exact = True if t0 in AVX_TYPES else None
     for i13 in range(ne13):
         for i12 in range(ne12):
             a = A[i13 // (ne13 // ne03), i12 // (ne12 // ne02)]
@@ -64,17 +70,21 @@ def check_node(d, ent):
             denom = np.maximum(np.maximum(np.abs(ref.astype(np.float64)), absdot), 1e-30)
             err = np.abs(C[i13, i12].astype(np.float64) - ref) / denom
             worst = max(worst, float(err.max()))
-    return worst
+            if exact:
+                avx = ORACLE.mul_mat_avx(t0, M, N, K, a, b)
+                exact = bool(np.array_equal(avx.view(np.uint32), np.ascontiguousarray(C[i13, i12]).view(np.uint32)))
+    return worst, exact
 
 
 def _one(args):
     d, ent = args
     return (ent["phase"], layer_of(ent["src0"]), node_kind(ent["src0"]), ent["name"],
-            (ent["ne0"][1], ent["ne1"][1], ent["ne0"][0], ent["ne0"][2]), check_node(d, ent))
+            (ent["ne0"][1], ent["ne1"][1], ent["ne0"][0], ent["ne0"][2])) + check_node(d, ent)
 
 
 def check_nodes(d, workers=8):
-    """[(phase, layer, kind, name, (M, N, K, slices), worst error)] for every dumped node, the
+    """[(phase, layer, kind, name, (M, N, K, slices), worst error, bit-exact in the reference's x86
+    order (None: no restatement for the type))] for every dumped node, the
     nodes spread over `workers` processes (each loads its own oracle)"""
     with open(os.path.join(d, "index.jsonl")) as f:
         ents = [json.loads(line) for line in f]

@@ -112,7 +112,13 @@ def test_non_compute_phases_and_unsupported(monkeypatch):
     p.type = la.TASK_FINALIZE
     assert not la.can_mul_mat(p, dst.t)
     p.type = la.TASK_INIT        # claimed whenever the GPU quantizes src1
-    assert la.can_mul_mat(p, dst.t)              # default: decode-sized q4_0 -> fused into the GEMV
+    # default (the reference's float order): decode-sized calls leave INIT to ggml, as
+    # the reference does; from 8 activation rows the GPU quantizer (the same bytes) takes it
+    assert not la.can_mul_mat(p, dst.t)
+    src0r, src1r, _, _ = make_node(t, M, 8, K)
+    assert la.can_mul_mat(p, ggml_emu.mul_mat_node(src0r, src1r).t)
+    monkeypatch.setenv("LAMM_HIP_ORDER", "fast")   # the fast engines: INIT fused into the GEMV
+    assert la.can_mul_mat(p, dst.t)              # decode-sized q4_0 -> fused into the GEMV
     monkeypatch.setenv("LAMM_HIP_FUSED", "0")
     assert not la.can_mul_mat(p, dst.t)          # N = 1 without fusion: ggml's CPU INIT
     monkeypatch.delenv("LAMM_HIP_FUSED")
@@ -157,6 +163,10 @@ def test_f16_policy(monkeypatch):
     dstb = ggml_emu.mul_mat_node(src0b, src1b)
     assert not la.can_mul_mat(p, dstb.t)
     monkeypatch.delenv("LAMM_HIP_VIEWS")
+    # unset: in the reference's float order (the default) the views stay with ggml, as the
+    # reference routes F16; with the fast engines prefill-sized views go to the GPU
+    assert not la.can_mul_mat(p, dstb.t)
+    monkeypatch.setenv("LAMM_HIP_ORDER", "fast")
     assert la.can_mul_mat(p, dstb.t)
 
 

@@ -1006,14 +1006,17 @@ def test_config1_f32_512_cube():
 Q2K_SHAPES = [(1, 256), (9, 4096), (133, 4352), (64, 8192), (37, 11008), (4096, 4096), (70, 12288)]
 
 
-@pytest.mark.parametrize("t", [ol.Q2_K, ol.Q4_K, ol.Q5_K], ids=["q2_k", "q4_k", "q5_k"])
-@pytest.mark.parametrize("shape", Q2K_SHAPES, ids=[f"{m}x1x{k}" for m, k in Q2K_SHAPES])
+@pytest.mark.parametrize("t", [ol.Q2_K, ol.Q4_K, ol.Q5_K, ol.Q6_K], ids=["q2_k", "q4_k", "q5_k", "q6_k"])
+@pytest.mark.parametrize("shape", Q2K_SHAPES + [(32000, 1024)], ids=[f"{m}x1x{k}" for m, k in Q2K_SHAPES + [(32000, 1024)]])
 def test_gemv_kq_row_per_wave(t, shape):
     """lamm_gemv_rpw.hip's k-quant kernel (one column, up to 48 super-blocks per row): lanes on
     quarter super-blocks, the quarters' integer sums combined in the quad (exact), one float
-    epilogue per super-block as the reference's ggml_vec_dot_q{2,4,5}_K_q8_K; ragged M, K from one
-    to 48 super-blocks, against the oracle."""
+    epilogue per super-block as the reference's ggml_vec_dot_q{2,4,5,6}_K_q8_K; ragged M, K from one
+    to 48 super-blocks, against the oracle.  q6_K (210-byte, 2-byte aligned super-blocks) takes every
+    row count: a Q4_0 model's 32000-row output.weight (LC/llama.cpp:11731-11742)."""
     M, K = shape
+    if M == 32000 and t != ol.Q6_K:
+        pytest.skip("the long grid is q6_K's case (output.weight)")
     rng = np.random.default_rng(M * 31 + K + t)
     A_q = ol.random_kq_blocks(t, M, K, rng)
     B_q = ORACLE.quantize(ol.Q8_K, rng.standard_normal((1, K), dtype=np.float32))

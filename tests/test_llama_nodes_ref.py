@@ -24,8 +24,10 @@ def test_reference_build_nodes_match_oracle(tmp_path):
                        capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     res = ln.check_nodes(str(d), workers=min(8, os.cpu_count() or 1))
-    kinds = {k for _, _, k, *_ in res}
+    kinds = {r[2] for r in res}
     assert kinds == {"wq", "wk", "wv", "wo", "w1", "w2", "w3", "KQ", "KQV", "output"}
     assert len(res) == 38
     # the reference's AVX2 float order against the oracle's scalar one: rounding only
-    assert max(err for *_, err in res) < 1e-6
+    assert max(r[5] for r in res) < 1e-6
+    # and bit for bit the oracle's restatement of that order (q4_0 projections, the q6_K output)
+    assert all(r[6] for r in res if r[6] is not None) and sum(r[6] is not None for r in res) == 30

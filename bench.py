@@ -232,9 +232,10 @@ def time_steps(ctx, step, steps, warmup, graph=True):
 _STEPS_LIB = None
 
 
-def isolated_launches(la, mats, R, Bm, Cm, n):
-    """median device time (s) of n lamm_hip_matmul launches, each isolated (tools/steps_loop.hip);
-    None when the helper is not built"""
+def isolated_launches(la, mats, R, Bm, Cm, n, sync_each=1):
+    """median duration (s) of n lamm_hip_matmul dispatches from their own timestamps
+    (lamm_hip_profile_next, tools/steps_loop.hip), each launched alone (sync_each) or back to back;
+    None when the helper is not built or the kernel took no timestamps"""
     global _STEPS_LIB
     import ctypes
     path = os.path.join(ROOT, "tools", "libsteps_loop.so")
@@ -244,19 +245,19 @@ def isolated_launches(la, mats, R, Bm, Cm, n):
         _STEPS_LIB = ctypes.CDLL(path)
         _STEPS_LIB.lamm_steps_isolated.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(la.Matrix),
                                                    ctypes.POINTER(la.Matrix), ctypes.c_int, ctypes.c_int,
-                                                   ctypes.c_void_p, ctypes.POINTER(ctypes.c_float)]
+                                                   ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.c_int]
     import torch
     arr = (la.Matrix * R)(*mats)
     out = (ctypes.c_float * n)()
     st = torch.cuda.Stream()
     torch.cuda.synchronize()
     rc = _STEPS_LIB.lamm_steps_isolated(ctypes.cast(arr, ctypes.c_void_p), R, ctypes.byref(Bm), ctypes.byref(Cm), 0, n,
-                                        ctypes.c_void_p(st.cuda_stream), out)
+                                        ctypes.c_void_p(st.cuda_stream), out, sync_each)
     torch.cuda.synchronize()
-    if rc != 0:
-        log("lamm_steps_isolated failed:", rc)
-        return None
     v = sorted(out)
+    if rc != 0 or v[0] <= 0.0:
+        log("lamm_steps_isolated failed:", rc, v[:3])
+        return None
     return v[n // 2] * 1e-6
 
 
@@ -324,12 +325,16 @@ def config2_gemv(ctx, fmt, M, K, steps, warmup):
     # (back-to-back launches overlap a dispatch's start with the previous one's tail, and under the
     # tracer are stretched by its own per-dispatch cost instead)
     iso = isolated_launches(la, mats, R, Bm, Cm, 300)
+    b2b = isolated_launches(la, mats, R, Bm, Cm, 300, sync_each=0)
     if iso is not None:
-        kern, kern_method = iso, "median of 300 isolated launches, HIP events around each (lamm_steps_isolated)"
+        kern = iso
+        kern_method = ("median of 300 single launches, each completed before the next, timed by the dispatch's "
+                       "own start / end timestamps (lamm_hip_profile_next -> hipExtLaunchKernel events)")
     else:
         _, kern, _ = time_steps(ctx, gemv, max(steps, 1000), 3)
         kern_method = "HIP events over 1000 back-to-back hipGraph-replayed launches on their stream"
-    res = dict(per_step=per_step, ev_step=ev_step, kern=kern, kern_method=kern_method, graphed=graphed, R=R, rows=rows,
+    res = dict(per_step=per_step, ev_step=ev_step, kern=kern, kern_method=kern_method, kern_b2b=b2b, graphed=graphed,
+               R=R, rows=rows,
                slab_bytes=slab_bytes + la.row_bytes(vt, K) + 4 * rows, gather_check=check, sample=sample)
     del A, B, C
     torch.cuda.empty_cache()
@@ -655,6 +660,7 @@ def main():
                      "kernel": "lamm::gemv_flat1_kernel (csrc/lamm_gemv_rpw.hip; gemv_rpw_kernel for other shapes)",
                      "per_launch_us": round(g["kern"] * 1e6, 3),
                      "per_launch_method": g["kern_method"],
+                     "per_launch_us_back_to_back": round(g["kern_b2b"] * 1e6, 3) if g["kern_b2b"] else None,
                      "algorithmic_bytes_per_launch": g["slab_bytes"]},
     }
     if trace and kname and trace.get("algorithmic_bytes_per_launch") == g["slab_bytes"]:

@@ -153,6 +153,13 @@ void lamm_hip_weights_destroy(lamm_weights *W);
  * activation types).  Host-only: no device is touched. */
 const char *lamm_hip_engine(int type, int64_t M, int N, int K, int slices, int stationary, int b_f32);
 
+/* Measurement hook: the next lamm_hip_matmul* call on this thread records the start and end of
+ * its decode-GEMV dispatch (one column, K = 4096: BASELINE config 2's kernel) in these two HIP
+ * events (hipEvent_t, created by the caller), from the dispatch's own timestamps
+ * (hipExtLaunchKernel) -- the duration a kernel tracer reports, with no event packets of their own
+ * around it.  Other engines ignore the request; it expires with that call either way. */
+int lamm_hip_profile_next(void *start_event, void *stop_event);
+
 const char *lamm_hip_last_error(void);
 int lamm_hip_device_count(void);
 /* Provenance: hash (sha256, 16 hex digits) of the sources this library was built from. */

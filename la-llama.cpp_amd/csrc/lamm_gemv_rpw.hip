@@ -14,6 +14,8 @@
 //   * the q4_0 / q5_0 offset is applied in the integer domain (sum (q-c) b = sum q b - c sum b);
 //   * the 64 lane partials reduce through DPP + readlane in a fixed order (deterministic).
 // Bytes per call are the algorithmic A + B + C (A streamed once, non-temporal).
+#include <hip/hip_ext.h>
+
 #include "lamm_rowdot.h"
 
 #include <cstdlib>
@@ -557,6 +559,14 @@ hipError_t launch_rpw_nc(const GemvArgs& p, hipStream_t s, int waves) {
       const bool sl = g.y > 1, sig = p.flag != nullptr;
       if (!sl && !sig) {
         const uint32_t lda = (uint32_t)p.lda;
+        const LaunchTiming tm = take_launch_timing();
+        if (tm.start) {   // lamm_hip_profile_next: the dispatch records its own start / end
+          if (bf) hipExtLaunchKernelGGL((gemv_flat1_kernel<T, true>), g, dim3(512), 0, s, tm.start, tm.stop, 0, p.A, p.B,
+                                        p.C, lda, p.M);
+          else hipExtLaunchKernelGGL((gemv_flat1_kernel<T, false>), g, dim3(512), 0, s, tm.start, tm.stop, 0, p.A, p.B,
+                                     p.C, lda, p.M);
+          return hipGetLastError();
+        }
         if (bf) hipLaunchKernelGGL((gemv_flat1_kernel<T, true>), g, dim3(512), 0, s, p.A, p.B, p.C, lda, p.M);
         else hipLaunchKernelGGL((gemv_flat1_kernel<T, false>), g, dim3(512), 0, s, p.A, p.B, p.C, lda, p.M);
         return hipGetLastError();

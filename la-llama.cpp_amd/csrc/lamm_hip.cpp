@@ -211,9 +211,21 @@ struct Completion {
   bool signaled;
 };
 thread_local Completion* g_completion = nullptr;
+// lamm_hip_profile_next's events, for the next launch on this thread that records them
+thread_local LaunchTiming g_timing;
+
+int matmul_impl_(const lamm_matrix* A, const lamm_matrix* B, const lamm_matrix* C, const lamm_batch* batch,
+                 void* hip_stream, const lamm_weights* W, int flags);
 
 int matmul_impl(const lamm_matrix* A, const lamm_matrix* B, const lamm_matrix* C, const lamm_batch* batch,
                 void* hip_stream, const lamm_weights* W, int flags = 0) {
+  const int rc = matmul_impl_(A, B, C, batch, hip_stream, W, flags);
+  g_timing = LaunchTiming{};   // a profiling request holds for this call only
+  return rc;
+}
+
+int matmul_impl_(const lamm_matrix* A, const lamm_matrix* B, const lamm_matrix* C, const lamm_batch* batch,
+                 void* hip_stream, const lamm_weights* W, int flags) {
   Completion* done = g_completion;
   g_completion = nullptr;
   if (!A || !B || !C) return fail(LAMM_ERR_SHAPE, "null matrix");
@@ -329,6 +341,17 @@ int matmul_impl(const lamm_matrix* A, const lamm_matrix* B, const lamm_matrix* C
 }
 
 }  // namespace
+
+LaunchTiming lamm::take_launch_timing() {
+  const LaunchTiming t = g_timing;
+  g_timing = LaunchTiming{};
+  return t;
+}
+
+extern "C" int lamm_hip_profile_next(void* start_event, void* stop_event) {
+  g_timing = LaunchTiming{static_cast<hipEvent_t>(start_event), static_cast<hipEvent_t>(stop_event)};
+  return LAMM_OK;
+}
 
 extern "C" int lamm_hip_matmul_batched(const lamm_matrix* A, const lamm_matrix* B, const lamm_matrix* C,
                                        const lamm_batch* batch, void* hip_stream) {

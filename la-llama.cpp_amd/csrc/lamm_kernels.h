@@ -29,6 +29,13 @@ struct GemvArgs {
 };
 
 hipError_t launch_gemv(int type, const GemvArgs& p, hipStream_t s);
+// lamm_hip_profile_next: HIP events the next decode-GEMV launch on this thread records its own
+// start / end in (hipExtLaunchKernel: the dispatch's timestamps, what a kernel tracer reports);
+// taking them clears them
+struct LaunchTiming {
+  hipEvent_t start = nullptr, stop = nullptr;
+};
+LaunchTiming take_launch_timing();
 // row-per-wave decode GEMV (lamm_gemv_rpw.hip): 32-element block formats, N <= 2, K <= 12288;
 // `waves` per workgroup (4 / 8 / 16; 8 at most for K > 4096)
 bool gemv_rpw_supported(int type, const GemvArgs& p);

@@ -251,6 +251,196 @@ __global__ __launch_bounds__(RR * 8) void ref_kernel(GemvArgs p) {
   }
 }
 
+// ---------------------------------------------------------------- prefill: the same order on MFMA
+// The lane sums X_l come from v_mfma_f32_32x32x16_f16 with a block-diagonal activation operand:
+// its 32 rows are (column n, lane l) pairs, row (n, l) carrying b_n's 4 quants of lane l (as f16,
+// the rest of its K zero), so C[(n, l)][m] = X_l(m, n) -- 16 integer products, exact in fp32 --
+// for the 16 elements of a half block; the other half block is a second MFMA.  Each lane (weight
+// row m) then holds all 8 lanes' sums of its 4 columns per n-group, so the reference's
+// acc_l = fma(d, X_l, acc_l) chains and the final reduce_sum tree run in registers, with
+// d = fp32(d_a) * fp32(d_b) rounded once on the VALU.
+//   workgroup: 4 waves = 2 (64 weight rows) x 2 (32 activation columns); a wave: 32 rows (its
+//   lanes) x 2 n-groups of 8 columns; K in chunks of 8 blocks through LDS (the rows' raw block
+//   bytes; the activation columns converted to f16 once per workgroup)
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef _Float16 half2v __attribute__((ext_vector_type(2)));
+constexpr int MR = 64, MC = 32, MKB = 8, MNT = 256;   // rows, columns, blocks per chunk, threads
+
+// four unsigned bytes q (0 .. 255) -> f16 (q - OFF) pairs: {lo dword: q0, q1; hi dword: q2, q3}
+template <int OFF>
+__device__ __forceinline__ void q4_to_f16(uint32_t q, uint32_t& lo, uint32_t& hi) {
+  // f16 bit pattern 0x6400 | q is 1024 + q exactly; subtract 1024 + OFF in f16 (exact: integers)
+  const uint32_t a = __builtin_amdgcn_perm(0u, q, 0x0c010c00u) | 0x64006400u;   // bytes 0, 1 -> halves
+  const uint32_t b = __builtin_amdgcn_perm(0u, q, 0x0c030c02u) | 0x64006400u;   // bytes 2, 3
+  const half2v off = {(_Float16)(-(1024 + OFF)), (_Float16)(-(1024 + OFF))};
+  lo = __builtin_bit_cast(uint32_t, __builtin_bit_cast(half2v, a) + off);
+  hi = __builtin_bit_cast(uint32_t, __builtin_bit_cast(half2v, b) + off);
+}
+
+template <int T, bool ONE_SLICE>
+__global__ __launch_bounds__(MNT) void ref_mfma_kernel(GemvArgs p) {
+  using F = RefFmt<T>;
+  static_assert(F::UE == 32, "32-element block formats");
+  constexpr bool AFF = F::M >= 0;
+  constexpr int SEG = MKB * F::BPB;                 // a row's chunk bytes
+  static_assert(SEG % 16 == 0, "chunks start 16-byte aligned");
+  constexpr int SEGW = SEG / 4 + 1;
+  constexpr int BP = MKB * 32 + 8;                  // f16 activation row pitch (halves)
+  __shared__ __attribute__((aligned(16))) uint32_t sa[MR * SEGW];
+  __shared__ __attribute__((aligned(16))) _Float16 sb[MC * BP];
+  __shared__ float sdb[MC][MKB];
+  __shared__ float ssb[AFF ? MC : 1][MKB];
+
+  const unsigned char* Az = p.A;
+  const unsigned char* Bz = p.B;
+  float* Cz = p.C;
+  if constexpr (!ONE_SLICE) {
+    const int z = blockIdx.z, i12 = z % p.ne12, i13 = z / p.ne12;
+    Az += (int64_t)(i12 / p.r2) * p.sa2 + (int64_t)(i13 / p.r3) * p.sa3;
+    Bz += (int64_t)i12 * p.sb2 + (int64_t)i13 * p.sb3;
+    Cz += (int64_t)i12 * p.sc2 + (int64_t)i13 * p.sc3;
+  }
+  const int t = threadIdx.x, lane = t & 63, lr = lane & 31, h = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6), wm = w & 1, wn = w >> 1;
+  const int m0 = blockIdx.x * MR, n0 = blockIdx.y * MC;
+  const int nrows = p.M - m0 < MR ? p.M - m0 : MR;
+  const int ncols = p.N - n0 < MC ? p.N - n0 : MC;
+  const int nunits = p.nblk;
+  const auto ra = make_rsrc(Az + (int64_t)m0 * p.lda,
+                            (uint32_t)(((int64_t)(nrows - 1) * p.lda + (int64_t)nunits * F::BPB + 3) & ~int64_t(3)));
+  const int64_t bbytes = (int64_t)(ncols - 1) * p.ldb + (int64_t)nunits * F::VB;
+  const auto rb = make_rsrc(Bz + (int64_t)n0 * p.ldb, (uint32_t)((bbytes + 3) & ~int64_t(3)));
+  const int ml = 32 * wm + lr;                      // this lane's weight row in the tile
+
+  // acc[g][half][r]: n-group g (columns 16 wn + 8 g ..), block half (lanes l = 4 half + (r & 3)),
+  // MFMA output element r: column 16 wn + 8 g + 2 (r >> 2) + h, lane 4 half + (r & 3)
+  f32x16 acc[2][2];
+  float summs[2][4];
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[g][q][r] = 0.f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) summs[g][c] = 0.f;
+  }
+  const uint32_t* arow = &sa[ml * SEGW];
+
+  for (int u0 = 0; u0 < nunits; u0 += MKB) {
+    const int nu = nunits - u0 < MKB ? nunits - u0 : MKB;
+    // ---- stage: the rows' raw chunk bytes; the columns' quants as f16, d_b (and s_b)
+    for (int it = t; it < MR * (SEG / 16); it += MNT) {
+      const int r = it / (SEG / 16), o = it % (SEG / 16);
+      const uint32_t off = r < nrows ? (uint32_t)((int64_t)r * p.lda + (int64_t)u0 * F::BPB) + 16 * o : 0x7ffffff0u;
+      const u32x4 v = bload16(ra, off);
+      uint32_t* dst = &sa[r * SEGW + 4 * o];
+      dst[0] = v[0]; dst[1] = v[1]; dst[2] = v[2]; dst[3] = v[3];
+    }
+    {
+      const int c = t >> 3, k = t & 7;              // 256 threads = 32 columns x 8 blocks
+      const bool ok = c < ncols && k < nu;
+      const uint32_t off = (uint32_t)((int64_t)c * p.ldb + (int64_t)(u0 + k) * F::VB);
+      const uint32_t base = ok ? (off & ~3u) : 0x7ffffff0u;
+      uint32_t wv[10];
+#pragma unroll
+      for (int i = 0; i < 10; ++i) wv[i] = bload4(rb, base + 4 * i);
+      const int sh = (int)(off & 3u) * 8;
+      uint32_t m[9];
+#pragma unroll
+      for (int i = 0; i < 9; ++i) m[i] = __builtin_amdgcn_alignbit(wv[i + 1], wv[i], sh);
+      uint32_t* dst = reinterpret_cast<uint32_t*>(&sb[c * BP + 32 * k]);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {   // quad q (signed bytes) -> 4 f16
+        const uint32_t qd = AFF ? m[1 + q] : __builtin_amdgcn_alignbit(m[q + 1], m[q], 16);
+        uint32_t lo, hi;
+        q4_to_f16<128>(qd ^ 0x80808080u, lo, hi);   // int8 b: b + 128 as an unsigned byte, less 128
+        dst[2 * q] = ok ? lo : 0u;
+        dst[2 * q + 1] = ok ? hi : 0u;
+      }
+      sdb[c][k] = ok ? h2f(m[0] & 0xffffu) : 0.f;
+      if constexpr (AFF) ssb[c][k] = ok ? h2f(m[0] >> 16) : 0.f;
+    }
+    __syncthreads();
+    for (int k = 0; k < nu; ++k) {
+      // ---- the weight operand: row ml, elements 8h .. 8h + 7 (half 0) and 16 + 8h .. (half 1)
+      const int ub = k * F::BPB;
+      const float da = h2f(lds32(arow, ub) & 0xffffu);
+      const float ma = AFF ? h2f(lds32(arow, ub + (AFF ? F::M : 0)) & 0xffffu) : 0.f;
+      uint32_t q0 = lds32(arow, ub + F::QS + 8 * h), q1 = lds32(arow, ub + F::QS + 8 * h + 4);
+      uint32_t wlo[2] = {q0 & 0x0f0f0f0fu, q1 & 0x0f0f0f0fu};            // elements 8h ..
+      uint32_t whi[2] = {(q0 >> 4) & 0x0f0f0f0fu, (q1 >> 4) & 0x0f0f0f0fu};   // elements 16 + 8h ..
+      if constexpr (F::QH >= 0) {
+        const uint32_t qh = lds32(arow, ub + (F::QH >= 0 ? F::QH : 0));
+        wlo[0] |= spread4_hi((qh >> (8 * h)) & 0xfu);
+        wlo[1] |= spread4_hi((qh >> (8 * h + 4)) & 0xfu);
+        whi[0] |= spread4_hi((qh >> (16 + 8 * h)) & 0xfu);
+        whi[1] |= spread4_hi((qh >> (16 + 8 * h + 4)) & 0xfu);
+      }
+      uint32_t wf[2][4];
+      q4_to_f16<F::OFF>(wlo[0], wf[0][0], wf[0][1]);
+      q4_to_f16<F::OFF>(wlo[1], wf[0][2], wf[0][3]);
+      q4_to_f16<F::OFF>(whi[0], wf[1][0], wf[1][1]);
+      q4_to_f16<F::OFF>(whi[1], wf[1][2], wf[1][3]);
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        const int nb = 16 * wn + 8 * g;             // the n-group's first column in the tile
+        // the block-diagonal activation operand: row lr = (column nb + lr / 4, lane lr % 4 of the
+        // half); this lane holds K = 8h .. 8h + 7 of it: that lane's 4 quants when lr % 4 is 2h or
+        // 2h + 1, else zeros
+        const int nn = nb + (lr >> 2), lq = lr & 3;
+        const bool mine = (lq >> 1) == h;
+        f32x16 S[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const uint2 v = *reinterpret_cast<const uint2*>(&sb[nn * BP + 32 * k + 16 * q + 4 * lq]);
+          uint32_t af[4] = {0u, 0u, 0u, 0u};
+          af[2 * (lq & 1)] = mine ? v.x : 0u;
+          af[2 * (lq & 1) + 1] = mine ? v.y : 0u;
+          const half8 A8 = __builtin_bit_cast(half8, u32x4{af[0], af[1], af[2], af[3]});
+          const half8 W8 = __builtin_bit_cast(half8, u32x4{wf[q][0], wf[q][1], wf[q][2], wf[q][3]});
+          const f32x16 zero = {};
+          S[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A8, W8, zero, 0, 0, 0);
+        }
+        // d per output column: 2 (r >> 2) + h of the group; one fused step per lane sum
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          float d = da * sdb[nb + 2 * c + h][k];
+          asm volatile("" : "+v"(d));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            acc[g][0][4 * c + e] = __builtin_fmaf(d, S[0][4 * c + e], acc[g][0][4 * c + e]);
+            acc[g][1][4 * c + e] = __builtin_fmaf(d, S[1][4 * c + e], acc[g][1][4 * c + e]);
+          }
+          if constexpr (AFF) {
+            float pm = ma * ssb[nb + 2 * c + h][k];
+            asm volatile("" : "+v"(pm));
+            summs[g][c] = summs[g][c] + pm;
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  // ---- reduce_sum's tree per output, in registers: lanes l = e (half 0) and 4 + e (half 1)
+  const int m = m0 + ml;
+#pragma unroll
+  for (int g = 0; g < 2; ++g)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int n = 16 * wn + 8 * g + 2 * c + h;
+      float v;
+      {
+#pragma clang fp contract(off)
+        const float x0 = acc[g][0][4 * c + 0] + acc[g][1][4 * c + 0], x1 = acc[g][0][4 * c + 1] + acc[g][1][4 * c + 1];
+        const float x2 = acc[g][0][4 * c + 2] + acc[g][1][4 * c + 2], x3 = acc[g][0][4 * c + 3] + acc[g][1][4 * c + 3];
+        v = (x0 + x2) + (x1 + x3);
+        if constexpr (AFF) v = v + summs[g][c];
+      }
+      if (m < p.M && n < ncols) Cz[(int64_t)(n0 + n) * p.ldc + m] = v;
+    }
+}
+
 }  // namespace
 
 bool ref_order_supported(int type, int btype) {
@@ -264,6 +454,23 @@ bool ref_order_supported(int type, int btype) {
 
 hipError_t launch_ref(int type, const GemvArgs& p, hipStream_t s) {
   const int slices = p.ne12 * p.ne13;
+  // prefill-sized calls on the 32-element formats: the MFMA form (ref_mfma_kernel)
+  if (p.N > 8 && type != kQ6_K) {
+    const dim3 gm((unsigned)((p.M + MR - 1) / MR), (unsigned)((p.N + MC - 1) / MC), (unsigned)slices);
+    auto gom = [&](auto tc) {
+      constexpr int T = decltype(tc)::value;
+      if (slices == 1) hipLaunchKernelGGL((ref_mfma_kernel<T, true>), gm, dim3(MNT), 0, s, p);
+      else hipLaunchKernelGGL((ref_mfma_kernel<T, false>), gm, dim3(MNT), 0, s, p);
+    };
+    switch (type) {
+      case kQ4_0: gom(std::integral_constant<int, kQ4_0>{}); break;
+      case kQ4_1: gom(std::integral_constant<int, kQ4_1>{}); break;
+      case kQ5_0: gom(std::integral_constant<int, kQ5_0>{}); break;
+      case kQ5_1: gom(std::integral_constant<int, kQ5_1>{}); break;
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
   // columns per workgroup: the N of a decode call (1, 2, 4), else 8
   const int nc = p.N <= 1 ? 1 : p.N <= 2 ? 2 : p.N <= 4 ? 4 : 8;
   const dim3 g((unsigned)((p.M + RR - 1) / RR), (unsigned)((p.N + nc - 1) / nc), (unsigned)slices);

@@ -5,11 +5,10 @@
 //   lamm_steps_matmul_paced  : launches paced slower than the kernel, so a kernel tracer times
 //                              every dispatch on its own (no dispatch queued behind it to fold the
 //                              tracer's per-dispatch cost into)
-//   lamm_steps_isolated      : per-launch durations by HIP events, each launch isolated: behind a
-//                              gate kernel that holds the stream until the host has enqueued the
-//                              events and the launch, so e1 - e0 is the device's own time for one
-//                              dispatch with nothing queued behind it -- what the kernel tracer
-//                              reports for the same dispatch (bench.py's roofline)
+//   lamm_steps_isolated      : per-launch durations from the dispatches' own timestamps
+//                              (lamm_hip_profile_next), launches isolated or back to back --
+//                              what the kernel tracer reports for the same dispatch (bench.py's
+//                              roofline)
 // hipcc --offload-arch=gfx950 -O2 -shared -fPIC -I include tools/steps_loop.hip -L la-llama.cpp_amd -llamm_hip
 #include <hip/hip_runtime.h>
 
@@ -22,16 +21,6 @@ namespace {
 
 double now_us() {
   return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
-}
-
-// one wave: wait until *flag >= want (host-coherent memory) or ~0.2 s have passed (s_memrealtime,
-// 100 MHz), whichever comes first -- every launch of it ends
-__global__ void gate_kernel(const unsigned* flag, unsigned want) {
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < want) {
-    if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) break;
-    __builtin_amdgcn_s_sleep(8);
-  }
 }
 
 }  // namespace
@@ -65,14 +54,12 @@ int lamm_steps_matmul_paced(const lamm_matrix* A, int nA, const lamm_matrix* B, 
   return hipStreamSynchronize(s) == hipSuccess ? LAMM_OK : -2;
 }
 
-// out_us[i] = device time of launch i alone (events around it, the stream held by a gate kernel
-// until the host has enqueued both events and the launch)
+// out_us[i] = the dispatch's own duration (start / end timestamps of the kernel dispatch,
+// lamm_hip_profile_next -> hipExtLaunchKernel: what a kernel tracer reports) of launch i.
+// sync_each: each launch alone (completed before the next is issued); otherwise back to back.
 int lamm_steps_isolated(const lamm_matrix* A, int nA, const lamm_matrix* B, const lamm_matrix* C, int first,
-                        int launches, void* stream, float* out_us) {
+                        int launches, void* stream, float* out_us, int sync_each) {
   const hipStream_t s = static_cast<hipStream_t>(stream);
-  unsigned* flag = nullptr;
-  if (hipHostMalloc(reinterpret_cast<void**>(&flag), sizeof(unsigned), hipHostMallocCoherent) != hipSuccess) return -3;
-  __atomic_store_n(flag, 0u, __ATOMIC_RELEASE);
   std::vector<hipEvent_t> e0(launches), e1(launches);
   int rc = LAMM_OK;
   for (int i = 0; i < launches; ++i) {
@@ -80,14 +67,10 @@ int lamm_steps_isolated(const lamm_matrix* A, int nA, const lamm_matrix* B, cons
     (void)hipEventCreate(&e1[i]);
   }
   for (int i = 0; i < launches && rc == LAMM_OK; ++i) {
-    hipLaunchKernelGGL(gate_kernel, dim3(1), dim3(64), 0, s, flag, (unsigned)(i + 1));
-    (void)hipEventRecord(e0[i], s);
+    (void)lamm_hip_profile_next(e0[i], e1[i]);
     rc = lamm_hip_matmul(&A[(first + i) % nA], B, C, stream);
-    (void)hipEventRecord(e1[i], s);
-    __atomic_store_n(flag, (unsigned)(i + 1), __ATOMIC_RELEASE);   // open the gate
-    if (hipEventSynchronize(e1[i]) != hipSuccess) rc = -2;
+    if (sync_each && hipEventSynchronize(e1[i]) != hipSuccess) rc = -2;
   }
-  __atomic_store_n(flag, 0xffffffffu, __ATOMIC_RELEASE);
   if (hipStreamSynchronize(s) != hipSuccess && rc == LAMM_OK) rc = -2;
   for (int i = 0; i < launches; ++i) {
     float ms = 0.f;
@@ -96,7 +79,6 @@ int lamm_steps_isolated(const lamm_matrix* A, int nA, const lamm_matrix* B, cons
     (void)hipEventDestroy(e0[i]);
     (void)hipEventDestroy(e1[i]);
   }
-  (void)hipHostFree(flag);
   return rc;
 }
 

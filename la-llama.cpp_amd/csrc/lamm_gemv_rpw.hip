@@ -24,23 +24,6 @@
 namespace lamm {
 namespace {
 
-// Completion signal (LAMM_HIP_KERNEL_SIGNAL=1, see GemvArgs): every workgroup releases its C
-// stores to system scope before it counts itself in; the last one to arrive acquires the others'
-// releases and only then stores the flag the host spins on (a relaxed counter alone
-// let the host see the flag before other workgroups' C reached host memory).
-__device__ __forceinline__ void signal_done(const GemvArgs& p) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's C stores have completed
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence_system();
-    if (atomicAdd(p.done_ctr, 1u) == gridDim.x * gridDim.y - 1) {
-      __threadfence_system();
-      __hip_atomic_store(p.done_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(p.flag, p.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
-}
-
 // One wave per row: the row's loads for ITER blocks per lane (K <= ITER * 2048) go out at once;
 // each wave also issues its NEXT row's loads before computing the current one (rows strided by
 // the grid), so a persistent grid keeps HBM busy across rows.

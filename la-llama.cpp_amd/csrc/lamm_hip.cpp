@@ -279,8 +279,14 @@ int matmul_impl_(const lamm_matrix* A, const lamm_matrix* B, const lamm_matrix* 
   p.b_f32 = b_f32 ? 1 : 0;
   hipError_t e;
   if (flags & LAMM_ORDER_REFERENCE) {   // the reference's x86 float order (lamm_ref.hip), bit for bit
-    if (!ref_order_supported(A->type, B->type))
-      return fail(LAMM_ERR_TYPE, "no reference-order kernel for A type %d with B type %d", A->type, B->type);
+    if (!ref_order_supported(A->type, vdt) || (b_f32 && !ref_gemv_supported(A->type, p)))
+      return fail(LAMM_ERR_TYPE, "no reference-order kernel for A type %d with B type %d (N %d)", A->type, B->type, N);
+    if (done && ref_gemv_supported(A->type, p) && p.ne12 * p.ne13 == 1) {
+      p.done_ctr = done->ctr;
+      p.flag = done->flag;
+      p.seq = done->seq;
+      done->signaled = true;
+    }
     e = launch_ref(A->type, p, s);
     if (e != hipSuccess) return fail(LAMM_ERR_HIP, "kernel launch: %s", hipGetErrorString(e));
     return LAMM_OK;
@@ -838,9 +844,7 @@ constexpr int64_t kViewMinRows = 8;
 bool views_accepted(const ggml::tensor* src0, const ggml::tensor* src1) {
   if (is_weight(src0)) return true;
   if (knobs().views >= 0) return knobs().views == 1;
-  // in the reference's float order the F16 views stay with ggml (no reference-order F16 kernel:
-  // the reference's own routing, LAMM_HIP_VIEWS=1 takes them anyway)
-  if (knobs().ref_order) return false;
+  // (in the reference's order the views compute in ggml_vec_dot_f16's order: ref_f16_kernel)
   return src1->ne[1] >= kViewMinRows;
 }
 
@@ -875,10 +879,11 @@ ActMode act_mode(const ggml::tensor* src0, const ggml::tensor* src1) {
   if (!f32_rows) return kCpuInit;
   const int gq = knobs().gpu_quant;
   if (gq == 0) return kCpuInit;
-  // the reference-order kernels take quantized rows: ggml's own INIT for decode-sized calls, the GPU
-  // quantizer (the same AVX2-flavour bytes) from 8 rows up
+  // in the reference's order only the one-column kernel (ref_gemv_kernel) quantizes in its staging;
+  // 2 .. 7 rows take ggml's own INIT, 8 and more the GPU quantizer (the same AVX2-flavour bytes)
+  const bool ref_fused = src1->ne[1] == 1 && src1->ne[2] * src1->ne[3] == 1 && src0->ne[0] / 32 <= 576;
   if (knobs().fused && gq != 1 && (vdt == kQ8_0 || vdt == kQ8_1) && src1->ne[1] <= 8 && is_weight(src0) &&
-      !boundary_ref_order(src0))
+      (!boundary_ref_order(src0) || ref_fused))
     return kFused;
   const int64_t rows = src1->ne[1] * src1->ne[2] * src1->ne[3];
   if (gq != 1 && rows < 8) return kCpuInit;

@@ -75,8 +75,11 @@ void set_max_lds(const void* kernel, int bytes);
 hipError_t launch_signal(unsigned* flag_dev, unsigned seq, hipStream_t s);
 
 // mul_mat in the reference's x86 float order, bit for bit (lamm_ref.hip): q4_0 / q5_0 x q8_0,
-// q4_1 / q5_1 x q8_1, q6_K x q8_K; any N, batch slices
+// q4_1 / q5_1 x q8_1, q6_K x q8_K; any N, batch slices.  One-column calls of the 32-element formats
+// (ref_gemv_supported) also take F32 activation rows (p.b_f32: ggml's AVX2 INIT quantization in
+// the kernel's staging), honour lamm_hip_profile_next and can signal their own completion (p.flag)
 bool ref_order_supported(int type, int btype);
+bool ref_gemv_supported(int type, const GemvArgs& p);
 hipError_t launch_ref(int type, const GemvArgs& p, hipStream_t s);
 
 hipError_t launch_gemm(int type, const GemvArgs& p, void* workspace, hipStream_t s);

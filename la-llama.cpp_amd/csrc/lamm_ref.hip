@@ -26,8 +26,11 @@
 // loads (the 2-byte aligned blocks read back with a realignment), the activation columns as quads
 // laid out [column][lane][unit].  The quants are turned into signed bytes (q - 8,
 // q - 16, q - 32) so each X_l is one v_dot4 -- integer, exact, any order.
+#include <hip/hip_ext.h>
+
 #include "lamm_device.h"
 #include "lamm_kernels.h"
+#include "lamm_rowdot.h"
 
 namespace lamm {
 namespace {
@@ -251,6 +254,294 @@ __global__ __launch_bounds__(RR * 8) void ref_kernel(GemvArgs p) {
   }
 }
 
+// ---------------------------------------------------------------- decode: producers and chains
+// A one-column call has only 8 chains per weight row -- 32768 for a 4096-row GEMV, half a wave
+// per SIMD -- so ref_kernel (each chain thread also decoding its own quads) ran one long
+// dependent stream per thread: 28 us per 4096 x 4096 call in llama.cpp's decode (rocprofv3,
+// profiles/r04/ref_order/).  Here the chains only do the part that must be sequential:
+//   producers  all 256 threads of the workgroup: 4 consecutive blocks of one of its 8 rows per
+//              thread (one wide load of 4 BPB bytes), each block's 8 exact lane sums X_l and
+//              d = fp32(d_a) * fp32(d_b) (and m_a * s_b) into LDS, a chunk of GKC blocks at a time;
+//   chains     wave 0, lane (row, l): acc_l = fma(d, X_l, acc_l) over the chunk (b128 LDS reads),
+//              then reduce_sum's tree across the row's 8 lanes.
+// The activation column is staged once per workgroup (ActStage; F32 rows quantized there, ggml's
+// AVX2 from_float bit for bit -- the boundary's fused INIT).  The chunk's A loads for the next
+// chunk are in flight while the chains run.
+constexpr int GR = 8, GKC = 128, GNT = 256, GP = GKC + 4;   // rows, blocks per chunk, threads, LDS pitch
+
+// dword at byte O of a register byte string, zero past its end (the last block's slack bytes)
+template <int O, int NW>
+__device__ __forceinline__ uint32_t get32z(const uint32_t (&w)[NW]) {
+  if constexpr ((O >> 2) >= NW) return 0u;
+  else if constexpr ((O & 3) == 0) return w[O >> 2];
+  else if constexpr ((O >> 2) + 1 < NW) return __builtin_amdgcn_alignbit(w[(O >> 2) + 1], w[O >> 2], (O & 3) * 8);
+  else return w[O >> 2] >> ((O & 3) * 8);
+}
+
+size_t ref_gemv_lds(int type, int nblk) {
+  const bool aff = type == kQ4_1 || type == kQ5_1;
+  return (((size_t)nblk * 40 + 15) & ~size_t(15)) + sizeof(float) * GP * (GR * 8 + GR + (aff ? GR : 0));
+}
+
+template <int T, bool BF32, bool ONE_SLICE>
+__global__ __launch_bounds__(GNT) void ref_gemv_kernel(GemvArgs p) {
+  using F = RFmt<T>;
+  constexpr bool AFF = T == kQ4_1 || T == kQ5_1;
+  // -OFF as four int8: sum (q - OFF) b = sum q b + sum (-OFF) b, both exact
+  constexpr uint32_t NEG = T == kQ4_0 ? 0xf8f8f8f8u : T == kQ5_0 ? 0xf0f0f0f0u : 0u;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  const int nb = p.nblk;
+  u32x4* sq0 = reinterpret_cast<u32x4*>(smem_raw);
+  u32x4* sq1 = sq0 + nb;
+  float* sbd = reinterpret_cast<float*>(sq1 + nb);
+  float* sbs = sbd + nb;
+  float* xs = reinterpret_cast<float*>(smem_raw + ((nb * 40 + 15) & ~15));   // [row * 8 + l][GP]
+  float* dsm = xs + GR * 8 * GP;                                             // [row][GP]
+  float* pms = dsm + GR * GP;                                                // [row][GP] (q4_1 / q5_1)
+
+  const unsigned char* Az = p.A;
+  const unsigned char* Bz = p.B;
+  float* Cz = p.C;
+  if constexpr (!ONE_SLICE) {
+    const int z = blockIdx.z, i12 = z % p.ne12, i13 = z / p.ne12;
+    Az += (int64_t)(i12 / p.r2) * p.sa2 + (int64_t)(i13 / p.r3) * p.sa3;
+    Bz += (int64_t)i12 * p.sb2 + (int64_t)i13 * p.sb3;
+    Cz += (int64_t)i12 * p.sc2 + (int64_t)i13 * p.sc3;
+  }
+  const int t = threadIdx.x;
+  const int row0 = blockIdx.x * GR;
+  const int nrows = p.M - row0 < GR ? p.M - row0 : GR;
+  const auto ra = make_rsrc(Az + (int64_t)row0 * p.lda,
+                            (uint32_t)(((int64_t)(nrows - 1) * p.lda + (int64_t)nb * F::BPB + 3) & ~int64_t(3)));
+  // producer: row pr, blocks 4 pg .. 4 pg + 3 of each chunk
+  const int pr = t >> 5, pg = t & 31;
+  uint32_t w[F::BPB];   // 4 blocks: 4 BPB bytes = BPB dwords, 16-byte aligned (4 BPB % 16 == 8 or 0)
+  auto issue = [&](int u0) {
+    const int u = u0 + 4 * pg;
+    const uint32_t off = pr < nrows && u < nb ? (uint32_t)((int64_t)pr * p.lda + (int64_t)u * F::BPB) : 0x7ffffff0u;
+    load_words<F::BPB, 2>(ra, off, w);   // non-temporal: A is read once
+  };
+  issue(0);
+  // ---- the activation column, once per workgroup
+  const auto rb = act_rsrc<T, 1, BF32>(p, Bz);
+  if constexpr (BF32) {
+    for (int it = t; it < 2 * nb; it += GNT) {   // two lanes per block (pairs stay together: GNT even)
+      ActStageL<T, 2> sl;
+      sl.template load<1>(p, rb, it);
+      sl.store(it, sq0, sq1, sbd, sbs);
+    }
+  } else {
+    for (int it = t; it < nb; it += GNT) {
+      ActStage<T, false> st;
+      st.template load<1>(p, rb, it);
+      st.store(it, sq0, sq1, sbd, sbs);
+    }
+  }
+  __syncthreads();
+
+  const int cl = t & 7, cr = t >> 3;   // chain lane (wave 0): row cr, lane cl
+  float chain = 0.f, summs = 0.f;
+  for (int u0 = 0; u0 < nb; u0 += GKC) {
+    // ---- producers: 4 blocks of row pr
+    {
+      f32x4 xv[8], dv, pv;
+      unroll<4>([&](auto J) {
+        constexpr int j = J;
+        const int u = u0 + 4 * pg + j;
+        const bool ok = pr < nrows && u < nb;
+        uint32_t m[F::BPB / 4 + 1];
+        unroll<F::BPB / 4 + 1>([&](auto K) { m[K] = get32z<j * F::BPB + 4 * K>(w); });
+        uint32_t q[8];
+        float da, ma;
+        unpack_a<T>(m, q, da, ma);
+        const int ub = ok ? u : 0;
+        const u32x4 b0 = sq0[ub], b1 = sq1[ub];
+        const uint32_t bq[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+        float d = da * sbd[ub];
+        asm volatile("" : "+v"(d));   // rounded on its own: never contracted into the chain's fma
+#pragma unroll
+        for (int l = 0; l < 8; ++l) {
+          const int c = NEG ? dot4(bq[l], NEG, 0) : 0;
+          xv[l][j] = ok ? (float)dot4(q[l], bq[l], c) : 0.f;
+        }
+        dv[j] = ok ? d : 0.f;
+        if constexpr (AFF) {
+          float pm = ma * sbs[ub];
+          asm volatile("" : "+v"(pm));
+          pv[j] = ok ? pm : 0.f;
+        }
+      });
+#pragma unroll
+      for (int l = 0; l < 8; ++l) *reinterpret_cast<f32x4*>(&xs[(pr * 8 + l) * GP + 4 * pg]) = xv[l];
+      *reinterpret_cast<f32x4*>(&dsm[pr * GP + 4 * pg]) = dv;
+      if constexpr (AFF) *reinterpret_cast<f32x4*>(&pms[pr * GP + 4 * pg]) = pv;
+    }
+    if (u0 + GKC < nb) issue(u0 + GKC);   // the next chunk's A under the chains
+    __syncthreads();
+    // ---- chains: wave 0, the chunk's blocks in order (zeros past nb leave a chain unchanged:
+    // fma(0, 0, acc) == acc, and no chain is ever -0)
+    if (t < 64) {
+      const int nu = nb - u0 < GKC ? nb - u0 : GKC;
+      const float* xr = &xs[(cr * 8 + cl) * GP];
+      const float* dr = &dsm[cr * GP];
+      for (int k = 0; k < nu; k += 4) {
+        const f32x4 x4 = *reinterpret_cast<const f32x4*>(&xr[k]);
+        const f32x4 d4 = *reinterpret_cast<const f32x4*>(&dr[k]);
+        chain = __builtin_fmaf(d4[0], x4[0], chain);
+        chain = __builtin_fmaf(d4[1], x4[1], chain);
+        chain = __builtin_fmaf(d4[2], x4[2], chain);
+        chain = __builtin_fmaf(d4[3], x4[3], chain);
+        if constexpr (AFF) {
+          const f32x4 p4 = *reinterpret_cast<const f32x4*>(&pms[cr * GP + k]);
+          summs = summs + p4[0];   // one rounding per block, in block order (no products here)
+          summs = summs + p4[1];
+          summs = summs + p4[2];
+          summs = summs + p4[3];
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (t < 64) {
+    float v = chain;
+    {
+#pragma clang fp contract(off)
+      v = v + __shfl_down(v, 4, 8);
+      v = v + __shfl_down(v, 2, 8);
+      v = v + __shfl_down(v, 1, 8);
+      if constexpr (AFF) v = v + summs;
+    }
+    if (cl == 0 && cr < nrows) Cz[row0 + cr] = v;
+  }
+  if (p.flag) signal_done(p);
+}
+
+// ---------------------------------------------------------------- F16 x F16: ggml_vec_dot_f16's order
+// The attention mul_mats (KQ over the F16 K cache, KQV over the F16 V cache) in ggml's AVX2
+// ggml_vec_dot_f16 order (LC/ggml.c:1589-1629, GGML_F32x8_REDUCE :946-964; oracle
+// f16_dot_avx, pinned to the reference's own attention nodes): element i of each 32-element step
+// feeds accumulator slot i % 32 (sum[(i % 32) / 8] lane i % 8) through one fp32 fma on the
+// F16-widened values (v_fma_mix_f32: the widening is exact, one rounding), then
+//     v_e = (s_e + s_{16+e}) + (s_{8+e} + s_{24+e}),  t_e = v_e + v_{e+4},  (t0 + t1) + (t2 + t3)
+// and the n % 32 leftovers in double.  Slots are independent chains, so a thread keeps all 32 of
+// each of its 2 x 2 outputs (128 accumulators) and the tree runs in registers; 32 x 32 outputs
+// per workgroup, K through LDS in steps of 64 halves (16-byte rows when the pitches allow).
+constexpr int FT = 32, FKC = 64, FNT = 256, FPITCH = FKC + 8;   // tile, K step, threads, LDS pitch (halves)
+
+// acc = fma(f16 half H of a, f16 half H of b, acc) with one rounding: v_fma_mix_f32 widens its f16
+// sources exactly (hipcc widens with separate v_cvt_f32_f16 instead, one per operand)
+template <int H>
+__device__ __forceinline__ void fma_mix(float& acc, uint32_t a, uint32_t b) {
+  if constexpr (H == 0)
+    asm("v_fma_mix_f32 %0, %1, %2, %0 op_sel_hi:[1,1,0]" : "+v"(acc) : "v"(a), "v"(b));
+  else
+    asm("v_fma_mix_f32 %0, %1, %2, %0 op_sel:[1,1,0] op_sel_hi:[1,1,0]" : "+v"(acc) : "v"(a), "v"(b));
+}
+
+template <bool VEC, bool ONE_SLICE>
+__global__ __launch_bounds__(FNT) void ref_f16_kernel(GemvArgs p) {
+  __shared__ __attribute__((aligned(16))) _Float16 sa[FT * FPITCH];
+  __shared__ __attribute__((aligned(16))) _Float16 sb[FT * FPITCH];
+  const unsigned char* Az = p.A;
+  const unsigned char* Bz = p.B;
+  float* Cz = p.C;
+  if constexpr (!ONE_SLICE) {
+    const int z = blockIdx.z, i12 = z % p.ne12, i13 = z / p.ne12;
+    Az += (int64_t)(i12 / p.r2) * p.sa2 + (int64_t)(i13 / p.r3) * p.sa3;
+    Bz += (int64_t)i12 * p.sb2 + (int64_t)i13 * p.sb3;
+    Cz += (int64_t)i12 * p.sc2 + (int64_t)i13 * p.sc3;
+  }
+  const int t = threadIdx.x, tc = t & 15, tr = t >> 4;
+  const int m0 = blockIdx.x * FT, n0 = blockIdx.y * FT;
+  const int nrows = p.M - m0 < FT ? p.M - m0 : FT;
+  const int ncols = p.N - n0 < FT ? p.N - n0 : FT;
+  const int K = p.K, np = K & ~31;
+  const auto ra = make_rsrc(Az + (int64_t)m0 * p.lda, (uint32_t)((int64_t)(nrows - 1) * p.lda + 2 * (int64_t)K));
+  const auto rb = make_rsrc(Bz + (int64_t)n0 * p.ldb, (uint32_t)((int64_t)(ncols - 1) * p.ldb + 2 * (int64_t)K));
+
+  float acc[2][2][32];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int s = 0; s < 32; ++s) acc[i][j][s] = 0.f;
+
+  // staging: thread t moves 8 halves of row / column t >> 3, elements 8 (t & 7) .. of the step
+  const int sr = t >> 3, se = 8 * (t & 7);
+  for (int k0 = 0; k0 < np; k0 += FKC) {
+    const int k = k0 + se;
+    const bool kin = k < np;   // np % 32 == 0: a group of 8 is wholly in or out
+    u32x4 va = {0u, 0u, 0u, 0u}, vb = {0u, 0u, 0u, 0u};
+    if constexpr (VEC) {
+      va = bload16(ra, sr < nrows && kin ? (uint32_t)((int64_t)sr * p.lda + 2 * k) : 0x7ffffff0u);
+      vb = bload16(rb, sr < ncols && kin ? (uint32_t)((int64_t)sr * p.ldb + 2 * k) : 0x7ffffff0u);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; e += 2) {
+        const uint32_t oa = sr < nrows && kin ? (uint32_t)((int64_t)sr * p.lda + 2 * (k + e)) : 0x7ffffff0u;
+        const uint32_t ob = sr < ncols && kin ? (uint32_t)((int64_t)sr * p.ldb + 2 * (k + e)) : 0x7ffffff0u;
+        va[e / 2] = (uint32_t)bload2(ra, oa) | ((uint32_t)bload2(ra, oa + 2) << 16);
+        vb[e / 2] = (uint32_t)bload2(rb, ob) | ((uint32_t)bload2(rb, ob + 2) << 16);
+      }
+    }
+    __syncthreads();   // the previous step's reads are done
+    *reinterpret_cast<u32x4*>(&sa[sr * FPITCH + se]) = va;
+    *reinterpret_cast<u32x4*>(&sb[sr * FPITCH + se]) = vb;
+    __syncthreads();
+#pragma unroll
+    for (int g = 0; g < FKC / 8; ++g) {
+      const int s0 = (8 * g) & 31;
+      const u32x4 a0 = *reinterpret_cast<const u32x4*>(&sa[(2 * tr) * FPITCH + 8 * g]);
+      const u32x4 a1 = *reinterpret_cast<const u32x4*>(&sa[(2 * tr + 1) * FPITCH + 8 * g]);
+      const u32x4 b0 = *reinterpret_cast<const u32x4*>(&sb[(2 * tc) * FPITCH + 8 * g]);
+      const u32x4 b1 = *reinterpret_cast<const u32x4*>(&sb[(2 * tc + 1) * FPITCH + 8 * g]);
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {   // halves 2w (low) and 2w + 1 (high) of the group
+        fma_mix<0>(acc[0][0][s0 + 2 * w], a0[w], b0[w]);
+        fma_mix<0>(acc[0][1][s0 + 2 * w], a0[w], b1[w]);
+        fma_mix<0>(acc[1][0][s0 + 2 * w], a1[w], b0[w]);
+        fma_mix<0>(acc[1][1][s0 + 2 * w], a1[w], b1[w]);
+        fma_mix<1>(acc[0][0][s0 + 2 * w + 1], a0[w], b0[w]);
+        fma_mix<1>(acc[0][1][s0 + 2 * w + 1], a0[w], b1[w]);
+        fma_mix<1>(acc[1][0][s0 + 2 * w + 1], a1[w], b0[w]);
+        fma_mix<1>(acc[1][1][s0 + 2 * w + 1], a1[w], b1[w]);
+      }
+    }
+  }
+  // GGML_F32x8_REDUCE per output, then the leftovers in double
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int m = m0 + 2 * tr + i, n = n0 + 2 * tc + j;
+      const float* s = acc[i][j];
+      float r;
+      {
+#pragma clang fp contract(off)
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = (s[e] + s[16 + e]) + (s[8 + e] + s[24 + e]);
+        const float t0 = v[0] + v[4], t1 = v[1] + v[5], t2 = v[2] + v[6], t3 = v[3] + v[7];
+        r = (t0 + t1) + (t2 + t3);
+      }
+      if (m < p.M && n < p.N) {
+        if (np < K) {
+          double sumf = (double)r;
+          for (int kk = np; kk < K; ++kk) {
+            const float x = h2f(bload2(ra, (uint32_t)((int64_t)(2 * tr + i) * p.lda + 2 * kk)));
+            const float y = h2f(bload2(rb, (uint32_t)((int64_t)(2 * tc + j) * p.ldb + 2 * kk)));
+            float xy = x * y;   // exact (11-bit significands), as the reference's float product
+            asm volatile("" : "+v"(xy));
+            sumf += (double)xy;
+          }
+          r = (float)sumf;
+        }
+        Cz[(int64_t)n * p.ldc + m] = r;
+      }
+    }
+}
+
 // ---------------------------------------------------------------- prefill: the same order on MFMA
 // The lane sums X_l come from v_mfma_f32_32x32x16_f16 with a block-diagonal activation operand:
 // its 32 rows are (column n, lane l) pairs, row (n, l) carrying b_n's 4 quants of lane l (as f16,
@@ -448,12 +739,59 @@ bool ref_order_supported(int type, int btype) {
     case kQ4_0: case kQ5_0: return btype == kQ8_0;
     case kQ4_1: case kQ5_1: return btype == kQ8_1;
     case kQ6_K: return btype == kQ8_K;
+    case kF16: return btype == kF16;
     default: return false;
   }
 }
 
+bool ref_gemv_supported(int type, const GemvArgs& p) {
+  const bool fmt = type == kQ4_0 || type == kQ4_1 || type == kQ5_0 || type == kQ5_1;
+  return fmt && p.N == 1 && p.nblk <= 576 && ref_gemv_lds(type, p.nblk) <= 65536;
+}
+
 hipError_t launch_ref(int type, const GemvArgs& p, hipStream_t s) {
   const int slices = p.ne12 * p.ne13;
+  if (ref_gemv_supported(type, p)) {   // one column: ref_gemv_kernel (F32 rows quantized in its staging)
+    const dim3 g((unsigned)((p.M + GR - 1) / GR), 1, (unsigned)slices);
+    const size_t lds = ref_gemv_lds(type, p.nblk);
+    const LaunchTiming tm = take_launch_timing();
+    auto gov = [&](auto tc) {
+      constexpr int T = decltype(tc)::value;
+      auto go3 = [&](auto kern) {
+        if (tm.start) hipExtLaunchKernelGGL(kern, g, dim3(GNT), lds, s, tm.start, tm.stop, 0, p);
+        else hipLaunchKernelGGL(kern, g, dim3(GNT), lds, s, p);
+      };
+      if (p.b_f32) {
+        if (slices == 1) go3(ref_gemv_kernel<T, true, true>);
+        else go3(ref_gemv_kernel<T, true, false>);
+      } else {
+        if (slices == 1) go3(ref_gemv_kernel<T, false, true>);
+        else go3(ref_gemv_kernel<T, false, false>);
+      }
+    };
+    switch (type) {
+      case kQ4_0: gov(std::integral_constant<int, kQ4_0>{}); break;
+      case kQ4_1: gov(std::integral_constant<int, kQ4_1>{}); break;
+      case kQ5_0: gov(std::integral_constant<int, kQ5_0>{}); break;
+      case kQ5_1: gov(std::integral_constant<int, kQ5_1>{}); break;
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
+  if (p.b_f32) return hipErrorInvalidValue;   // F32 activations: the one-column kernel only
+  if (type == kF16) {   // ggml_vec_dot_f16's order (ref_f16_kernel); 16-byte rows take wide loads
+    const dim3 g((unsigned)((p.M + FT - 1) / FT), (unsigned)((p.N + FT - 1) / FT), (unsigned)slices);
+    const bool vec = ((uintptr_t)p.B & 15) == 0 && (p.ldb & 15) == 0 && (p.sb2 & 15) == 0 && (p.sb3 & 15) == 0 &&
+                     (p.lda & 15) == 0 && ((uintptr_t)p.A & 15) == 0;
+    if (vec) {
+      if (slices == 1) hipLaunchKernelGGL((ref_f16_kernel<true, true>), g, dim3(FNT), 0, s, p);
+      else hipLaunchKernelGGL((ref_f16_kernel<true, false>), g, dim3(FNT), 0, s, p);
+    } else {
+      if (slices == 1) hipLaunchKernelGGL((ref_f16_kernel<false, true>), g, dim3(FNT), 0, s, p);
+      else hipLaunchKernelGGL((ref_f16_kernel<false, false>), g, dim3(FNT), 0, s, p);
+    }
+    return hipGetLastError();
+  }
   // prefill-sized calls on the 32-element formats: the MFMA form (ref_mfma_kernel)
   if (p.N > 8 && type != kQ6_K) {
     const dim3 gm((unsigned)((p.M + MR - 1) / MR), (unsigned)((p.N + MC - 1) / MC), (unsigned)slices);

@@ -641,6 +641,30 @@ static float tree8(const float *a) {
   return (x0 + x2) + (x1 + x3);
 }
 
+/* ggml's AVX2 ggml_vec_dot_f16 (LC/ggml.c:1589-1629; GGML_F16_STEP 32, GGML_F16_EPR 8 :979-1027):
+ * FOUR __m256 accumulators, element i of each 32-element step into sum[(i % 32) / 8] lane i % 8,
+ * sum = fma(x, y, sum) on the F16C-widened values; then GGML_F32x8_REDUCE (:946-964):
+ * sum0 += sum2, sum1 += sum3, sum0 += sum1 lanewise, t0 = low half + high half, two hadds:
+ * ((t0 + t1) + (t2 + t3)) with t_e = v_e + v_{e+4}.  The n % 32 leftovers are added after that in
+ * double (ggml_float) and the result rounded to float. */
+static float f16_dot_avx(int n, const uint16_t *x, const uint16_t *y) {
+  float s[4][8];
+  memset(s, 0, sizeof s);
+  const int np = n & ~31;
+  for (int i = 0; i < np; i += 32)
+    for (int j = 0; j < 4; ++j)
+      for (int e = 0; e < 8; ++e) {
+        const int ii = i + 8 * j + e;
+        s[j][e] = fmaf(H2F(x[ii]), H2F(y[ii]), s[j][e]);
+      }
+  float v[8], t[4];
+  for (int e = 0; e < 8; ++e) v[e] = (s[0][e] + s[2][e]) + (s[1][e] + s[3][e]);
+  for (int e = 0; e < 4; ++e) t[e] = v[e] + v[e + 4];
+  double sumf = (double)((t[0] + t[1]) + (t[2] + t[3]));
+  for (int i = np; i < n; ++i) sumf += (double)(H2F(x[i]) * H2F(y[i]));
+  return (float)sumf;
+}
+
 /* quant e (0..31) of a 32-element block, with the format's offset (q4_0: q - 8, q5_0: q - 16) */
 static int blk_q(int type, const uint8_t *a, int e) {
   const int j = e & 15, hi = e >= 16;
@@ -666,6 +690,7 @@ float lo_vec_dot_avx(int type, int k, const void *va, const void *vb) {
       for (int l = 0; l < 8; ++l) acc[l] = fmaf(x[i + l], y[i + l], acc[l]);
     return tree8(acc);
   }
+  if (type == LO_F16) return f16_dot_avx(k, (const uint16_t *)va, (const uint16_t *)vb);
   const size_t ab = lo_block_bytes(type), bb = lo_block_bytes(lo_vec_dot_type(type));
   if (type == LO_Q6_K) {
     for (int i = 0; i < k / 256; ++i, a += ab, b += bb) {

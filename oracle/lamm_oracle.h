@@ -51,7 +51,9 @@ void lo_mul_mat(int type, int M, int N, int K, const void *A, size_t lda_bytes,
 
 /* The reference's x86 CPU float order (the lamm opt-3 AVX2 kernels; ggml's AVX2 q6_K): eight
  * fp32 FMA chains per output, one per __m256 lane, then reduce_sum's fixed tree.  Types f32, q4_0,
- * q4_1, q5_0, q5_1, q6_K (0 for the others).  Pinned bit-for-bit to the golden C_lamm3. */
+ * q4_1, q5_0, q5_1, q6_K (0 for the others).  Pinned bit-for-bit to the golden C_lamm3.
+ * f16 (x f16): ggml's AVX2 ggml_vec_dot_f16 -- 32 FMA chains, GGML_F32x8_REDUCE's tree, the
+ * n % 32 leftovers in double -- pinned to the reference's own attention nodes (tests/golden/ref_nodes/f16_attention.npz). */
 float lo_vec_dot_avx(int type, int k, const void *a, const void *b);
 void lo_mul_mat_avx(int type, int M, int N, int K, const void *A, size_t lda_bytes,
                     const void *B, size_t ldb_bytes, float *C, size_t ldc);

@@ -40,7 +40,7 @@ def layer_of(src0):
     return int(src0.split(".")[1])
 
 
-AVX_TYPES = (ol.Q4_0, ol.Q4_1, ol.Q5_0, ol.Q5_1, ol.Q6_K)   # lo_mul_mat_avx: the reference's x86 order
+AVX_TYPES = (ol.Q4_0, ol.Q4_1, ol.Q5_0, ol.Q5_1, ol.Q6_K, ol.F16)   # lo_mul_mat_avx: the reference's x86 order
 
 
 def check_node(d, ent):

@@ -4,6 +4,8 @@ C_lamm3, tools/gen_golden.py) and against the oracle's restatement of that order
 (lo_mul_mat_avx, itself pinned to C_lamm3 in tests/test_oracle_golden.py), on ragged shapes,
 strided operands and batch slices; and through the ggml boundary, which runs this order by
 default (LAMM_HIP_ORDER)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -48,8 +50,10 @@ def test_reference_order_matches_lamm3_golden(path):
     assert np.array_equal(bits(c[:, :done]), bits(z["C_lamm3"][:, :done]))
 
 
+# N = 1: ref_gemv_kernel (chunks of 128 blocks: K = 11008 is 3; past 576 blocks ref_kernel)
 SHAPES = [(1, 1, 256), (17, 3, 512), (31, 9, 768), (67, 1, 4096), (33, 18, 4096), (40, 7, 4096 + 256),
-          (130, 2, 11008 - 256 * 3), (257, 33, 1024), (4096, 1, 4096)]
+          (130, 2, 11008 - 256 * 3), (257, 33, 1024), (4096, 1, 4096), (45, 1, 11008), (13, 1, 4096 + 32 * 5),
+          (40, 1, 32 * 600)]
 
 
 def random_blocks(t, M, N, K, seed):
@@ -101,6 +105,114 @@ def test_reference_order_strides_and_slices(t):
         want = ORACLE.mul_mat_avx(t, M, N, K, A_q[z // 3], B_q[z])
         sl = got[z * N * ldc:(z + 1) * N * ldc].reshape(N, ldc)[:, :M]
         assert np.array_equal(bits(sl), bits(want)), f"slice {z}"
+
+
+GEMV_TYPES = [ol.Q4_0, ol.Q4_1, ol.Q5_0, ol.Q5_1]
+
+
+@pytest.mark.parametrize("t", GEMV_TYPES, ids=[ol.NAMES[t] for t in GEMV_TYPES])
+@pytest.mark.parametrize("shape", [(1, 256), (67, 4096), (4096, 4096), (45, 11008), (9, 32 * 577)],
+                         ids=["1x256", "67x4096", "4096x4096", "45x11008", "9x18464"])
+def test_reference_order_gemv_f32_rows(t, shape):
+    """One F32 activation row (the boundary's decode calls, kFused): ref_gemv_kernel quantizes it
+    in its staging the way ggml's AVX2 INIT does, then computes in the reference's order -- the
+    same bits as quantizing with the oracle's AVX2 flavour and running mul_mat_avx.  Past 576
+    blocks the kernel declines F32 rows (LammError), as the boundary's routing expects."""
+    M, K = shape
+    rng = np.random.default_rng(M + K)
+    A_q = ORACLE.quantize(t, rng.standard_normal((M, K), dtype=np.float32), ol.QUANT_REF)
+    x = (rng.standard_normal((1, K)) * rng.uniform(0.1, 3.0)).astype(np.float32)
+    x[0, :7] = 0.0                       # a zero run inside the first block
+    kb = K // 32
+    lda = pitch_blocks(t, kb)
+    A = dev_bytes(pitched_A(t, A_q, M, kb, lda))
+    B = torch.from_numpy(x.reshape(-1)).to("cuda")
+    C = torch.full((M + 16,), float("nan"), dtype=torch.float32, device="cuda")
+    Am = la.Matrix(A.data_ptr(), t, M, kb, lda)
+    Bm = la.Matrix(B.data_ptr(), la.F32, K, 1, K)
+    Cm = la.Matrix(C.data_ptr(), la.F32, M, 1, M)
+    if kb > 576:
+        with pytest.raises(la.LammError):
+            la.matmul_ex(Am, Bm, Cm, None, la.ORDER_REFERENCE, torch.cuda.current_stream().cuda_stream)
+        return
+    la.matmul_ex(Am, Bm, Cm, None, la.ORDER_REFERENCE, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    got = C.cpu().numpy()[:M]
+    B_q = ORACLE.quantize(la.vec_dot_type(t), x, ol.QUANT_AVX)
+    want = ORACLE.mul_mat_avx(t, M, 1, K, A_q, B_q)[0]
+    assert np.array_equal(bits(got), bits(want)), f"{(got != want).sum()} of {M} differ"
+
+
+@pytest.mark.parametrize("t", [ol.Q4_0, ol.Q5_1], ids=["q4_0", "q5_1"])
+def test_reference_order_gemv_slices(t):
+    """N = 1 over 3 x 2 batch slices (one A slice per 3 B slices): ref_gemv_kernel's slice path."""
+    M, N, K = 37, 1, 4096
+    kb = K // 32
+    lda = pitch_blocks(t, kb)
+    vt = la.vec_dot_type(t)
+    rbB = kb * la.type_size(vt)
+    A_q = [random_blocks(t, M, 1, K, seed=20 + s)[0] for s in range(2)]
+    B_q = [random_blocks(t, 1, N, K, seed=30 + s)[1] for s in range(6)]
+    arow = lda * la.type_size(t)
+    bt = la.Batch(2, 1, 6, 1, M * arow, 2 * M * arow, N * rbB, 6 * N * rbB, 4 * M * N, 4 * M * N * 6)
+    A = dev_bytes(np.concatenate([pitched_A(t, A_q[s], M, kb, lda)[:M * arow] for s in range(2)] +
+                                 [np.zeros(64, np.uint8)]))
+    B = dev_bytes(np.concatenate(B_q))
+    C = torch.full((6 * M + 16,), float("nan"), dtype=torch.float32, device="cuda")
+    la.mul_mat_torch(t, A, B, C, M, N, K, lda=lda, batch=bt, flags=la.ORDER_REFERENCE)
+    torch.cuda.synchronize()
+    got = C.cpu().numpy()
+    for z in range(6):
+        want = ORACLE.mul_mat_avx(t, M, N, K, A_q[z // 3], B_q[z])[0]
+        assert np.array_equal(bits(got[z * M:(z + 1) * M]), bits(want)), f"slice {z}"
+
+
+F16_NODES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ref_nodes", "f16_attention.npz")
+
+
+@pytest.mark.parametrize("tag", ["prefill_kq", "prefill_kqv", "decode_kq", "decode_kqv"])
+def test_reference_order_f16_matches_reference_attention_nodes(tag):
+    """F16 x F16 (ref_f16_kernel, ggml_vec_dot_f16's AVX2 order): the reference's own KQ / KQV
+    nodes (tools/gen_golden_f16.py: its CPU build, 4 heads) bit for bit, the heads as batch slices."""
+    z = np.load(F16_NODES, allow_pickle=False)
+    A16, X, Cref = z[tag + "_src0"], z[tag + "_src1"], z[tag + "_dst"]
+    heads, M, K = A16.shape
+    N = X.shape[1]
+    B = np.concatenate([ORACLE.quantize(ol.F16, X[h], ol.QUANT_REF) for h in range(heads)])
+    A = dev_bytes(np.concatenate([A16.reshape(-1).view(np.uint8), np.zeros(64, np.uint8)]))
+    Bd = dev_bytes(np.concatenate([B, np.zeros(64, np.uint8)]))
+    C = torch.full((heads * N * M + 16,), float("nan"), dtype=torch.float32, device="cuda")
+    bt = la.Batch(heads, 1, heads, 1, 2 * M * K, 2 * M * K * heads, 2 * N * K, 2 * N * K * heads, 4 * M * N,
+                  4 * M * N * heads)
+    la.mul_mat_torch(la.F16, A, Bd, C, M, N, K, batch=bt, flags=la.ORDER_REFERENCE)
+    torch.cuda.synchronize()
+    got = C.cpu().numpy()[:heads * N * M].reshape(heads, N, M)
+    assert np.array_equal(bits(got), bits(np.ascontiguousarray(Cref))), f"{(got != Cref).sum()} differ"
+
+
+@pytest.mark.parametrize("shape", [(64, 40, 128), (33, 7, 100), (128, 1, 64), (97, 65, 544), (5, 3, 20), (32, 32, 4096)],
+                         ids=["64x40x128", "33x7x100", "128x1x64", "97x65x544", "5x3x20", "32x32x4096"])
+def test_reference_order_f16_vs_oracle(shape):
+    """Ragged tiles, n % 32 leftovers (added in double after the tree), the 2-byte-load staging
+    (K = 100, 20: rows not 16-byte multiples) and f16 subnormals in both operands."""
+    M, N, K = shape
+    rng = np.random.default_rng(M * 3 + N * 5 + K)
+    a = (rng.standard_normal((M, K)) * 0.5).astype(np.float16)
+    b32 = (rng.standard_normal((N, K)) * 2.0).astype(np.float32)
+    a.reshape(-1)[::17] = np.float16(3e-6)            # f16 subnormals
+    b32.reshape(-1)[::13] = 1e-7
+    lda = (K + 7) // 8 * 8
+    ap = np.zeros((M, lda), np.float16)
+    ap[:, :K] = a
+    B = ORACLE.quantize(ol.F16, b32, ol.QUANT_REF)
+    A = dev_bytes(np.concatenate([ap.reshape(-1).view(np.uint8), np.zeros(64, np.uint8)]))
+    Bd = dev_bytes(np.concatenate([B, np.zeros(64, np.uint8)]))
+    C = torch.full((N * M + 16,), float("nan"), dtype=torch.float32, device="cuda")
+    la.mul_mat_torch(la.F16, A, Bd, C, M, N, K, lda=lda, flags=la.ORDER_REFERENCE)
+    torch.cuda.synchronize()
+    got = C.cpu().numpy()[:N * M].reshape(N, M)
+    want = ORACLE.mul_mat_avx(ol.F16, M, N, K, a.view(np.uint8).reshape(M, 2 * K), B)
+    assert np.array_equal(bits(got), bits(want)), f"{(got != want).sum()} of {got.size} differ"
 
 
 def test_reference_order_rejects_other_types():

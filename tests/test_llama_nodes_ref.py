@@ -29,5 +29,6 @@ def test_reference_build_nodes_match_oracle(tmp_path):
     assert len(res) == 38
     # the reference's AVX2 float order against the oracle's scalar one: rounding only
     assert max(r[5] for r in res) < 1e-6
-    # and bit for bit the oracle's restatement of that order (q4_0 projections, the q6_K output)
-    assert all(r[6] for r in res if r[6] is not None) and sum(r[6] is not None for r in res) == 30
+    # and bit for bit the oracle's restatement of that order (q4_0 projections, the q6_K output,
+    # and the F16 attention nodes KQ / KQV in ggml_vec_dot_f16's AVX2 order): every node
+    assert all(r[6] for r in res) and sum(r[6] is not None for r in res) == 38

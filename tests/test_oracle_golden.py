@@ -3,6 +3,7 @@
 CPU-only.  Every assertion here is BIT-EXACT: the oracle restates the reference's
 scalar arithmetic in the same evaluation order, so any difference is a restatement bug.
 """
+import os
 import numpy as np
 import pytest
 
@@ -114,3 +115,28 @@ def test_known_answer_constant_inputs():
         B = ORACLE.quantize(vt, np.full((N, K), 2.0, np.float32))
         c = ORACLE.mul_mat(t, M, N, K, A, B)
         assert abs(c.sum(dtype=np.float64) - 2.0 * K * M * N) / (2.0 * K * M * N) < 1e-2, ol.NAMES[t]
+
+
+F16_NODES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ref_nodes", "f16_attention.npz")
+
+
+@pytest.mark.parametrize("tag", ["prefill_kq", "prefill_kqv", "decode_kq", "decode_kqv"])
+def test_f16_avx_order_matches_reference_attention_nodes(tag):
+    """ggml's AVX2 ggml_vec_dot_f16 order (lo_vec_dot_avx for F16) reproduces the reference's own
+    KQ / KQV nodes bit for bit: src1 rounded to F16 the way ggml's INIT does (RNE), then 32 FMA
+    chains and GGML_F32x8_REDUCE's tree (tools/gen_golden_f16.py ran the reference's CPU build)."""
+    z = np.load(F16_NODES, allow_pickle=False)
+    A, X, C = z[tag + "_src0"], z[tag + "_src1"], z[tag + "_dst"]
+    heads, M, K = A.shape
+    N = X.shape[1]
+    for h in range(heads):
+        B = ORACLE.quantize(ol.F16, X[h], ol.QUANT_REF)
+        c = ORACLE.mul_mat_avx(ol.F16, M, N, K, A[h].view(np.uint8), B)
+        assert np.array_equal(c.view(np.uint32), np.ascontiguousarray(C[h]).view(np.uint32)), f"head {h}"
+    # the scalar order (one double sum) is a different order: the fixture does discriminate
+    B = ORACLE.quantize(ol.F16, X[0], ol.QUANT_REF)
+    Af = A[0].view(np.float16).astype(np.float64)
+    Bf = B.view(np.float16).reshape(N, K).astype(np.float64)
+    naive = (Bf @ Af.T).astype(np.float32)
+    if tag.startswith("prefill"):
+        assert not np.array_equal(naive.view(np.uint32), np.ascontiguousarray(C[0]).view(np.uint32))

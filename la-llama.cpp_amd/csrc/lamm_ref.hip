@@ -31,6 +31,7 @@
 #include "lamm_device.h"
 #include "lamm_kernels.h"
 #include "lamm_rowdot.h"
+#include "lamm_knobs.h"
 
 namespace lamm {
 namespace {
@@ -732,6 +733,372 @@ __global__ __launch_bounds__(MNT) void ref_mfma_kernel(GemvArgs p) {
     }
 }
 
+// The same arithmetic, pipelined (ref_mfma_kernel measured ~0.4 ms per Llama-7B prefill
+// projection in llama.cpp, profiles/r04/ref_order/: every chunk waited for its own HBM loads and
+// built the block-diagonal operand with four per-lane selects per MFMA):
+//   * the next chunk's A and activation bytes are loaded into registers while the current chunk
+//     computes, then written to LDS between two barriers;
+//   * the activation image in LDS is already block-diagonal: per (column, block, half) the four
+//     quads as f16, each in its own 16-byte slot at the position its lanes need ({q, 0} for even
+//     lanes l % 4, {0, q} for odd) -- one ds_read_b128 per MFMA operand, lanes whose slot is zero
+//     read a shared zero quad;
+//   * G groups of 8 columns per wave (G = 4: 64 columns per workgroup, the weight operand built
+//     once per block for 4 groups).
+template <int T, int G, bool ONE_SLICE>
+__global__ __launch_bounds__(MNT) void ref_mfma2_kernel(GemvArgs p) {
+  using F = RefFmt<T>;
+  static_assert(F::UE == 32, "32-element block formats");
+  constexpr bool AFF = F::M >= 0;
+  constexpr int MC2 = 16 * G;                       // columns per workgroup
+  constexpr int SEG = MKB * F::BPB;
+  static_assert(SEG % 16 == 0, "chunks start 16-byte aligned");
+  constexpr int SEGW = SEG / 4 + 1;
+  constexpr int NAL = MR * (SEG / 16);              // A b128 loads per chunk
+  constexpr int NA = (NAL + MNT - 1) / MNT;
+  constexpr int NB = MC2 * MKB / MNT;               // activation blocks per thread per chunk
+  static_assert(MC2 * MKB % MNT == 0, "whole activation items per thread");
+  constexpr int NPC = MKB * 32 + 4;                 // dwords per column of the padded image (+4: banks)
+  constexpr int ZQ = MC2 * NPC;                     // the zero quad
+  __shared__ __attribute__((aligned(16))) uint32_t sa[MR * SEGW];
+  __shared__ __attribute__((aligned(16))) uint32_t sbp[MC2 * NPC + 4];
+  __shared__ float sdb[MKB][MC2];
+  __shared__ float ssb[AFF ? MKB : 1][AFF ? MC2 : 1];
+
+  const unsigned char* Az = p.A;
+  const unsigned char* Bz = p.B;
+  float* Cz = p.C;
+  if constexpr (!ONE_SLICE) {
+    const int z = blockIdx.z, i12 = z % p.ne12, i13 = z / p.ne12;
+    Az += (int64_t)(i12 / p.r2) * p.sa2 + (int64_t)(i13 / p.r3) * p.sa3;
+    Bz += (int64_t)i12 * p.sb2 + (int64_t)i13 * p.sb3;
+    Cz += (int64_t)i12 * p.sc2 + (int64_t)i13 * p.sc3;
+  }
+  const int t = threadIdx.x, lane = t & 63, lr = lane & 31, h = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6), wm = w & 1, wn = w >> 1;
+  const int m0 = blockIdx.x * MR, n0 = blockIdx.y * MC2;
+  const int nrows = p.M - m0 < MR ? p.M - m0 : MR;
+  const int ncols = p.N - n0 < MC2 ? p.N - n0 : MC2;
+  const int nunits = p.nblk;
+  const auto ra = make_rsrc(Az + (int64_t)m0 * p.lda,
+                            (uint32_t)(((int64_t)(nrows - 1) * p.lda + (int64_t)nunits * F::BPB + 3) & ~int64_t(3)));
+  const int64_t bbytes = (int64_t)(ncols - 1) * p.ldb + (int64_t)nunits * F::VB;
+  const auto rb = make_rsrc(Bz + (int64_t)n0 * p.ldb, (uint32_t)((bbytes + 3) & ~int64_t(3)));
+  const int ml = 32 * wm + lr;
+
+  u32x4 pa[NA];
+  uint32_t pb[NB][10];
+  auto fetch = [&](int u0) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int it = t + i * MNT, r = it / (SEG / 16), o = it % (SEG / 16);
+      const uint32_t off = it < NAL && r < nrows ? (uint32_t)((int64_t)r * p.lda + (int64_t)u0 * F::BPB) + 16 * o
+                                                 : 0x7ffffff0u;
+      pa[i] = bload16(ra, off);
+    }
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int item = t + j * MNT, c = item / MKB, k = item % MKB;
+      const bool ok = c < ncols && u0 + k < nunits;
+      const uint32_t off = (uint32_t)((int64_t)c * p.ldb + (int64_t)(u0 + k) * F::VB);
+      const uint32_t base = ok ? (off & ~3u) : 0x7ffffff0u;
+#pragma unroll
+      for (int i = 0; i < 10; ++i) pb[j][i] = bload4(rb, base + 4 * i);
+    }
+  };
+  auto commit = [&](int u0) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int it = t + i * MNT, r = it / (SEG / 16), o = it % (SEG / 16);
+      if (it < NAL) {
+        uint32_t* dst = &sa[r * SEGW + 4 * o];
+        dst[0] = pa[i][0]; dst[1] = pa[i][1]; dst[2] = pa[i][2]; dst[3] = pa[i][3];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int item = t + j * MNT, c = item / MKB, k = item % MKB;
+      const bool ok = c < ncols && u0 + k < nunits;
+      const int sh = (int)((uint32_t)((int64_t)c * p.ldb + (int64_t)(u0 + k) * F::VB) & 3u) * 8;
+      uint32_t m[9];
+#pragma unroll
+      for (int i = 0; i < 9; ++i) m[i] = __builtin_amdgcn_alignbit(pb[j][i + 1], pb[j][i], sh);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {   // quad q = lane q of the block: half q >> 2, slot q & 3
+        const uint32_t qd = AFF ? m[1 + q] : __builtin_amdgcn_alignbit(m[q + 1], m[q], 16);
+        uint32_t lo, hi;
+        q4_to_f16<128>(qd ^ 0x80808080u, lo, hi);
+        if (!ok) lo = hi = 0u;
+        const u32x4 v = (q & 1) ? u32x4{0u, 0u, lo, hi} : u32x4{lo, hi, 0u, 0u};
+        *reinterpret_cast<u32x4*>(&sbp[c * NPC + k * 32 + (q >> 2) * 16 + (q & 3) * 4]) = v;
+      }
+      sdb[k][c] = ok ? h2f(m[0] & 0xffffu) : 0.f;
+      if constexpr (AFF) ssb[k][c] = ok ? h2f(m[0] >> 16) : 0.f;
+    }
+  };
+
+  f32x16 acc[G][2];
+  float summs[G][4];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[g][q][r] = 0.f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) summs[g][c] = 0.f;
+  }
+  // this lane's operand slot in the padded image: row lr = (column lr / 4, slot lr % 4) of the
+  // group, K = 8h .. 8h + 7 of the half -- nonzero only when the slot's quad lies there
+  const int lq = lr & 3;
+  const bool mine = (lq >> 1) == h;
+  const uint32_t* arow = &sa[ml * SEGW];
+  if (t < 4) sbp[ZQ + t] = 0u;
+  fetch(0);
+  for (int u0 = 0; u0 < nunits; u0 += MKB) {
+    const int nu = nunits - u0 < MKB ? nunits - u0 : MKB;
+    if (u0 > 0) __syncthreads();   // every wave is done reading the previous chunk
+    commit(u0);
+    __syncthreads();
+    if (u0 + MKB < nunits) fetch(u0 + MKB);   // the next chunk's bytes fly under this one's math
+    for (int k = 0; k < nu; ++k) {
+      const int ub = k * F::BPB;
+      const float da = h2f(lds32(arow, ub) & 0xffffu);
+      const float ma = AFF ? h2f(lds32(arow, ub + (AFF ? F::M : 0)) & 0xffffu) : 0.f;
+      uint32_t q0 = lds32(arow, ub + F::QS + 8 * h), q1 = lds32(arow, ub + F::QS + 8 * h + 4);
+      uint32_t wlo[2] = {q0 & 0x0f0f0f0fu, q1 & 0x0f0f0f0fu};
+      uint32_t whi[2] = {(q0 >> 4) & 0x0f0f0f0fu, (q1 >> 4) & 0x0f0f0f0fu};
+      if constexpr (F::QH >= 0) {
+        const uint32_t qh = lds32(arow, ub + (F::QH >= 0 ? F::QH : 0));
+        wlo[0] |= spread4_hi((qh >> (8 * h)) & 0xfu);
+        wlo[1] |= spread4_hi((qh >> (8 * h + 4)) & 0xfu);
+        whi[0] |= spread4_hi((qh >> (16 + 8 * h)) & 0xfu);
+        whi[1] |= spread4_hi((qh >> (16 + 8 * h + 4)) & 0xfu);
+      }
+      uint32_t wf[2][4];
+      q4_to_f16<F::OFF>(wlo[0], wf[0][0], wf[0][1]);
+      q4_to_f16<F::OFF>(wlo[1], wf[0][2], wf[0][3]);
+      q4_to_f16<F::OFF>(whi[0], wf[1][0], wf[1][1]);
+      q4_to_f16<F::OFF>(whi[1], wf[1][2], wf[1][3]);
+      const half8 W0 = __builtin_bit_cast(half8, u32x4{wf[0][0], wf[0][1], wf[0][2], wf[0][3]});
+      const half8 W1 = __builtin_bit_cast(half8, u32x4{wf[1][0], wf[1][1], wf[1][2], wf[1][3]});
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const int nb = 8 * G * wn + 8 * g;
+        const int slot = mine ? (nb + (lr >> 2)) * NPC + k * 32 + lq * 4 : ZQ;
+        const u32x4 a0 = *reinterpret_cast<const u32x4*>(&sbp[slot]);
+        const u32x4 a1 = *reinterpret_cast<const u32x4*>(&sbp[mine ? slot + 16 : ZQ]);
+        const f32x16 zero = {};
+        const f32x16 S0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, a0), W0, zero, 0, 0, 0);
+        const f32x16 S1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, a1), W1, zero, 0, 0, 0);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          float d = da * sdb[k][nb + 2 * c + h];
+          asm volatile("" : "+v"(d));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            acc[g][0][4 * c + e] = __builtin_fmaf(d, S0[4 * c + e], acc[g][0][4 * c + e]);
+            acc[g][1][4 * c + e] = __builtin_fmaf(d, S1[4 * c + e], acc[g][1][4 * c + e]);
+          }
+          if constexpr (AFF) {
+            float pm = ma * ssb[k][nb + 2 * c + h];
+            asm volatile("" : "+v"(pm));
+            summs[g][c] = summs[g][c] + pm;
+          }
+        }
+      }
+    }
+  }
+  const int m = m0 + ml;
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int n = 8 * G * wn + 8 * g + 2 * c + h;
+      float v;
+      {
+#pragma clang fp contract(off)
+        const float x0 = acc[g][0][4 * c + 0] + acc[g][1][4 * c + 0], x1 = acc[g][0][4 * c + 1] + acc[g][1][4 * c + 1];
+        const float x2 = acc[g][0][4 * c + 2] + acc[g][1][4 * c + 2], x3 = acc[g][0][4 * c + 3] + acc[g][1][4 * c + 3];
+        v = (x0 + x2) + (x1 + x3);
+        if constexpr (AFF) v = v + summs[g][c];
+      }
+      if (m < p.M && n < ncols) Cz[(int64_t)(n0 + n) * p.ldc + m] = v;
+    }
+}
+
+// q6_K x q8_K prefill in ggml's AVX2 order (ggml_vec_dot_q6_K_q8_K): per super-block
+//   X_l = sum_h sc[2h + (l >= 4)] * (4-element dot of group h, lane l)   (exact int32)
+//   acc_l = fma(y.d * fp32(x.d), (float)X_l, acc_l)
+// Each 32-element group h is one "block" of ref_mfma2_kernel's block-diagonal MFMA (the lane dots
+// of 32 weight rows x 8 columns, two MFMAs per group); X accumulates in fp32 registers
+// (X += sc * S: integers below 2^24, exact) and the chain step runs once per super-block.
+// One super-block per chunk: the rows' 210 bytes come by dword loads from the dword below their
+// start (a 2-byte shift on odd super-blocks), the activation quads go to the padded f16 image.
+template <int G, bool ONE_SLICE>
+__global__ __launch_bounds__(MNT) void ref_mfma_kq_kernel(GemvArgs p) {
+  constexpr int MC2 = 16 * G;
+  constexpr int AW = 54;                            // dwords per row image (210 bytes + a 2-byte shift)
+  constexpr int NAL = MR * AW;
+  constexpr int NA = (NAL + MNT - 1) / MNT;
+  constexpr int NQ = MC2 * 64;                      // activation quads per super-block
+  constexpr int NB = NQ / MNT;
+  static_assert(NQ % MNT == 0, "whole quads per thread");
+  constexpr int NPC = 256 + 4;                      // dwords per column: 8 groups x 2 halves x 4 slots x 4
+  constexpr int ZQ = MC2 * NPC;
+  __shared__ __attribute__((aligned(16))) uint32_t sa[MR * (AW + 1)];
+  __shared__ __attribute__((aligned(16))) uint32_t sbp[MC2 * NPC + 4];
+  __shared__ float sdb[MC2];
+
+  const unsigned char* Az = p.A;
+  const unsigned char* Bz = p.B;
+  float* Cz = p.C;
+  if constexpr (!ONE_SLICE) {
+    const int z = blockIdx.z, i12 = z % p.ne12, i13 = z / p.ne12;
+    Az += (int64_t)(i12 / p.r2) * p.sa2 + (int64_t)(i13 / p.r3) * p.sa3;
+    Bz += (int64_t)i12 * p.sb2 + (int64_t)i13 * p.sb3;
+    Cz += (int64_t)i12 * p.sc2 + (int64_t)i13 * p.sc3;
+  }
+  const int t = threadIdx.x, lane = t & 63, lr = lane & 31, h = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6), wm = w & 1, wn = w >> 1;
+  const int m0 = blockIdx.x * MR, n0 = blockIdx.y * MC2;
+  const int nrows = p.M - m0 < MR ? p.M - m0 : MR;
+  const int ncols = p.N - n0 < MC2 ? p.N - n0 : MC2;
+  const int nsb = p.nblk;
+  const auto ra = make_rsrc(Az + (int64_t)m0 * p.lda,
+                            (uint32_t)(((int64_t)(nrows - 1) * p.lda + (int64_t)nsb * 210 + 3) & ~int64_t(3)));
+  const auto rb = make_rsrc(Bz + (int64_t)n0 * p.ldb, (uint32_t)((int64_t)(ncols - 1) * p.ldb + (int64_t)nsb * 292));
+  const int ml = 32 * wm + lr;
+
+  uint32_t pa[NA], pb[NB];
+  float pd = 0.f;
+  auto fetch = [&](int u) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int it = t + i * MNT, r = it / AW, o = it % AW;
+      const uint32_t off = it < NAL && r < nrows ? (uint32_t)(((int64_t)r * p.lda + (int64_t)u * 210) & ~int64_t(3)) + 4 * o
+                                                 : 0x7ffffff0u;
+      pa[i] = bload4(ra, off);
+    }
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int item = t + j * MNT, c = item >> 6, qi = item & 63;
+      pb[j] = bload4(rb, c < ncols ? (uint32_t)((int64_t)c * p.ldb + (int64_t)u * 292 + 4 + 4 * qi) : 0x7ffffff0u);
+    }
+    if (t < MC2) pd = __builtin_bit_cast(float, bload4(rb, t < ncols ? (uint32_t)((int64_t)t * p.ldb + (int64_t)u * 292)
+                                                                      : 0x7ffffff0u));
+  };
+  auto commit = [&]() {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int it = t + i * MNT, r = it / AW, o = it % AW;
+      if (it < NAL) sa[r * (AW + 1) + o] = pa[i];
+    }
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int item = t + j * MNT, c = item >> 6, qi = item & 63;   // quad qi: group qi / 8, lane qi % 8
+      uint32_t lo, hi;
+      q4_to_f16<128>(pb[j] ^ 0x80808080u, lo, hi);
+      const int l = qi & 7;
+      const u32x4 v = (l & 1) ? u32x4{0u, 0u, lo, hi} : u32x4{lo, hi, 0u, 0u};
+      *reinterpret_cast<u32x4*>(&sbp[c * NPC + (qi >> 3) * 32 + (l >> 2) * 16 + (l & 3) * 4]) = v;
+    }
+    if (t < MC2) sdb[t] = pd;
+  };
+
+  f32x16 acc[G][2];
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[g][q][r] = 0.f;
+  const int lq = lr & 3;
+  const bool mine = (lq >> 1) == h;
+  const uint32_t* arow = &sa[ml * (AW + 1)];
+  if (t < 4) sbp[ZQ + t] = 0u;
+  fetch(0);
+  for (int u = 0; u < nsb; ++u) {
+    const int sh = (int)(((int64_t)ml * p.lda + (int64_t)u * 210) & 3);   // this row's shift in its image
+    if (u > 0) __syncthreads();
+    commit();
+    __syncthreads();
+    if (u + 1 < nsb) fetch(u + 1);
+    const float da = h2f(lds32(arow, sh + 208) & 0xffffu);
+    const uint32_t scw[4] = {lds32(arow, sh + 192), lds32(arow, sh + 196), lds32(arow, sh + 200), lds32(arow, sh + 204)};
+    f32x16 X[G][2];
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) X[g][q][r] = 0.f;
+#pragma unroll 1
+    for (int gh = 0; gh < 8; ++gh) {   // group gh = 4 j + gg: ql[64 j + 32 (gg & 1) + e], qh[32 j + e] >> 2 gg
+      const int j = gh >> 2, gg = gh & 3;
+      uint32_t wf[2][4];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {   // half q: elements 16 q + 8 h .. + 7 of the group
+        const int e0 = 16 * q + 8 * h;
+        const uint32_t l0 = lds32(arow, sh + 64 * j + 32 * (gg & 1) + e0), l1 = lds32(arow, sh + 64 * j + 32 * (gg & 1) + e0 + 4);
+        const uint32_t h0 = lds32(arow, sh + 128 + 32 * j + e0), h1 = lds32(arow, sh + 128 + 32 * j + e0 + 4);
+        const uint32_t v0 = ((gg < 2 ? l0 : l0 >> 4) & 0x0f0f0f0fu) | (((h0 >> (2 * gg)) & 0x03030303u) << 4);
+        const uint32_t v1 = ((gg < 2 ? l1 : l1 >> 4) & 0x0f0f0f0fu) | (((h1 >> (2 * gg)) & 0x03030303u) << 4);
+        q4_to_f16<32>(v0, wf[q][0], wf[q][1]);
+        q4_to_f16<32>(v1, wf[q][2], wf[q][3]);
+      }
+      const half8 W0 = __builtin_bit_cast(half8, u32x4{wf[0][0], wf[0][1], wf[0][2], wf[0][3]});
+      const half8 W1 = __builtin_bit_cast(half8, u32x4{wf[1][0], wf[1][1], wf[1][2], wf[1][3]});
+      // scales of the group's two 16-element halves (lanes 0-3 / 4-7): sc[2 gh], sc[2 gh + 1]
+      const float s0 = (float)(int8_t)((scw[gh >> 1] >> (16 * (gh & 1))) & 0xffu);
+      const float s1 = (float)(int8_t)((scw[gh >> 1] >> (16 * (gh & 1) + 8)) & 0xffu);
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const int nb = 8 * G * wn + 8 * g;
+        const int slot = mine ? (nb + (lr >> 2)) * NPC + gh * 32 + lq * 4 : ZQ;
+        const u32x4 a0 = *reinterpret_cast<const u32x4*>(&sbp[slot]);
+        const u32x4 a1 = *reinterpret_cast<const u32x4*>(&sbp[mine ? slot + 16 : ZQ]);
+        const f32x16 zero = {};
+        const f32x16 S0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, a0), W0, zero, 0, 0, 0);
+        const f32x16 S1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, a1), W1, zero, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {   // exact: |X| < 2^24
+          X[g][0][r] = __builtin_fmaf(s0, S0[r], X[g][0][r]);
+          X[g][1][r] = __builtin_fmaf(s1, S1[r], X[g][1][r]);
+        }
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int nb = 8 * G * wn + 8 * g;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        float d = sdb[nb + 2 * c + h] * da;   // y.d * fp32(x.d)
+        asm volatile("" : "+v"(d));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          acc[g][0][4 * c + e] = __builtin_fmaf(d, X[g][0][4 * c + e], acc[g][0][4 * c + e]);
+          acc[g][1][4 * c + e] = __builtin_fmaf(d, X[g][1][4 * c + e], acc[g][1][4 * c + e]);
+        }
+      }
+    }
+  }
+  const int m = m0 + ml;
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int n = 8 * G * wn + 8 * g + 2 * c + h;
+      float v;
+      {
+#pragma clang fp contract(off)
+        const float x0 = acc[g][0][4 * c + 0] + acc[g][1][4 * c + 0], x1 = acc[g][0][4 * c + 1] + acc[g][1][4 * c + 1];
+        const float x2 = acc[g][0][4 * c + 2] + acc[g][1][4 * c + 2], x3 = acc[g][0][4 * c + 3] + acc[g][1][4 * c + 3];
+        v = (x0 + x2) + (x1 + x3);
+      }
+      if (m < p.M && n < ncols) Cz[(int64_t)(n0 + n) * p.ldc + m] = v;
+    }
+}
+
 }  // namespace
 
 bool ref_order_supported(int type, int btype) {
@@ -793,12 +1160,30 @@ hipError_t launch_ref(int type, const GemvArgs& p, hipStream_t s) {
     return hipGetLastError();
   }
   // prefill-sized calls on the 32-element formats: the MFMA form (ref_mfma_kernel)
+  if (p.N > 8 && type == kQ6_K && knobs().ref_mfma != 1) {   // q6_K prefill: ref_mfma_kq_kernel
+    const dim3 gm((unsigned)((p.M + MR - 1) / MR), (unsigned)((p.N + 31) / 32), (unsigned)slices);
+    if (slices == 1) hipLaunchKernelGGL((ref_mfma_kq_kernel<2, true>), gm, dim3(MNT), 0, s, p);
+    else hipLaunchKernelGGL((ref_mfma_kq_kernel<2, false>), gm, dim3(MNT), 0, s, p);
+    return hipGetLastError();
+  }
   if (p.N > 8 && type != kQ6_K) {
-    const dim3 gm((unsigned)((p.M + MR - 1) / MR), (unsigned)((p.N + MC - 1) / MC), (unsigned)slices);
+    // ref_mfma2_kernel with 4 column groups per wave from 64 columns, else 2 (LAMM_REF_MFMA=1:
+    // the unpipelined ref_mfma_kernel)
+    const int sel = knobs().ref_mfma > 0 ? knobs().ref_mfma : p.N >= 64 ? 4 : 2;
+    const int mc = sel == 4 ? 64 : 32;
+    const dim3 gm((unsigned)((p.M + MR - 1) / MR), (unsigned)((p.N + mc - 1) / mc), (unsigned)slices);
     auto gom = [&](auto tc) {
       constexpr int T = decltype(tc)::value;
-      if (slices == 1) hipLaunchKernelGGL((ref_mfma_kernel<T, true>), gm, dim3(MNT), 0, s, p);
-      else hipLaunchKernelGGL((ref_mfma_kernel<T, false>), gm, dim3(MNT), 0, s, p);
+      if (sel == 1) {
+        if (slices == 1) hipLaunchKernelGGL((ref_mfma_kernel<T, true>), gm, dim3(MNT), 0, s, p);
+        else hipLaunchKernelGGL((ref_mfma_kernel<T, false>), gm, dim3(MNT), 0, s, p);
+      } else if (sel == 4) {
+        if (slices == 1) hipLaunchKernelGGL((ref_mfma2_kernel<T, 4, true>), gm, dim3(MNT), 0, s, p);
+        else hipLaunchKernelGGL((ref_mfma2_kernel<T, 4, false>), gm, dim3(MNT), 0, s, p);
+      } else {
+        if (slices == 1) hipLaunchKernelGGL((ref_mfma2_kernel<T, 2, true>), gm, dim3(MNT), 0, s, p);
+        else hipLaunchKernelGGL((ref_mfma2_kernel<T, 2, false>), gm, dim3(MNT), 0, s, p);
+      }
     };
     switch (type) {
       case kQ4_0: gom(std::integral_constant<int, kQ4_0>{}); break;

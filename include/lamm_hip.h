@@ -157,7 +157,9 @@ const char *lamm_hip_engine(int type, int64_t M, int N, int K, int slices, int s
  * its decode-GEMV dispatch (one column, K = 4096: BASELINE config 2's kernel) in these two HIP
  * events (hipEvent_t, created by the caller), from the dispatch's own timestamps
  * (hipExtLaunchKernel) -- the duration a kernel tracer reports, with no event packets of their own
- * around it.  Other engines ignore the request; it expires with that call either way. */
+ * around it.  The one-column decode kernels take it this way (the block-format GEMV, the k-quant
+ * GEMV, the reference-order GEMV); for every other engine the two events are recorded on the
+ * stream around the call's launches.  The request expires with that call either way. */
 int lamm_hip_profile_next(void *start_event, void *stop_event);
 
 const char *lamm_hip_last_error(void);

@@ -603,9 +603,14 @@ hipError_t launch_gemv_kq(int type, const GemvArgs& p, hipStream_t s) {
   const dim3 g((unsigned)((p.M + 7) / 8));
   auto go = [&](auto tc) {
     constexpr int T = decltype(tc)::value;
-    if (p.nblk <= 16) hipLaunchKernelGGL((gemv_kq_kernel<T, 1>), g, dim3(512), 0, s, p.A, p.lda, p.B, p.C, p.M, p.nblk);
-    else if (p.nblk <= 32) hipLaunchKernelGGL((gemv_kq_kernel<T, 2>), g, dim3(512), 0, s, p.A, p.lda, p.B, p.C, p.M, p.nblk);
-    else hipLaunchKernelGGL((gemv_kq_kernel<T, 3>), g, dim3(512), 0, s, p.A, p.lda, p.B, p.C, p.M, p.nblk);
+    const LaunchTiming tm = take_launch_timing();
+    auto go = [&](auto kern) {
+      if (tm.start) hipExtLaunchKernelGGL(kern, g, dim3(512), 0, s, tm.start, tm.stop, 0, p.A, p.lda, p.B, p.C, p.M, p.nblk);
+      else hipLaunchKernelGGL(kern, g, dim3(512), 0, s, p.A, p.lda, p.B, p.C, p.M, p.nblk);
+    };
+    if (p.nblk <= 16) go(gemv_kq_kernel<T, 1>);
+    else if (p.nblk <= 32) go(gemv_kq_kernel<T, 2>);
+    else go(gemv_kq_kernel<T, 3>);
   };
   switch (type) {
     case kQ2_K: go(std::integral_constant<int, kQ2_K>{}); break;

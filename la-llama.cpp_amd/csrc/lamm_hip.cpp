@@ -219,8 +219,14 @@ int matmul_impl_(const lamm_matrix* A, const lamm_matrix* B, const lamm_matrix* 
 
 int matmul_impl(const lamm_matrix* A, const lamm_matrix* B, const lamm_matrix* C, const lamm_batch* batch,
                 void* hip_stream, const lamm_weights* W, int flags = 0) {
+  // a profiling request (lamm_hip_profile_next) holds for this call only: kernels launched with
+  // hipExtLaunchKernel take it and record the dispatch's own start / end; for any other engine the
+  // two events bracket the call's launches on the stream instead
+  const LaunchTiming tm = g_timing;
+  if (tm.start) (void)hipEventRecord(tm.start, static_cast<hipStream_t>(hip_stream));
   const int rc = matmul_impl_(A, B, C, batch, hip_stream, W, flags);
-  g_timing = LaunchTiming{};   // a profiling request holds for this call only
+  if (g_timing.start) (void)hipEventRecord(tm.stop, static_cast<hipStream_t>(hip_stream));
+  g_timing = LaunchTiming{};
   return rc;
 }
 

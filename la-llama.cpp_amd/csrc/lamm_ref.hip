@@ -757,10 +757,13 @@ __global__ __launch_bounds__(MNT) void ref_mfma2_kernel(GemvArgs p) {
   constexpr int NA = (NAL + MNT - 1) / MNT;
   constexpr int NB = MC2 * MKB / MNT;               // activation blocks per thread per chunk
   static_assert(MC2 * MKB % MNT == 0, "whole activation items per thread");
-  constexpr int NPC = MKB * 32 + 4;                 // dwords per column of the padded image (+4: banks)
-  constexpr int ZQ = MC2 * NPC;                     // the zero quad
+  // the padded image: per column, block, half and k-group h of the MFMA operand, the 4 slots
+  // (16 bytes each) lanes (slot, h) read: the quad for slots of that k-group, zeros otherwise --
+  // the zero slots are written once; column pitch = 16 banks mod 64, so a ds_read_b128 lane
+  // group (4 columns x 4 slots) covers the 64 banks once
+  constexpr int NPC = MKB * 64 + 16;
   __shared__ __attribute__((aligned(16))) uint32_t sa[MR * SEGW];
-  __shared__ __attribute__((aligned(16))) uint32_t sbp[MC2 * NPC + 4];
+  __shared__ __attribute__((aligned(16))) uint32_t sbp[MC2 * NPC];
   __shared__ float sdb[MKB][MC2];
   __shared__ float ssb[AFF ? MKB : 1][AFF ? MC2 : 1];
 
@@ -829,7 +832,7 @@ __global__ __launch_bounds__(MNT) void ref_mfma2_kernel(GemvArgs p) {
         q4_to_f16<128>(qd ^ 0x80808080u, lo, hi);
         if (!ok) lo = hi = 0u;
         const u32x4 v = (q & 1) ? u32x4{0u, 0u, lo, hi} : u32x4{lo, hi, 0u, 0u};
-        *reinterpret_cast<u32x4*>(&sbp[c * NPC + k * 32 + (q >> 2) * 16 + (q & 3) * 4]) = v;
+        *reinterpret_cast<u32x4*>(&sbp[c * NPC + ((k * 2 + (q >> 2)) * 2 + ((q & 3) >> 1)) * 16 + (q & 3) * 4]) = v;
       }
       sdb[k][c] = ok ? h2f(m[0] & 0xffffu) : 0.f;
       if constexpr (AFF) ssb[k][c] = ok ? h2f(m[0] >> 16) : 0.f;
@@ -850,9 +853,12 @@ __global__ __launch_bounds__(MNT) void ref_mfma2_kernel(GemvArgs p) {
   // this lane's operand slot in the padded image: row lr = (column lr / 4, slot lr % 4) of the
   // group, K = 8h .. 8h + 7 of the half -- nonzero only when the slot's quad lies there
   const int lq = lr & 3;
-  const bool mine = (lq >> 1) == h;
   const uint32_t* arow = &sa[ml * SEGW];
-  if (t < 4) sbp[ZQ + t] = 0u;
+  const uint32_t* bl = &sbp[(8 * G * wn + (lr >> 2)) * NPC + h * 16 + lq * 4];   // + g, block, half offsets
+  for (int z = t; z < MC2 * MKB * 8; z += MNT) {   // the slots of the other k-group: zero for good
+    const int c = z / (MKB * 8), rest = z % (MKB * 8), kh = rest >> 2, s = rest & 3;   // kh = (block, half, h)
+    if ((s >> 1) != (kh & 1)) *reinterpret_cast<u32x4*>(&sbp[c * NPC + kh * 16 + s * 4]) = u32x4{0u, 0u, 0u, 0u};
+  }
   fetch(0);
   for (int u0 = 0; u0 < nunits; u0 += MKB) {
     const int nu = nunits - u0 < MKB ? nunits - u0 : MKB;
@@ -884,9 +890,8 @@ __global__ __launch_bounds__(MNT) void ref_mfma2_kernel(GemvArgs p) {
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         const int nb = 8 * G * wn + 8 * g;
-        const int slot = mine ? (nb + (lr >> 2)) * NPC + k * 32 + lq * 4 : ZQ;
-        const u32x4 a0 = *reinterpret_cast<const u32x4*>(&sbp[slot]);
-        const u32x4 a1 = *reinterpret_cast<const u32x4*>(&sbp[mine ? slot + 16 : ZQ]);
+        const u32x4 a0 = *reinterpret_cast<const u32x4*>(&bl[g * 8 * NPC + k * 64]);
+        const u32x4 a1 = *reinterpret_cast<const u32x4*>(&bl[g * 8 * NPC + k * 64 + 32]);
         const f32x16 zero = {};
         const f32x16 S0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, a0), W0, zero, 0, 0, 0);
         const f32x16 S1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, a1), W1, zero, 0, 0, 0);
@@ -943,10 +948,9 @@ __global__ __launch_bounds__(MNT) void ref_mfma_kq_kernel(GemvArgs p) {
   constexpr int NQ = MC2 * 64;                      // activation quads per super-block
   constexpr int NB = NQ / MNT;
   static_assert(NQ % MNT == 0, "whole quads per thread");
-  constexpr int NPC = 256 + 4;                      // dwords per column: 8 groups x 2 halves x 4 slots x 4
-  constexpr int ZQ = MC2 * NPC;
+  constexpr int NPC = 512 + 16;                     // per column: 8 groups x 2 halves x 2 k-groups x 4 slots x 4
   __shared__ __attribute__((aligned(16))) uint32_t sa[MR * (AW + 1)];
-  __shared__ __attribute__((aligned(16))) uint32_t sbp[MC2 * NPC + 4];
+  __shared__ __attribute__((aligned(16))) uint32_t sbp[MC2 * NPC];
   __shared__ float sdb[MC2];
 
   const unsigned char* Az = p.A;
@@ -1000,7 +1004,7 @@ __global__ __launch_bounds__(MNT) void ref_mfma_kq_kernel(GemvArgs p) {
       q4_to_f16<128>(pb[j] ^ 0x80808080u, lo, hi);
       const int l = qi & 7;
       const u32x4 v = (l & 1) ? u32x4{0u, 0u, lo, hi} : u32x4{lo, hi, 0u, 0u};
-      *reinterpret_cast<u32x4*>(&sbp[c * NPC + (qi >> 3) * 32 + (l >> 2) * 16 + (l & 3) * 4]) = v;
+      *reinterpret_cast<u32x4*>(&sbp[c * NPC + (((qi >> 3) * 2 + (l >> 2)) * 2 + ((l & 3) >> 1)) * 16 + (l & 3) * 4]) = v;
     }
     if (t < MC2) sdb[t] = pd;
   };
@@ -1013,9 +1017,12 @@ __global__ __launch_bounds__(MNT) void ref_mfma_kq_kernel(GemvArgs p) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[g][q][r] = 0.f;
   const int lq = lr & 3;
-  const bool mine = (lq >> 1) == h;
   const uint32_t* arow = &sa[ml * (AW + 1)];
-  if (t < 4) sbp[ZQ + t] = 0u;
+  const uint32_t* bl = &sbp[(8 * G * wn + (lr >> 2)) * NPC + h * 16 + lq * 4];
+  for (int z = t; z < MC2 * 64; z += MNT) {   // the other k-group's slots: zero for good
+    const int c = z >> 6, kh = (z & 63) >> 2, s = z & 3;
+    if ((s >> 1) != (kh & 1)) *reinterpret_cast<u32x4*>(&sbp[c * NPC + kh * 16 + s * 4]) = u32x4{0u, 0u, 0u, 0u};
+  }
   fetch(0);
   for (int u = 0; u < nsb; ++u) {
     const int sh = (int)(((int64_t)ml * p.lda + (int64_t)u * 210) & 3);   // this row's shift in its image
@@ -1053,10 +1060,8 @@ __global__ __launch_bounds__(MNT) void ref_mfma_kq_kernel(GemvArgs p) {
       const float s1 = (float)(int8_t)((scw[gh >> 1] >> (16 * (gh & 1) + 8)) & 0xffu);
 #pragma unroll
       for (int g = 0; g < G; ++g) {
-        const int nb = 8 * G * wn + 8 * g;
-        const int slot = mine ? (nb + (lr >> 2)) * NPC + gh * 32 + lq * 4 : ZQ;
-        const u32x4 a0 = *reinterpret_cast<const u32x4*>(&sbp[slot]);
-        const u32x4 a1 = *reinterpret_cast<const u32x4*>(&sbp[mine ? slot + 16 : ZQ]);
+        const u32x4 a0 = *reinterpret_cast<const u32x4*>(&bl[g * 8 * NPC + gh * 64]);
+        const u32x4 a1 = *reinterpret_cast<const u32x4*>(&bl[g * 8 * NPC + gh * 64 + 32]);
         const f32x16 zero = {};
         const f32x16 S0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, a0), W0, zero, 0, 0, 0);
         const f32x16 S1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, a1), W1, zero, 0, 0, 0);
@@ -1167,9 +1172,9 @@ hipError_t launch_ref(int type, const GemvArgs& p, hipStream_t s) {
     return hipGetLastError();
   }
   if (p.N > 8 && type != kQ6_K) {
-    // ref_mfma2_kernel with 4 column groups per wave from 64 columns, else 2 (LAMM_REF_MFMA=1:
+    // ref_mfma2_kernel, 2 column groups per wave (LAMM_REF_MFMA=4: 4 groups, one wave per SIMD; =1:
     // the unpipelined ref_mfma_kernel)
-    const int sel = knobs().ref_mfma > 0 ? knobs().ref_mfma : p.N >= 64 ? 4 : 2;
+    const int sel = knobs().ref_mfma > 0 ? knobs().ref_mfma : 2;
     const int mc = sel == 4 ? 64 : 32;
     const dim3 gm((unsigned)((p.M + MR - 1) / MR), (unsigned)((p.N + mc - 1) / mc), (unsigned)slices);
     auto gom = [&](auto tc) {

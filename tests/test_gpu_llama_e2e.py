@@ -10,9 +10,9 @@ decode steps (GEMV).
 
 Parity.  The boundary computes in the reference's own x86 float order by default
 (LAMM_HIP_ORDER=reference, csrc/lamm_ref.hip: the lamm opt-3 AVX2 lanes for the q4_0 projections,
-ggml's AVX2 order for the q6_K output; the F16 attention views stay with ggml as in the reference),
-so the logits must be BIT-IDENTICAL to the reference's lamm3 build.  With the fast engines
-(LAMM_HIP_ORDER=fast, or the attention on the GPU) each node still matches within ~3e-7, but a
+ggml's AVX2 order for the q6_K output and for the F16 attention matmuls), so the logits must be
+BIT-IDENTICAL to the reference's lamm3 build.  With the fast engines (LAMM_HIP_ORDER=fast) each
+node still matches within ~3e-7, but a
 quantized network does not carry that through: a 1-ulp change in a K row flips an F16 rounding of
 the KV cache, a q8_0 activation quant flips by 1/127, and the logits move by ~1e-2 of their range
 after two blocks -- as between the reference's own scalar and AVX2 builds (~2e-2).  There the bar
@@ -65,15 +65,15 @@ def ref_spread(model2, cpu_ref, tmp_path_factory):
     return spread
 
 
-EXACT_MODES = ("default", "cpu_init", "two_devices", "zero_copy_split")
+EXACT_MODES = ("default", "cpu_init", "two_devices", "zero_copy_split", "views_on_gpu")
 
 
 @pytest.mark.parametrize("mode", ["default", "cpu_init", "two_devices", "zero_copy_split", "views_on_gpu", "fast"])
 def test_llama_logits_match_reference(model2, cpu_ref, ref_spread, mode, tmp_path):
     """default / cpu_init (ggml's CPU INIT for every call) / two_devices (every weight's rows split
     over two devices, LAMM_HIP_DEVICES, rehearsed on one GPU listed twice, as bench.py runs config 5
-    on N GPUs; zero_copy_split: with decode zero copy on both): the reference's float order, logits
-    bit-identical to the reference's.  views_on_gpu (the F16 attention on the GPU's fast engine) and
+    on N GPUs; zero_copy_split: with decode zero copy on both; views_on_gpu: the decode steps' F16
+    attention on the GPU too): the reference's float order, logits bit-identical to the reference's.
     fast (LAMM_HIP_ORDER=fast): within 1.5x the reference's own scalar-vs-AVX2 spread."""
     env = {"default": {}, "views_on_gpu": {"LAMM_HIP_VIEWS": "1"},
            "cpu_init": {"LAMM_HIP_GPU_QUANT": "0"},
@@ -183,10 +183,12 @@ def test_llama_32_layers_matmul_nodes_vs_oracle(model32, tmp_path, views):
     block of the 32-layer model, plus the Q6_K output.weight, in the prefill and in a decode step:
     the HIP build dumps each node's operands and result (llama_e2e --dump-mm) and the oracle
     recomputes the node from exactly those operands.  Bar: the north-star 1e-3 of max(|c|, sum |a b|)
-    per element for every node, and the 30 q4_0 / q6_K nodes bit-identical to the oracle's
-    restatement of the reference's x86 float order (the boundary's default).
-    views_on_gpu: the attention matmuls on the GPU too (LAMM_HIP_VIEWS=1, the F16 engines; by
-    default ggml keeps them in the reference order)."""
+    per element for every node, and EVERY node (the q4_0 projections, the q6_K output, the F16
+    attention KQ / KQV) bit-identical to the oracle's restatement of the reference's x86 float order
+    (the boundary's default; the F16 order is pinned to the reference's own attention
+    nodes, tests/test_oracle_golden.py).  default: the prefill's attention on the GPU
+    (ref_f16_kernel), the decode step's with ggml; views_on_gpu (LAMM_HIP_VIEWS=1): the decode
+    step's on the GPU too."""
     import llama_nodes as ln
     d = tmp_path / "mm"
     d.mkdir()
@@ -199,8 +201,8 @@ def test_llama_32_layers_matmul_nodes_vs_oracle(model32, tmp_path, views):
         print(f"{phase:8s} layer {layer:3d} {kind:6s} {name:16s} M,N,K,slices={shape}: {err:.2e}"
               f"{'' if exact is None else ', bit-exact in the reference order' if exact else ', NOT bit-exact'}")
     assert all(r[5] < 1e-3 for r in res), [r for r in res if r[5] >= 1e-3]
-    # the q4_0 projections and the q6_K output run in the reference's x86 float order (default)
-    assert all(r[6] for r in res if r[6] is not None) and sum(r[6] is not None for r in res) == 30
+    # every node in the reference's x86 float order (default)
+    assert all(r[6] for r in res) and sum(r[6] is not None for r in res) == 38
     seen = {(p, l, k) for p, l, k, *_ in res}
     for phase in ("prefill", "decode"):
         assert (phase, -1, "output") in seen

@@ -20,6 +20,11 @@
 // API keeps the fast engines (lamm_hip_matmul) and offers this order as lamm_hip_matmul_ex(...,
 // LAMM_ORDER_REFERENCE, ...).
 //
+// Roundings that must stay separate (d = d_a * d_b before the chain's fma) sit behind an empty
+// NON-volatile asm: it hides the value from contraction, and unlike a volatile one it does not
+// order every memory access around it (which serialised the MFMA kernels' LDS reads behind the
+// previous block's FMAs).
+//
 // Layout: a workgroup owns 16 / 32 rows x NCOL columns (1, 2, 4 or 8 by N); thread (row r, lane l)
 // runs the NCOL column chains of lane l for row r (the A quads it decodes are shared by the columns).
 // Per chunk of K both operands come through LDS: the rows' raw block bytes by coalesced 16-byte
@@ -227,11 +232,11 @@ __global__ __launch_bounds__(RR * 8) void ref_kernel(GemvArgs p) {
             }
             // d = fp32(d_a) * fp32(d_b) rounded once (q6_K: y.d * fp32(x.d)), then one fused step
             float d = KQ ? db[u] * da[u] : da[u] * db[u];
-            asm volatile("" : "+v"(d));   // a separate rounding of the product: never contracted into the fma
+            asm("" : "+v"(d));   // a separate rounding of the product: never contracted into the fma
             chain[c] = __builtin_fmaf(d, (float)X, chain[c]);
             if constexpr (AFF) {
               float pm = ma[u] * sb[u];
-              asm volatile("" : "+v"(pm));
+              asm("" : "+v"(pm));
               summs[c] = summs[c] + pm;
             }
           }
@@ -359,7 +364,7 @@ __global__ __launch_bounds__(GNT) void ref_gemv_kernel(GemvArgs p) {
         const u32x4 b0 = sq0[ub], b1 = sq1[ub];
         const uint32_t bq[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
         float d = da * sbd[ub];
-        asm volatile("" : "+v"(d));   // rounded on its own: never contracted into the chain's fma
+        asm("" : "+v"(d));   // rounded on its own: never contracted into the chain's fma
 #pragma unroll
         for (int l = 0; l < 8; ++l) {
           const int c = NEG ? dot4(bq[l], NEG, 0) : 0;
@@ -368,7 +373,7 @@ __global__ __launch_bounds__(GNT) void ref_gemv_kernel(GemvArgs p) {
         dv[j] = ok ? d : 0.f;
         if constexpr (AFF) {
           float pm = ma * sbs[ub];
-          asm volatile("" : "+v"(pm));
+          asm("" : "+v"(pm));
           pv[j] = ok ? pm : 0.f;
         }
       });
@@ -382,10 +387,12 @@ __global__ __launch_bounds__(GNT) void ref_gemv_kernel(GemvArgs p) {
     // ---- chains: wave 0, the chunk's blocks in order (zeros past nb leave a chain unchanged:
     // fma(0, 0, acc) == acc, and no chain is ever -0)
     if (t < 64) {
-      const int nu = nb - u0 < GKC ? nb - u0 : GKC;
+      // the whole chunk, always: the producers zero-filled it past nb, and a fixed trip count
+      // lets the LDS reads run ahead of the chain instead of one wait per 4 blocks
       const float* xr = &xs[(cr * 8 + cl) * GP];
       const float* dr = &dsm[cr * GP];
-      for (int k = 0; k < nu; k += 4) {
+#pragma unroll 8
+      for (int k = 0; k < GKC; k += 4) {
         const f32x4 x4 = *reinterpret_cast<const f32x4*>(&xr[k]);
         const f32x4 d4 = *reinterpret_cast<const f32x4*>(&dr[k]);
         chain = __builtin_fmaf(d4[0], x4[0], chain);
@@ -533,7 +540,7 @@ __global__ __launch_bounds__(FNT) void ref_f16_kernel(GemvArgs p) {
             const float x = h2f(bload2(ra, (uint32_t)((int64_t)(2 * tr + i) * p.lda + 2 * kk)));
             const float y = h2f(bload2(rb, (uint32_t)((int64_t)(2 * tc + j) * p.ldb + 2 * kk)));
             float xy = x * y;   // exact (11-bit significands), as the reference's float product
-            asm volatile("" : "+v"(xy));
+            asm("" : "+v"(xy));
             sumf += (double)xy;
           }
           r = (float)sumf;
@@ -698,7 +705,7 @@ __global__ __launch_bounds__(MNT) void ref_mfma_kernel(GemvArgs p) {
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
           float d = da * sdb[nb + 2 * c + h][k];
-          asm volatile("" : "+v"(d));
+          asm("" : "+v"(d));
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             acc[g][0][4 * c + e] = __builtin_fmaf(d, S[0][4 * c + e], acc[g][0][4 * c + e]);
@@ -706,7 +713,7 @@ __global__ __launch_bounds__(MNT) void ref_mfma_kernel(GemvArgs p) {
           }
           if constexpr (AFF) {
             float pm = ma * ssb[nb + 2 * c + h][k];
-            asm volatile("" : "+v"(pm));
+            asm("" : "+v"(pm));
             summs[g][c] = summs[g][c] + pm;
           }
         }
@@ -855,8 +862,8 @@ __global__ __launch_bounds__(MNT) void ref_mfma2_kernel(GemvArgs p) {
   const int lq = lr & 3;
   const uint32_t* arow = &sa[ml * SEGW];
   const uint32_t* bl = &sbp[(8 * G * wn + (lr >> 2)) * NPC + h * 16 + lq * 4];   // + g, block, half offsets
-  for (int z = t; z < MC2 * MKB * 8; z += MNT) {   // the slots of the other k-group: zero for good
-    const int c = z / (MKB * 8), rest = z % (MKB * 8), kh = rest >> 2, s = rest & 3;   // kh = (block, half, h)
+  for (int z = t; z < MC2 * MKB * 16; z += MNT) {   // the slots of the other k-group: zero for good
+    const int c = z / (MKB * 16), rest = z % (MKB * 16), kh = rest >> 2, s = rest & 3;   // kh = (block, half, h)
     if ((s >> 1) != (kh & 1)) *reinterpret_cast<u32x4*>(&sbp[c * NPC + kh * 16 + s * 4]) = u32x4{0u, 0u, 0u, 0u};
   }
   fetch(0);
@@ -866,7 +873,7 @@ __global__ __launch_bounds__(MNT) void ref_mfma2_kernel(GemvArgs p) {
     commit(u0);
     __syncthreads();
     if (u0 + MKB < nunits) fetch(u0 + MKB);   // the next chunk's bytes fly under this one's math
-    for (int k = 0; k < nu; ++k) {
+    auto block = [&](int k) {
       const int ub = k * F::BPB;
       const float da = h2f(lds32(arow, ub) & 0xffffu);
       const float ma = AFF ? h2f(lds32(arow, ub + (AFF ? F::M : 0)) & 0xffffu) : 0.f;
@@ -898,7 +905,7 @@ __global__ __launch_bounds__(MNT) void ref_mfma2_kernel(GemvArgs p) {
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
           float d = da * sdb[k][nb + 2 * c + h];
-          asm volatile("" : "+v"(d));
+          asm("" : "+v"(d));
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             acc[g][0][4 * c + e] = __builtin_fmaf(d, S0[4 * c + e], acc[g][0][4 * c + e]);
@@ -906,11 +913,17 @@ __global__ __launch_bounds__(MNT) void ref_mfma2_kernel(GemvArgs p) {
           }
           if constexpr (AFF) {
             float pm = ma * ssb[k][nb + 2 * c + h];
-            asm volatile("" : "+v"(pm));
+            asm("" : "+v"(pm));
             summs[g][c] = summs[g][c] + pm;
           }
         }
       }
+    };
+    if (nu == MKB) {   // a whole chunk: unrolled, so the next block's LDS reads run ahead
+#pragma unroll
+      for (int k = 0; k < MKB; ++k) block(k);
+    } else {
+      for (int k = 0; k < nu; ++k) block(k);
     }
   }
   const int m = m0 + ml;
@@ -1019,8 +1032,8 @@ __global__ __launch_bounds__(MNT) void ref_mfma_kq_kernel(GemvArgs p) {
   const int lq = lr & 3;
   const uint32_t* arow = &sa[ml * (AW + 1)];
   const uint32_t* bl = &sbp[(8 * G * wn + (lr >> 2)) * NPC + h * 16 + lq * 4];
-  for (int z = t; z < MC2 * 64; z += MNT) {   // the other k-group's slots: zero for good
-    const int c = z >> 6, kh = (z & 63) >> 2, s = z & 3;
+  for (int z = t; z < MC2 * 128; z += MNT) {   // the other k-group's slots: zero for good
+    const int c = z >> 7, kh = (z & 127) >> 2, s = z & 3;
     if ((s >> 1) != (kh & 1)) *reinterpret_cast<u32x4*>(&sbp[c * NPC + kh * 16 + s * 4]) = u32x4{0u, 0u, 0u, 0u};
   }
   fetch(0);
@@ -1078,7 +1091,7 @@ __global__ __launch_bounds__(MNT) void ref_mfma_kq_kernel(GemvArgs p) {
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         float d = sdb[nb + 2 * c + h] * da;   // y.d * fp32(x.d)
-        asm volatile("" : "+v"(d));
+        asm("" : "+v"(d));
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           acc[g][0][4 * c + e] = __builtin_fmaf(d, X[g][0][4 * c + e], acc[g][0][4 * c + e]);

@@ -763,7 +763,12 @@ def main():
                    "t16": llama_e2e(devs, threads=min(16, host_cores()[0])),
                    # the GPU build leaves ggml fewer CPU ops: 8 pool threads spin less against the
                    # boundary's thread (short-context decode 69 -> 97 tok/s, profiles/r03/boundary/)
-                   "t8": llama_e2e(devs, threads=min(8, host_cores()[0]))}
+                   "t8": llama_e2e(devs, threads=min(8, host_cores()[0])),
+                   # the boundary computes in the reference's own float order by default (bit-identical
+                   # logits); the fast engines' order for comparison
+                   "t16_fast_order": llama_e2e(devs, threads=min(16, host_cores()[0]),
+                                               extra_env={"LAMM_HIP_ORDER": "fast"}),
+                   "float_order": "reference (LAMM_HIP_ORDER default): t16 / t8; t16_fast_order: LAMM_HIP_ORDER=fast"}
             if world == 1:
                 extras["llama7b_matmul_step"] = llama_step(fmt)
             extras["llama7b_e2e"] = e2e

@@ -762,8 +762,9 @@ __global__ __launch_bounds__(MNT) void ref_mfma2_kernel(GemvArgs p) {
   constexpr int SEGW = SEG / 4 + 1;
   constexpr int NAL = MR * (SEG / 16);              // A b128 loads per chunk
   constexpr int NA = (NAL + MNT - 1) / MNT;
-  constexpr int NB = MC2 * MKB / MNT;               // activation blocks per thread per chunk
-  static_assert(MC2 * MKB % MNT == 0, "whole activation items per thread");
+  constexpr int NITEM = MC2 * MKB;                  // activation blocks per chunk
+  constexpr int NB = (NITEM + MNT - 1) / MNT;       // per thread
+  static_assert(NITEM % MNT == 0 || NITEM < MNT, "whole activation items per thread");
   // the padded image: per column, block, half and k-group h of the MFMA operand, the 4 slots
   // (16 bytes each) lanes (slot, h) read: the quad for slots of that k-group, zeros otherwise --
   // the zero slots are written once; column pitch = 16 banks mod 64, so a ds_read_b128 lane
@@ -808,7 +809,7 @@ __global__ __launch_bounds__(MNT) void ref_mfma2_kernel(GemvArgs p) {
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
       const int item = t + j * MNT, c = item / MKB, k = item % MKB;
-      const bool ok = c < ncols && u0 + k < nunits;
+      const bool ok = item < NITEM && c < ncols && u0 + k < nunits;
       const uint32_t off = (uint32_t)((int64_t)c * p.ldb + (int64_t)(u0 + k) * F::VB);
       const uint32_t base = ok ? (off & ~3u) : 0x7ffffff0u;
 #pragma unroll
@@ -827,6 +828,7 @@ __global__ __launch_bounds__(MNT) void ref_mfma2_kernel(GemvArgs p) {
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
       const int item = t + j * MNT, c = item / MKB, k = item % MKB;
+      if (item >= NITEM) break;
       const bool ok = c < ncols && u0 + k < nunits;
       const int sh = (int)((uint32_t)((int64_t)c * p.ldb + (int64_t)(u0 + k) * F::VB) & 3u) * 8;
       uint32_t m[9];
@@ -1188,7 +1190,7 @@ hipError_t launch_ref(int type, const GemvArgs& p, hipStream_t s) {
     // ref_mfma2_kernel, 2 column groups per wave (LAMM_REF_MFMA=4: 4 groups, one wave per SIMD; =1:
     // the unpipelined ref_mfma_kernel)
     const int sel = knobs().ref_mfma > 0 ? knobs().ref_mfma : 2;
-    const int mc = sel == 4 ? 64 : 32;
+    const int mc = sel == 4 ? 64 : sel == 3 ? 16 : 32;
     const dim3 gm((unsigned)((p.M + MR - 1) / MR), (unsigned)((p.N + mc - 1) / mc), (unsigned)slices);
     auto gom = [&](auto tc) {
       constexpr int T = decltype(tc)::value;
@@ -1198,6 +1200,9 @@ hipError_t launch_ref(int type, const GemvArgs& p, hipStream_t s) {
       } else if (sel == 4) {
         if (slices == 1) hipLaunchKernelGGL((ref_mfma2_kernel<T, 4, true>), gm, dim3(MNT), 0, s, p);
         else hipLaunchKernelGGL((ref_mfma2_kernel<T, 4, false>), gm, dim3(MNT), 0, s, p);
+      } else if (sel == 3) {   // one column group per wave (occupancy over reuse)
+        if (slices == 1) hipLaunchKernelGGL((ref_mfma2_kernel<T, 1, true>), gm, dim3(MNT), 0, s, p);
+        else hipLaunchKernelGGL((ref_mfma2_kernel<T, 1, false>), gm, dim3(MNT), 0, s, p);
       } else {
         if (slices == 1) hipLaunchKernelGGL((ref_mfma2_kernel<T, 2, true>), gm, dim3(MNT), 0, s, p);
         else hipLaunchKernelGGL((ref_mfma2_kernel<T, 2, false>), gm, dim3(MNT), 0, s, p);

@@ -191,11 +191,21 @@ int gemv_max_n(int type) {
 // Which engine lamm_hip_matmul* runs a call on (lamm_hip_engine reports the same choice to
 // callers and tests).  stationary: the weights' packed prefill form is resident (lamm_weights);
 // b_al4: B and its slice strides are 4-byte aligned (the super-block GEMM reads q8_K as dwords).
-enum Engine { kEngGemv, kEngDense, kEngKq, kEngFp6, kEngI8, kEngGemvGroups };
+enum Engine { kEngGemv, kEngDense, kEngKq, kEngFp6, kEngI8, kEngGemvGroups, kEngDq };
+// The dequantizing f16 GEMM (lamm_gemm_dq.hip) takes the 32-element formats' prefill calls whose
+// 128 x 64 tiles fill at least half the chip (it has no K-split); LAMM_GEMM_PATH=dq16 forces it,
+// fp6 / i8 force the exact engines.
+constexpr int kDqMinTiles = 128;
+bool use_dq(int type, const GemvArgs& p) {
+  if (!gemm_dq_supported(type) || !gemm_dq_args_ok(p)) return false;
+  if (knobs().gemm_path == 2) return true;
+  return knobs().gemm_path < 0 && gemm_dq_tiles(p) >= kDqMinTiles;
+}
 Engine pick_engine(int type, const GemvArgs& p, bool stationary, bool b_al4) {
   if (p.N <= gemv_max_n(type) || (p.b_f32 && p.N <= 8)) return kEngGemv;
   if (gemm_dense_supported(type) && knobs().dense_gemm) return kEngDense;
   if (gemm_kq_supported(type) && knobs().kq_gemm && b_al4) return kEngKq;
+  if (use_dq(type, p)) return kEngDq;
   if (gemm_fp6_supported(type) && gemm_path(p, stationary) == 0) return kEngFp6;
   if (gemm_supported(type) && gemm_args_ok(type, p)) return kEngI8;
   return kEngGemvGroups;
@@ -331,6 +341,9 @@ int matmul_impl_(const lamm_matrix* A, const lamm_matrix* B, const lamm_matrix* 
       e = launch_gemm_fp6(A->type, p, prepA, ws, s);
       break;
     }
+    case kEngDq:
+      e = launch_gemm_dq(A->type, p, s);
+      break;
     case kEngI8: {
       void* ws = nullptr;
       const size_t wsb = gemm_workspace_bytes(A->type, p);
@@ -371,7 +384,7 @@ extern "C" int lamm_hip_matmul_batched(const lamm_matrix* A, const lamm_matrix* 
 }
 
 extern "C" const char* lamm_hip_engine(int type, int64_t M, int N, int K, int slices, int stationary, int b_f32) {
-  static const char* const names[] = {"gemv", "dense", "superblock", "fp6", "i8", "gemv-groups"};
+  static const char* const names[] = {"gemv", "dense", "superblock", "fp6", "i8", "gemv-groups", "dq16"};
   if (!is_weight_type(type) || M < 1 || N < 1 || K < 1 || slices < 1 || K % block_elems(type)) return "";
   const int kb = K / block_elems(type);
   GemvArgs p{nullptr, (int64_t)kb * (int64_t)block_bytes(type), nullptr, 0, nullptr, M, (int)M, N, K, kb};

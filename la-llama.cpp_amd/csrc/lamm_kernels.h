@@ -99,4 +99,11 @@ bool gemm_fp6_supported(int type);
 int gemm_fp6_tiles(const GemvArgs& p);   // 256x128 output tiles of the fp6 GEMM (before K-splits)
 int gemm_fp6_grid(const GemvArgs& p);    // its main-kernel workgroups (tiles x K-splits)
 
+// q4_0 / q4_1 / q5_0 / q5_1 / q8_0 prefill GEMM on f16 MFMAs with the block scales folded into the
+// operands as the raw blocks are unpacked (lamm_gemm_dq.hip): one launch, no workspace, 1e-3 bar
+hipError_t launch_gemm_dq(int type, const GemvArgs& p, hipStream_t s);
+bool gemm_dq_supported(int type);
+bool gemm_dq_args_ok(const GemvArgs& p);
+int gemm_dq_tiles(const GemvArgs& p);   // its workgroups (128 x 64 output tiles over all slices)
+
 }  // namespace lamm

@@ -28,6 +28,7 @@ Knobs* read_env() {
   if (const char* e = getenv("LAMM_GEMM_PATH")) {
     if (!strcmp(e, "i8") || !strcmp(e, "1")) k->gemm_path = 1;
     if (!strcmp(e, "fp6") || !strcmp(e, "0")) k->gemm_path = 0;
+    if (!strcmp(e, "dq16") || !strcmp(e, "2")) k->gemm_path = 2;
   }
   k->gemv_max_n = env_int("LAMM_GEMV_MAX_N", -1);
   k->dense_gemm = !env_off("LAMM_DENSE_GEMM");

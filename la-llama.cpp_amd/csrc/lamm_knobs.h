@@ -8,7 +8,8 @@ namespace lamm {
 
 struct Knobs {
   // ---- operator API: engine and plan selection
-  int gemm_path = -1;          // LAMM_GEMM_PATH: fp6|0 / i8|1 forces the q4_0/q4_1/q5_0 prefill engine
+  int gemm_path = -1;          // LAMM_GEMM_PATH: fp6|0 / i8|1 forces the exact q4_0/q4_1/q5_0 prefill engine,
+                               // dq16|2 the dequantizing f16 one (every 32-element format)
   int gemv_max_n = -1;         // LAMM_GEMV_MAX_N: widest N on the decode GEMV (-1 unset: per-type default;
                                // 0 and 1 both mean N = 1 only, the floor)
   bool dense_gemm = true;      // LAMM_DENSE_GEMM=0: F32/F16 prefill on the grouped GEMV instead

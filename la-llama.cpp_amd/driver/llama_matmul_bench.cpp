@@ -45,7 +45,10 @@
 // (ggml's INIT) on the GPU: every mul_mat of a llama.cpp decode step, with nothing crossing
 // PCIe.  Softmax / RoPE / norms are llama.cpp ops outside the hook and stay out.  --check
 // recomputes the last layer's attention on the host from the device buffers after the replays.
+#include <execinfo.h>
 #include <hip/hip_runtime.h>
+#include <signal.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <cmath>
@@ -630,7 +633,18 @@ int run_sharded(const ShardOpts& o, int type, int out_type, int N, int iters, in
 
 }  // namespace
 
+// a host-side fault prints its call stack before the process ends (the tests see only the exit code)
+void on_fault(int sig) {
+  void* frames[64];
+  const int n = backtrace(frames, 64);
+  const char msg[] = "llama-matmul-bench: fatal signal, call stack:\n";
+  (void)!write(2, msg, sizeof msg - 1);
+  backtrace_symbols_fd(frames, n, 2);
+  _exit(128 + sig);
+}
+
 int main(int argc, char** argv) {
+  setvbuf(stdout, nullptr, _IOLBF, 0);
   int type = 2, N = 1, iters = 20, layers = 32, out_type = 14, ctx = 0;
   bool graph = true, stationary = false, batch_proj = false, concurrent = false, check = false;
   ShardOpts so;
@@ -681,6 +695,11 @@ int main(int argc, char** argv) {
     fprintf(stderr, "llama-matmul-bench: no gfx950 device (%s)\n", lamm_hip_last_error());
     return 1;
   }
+  // after the HIP runtime's own start-up (it installs handlers of its own)
+  struct sigaction sa = {};
+  sa.sa_handler = on_fault;
+  sigaction(SIGSEGV, &sa, nullptr);
+  sigaction(SIGBUS, &sa, nullptr);
   if (so.rank >= 0 || shard > 0 || !so.devices.empty() || !so.dump.empty() || !so.dump_q.empty()) {   // the row-sharded form
     if (so.rank >= 0) {
       if (so.world < 1 || so.rank >= so.world || so.comm_id.empty()) {

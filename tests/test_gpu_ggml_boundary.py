@@ -112,9 +112,12 @@ def test_non_compute_phases_and_unsupported(monkeypatch):
     p.type = la.TASK_FINALIZE
     assert not la.can_mul_mat(p, dst.t)
     p.type = la.TASK_INIT        # claimed whenever the GPU quantizes src1
-    # default (the reference's float order): decode-sized calls leave INIT to ggml, as
-    # the reference does; from 8 activation rows the GPU quantizer (the same bytes) takes it
-    assert not la.can_mul_mat(p, dst.t)
+    # default (the reference's float order): a one-column call is quantized inside the
+    # one-column reference kernel (ggml's AVX2 INIT bytes), 2 .. 7 rows leave INIT to ggml as the
+    # reference does, and from 8 activation rows the GPU quantizer (the same bytes) takes it
+    assert la.can_mul_mat(p, dst.t)
+    src02, src12, _, _ = make_node(t, M, 2, K)
+    assert not la.can_mul_mat(p, ggml_emu.mul_mat_node(src02, src12).t)
     src0r, src1r, _, _ = make_node(t, M, 8, K)
     assert la.can_mul_mat(p, ggml_emu.mul_mat_node(src0r, src1r).t)
     monkeypatch.setenv("LAMM_HIP_ORDER", "fast")   # the fast engines: INIT fused into the GEMV
@@ -163,9 +166,10 @@ def test_f16_policy(monkeypatch):
     dstb = ggml_emu.mul_mat_node(src0b, src1b)
     assert not la.can_mul_mat(p, dstb.t)
     monkeypatch.delenv("LAMM_HIP_VIEWS")
-    # unset: in the reference's float order (the default) the views stay with ggml, as the
-    # reference routes F16; with the fast engines prefill-sized views go to the GPU
-    assert not la.can_mul_mat(p, dstb.t)
+    # unset: prefill-sized views go to the GPU in either float order (the reference's order runs
+    # them in ggml_vec_dot_f16's AVX2 order, ref_f16_kernel), decode-sized ones stay
+    assert la.can_mul_mat(p, dstb.t)
+    assert not la.can_mul_mat(p, dst.t)
     monkeypatch.setenv("LAMM_HIP_ORDER", "fast")
     assert la.can_mul_mat(p, dstb.t)
 

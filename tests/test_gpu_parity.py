@@ -235,20 +235,102 @@ FP6_TYPES = [ol.Q4_0, ol.Q4_1, ol.Q5_0]
 GEMM_SHAPES = [(33, 17, 1024), (130, 9, 8192 + 512), (257, 129, 4096 + 64), (300, 40, 96)]
 
 
-@pytest.mark.parametrize("engine", ["fp6", "i8"])
-@pytest.mark.parametrize("t", FP6_TYPES, ids=[ol.NAMES[t] for t in FP6_TYPES])
+DQ_TYPES = [ol.Q4_0, ol.Q4_1, ol.Q5_0, ol.Q5_1, ol.Q8_0]
+ENGINE_CASES = [(t, e) for e in ("fp6", "i8") for t in FP6_TYPES] + [(t, "dq16") for t in DQ_TYPES]
+
+
+@pytest.mark.parametrize("t,engine", ENGINE_CASES, ids=[f"{ol.NAMES[t]}-{e}" for t, e in ENGINE_CASES])
 @pytest.mark.parametrize("shape", GEMM_SHAPES, ids=[f"{m}x{n}x{k}" for m, n, k in GEMM_SHAPES])
 def test_gemm_engines_vs_oracle(t, shape, engine, monkeypatch):
-    """Both prefill engines (LAMM_GEMM_PATH: block-scaled fp6 MFMA / MFMA-i8) on ragged
-    shapes: M and N not multiples of the 256x128 / 128x64 tiles, K not a multiple of the
-    K-step (odd block counts: K=96 is 3 blocks, 4160 is 130)."""
+    """The prefill engines (LAMM_GEMM_PATH: block-scaled fp6 MFMA / MFMA-i8 / the dequantizing f16
+    engine of every 32-element format) on ragged shapes: M and N not multiples of the 256x128 /
+    128x64 tiles, K not a multiple of the K-step or of dq16's 4-block quads (odd block counts: K=96
+    is 3 blocks, 4160 is 130)."""
     monkeypatch.setenv("LAMM_GEMM_PATH", engine)
+    if engine == "dq16":
+        assert la.gemm_engine(t, *shape) == "dq16"
     M, N, K = shape
     A_q, B_q = random_case(t, M, N, K, seed=M * 7 + N * 3 + K)
     c, _ = gpu_mul_mat(t, A_q, B_q, M, N, K)
     ref = ORACLE.mul_mat(t, M, N, K, A_q, B_q)
     err = rel_err(c, ref, absdot(t, A_q, B_q, M, N, K)).max()
     assert err < TOL, err
+
+
+@pytest.mark.parametrize("t", DQ_TYPES, ids=[ol.NAMES[t] for t in DQ_TYPES])
+def test_gemm_dq16_batched_strided(t, monkeypatch):
+    """dq16 with ggml batch dims (2 weight slices broadcast over 4 activation slices, r2 = 2), a
+    padded C pitch (untouched tail stays NaN) and padded A / B row pitches."""
+    monkeypatch.setenv("LAMM_GEMM_PATH", "dq16")
+    M, N, K, ne02, ne12 = 200, 70, 1024 + 160, 2, 4
+    vt = la.vec_dot_type(t)
+    kb = K // 32
+    lda, ldb, ldc = pitch_blocks(t, kb) + 1, kb + 3, M + 5
+    arow, brow = lda * la.type_size(t), ldb * la.type_size(vt)
+    rng = np.random.default_rng(5 + t)
+    As = [ORACLE.quantize(t, rng.standard_normal((M, K), dtype=np.float32), ol.QUANT_REF) for _ in range(ne02)]
+    Bs = [ORACLE.quantize(vt, rng.standard_normal((N, K), dtype=np.float32), ol.QUANT_AVX) for _ in range(ne12)]
+    Ap = np.zeros((ne02, M, arow), np.uint8)
+    for a in range(ne02):
+        Ap[a, :, :kb * la.type_size(t)] = As[a].reshape(M, -1)
+    Bp = np.zeros((ne12, N, brow), np.uint8)
+    for z in range(ne12):
+        Bp[z, :, :kb * la.type_size(vt)] = Bs[z].reshape(N, -1)
+    A = dev_bytes(np.concatenate([Ap.reshape(-1), np.zeros(64, np.uint8)]))
+    B = dev_bytes(Bp)
+    C = torch.full((ne12 * N * ldc,), float("nan"), dtype=torch.float32, device="cuda")
+    bt = la.Batch(ne02, 1, ne12, 1, M * arow, ne02 * M * arow, N * brow, ne12 * N * brow, 4 * N * ldc,
+                  4 * ne12 * N * ldc)
+    la.matmul_batched(la.Matrix(A.data_ptr(), t, M, kb, lda), la.Matrix(B.data_ptr(), vt, kb, N, ldb),
+                      la.Matrix(C.data_ptr(), la.F32, M, N, ldc), bt, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    c = C.cpu().numpy().reshape(ne12, N, ldc)
+    assert np.isnan(c[:, :, M:]).all()
+    for z in range(ne12):
+        a = As[z // (ne12 // ne02)]
+        ref = ORACLE.mul_mat(t, M, N, K, a, Bs[z])
+        assert rel_err(c[z, :, :M], ref, absdot(t, a, Bs[z], M, N, K)).max() < TOL, z
+
+
+def test_gemm_dq16_rows_invariant(monkeypatch):
+    """A row's dq16 value does not depend on the launch (the multi-GPU gather is bit-exact only if
+    rank r's slab equals the same rows of the one-GPU call): slabs of 1000 / 512 / 128 rows starting
+    at row 128 k, against the full 4096-row call, bit for bit."""
+    monkeypatch.setenv("LAMM_GEMM_PATH", "dq16")
+    M, N, K = 4096, 96, 2048
+    A_q, B_q = random_case(ol.Q4_0, M, N, K, seed=99)
+    full, _ = gpu_mul_mat(ol.Q4_0, A_q, B_q, M, N, K)
+    arow = la.row_bytes(ol.Q4_0, K)
+    for r0, rows in ((0, 1000), (1024, 512), (3968, 128)):
+        part, _ = gpu_mul_mat(ol.Q4_0, A_q[r0 * arow:(r0 + rows) * arow], B_q, rows, N, K)
+        assert np.array_equal(part, full[:, r0:r0 + rows]), (r0, rows)
+
+
+@pytest.mark.parametrize("case", ["tiny_scales", "large_activations", "extremes"])
+def test_gemm_dq16_value_range(case, monkeypatch):
+    """dq16 folds the block scales into f16 operands: weights pre-scaled by 2^8 (exact) so block
+    scales down to ~1e-7 stay normal, activations as d_b * b (|x| < 65504, the f16 range).
+    tiny_scales: weight rows of magnitude 1e-5 (block scales ~1e-6); large_activations: rows
+    with |x| up to 3e4; extremes: all-max / all-min quants (q4 nibbles 0 / 15, q8 -127 / 127)."""
+    monkeypatch.setenv("LAMM_GEMM_PATH", "dq16")
+    M, N, K = 128, 64, 1024
+    rng = np.random.default_rng(3)
+    a = rng.standard_normal((M, K), dtype=np.float32)
+    b = rng.standard_normal((N, K), dtype=np.float32)
+    if case == "tiny_scales":
+        a *= 1e-5
+    elif case == "large_activations":
+        b *= 3e4 / np.abs(b).max()
+    else:
+        a = np.where(np.arange(K) % 3 == 0, -1.0, 1.0).astype(np.float32) * np.ones((M, 1), np.float32)
+        b = np.where(np.arange(K) % 2 == 0, 1.0, -1.0).astype(np.float32) * np.ones((N, 1), np.float32)
+    for t in (ol.Q4_0, ol.Q8_0):
+        A_q = ORACLE.quantize(t, a, ol.QUANT_REF)
+        B_q = ORACLE.quantize(ol.Q8_0, b, ol.QUANT_AVX)
+        c, _ = gpu_mul_mat(t, A_q, B_q, M, N, K)
+        ref = ORACLE.mul_mat(t, M, N, K, A_q, B_q)
+        assert np.isfinite(c).all()
+        assert rel_err(c, ref, absdot(t, A_q, B_q, M, N, K)).max() < TOL, ol.NAMES[t]
 
 
 @pytest.mark.parametrize("split", [1, 3, 8])
@@ -775,18 +857,21 @@ def _config3_check(c, A_q, B_q, rows):
 CONFIG3_ROWS = np.unique(np.concatenate([np.arange(0, 4096, 16), [1, 127, 128, 255, 256, 2047, 2048, 4095]]))
 
 
-@pytest.mark.parametrize("path", ["stationary_fp6_auto", "stationary_fp6_split_k", "stationary_fp6_kgroups2",
-                                  "per_call_default", "per_call_fp6", "per_call_i8"])
+@pytest.mark.parametrize("path", ["stationary_auto", "stationary_fp6", "stationary_fp6_split_k",
+                                  "stationary_fp6_kgroups2", "per_call_default", "per_call_fp6", "per_call_i8"])
 def test_config3_full_size_gemm(path, monkeypatch):
     """BASELINE config 3 at its real size: Q4_0 x Q8_0 M=4096 N=512 K=4096, one slice.
-    Paths: the weight-stationary handle (the ggml boundary's and bench.py's; fp6 engine, by
-    default 256 128x64 tiles with 4 K-groups each, or forced: K split over the 64 256x128 tiles,
-    2 K-groups), the per-call API's default engine, and both engines forced per call.  >= 256
-    sampled rows x all 512 columns vs the oracle."""
+    Paths: the weight-stationary handle (the ggml boundary's and bench.py's: by default the
+    dequantizing f16 engine, 256 128x64 tiles with 4 K-groups; the exact fp6 engine forced, its
+    default 4 K-groups, or K split over the 64 256x128 tiles, or 2 K-groups), the per-call API's
+    default engine, and both exact engines forced per call.  >= 256 sampled rows x all 512 columns
+    vs the oracle."""
     M, N, K = 4096, 512, 4096
     (A_q,), (B_q,) = _config3_operands(2024, 1)
     if path in ("per_call_fp6", "per_call_i8"):
         monkeypatch.setenv("LAMM_GEMM_PATH", path.rsplit("_", 1)[1])
+    if path.startswith("stationary_fp6"):
+        monkeypatch.setenv("LAMM_GEMM_PATH", "fp6")
     if path == "stationary_fp6_split_k":
         monkeypatch.setenv("LAMM_FP6_SUB", "0")
     if path == "stationary_fp6_kgroups2":
@@ -795,7 +880,8 @@ def test_config3_full_size_gemm(path, monkeypatch):
     B = dev_bytes(B_q)
     C = torch.full((N * M,), float("nan"), dtype=torch.float32, device="cuda")
     if path.startswith("stationary"):
-        assert la.gemm_engine("q4_0", M, N, K, 1, stationary=True) == "fp6"
+        want = "dq16" if path == "stationary_auto" else "fp6"
+        assert la.gemm_engine("q4_0", M, N, K, 1, stationary=True) == want
         W = la.Weights(ol.Q4_0, A, M, K)
         W.matmul_torch(B, C, N)
         torch.cuda.synchronize()
@@ -838,9 +924,13 @@ def test_config3_repeated_calls_fresh_activations(act, monkeypatch):
     W.close()
 
 
-def test_config3_four_slice_batched_launch():
-    """The 4-slice batched launch bench.py times (ne02 = ne12 = 4, stationary weights, fp6
-    engine with 256 tiles): every slice's sampled rows x all columns vs the oracle."""
+@pytest.mark.parametrize("engine", ["dq16", "fp6"])
+def test_config3_four_slice_batched_launch(engine, monkeypatch):
+    """The 4-slice batched launch bench.py times (ne02 = ne12 = 4, stationary weights; the default
+    dq16 engine with 1024 tiles, or the exact fp6 engine with 256): every slice's sampled rows x
+    all columns vs the oracle."""
+    if engine == "fp6":
+        monkeypatch.setenv("LAMM_GEMM_PATH", "fp6")
     M, N, K = 4096, 512, 4096
     As, Bs = _config3_operands(77, 4)
     arow, brow = la.row_bytes(ol.Q4_0, K), la.row_bytes(ol.Q8_0, K)
@@ -848,7 +938,7 @@ def test_config3_four_slice_batched_launch():
     B = dev_bytes(np.concatenate(Bs))
     C = torch.full((4 * N * M,), float("nan"), dtype=torch.float32, device="cuda")
     bt = la.Batch(4, 1, 4, 1, M * arow, 4 * M * arow, N * brow, 4 * N * brow, 4 * M * N, 16 * M * N)
-    assert la.gemm_engine("q4_0", M, N, K, 4, stationary=True) == "fp6"
+    assert la.gemm_engine("q4_0", M, N, K, 4, stationary=True) == engine
     W = la.Weights(ol.Q4_0, A, M, K, ne02=4, ne03=1, nba2=M * arow, nba3=4 * M * arow)
     W.matmul_torch(B, C, N, batch=bt)
     torch.cuda.synchronize()

@@ -63,6 +63,12 @@ FP16_FIELDS = {  # byte offsets of fp16 scale fields inside one block (lamm_form
     "q4_k": [0, 2], "q5_k": [0, 2], "q6_k": [208]}
 
 
+GEMM_KERNELS = {"dq16": "lamm::gemm_dq2_kernel (csrc/lamm_gemm_dq.hip; f16 MFMA, block scales folded into the "
+                        "operands, 1e-3 bar)",
+                "fp6": "lamm::gemm_fp6_kv_kernel (csrc/lamm_gemm_fp6.hip; exact block dots)",
+                "i8": "lamm::gemm3_kernel (csrc/lamm_gemm.hip; exact block dots)"}
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -696,10 +702,10 @@ def main():
                                  else ""),
                     "engine": engine, "value": round(ops / step / 1e9, 1), "unit": "GFLOPS",
                     "ms_per_step": round(step * 1e3, 4),
-                    "roofline": {"bound": "mfma", "scope": "whole launch (activation prep + main loop + split-K "
-                                                           "reduce) of this rank's slab",
-                                 "kernel": "lamm::gemm_fp6_kernel (csrc/lamm_gemm_fp6.hip)" if engine == "fp6"
-                                 else "lamm::gemm3_kernel (csrc/lamm_gemm.hip)",
+                    "roofline": {"bound": "mfma", "scope": "whole launch of this rank's slab (dq16: the one "
+                                                           "kernel; exact engines: activation prep + main loop + "
+                                                           "split-K reduce)",
+                                 "kernel": GEMM_KERNELS.get(engine, engine),
                                  "achieved": round(rops / kern / 1e12, 2), "peak": I8_DENSE_PEAK_TOPS,
                                  "unit": "TFLOP/s", "frac": round(rops / kern / 1e12 / I8_DENSE_PEAK_TOPS, 4),
                                  "per_launch_us": round(kern * 1e6, 2)}}

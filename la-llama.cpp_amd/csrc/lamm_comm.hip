@@ -105,6 +105,26 @@ __global__ void unshard_rows_kernel(const float* __restrict__ g, float* __restri
   }
 }
 
+// Loopback exchange (ranks sharing a device): destination rank `self` copies every other rank's
+// segment [k * count, (k + 1) * count) of its gather buffer from that rank's buffer -- one launch
+// per rank instead of world - 1 copies (a graph-captured step with G ranks would otherwise hold
+// G (G - 1) copy nodes per all-gather: 56 at G = 8, which the HIP runtime's graph code does not
+// survive -- tests/test_benchmark_driver.py::test_llama_bench_sharded_decode_bitexact)
+constexpr int kLoopbackMax = 64;
+struct LoopbackSrcs {
+  const float* p[kLoopbackMax];
+};
+__global__ void loopback_gather_kernel(LoopbackSrcs src, float* __restrict__ dst, int64_t count, int nl, int rank0,
+                                       int self) {
+  const int64_t per = (int64_t)(nl - 1) * count;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < per; idx += (int64_t)gridDim.x * blockDim.x) {
+    int k = (int)(idx / count);
+    k += k >= self ? 1 : 0;   // skip this rank's own segment
+    const int64_t e = (int64_t)(rank0 + k) * count + idx % count;
+    dst[e] = src.p[k][e];
+  }
+}
+
 }  // namespace
 
 struct lamm_comm {
@@ -289,16 +309,31 @@ extern "C" int lamm_hip_allgather_rows(lamm_comm* c, const float* const* slabs, 
       (void)hipSetDevice(c->devices[i]);
       if (!ok(hipEventRecord(c->packed[i], st(i)))) return cfail(LAMM_ERR_HIP, "hipEventRecord");
     }
+    // every rank on ONE device (the one-GPU rehearsal): one gather launch per rank; ranks on
+    // several devices (some of them shared): device copies, which cross devices
+    const bool one_dev = std::all_of(c->devices.begin(), c->devices.end(), [&](int d) { return d == c->devices[0]; });
+    LoopbackSrcs srcs{};
+    if (one_dev && nl <= kLoopbackMax)
+      for (int k = 0; k < nl; ++k) srcs.p[k] = direct ? C[k] : c->gbuf[k];
     for (int i = 0; i < nl; ++i) {
       (void)hipSetDevice(c->devices[i]);
       float* dst = direct ? C[i] : c->gbuf[i];
-      for (int k = 0; k < nl; ++k) {
-        if (k == i) continue;
-        if (!ok(hipStreamWaitEvent(st(i), c->packed[k], 0))) return cfail(LAMM_ERR_HIP, "hipStreamWaitEvent");
-        const float* src = direct ? C[k] : c->gbuf[k];
-        const size_t off = (size_t)(c->rank0 + k) * count;
-        if (!ok(hipMemcpyAsync(dst + off, src + off, count * sizeof(float), hipMemcpyDeviceToDevice, st(i))))
-          return cfail(LAMM_ERR_HIP, "loopback copy");
+      for (int k = 0; k < nl; ++k)
+        if (k != i && !ok(hipStreamWaitEvent(st(i), c->packed[k], 0))) return cfail(LAMM_ERR_HIP, "hipStreamWaitEvent");
+      if (one_dev && nl <= kLoopbackMax) {
+        const int64_t per = (int64_t)(nl - 1) * (int64_t)count;
+        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((per + 255) / 256, 2048));
+        hipLaunchKernelGGL(loopback_gather_kernel, dim3(grid), dim3(256), 0, st(i), srcs, dst, (int64_t)count, nl,
+                           c->rank0, i);
+        if (!ok(hipGetLastError())) return cfail(LAMM_ERR_HIP, "loopback gather launch");
+      } else {
+        for (int k = 0; k < nl; ++k) {
+          if (k == i) continue;
+          const float* src = direct ? C[k] : c->gbuf[k];
+          const size_t off = (size_t)(c->rank0 + k) * count;
+          if (!ok(hipMemcpyAsync(dst + off, src + off, count * sizeof(float), hipMemcpyDeviceToDevice, st(i))))
+            return cfail(LAMM_ERR_HIP, "loopback copy");
+        }
       }
       if (!ok(hipEventRecord(c->done[i], st(i)))) return cfail(LAMM_ERR_HIP, "hipEventRecord");
     }

@@ -72,7 +72,7 @@ constexpr size_t DQ_LDS = (size_t)DQ_KG * DQ_TJ * DQ_PI * 4;
 constexpr float DQ_ASCALE = 256.f, DQ_CSCALE = 1.f / 256.f;
 
 // load_words' vector-memory instructions for NW dwords (b128s, then b64 / b32)
-constexpr int vm_ops(int nw) { return nw / 4 + (nw % 4 >= 2 ? 1 : 0) + (nw % 2 ? 1 : 0); }
+[[maybe_unused]] constexpr int vm_ops(int nw) { return nw / 4 + (nw % 4 >= 2 ? 1 : 0) + (nw % 2 ? 1 : 0); }
 
 __device__ __forceinline__ uint32_t perm(uint32_t s0, uint32_t s1, uint32_t sel) {
   return __builtin_amdgcn_perm(s0, s1, sel);
@@ -497,6 +497,204 @@ __global__ __launch_bounds__(DQ_NT) void gemm_dq2_kernel(GemvArgs p) {
   }
 }
 
+// ---------------------------------------------------------------- activation-prepped form (v3)
+// The activations, shared by every row tile, are unpacked ONCE per call instead of once per CU:
+// dq_prep_b writes them as plain f16 rows d_b * b (zero past K, rows padded to whole quads), and
+// the main kernel reads each k-step's 8 activation values with one ds_read_b128 from its LDS image
+// (column pitch 4 * 64 + 16 bytes: conflict-free b128 reads) -- only the weights are unpacked.
+constexpr int DQ3_BP = 4 * 64 + 16;   // LDS pitch of a column's quad (256 bytes of f16 + pad)
+
+template <int V>
+__global__ __launch_bounds__(256) void dq_prep_b(GemvArgs p, _Float16* __restrict__ out, int64_t kpad) {
+  using F = DqFmt<V>;
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;   // (slice, row, block) of the padded image
+  const int64_t nbp = kpad / 32;
+  const int64_t per = (int64_t)p.N * nbp;
+  if (idx >= per * p.ne12 * p.ne13) return;
+  const int z = (int)(idx / per);
+  const int64_t r = idx % per, j = r / nbp, b = r % nbp;
+  const int i12 = z % p.ne12, i13 = z / p.ne12;
+  half8 v[4];
+  if (b < p.nblk) {
+    // the row through a buffer resource (nothing past its last block is read); the block sits at a
+    // 2- or 4-byte aligned offset: dwords from the one below, realigned
+    const unsigned char* row = p.B + (int64_t)i12 * p.sb2 + (int64_t)i13 * p.sb3 + j * p.ldb;
+    const auto rr = make_rsrc(row, (uint32_t)(p.nblk * F::BPB));
+    const uint32_t o = (uint32_t)(b * F::BPB), o4 = o & ~3u;
+    const int sh = (int)(o - o4) * 8;
+    uint32_t w[F::BPB / 4 + 1], raw[F::BPB / 4 + 2];
+#pragma unroll
+    for (int k = 0; k < F::BPB / 4 + 2; ++k) raw[k] = bload4(rr, o4 + 4 * k);
+#pragma unroll
+    for (int k = 0; k < F::BPB / 4 + 1; ++k) w[k] = __builtin_amdgcn_alignbit(raw[k + 1], raw[k], sh);
+    // the block now starts at byte 0 of w: reuse the pair unpacker with JB = 0
+    uint32_t d2, m2, qh;
+    dq_scalars<V, 0>(w, true, (_Float16)1, d2, m2, qh);
+    unroll<4>([&](auto CG) { v[CG] = dq_operand<V, 0, CG>(w, d2, 0u, 0u); });
+  } else {
+    unroll<4>([&](auto CG) { v[CG] = half8{}; });
+  }
+  half8* dst = reinterpret_cast<half8*>(out + ((int64_t)z * p.N + j) * kpad + b * 32);
+  unroll<4>([&](auto CG) { __builtin_nontemporal_store(v[CG], dst + CG); });
+}
+
+template <int T, int NBV>
+__global__ __launch_bounds__(DQ_NT) void gemm_dq3_kernel(GemvArgs p, const _Float16* __restrict__ bimg, int64_t kpad) {
+  using FA = DqFmt<T>;
+  constexpr int NWA = FA::BPB / 2;
+  constexpr int QA = 4 * FA::BPB, PA = QA / 8;
+  constexpr int LA = DQ_TI * PA / 64, LB = DQ_TJ * 16 / 64;   // b64 weight pieces, b128 activation pieces
+  constexpr int QBYTES = DQ_TI * QA + DQ_TJ * DQ3_BP;
+  static_assert((DQ_TI * PA) % 64 == 0, "whole loads");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int t = threadIdx.x, lane = t & 63, lr = lane & 31, h = lane >> 5;
+  const int g = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int nsi = (p.M + DQ_TI - 1) / DQ_TI, nsj = (p.N + DQ_TJ - 1) / DQ_TJ;
+  int ti, tj, z;
+  {
+    const int ntile = nsi * nsj * p.ne12 * p.ne13;
+    const int id = blockIdx.x, x = id & 7, k = id >> 3, q = ntile >> 3, rmd = ntile & 7;
+    const int wv = x < rmd ? x * (q + 1) + k : rmd * (q + 1) + (x - rmd) * q + k;
+    const int per = nsi * nsj;
+    z = wv / per;
+    ti = (wv % per) / nsj;
+    tj = (wv % per) % nsj;
+  }
+  const int i12 = z % p.ne12, i13 = z / p.ne12;
+  const int i02 = i12 / p.r2, i03 = i13 / p.r3;
+  const int64_t i0 = (int64_t)ti * DQ_TI, j0 = (int64_t)tj * DQ_TJ;
+  const int64_t arows = min((int64_t)DQ_TI, (int64_t)p.M - i0), bcols = min((int64_t)DQ_TJ, (int64_t)p.N - j0);
+  const auto ra = make_rsrc(p.A + (int64_t)i02 * p.sa2 + (int64_t)i03 * p.sa3 + i0 * p.lda,
+                            (uint32_t)min(arows * p.lda, (int64_t)0x7fffffff));
+  const int64_t ldbb = kpad * 2;   // bytes of an f16 activation row
+  const auto rb = make_rsrc(bimg + ((int64_t)z * p.N + j0) * kpad, (uint32_t)min(bcols * ldbb, (int64_t)0x7fffffff));
+  const int nblk = p.nblk;
+  const int nq = (nblk + 3) / 4;
+  const int mine = nq > g ? (nq - g + DQ_KG - 1) / DQ_KG : 0;
+  uint32_t a_off[LA], b_off[LB];
+  {
+    const uint32_t lda = (uint32_t)p.lda;
+#pragma unroll
+    for (int i = 0; i < LA; ++i) {
+      const int pc = i * 64 + lane;
+      a_off[i] = (uint32_t)(pc / PA) * lda + (uint32_t)(pc % PA) * 8;
+    }
+#pragma unroll
+    for (int i = 0; i < LB; ++i) {
+      const int pc = i * 64 + lane;
+      b_off[i] = (uint32_t)(pc / 16) * (uint32_t)ldbb + (uint32_t)(pc % 16) * 16;
+    }
+  }
+  unsigned char* img = smem + g * QBYTES;   // weight rows [128][QA], then activation columns [64][DQ3_BP]
+  u32x2 sta[NBV][LA];
+  u32x4 stb[NBV][LB];
+  auto issue = [&](int u, auto S_) __attribute__((always_inline)) {
+    constexpr int S = decltype(S_)::value;
+    const int q = g + DQ_KG * min(u, mine - 1);
+    const uint32_t qa = (uint32_t)q * QA, qb = (uint32_t)q * 256;
+#pragma unroll
+    for (int i = 0; i < LA; ++i) sta[S][i] = __builtin_amdgcn_raw_buffer_load_b64(ra, a_off[i] + qa, 0, 0);
+#pragma unroll
+    for (int i = 0; i < LB; ++i) stb[S][i] = __builtin_amdgcn_raw_buffer_load_b128(rb, b_off[i] + qb, 0, 0);
+  };
+  auto stage = [&](auto S_) __attribute__((always_inline)) {
+    constexpr int S = decltype(S_)::value;
+#pragma unroll
+    for (int i = 0; i < LA; ++i) *reinterpret_cast<u32x2*>(img + 8 * (i * 64 + lane)) = sta[S][i];
+#pragma unroll
+    for (int i = 0; i < LB; ++i) {
+      const int pc = i * 64 + lane;
+      *reinterpret_cast<u32x4*>(img + DQ_TI * QA + (pc / 16) * DQ3_BP + (pc % 16) * 16) = stb[S][i];
+    }
+  };
+
+  f32x16 acc[2][4];
+  unroll<2>([&](auto X) __attribute__((always_inline)) { unroll<4>([&](auto Y) __attribute__((always_inline)) { acc[X][Y] = f32x16{}; }); });
+
+  auto quad = [&](int u) __attribute__((always_inline)) {
+    const int q = g + DQ_KG * u;
+    uint32_t wa[4][NWA];
+#pragma unroll
+    for (int y = 0; y < 4; ++y) {
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(img + (32 * y + lr) * QA + h * 2 * FA::BPB);
+#pragma unroll
+      for (int k = 0; k < NWA; ++k) wa[y][k] = src[k];
+    }
+    unroll<2>([&](auto JB_) __attribute__((always_inline)) {
+      constexpr int JB = JB_;
+      const bool valid = 4 * q + 2 * h + JB < nblk;
+      uint32_t ad[4], am[4], aq[4];
+      unroll<4>([&](auto Y) __attribute__((always_inline)) { dq_scalars<T, JB>(wa[Y], valid, (_Float16)DQ_ASCALE, ad[Y], am[Y], aq[Y]); });
+      unroll<4>([&](auto CG_) __attribute__((always_inline)) {
+        constexpr int CG = CG_;
+        half8 bo[2];
+        unroll<2>([&](auto X) __attribute__((always_inline)) {
+          bo[X] = *reinterpret_cast<const half8*>(img + DQ_TI * QA + (32 * X + lr) * DQ3_BP + ((2 * h + JB) * 4 + CG) * 16);
+        });
+        unroll<4>([&](auto Y) __attribute__((always_inline)) {
+          const half8 ao = dq_operand<T, JB, CG>(wa[Y], ad[Y], am[Y], aq[Y]);
+          unroll<2>([&](auto X) __attribute__((always_inline)) { acc[X][Y] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bo[X], ao, acc[X][Y], 0, 0, 0); });
+        });
+      });
+    });
+  };
+
+  constexpr int LPQ = LA + LB;
+  if (mine > 0) {
+    unroll<NBV>([&](auto K) __attribute__((always_inline)) { issue(K, K); });
+    int u0 = 0;
+    for (; u0 + NBV <= mine; u0 += NBV) {
+      unroll<NBV>([&](auto K) __attribute__((always_inline)) {
+        wait_vm<LPQ * (NBV - 1)>();
+        stage(K);
+        issue(u0 + K + NBV, K);
+        quad(u0 + K);
+      });
+    }
+    unroll<NBV>([&](auto K) __attribute__((always_inline)) {
+      if (u0 + (int)K < mine) {
+        wait_vm<LPQ * (NBV - 1)>();
+        stage(K);
+        issue(u0 + K + NBV, K);
+        quad(u0 + K);
+      }
+    });
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(smem);
+  unroll<2>([&](auto X) __attribute__((always_inline)) {
+    unroll<4>([&](auto Y) __attribute__((always_inline)) {
+      unroll<16>([&](auto E) __attribute__((always_inline)) {
+        constexpr int e = E;
+        const int j = 32 * X + (e & 3) + 8 * (e >> 2) + 4 * h, i = 32 * Y + lr;
+        red[(g * DQ_TJ + j) * DQ_PI + i] = acc[X][Y][e];
+      });
+    });
+  });
+  __syncthreads();
+  float* C = p.C + (int64_t)i12 * p.sc2 + (int64_t)i13 * p.sc3;
+  const bool pair = (p.ldc & 1) == 0 && ((uintptr_t)C & 7) == 0;
+#pragma unroll
+  for (int r = 0; r < DQ_TJ * DQ_TI / (2 * DQ_NT); ++r) {
+    const int idx = 2 * (r * DQ_NT + t), jl = idx / DQ_TI, il = idx % DQ_TI;
+    f32x2 v = *reinterpret_cast<const f32x2*>(&red[jl * DQ_PI + il]);
+#pragma unroll
+    for (int g_ = 1; g_ < DQ_KG; ++g_) v += *reinterpret_cast<const f32x2*>(&red[(g_ * DQ_TJ + jl) * DQ_PI + il]);
+    v *= DQ_CSCALE;
+    const int64_t j = j0 + jl, i = i0 + il;
+    if (j < p.N) {
+      float* c = C + j * p.ldc + i;
+      if (pair && i + 1 < p.M) {
+        __builtin_nontemporal_store(v, reinterpret_cast<f32x2*>(c));
+      } else {
+        if (i < p.M) c[0] = v[0];
+        if (i + 1 < p.M) c[1] = v[1];
+      }
+    }
+  }
+}
+
 template <int T, int V>
 constexpr size_t dq2_lds() {
   constexpr size_t img = (size_t)8 * DQ_KG * (DQ_TI * (4 * DqFmt<T>::BPB / 8) + DQ_TJ * (4 * DqFmt<V>::BPB / 8));
@@ -504,15 +702,29 @@ constexpr size_t dq2_lds() {
 }
 
 #ifndef DQ_FORM
-#define DQ_FORM 2   // 1: per-lane window loads into VGPRs (gemm_dq_kernel); 2: coalesced, LDS-staged
+#define DQ_FORM 2   // 1: per-lane window loads into VGPRs (gemm_dq_kernel); 2: coalesced, LDS-staged; 3: + activations prepped to f16 once per call
 #endif
 #ifndef DQ_NBV
 #define DQ_NBV 1    // the LDS-staged form's quads in flight in VGPRs
 #endif
 
+int64_t dq3_kpad(const GemvArgs& p) { return (int64_t)((p.nblk + 3) / 4) * 128; }
+
 template <int T, int V>
-hipError_t launch_dq_t(const GemvArgs& p, hipStream_t s) {
+hipError_t launch_dq_t(const GemvArgs& p, void* ws, hipStream_t s) {
   const int tiles = gemm_dq_tiles(p);
+  if constexpr (DQ_FORM == 3) {
+    const int64_t kpad = dq3_kpad(p), items = (int64_t)p.ne12 * p.ne13 * p.N * (kpad / 32);
+    auto* bimg = static_cast<_Float16*>(ws);
+    hipLaunchKernelGGL(dq_prep_b<V>, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, s, p, bimg, kpad);
+    auto kern = gemm_dq3_kernel<T, DQ_NBV>;
+    constexpr size_t img = (size_t)DQ_KG * (DQ_TI * 4 * DqFmt<T>::BPB + DQ_TJ * DQ3_BP);
+    constexpr size_t lds = img > DQ_LDS ? img : DQ_LDS;
+    static_assert(lds <= 160 * 1024, "LDS");
+    set_max_lds((const void*)kern, (int)lds);
+    hipLaunchKernelGGL(kern, dim3((unsigned)tiles), dim3(DQ_NT), lds, s, p, bimg, kpad);
+    return hipGetLastError();
+  }
   if constexpr (DQ_FORM == 1) {
     auto kern = gemm_dq_kernel<T, V, DQ_NBUF>;
     set_max_lds((const void*)kern, (int)DQ_LDS);
@@ -544,13 +756,17 @@ bool gemm_dq_args_ok(const GemvArgs& p) {
          (int64_t)DQ_TI * p.lda < 0x7fffffff && (int64_t)DQ_TJ * p.ldb < 0x7fffffff;
 }
 
-hipError_t launch_gemm_dq(int type, const GemvArgs& p, hipStream_t s) {
+size_t gemm_dq_workspace_bytes(const GemvArgs& p) {
+  return DQ_FORM == 3 ? (size_t)p.ne12 * p.ne13 * p.N * dq3_kpad(p) * 2 + 256 : 0;
+}
+
+hipError_t launch_gemm_dq(int type, const GemvArgs& p, void* ws, hipStream_t s) {
   switch (type) {
-    case kQ4_0: return launch_dq_t<kQ4_0, kQ8_0>(p, s);
-    case kQ4_1: return launch_dq_t<kQ4_1, kQ8_1>(p, s);
-    case kQ5_0: return launch_dq_t<kQ5_0, kQ8_0>(p, s);
-    case kQ5_1: return launch_dq_t<kQ5_1, kQ8_1>(p, s);
-    case kQ8_0: return launch_dq_t<kQ8_0, kQ8_0>(p, s);
+    case kQ4_0: return launch_dq_t<kQ4_0, kQ8_0>(p, ws, s);
+    case kQ4_1: return launch_dq_t<kQ4_1, kQ8_1>(p, ws, s);
+    case kQ5_0: return launch_dq_t<kQ5_0, kQ8_0>(p, ws, s);
+    case kQ5_1: return launch_dq_t<kQ5_1, kQ8_1>(p, ws, s);
+    case kQ8_0: return launch_dq_t<kQ8_0, kQ8_0>(p, ws, s);
     default: return hipErrorInvalidValue;
   }
 }

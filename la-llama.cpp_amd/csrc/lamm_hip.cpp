@@ -7,7 +7,14 @@
 //                        device-resident weight cache and strided B/C transfers.
 #include <hip/hip_runtime.h>
 
+#include <linux/futex.h>
+#include <sched.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
+#include <atomic>
 #include <chrono>
+#include <climits>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -192,14 +199,17 @@ int gemv_max_n(int type) {
 // callers and tests).  stationary: the weights' packed prefill form is resident (lamm_weights);
 // b_al4: B and its slice strides are 4-byte aligned (the super-block GEMM reads q8_K as dwords).
 enum Engine { kEngGemv, kEngDense, kEngKq, kEngFp6, kEngI8, kEngGemvGroups, kEngDq };
-// The dequantizing f16 GEMM (lamm_gemm_dq.hip) takes the 32-element formats' prefill calls whose
-// 128 x 64 tiles fill at least half the chip (it has no K-split); LAMM_GEMM_PATH=dq16 forces it,
-// fp6 / i8 force the exact engines.
+// The dequantizing f16 GEMM (lamm_gemm_dq.hip) runs every 32-element format; by default it takes the
+// q5_1 / q8_0 prefill calls whose 128 x 64 tiles fill at least half the chip (it has no K-split):
+// there it beats the exact MFMA-i8 engine (config 4, 4096 x 512 x 4096: q5_1 37.7 vs 49.5 us, q8_0
+// 39.6 vs 47.3 us, profiles/r04/dq16/), while for q4_0 / q4_1 / q5_0 the exact fp6 engine stays ahead
+// (q4_0 28.5 vs 34.4 us).  LAMM_GEMM_PATH=dq16 forces it for every format, fp6 / i8 force the exact
+// engines.
 constexpr int kDqMinTiles = 128;
 bool use_dq(int type, const GemvArgs& p) {
   if (!gemm_dq_supported(type) || !gemm_dq_args_ok(p)) return false;
   if (knobs().gemm_path == 2) return true;
-  return knobs().gemm_path < 0 && gemm_dq_tiles(p) >= kDqMinTiles;
+  return knobs().gemm_path < 0 && (type == kQ5_1 || type == kQ8_0) && gemm_dq_tiles(p) >= kDqMinTiles;
 }
 Engine pick_engine(int type, const GemvArgs& p, bool stationary, bool b_al4) {
   if (p.N <= gemv_max_n(type) || (p.b_f32 && p.N <= 8)) return kEngGemv;
@@ -341,9 +351,13 @@ int matmul_impl_(const lamm_matrix* A, const lamm_matrix* B, const lamm_matrix* 
       e = launch_gemm_fp6(A->type, p, prepA, ws, s);
       break;
     }
-    case kEngDq:
-      e = launch_gemm_dq(A->type, p, s);
+    case kEngDq: {
+      const size_t wsb = gemm_dq_workspace_bytes(p);
+      void* ws = nullptr;
+      if (wsb && !(ws = workspace(wsb, s))) return fail(LAMM_ERR_HIP, "workspace allocation of %zu bytes failed", wsb);
+      e = launch_gemm_dq(A->type, p, ws, s);
       break;
+    }
     case kEngI8: {
       void* ws = nullptr;
       const size_t wsb = gemm_workspace_bytes(A->type, p);
@@ -991,13 +1005,55 @@ constexpr size_t kZeroCopyMax = (size_t)256 << 10;
 // call: the D2H into ggml's pageable dst blocks), in only 72, out only 74, both 89 (24.4 us).
 bool zero_copy(size_t bytes, bool in) { return (knobs().zero_copy & (in ? 1 : 2)) && bytes <= kZeroCopyMax; }
 
+// ggml's pool threads other than 0 have nothing to do in a claimed COMPUTE phase.  Returning at once
+// (the default) parks them in ggml's node barrier, which spins without yielding
+// (LC/ggml.c:18440-18447, ggml_graph_compute_thread_sync_task(.., false)); LAMM_HIP_HELPERS=1 / 2
+// keeps them here instead, yielding / asleep on a futex, until thread 0 publishes the node as done,
+// so a pool as wide as the cores leaves the CPU to thread 0 and the HIP runtime.  A helper never
+// waits more than 20 ms (a node thread 0 does not compute -- none exists -- cannot hang the pool).
+std::atomic<const void*> g_node_done{nullptr};
+std::atomic<uint32_t> g_node_gen{0};
+
+void helper_wait(const void* dst, int mode) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int i = 0;; ++i) {
+    const uint32_t gen = g_node_gen.load(std::memory_order_acquire);
+    if (g_node_done.load(std::memory_order_acquire) == dst) return;
+    if ((i & 15) == 15 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20)) return;
+    if (mode == 2) {
+      const timespec ts{0, 200000};   // re-check at least every 0.2 ms
+      syscall(SYS_futex, reinterpret_cast<uint32_t*>(&g_node_gen), FUTEX_WAIT_PRIVATE, gen, &ts, nullptr, 0);
+    } else {
+      sched_yield();
+    }
+  }
+}
+
+void mul_mat_thread0(const ggml::compute_params* params, ggml::tensor* dst);
+
 }  // namespace
 
 extern "C" void lamm_mul_mat(const struct ggml_compute_params* vparams, struct ggml_tensor* vdst) {
   const auto* params = reinterpret_cast<const ggml::compute_params*>(vparams);
   auto* dst = reinterpret_cast<ggml::tensor*>(vdst);
   if (params->type != ggml::TASK_COMPUTE) return;  // INIT claimed for the GPU quantizer: nothing to do
-  if (params->ith != 0) return;  // thread 0 owns the device work; ggml's barrier follows
+  const int helpers = knobs().helpers;
+  if (params->ith != 0) {   // thread 0 owns the device work; ggml's barrier follows
+    if (helpers > 0 && params->nth > 1) helper_wait(dst, helpers);
+    return;
+  }
+  if (helpers > 0) g_node_done.store(nullptr, std::memory_order_release);
+  mul_mat_thread0(params, dst);
+  if (helpers > 0) {
+    g_node_done.store(dst, std::memory_order_release);
+    g_node_gen.fetch_add(1, std::memory_order_acq_rel);
+    if (helpers == 2) syscall(SYS_futex, reinterpret_cast<uint32_t*>(&g_node_gen), FUTEX_WAKE_PRIVATE, INT32_MAX, nullptr, nullptr, 0);
+  }
+}
+
+namespace {
+
+void mul_mat_thread0(const ggml::compute_params* params, ggml::tensor* dst) {
 
   const ggml::tensor* src0 = dst->src[0];
   const ggml::tensor* src1 = dst->src[1];
@@ -1202,6 +1258,8 @@ extern "C" void lamm_mul_mat(const struct ggml_compute_params* vparams, struct g
   }
   stat.phase(6);
 }
+
+}  // namespace
 
 extern "C" void lamm_hip_cache_clear(void) {
   Runtime& rt = Runtime::get();

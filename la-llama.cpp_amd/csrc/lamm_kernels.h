@@ -101,7 +101,8 @@ int gemm_fp6_grid(const GemvArgs& p);    // its main-kernel workgroups (tiles x 
 
 // q4_0 / q4_1 / q5_0 / q5_1 / q8_0 prefill GEMM on f16 MFMAs with the block scales folded into the
 // operands as the raw blocks are unpacked (lamm_gemm_dq.hip): one launch, no workspace, 1e-3 bar
-hipError_t launch_gemm_dq(int type, const GemvArgs& p, hipStream_t s);
+hipError_t launch_gemm_dq(int type, const GemvArgs& p, void* workspace, hipStream_t s);
+size_t gemm_dq_workspace_bytes(const GemvArgs& p);   // 0: no workspace (the one-launch forms)
 bool gemm_dq_supported(int type);
 bool gemm_dq_args_ok(const GemvArgs& p);
 int gemm_dq_tiles(const GemvArgs& p);   // its workgroups (128 x 64 output tiles over all slices)

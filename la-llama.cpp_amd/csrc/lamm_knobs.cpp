@@ -62,6 +62,7 @@ Knobs* read_env() {
   k->zero_copy = !k->pinned || (zc && zc[0] == '0') ? 0 : zc && !strcmp(zc, "in") ? 1 : zc && !strcmp(zc, "out") ? 2 : 3;
   k->zero_copy_split = env_on("LAMM_HIP_ZERO_COPY_SPLIT");
   k->ref_mfma = env_int("LAMM_REF_MFMA", -1);
+  k->helpers = env_int("LAMM_HIP_HELPERS", 0);
   if (const char* e = getenv("LAMM_HIP_ORDER")) k->ref_order = strcmp(e, "fast") != 0;
   return k;
 }

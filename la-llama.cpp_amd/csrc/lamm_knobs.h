@@ -41,6 +41,9 @@ struct Knobs {
   bool kernel_signal = false;  // LAMM_HIP_KERNEL_SIGNAL=1: the GEMV writes the completion flag
   int zero_copy = 3;           // LAMM_HIP_ZERO_COPY: 0 off, 1 in, 2 out, 3 both
   bool zero_copy_split = false;
+  int helpers = 0;             // LAMM_HIP_HELPERS: ggml's other pool threads during thread 0's device work:
+                               // 0 return at once (ggml's barrier spins on them), 1 wait here yielding,
+                               // 2 wait here asleep (futex)
   int ref_mfma = -1;           // LAMM_REF_MFMA: reference-order prefill kernel (1: ref_mfma_kernel, 2 / 4: ref_mfma2 G)
   bool ref_order = true;       // LAMM_HIP_ORDER=fast: the boundary runs the fast engines instead of the
                                // reference's float order (lamm_ref.hip) for the formats that have both  // LAMM_HIP_ZERO_COPY_SPLIT=1: zero copy also when rows split over devices

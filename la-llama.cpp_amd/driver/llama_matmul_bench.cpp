@@ -46,6 +46,7 @@
 // PCIe.  Softmax / RoPE / norms are llama.cpp ops outside the hook and stay out.  --check
 // recomputes the last layer's attention on the host from the device buffers after the replays.
 #include <execinfo.h>
+#include <pthread.h>
 #include <hip/hip_runtime.h>
 #include <signal.h>
 #include <unistd.h>
@@ -545,7 +546,20 @@ int run_sharded(const ShardOpts& o, int type, int out_type, int N, int iters, in
     hip_ok(hipSetDevice(r.dev), "hipSetDevice");
     hip_ok(hipStreamSynchronize(r.s), "warm-up");
   }
-  // one graph: the step on rank 0's stream, the other local ranks' streams forked from it
+  // one graph: the step on rank 0's stream, the other local ranks' streams forked from it.  More than
+  // 4 local ranks replay the step eagerly instead: capturing 8 streams joined by events at every
+  // all-gather sends the HIP runtime's graph code into unbounded recursion (one libamdhip64 frame
+  // calling itself until the stack is gone, with a 1 GiB stack as with 8 MiB; ROCm 7.2).  One
+  // process per GPU (--rank) always captures: it has one stream.
+  const bool graphed = R.size() <= 4;
+  if (!graphed) {
+    printf("llama-matmul-bench: %zu local ranks: eager replays (no hipGraph)\n", R.size());
+    step_sharded(R, comm, layers, N, tall);
+    for (Rank& r : R) {
+      hip_ok(hipSetDevice(r.dev), "hipSetDevice");
+      hip_ok(hipStreamSynchronize(r.s), "eager warm-up");
+    }
+  }
   hip_ok(hipSetDevice(R[0].dev), "hipSetDevice");
   hipEvent_t fork;
   std::vector<hipEvent_t> join(R.size());
@@ -557,6 +571,7 @@ int run_sharded(const ShardOpts& o, int type, int out_type, int N, int iters, in
   hip_ok(hipSetDevice(R[0].dev), "hipSetDevice");
   hipGraph_t g;
   hipGraphExec_t exec = nullptr;
+  if (graphed) {
   hip_ok(hipStreamBeginCapture(R[0].s, hipStreamCaptureModeRelaxed), "hipStreamBeginCapture");
   hip_ok(hipEventRecord(fork, R[0].s), "hipEventRecord");
   for (size_t i = 1; i < R.size(); ++i) hip_ok(hipStreamWaitEvent(R[i].s, fork, 0), "hipStreamWaitEvent");
@@ -572,11 +587,29 @@ int run_sharded(const ShardOpts& o, int type, int out_type, int N, int iters, in
   hip_ok(hipGraphDestroy(g), "hipGraphDestroy");
   hip_ok(hipGraphLaunch(exec, R[0].s), "hipGraphLaunch");
   hip_ok(hipStreamSynchronize(R[0].s), "graph warm-up");
+  }
   hipEvent_t e0, e1;
   hip_ok(hipEventCreate(&e0), "hipEventCreate");
   hip_ok(hipEventCreate(&e1), "hipEventCreate");
   hip_ok(hipEventRecord(e0, R[0].s), "hipEventRecord");
-  for (int it = 0; it < iters; ++it) hip_ok(hipGraphLaunch(exec, R[0].s), "hipGraphLaunch");
+  for (int it = 0; it < iters; ++it) {
+    if (graphed) {
+      hip_ok(hipGraphLaunch(exec, R[0].s), "hipGraphLaunch");
+      continue;
+    }
+    hip_ok(hipEventRecord(fork, R[0].s), "hipEventRecord");
+    for (size_t i = 1; i < R.size(); ++i) {
+      hip_ok(hipSetDevice(R[i].dev), "hipSetDevice");
+      hip_ok(hipStreamWaitEvent(R[i].s, fork, 0), "hipStreamWaitEvent");
+    }
+    step_sharded(R, comm, layers, N, tall);
+    for (size_t i = 1; i < R.size(); ++i) {
+      hip_ok(hipSetDevice(R[i].dev), "hipSetDevice");
+      hip_ok(hipEventRecord(join[i], R[i].s), "hipEventRecord");
+      hip_ok(hipSetDevice(R[0].dev), "hipSetDevice");
+      hip_ok(hipStreamWaitEvent(R[0].s, join[i], 0), "hipStreamWaitEvent");
+    }
+  }
   hip_ok(hipEventRecord(e1, R[0].s), "hipEventRecord");
   hip_ok(hipEventSynchronize(e1), "hipEventSynchronize");
   float ms = 0;
@@ -621,10 +654,10 @@ int run_sharded(const ShardOpts& o, int type, int out_type, int N, int iters, in
          "per step  |  logits |sum| %.6g\n",
          t * 1e3, N / t, wbytes / t / 1e9, projections, projections, cs);
   printf("{\"tool\": \"llama-matmul-bench\", \"layers\": %d, \"tokens_per_step\": %d, \"ms_per_step\": %.4f, "
-         "\"tok_per_s\": %.2f, \"weight_GBps\": %.1f, \"TFLOPs\": %.2f, \"graph\": true, \"stationary\": %s, "
+         "\"tok_per_s\": %.2f, \"weight_GBps\": %.1f, \"TFLOPs\": %.2f, \"graph\": %s, \"stationary\": %s, "
          "\"type\": \"%s\", \"mode\": \"%s\", \"launches\": %d, \"world\": %d, \"rank\": %d, \"local_ranks\": %zu, "
          "\"allgathers\": %d, \"logits_abs_sum\": %.9g}\n",
-         layers, N, t * 1e3, N / t, wbytes / t / 1e9, 2.0 * params * N / t / 1e12, stationary ? "true" : "false",
+         layers, N, t * 1e3, N / t, wbytes / t / 1e9, 2.0 * params * N / t / 1e12, graphed ? "true" : "false", stationary ? "true" : "false",
          type_name(type), tall ? "sharded-batch-proj" : "sharded", projections, world, o.rank >= 0 ? o.rank : 0,
          R.size(), projections, cs);
   lamm_hip_comm_destroy(comm);
@@ -643,7 +676,34 @@ void on_fault(int sig) {
   _exit(128 + sig);
 }
 
+int real_main(int argc, char** argv);
+
+// The HIP runtime walks a captured graph's dependencies recursively: the 8-rank sharded step (8
+// streams joined by events at every all-gather) took it past the default 8 MiB main-thread stack
+// (call stack of the fault: libamdhip64 recursing in one frame).  The whole program runs on a
+// thread with a 1 GiB stack (address space; only the pages it touches are committed).
 int main(int argc, char** argv) {
+  struct Args {
+    int argc;
+    char** argv;
+    int rc;
+  } a{argc, argv, 1};
+  pthread_attr_t attr;
+  pthread_attr_init(&attr);
+  pthread_attr_setstacksize(&attr, (size_t)1 << 30);
+  pthread_t th;
+  if (pthread_create(&th, &attr, [](void* p) -> void* {
+        auto* x = static_cast<Args*>(p);
+        x->rc = real_main(x->argc, x->argv);
+        return nullptr;
+      }, &a) != 0) {
+    return real_main(argc, argv);
+  }
+  pthread_join(th, nullptr);
+  return a.rc;
+}
+
+int real_main(int argc, char** argv) {
   setvbuf(stdout, nullptr, _IOLBF, 0);
   int type = 2, N = 1, iters = 20, layers = 32, out_type = 14, ctx = 0;
   bool graph = true, stationary = false, batch_proj = false, concurrent = false, check = false;
@@ -696,8 +756,14 @@ int main(int argc, char** argv) {
     return 1;
   }
   // after the HIP runtime's own start-up (it installs handlers of its own)
+  static char altstack[1 << 16];   // the handler also runs when the fault is a stack overflow
+  stack_t ss = {};
+  ss.ss_sp = altstack;
+  ss.ss_size = sizeof altstack;
+  sigaltstack(&ss, nullptr);
   struct sigaction sa = {};
   sa.sa_handler = on_fault;
+  sa.sa_flags = SA_ONSTACK;
   sigaction(SIGSEGV, &sa, nullptr);
   sigaction(SIGBUS, &sa, nullptr);
   if (so.rank >= 0 || shard > 0 || !so.devices.empty() || !so.dump.empty() || !so.dump_q.empty()) {   // the row-sharded form

@@ -265,7 +265,7 @@ def test_gemm_dq16_batched_strided(t, monkeypatch):
     M, N, K, ne02, ne12 = 200, 70, 1024 + 160, 2, 4
     vt = la.vec_dot_type(t)
     kb = K // 32
-    lda, ldb, ldc = pitch_blocks(t, kb) + 1, kb + 3, M + 5
+    lda, ldb, ldc = pitch_blocks(t, kb + 1), kb + 3, M + 5   # A pitches stay 16-byte multiples
     arow, brow = lda * la.type_size(t), ldb * la.type_size(vt)
     rng = np.random.default_rng(5 + t)
     As = [ORACLE.quantize(t, rng.standard_normal((M, K), dtype=np.float32), ol.QUANT_REF) for _ in range(ne02)]
@@ -857,21 +857,18 @@ def _config3_check(c, A_q, B_q, rows):
 CONFIG3_ROWS = np.unique(np.concatenate([np.arange(0, 4096, 16), [1, 127, 128, 255, 256, 2047, 2048, 4095]]))
 
 
-@pytest.mark.parametrize("path", ["stationary_auto", "stationary_fp6", "stationary_fp6_split_k",
-                                  "stationary_fp6_kgroups2", "per_call_default", "per_call_fp6", "per_call_i8"])
+@pytest.mark.parametrize("path", ["stationary_auto", "stationary_fp6_split_k", "stationary_fp6_kgroups2",
+                                  "per_call_default", "per_call_fp6", "per_call_i8", "per_call_dq16"])
 def test_config3_full_size_gemm(path, monkeypatch):
     """BASELINE config 3 at its real size: Q4_0 x Q8_0 M=4096 N=512 K=4096, one slice.
-    Paths: the weight-stationary handle (the ggml boundary's and bench.py's: by default the
-    dequantizing f16 engine, 256 128x64 tiles with 4 K-groups; the exact fp6 engine forced, its
-    default 4 K-groups, or K split over the 64 256x128 tiles, or 2 K-groups), the per-call API's
-    default engine, and both exact engines forced per call.  >= 256 sampled rows x all 512 columns
-    vs the oracle."""
+    Paths: the weight-stationary handle (the ggml boundary's and bench.py's; fp6 engine, by
+    default 256 128x64 tiles with 4 K-groups each, or forced: K split over the 64 256x128 tiles,
+    2 K-groups), the per-call API's default engine, and the exact engines and the dequantizing f16
+    engine forced per call.  >= 256 sampled rows x all 512 columns vs the oracle."""
     M, N, K = 4096, 512, 4096
     (A_q,), (B_q,) = _config3_operands(2024, 1)
-    if path in ("per_call_fp6", "per_call_i8"):
+    if path in ("per_call_fp6", "per_call_i8", "per_call_dq16"):
         monkeypatch.setenv("LAMM_GEMM_PATH", path.rsplit("_", 1)[1])
-    if path.startswith("stationary_fp6"):
-        monkeypatch.setenv("LAMM_GEMM_PATH", "fp6")
     if path == "stationary_fp6_split_k":
         monkeypatch.setenv("LAMM_FP6_SUB", "0")
     if path == "stationary_fp6_kgroups2":
@@ -880,8 +877,7 @@ def test_config3_full_size_gemm(path, monkeypatch):
     B = dev_bytes(B_q)
     C = torch.full((N * M,), float("nan"), dtype=torch.float32, device="cuda")
     if path.startswith("stationary"):
-        want = "dq16" if path == "stationary_auto" else "fp6"
-        assert la.gemm_engine("q4_0", M, N, K, 1, stationary=True) == want
+        assert la.gemm_engine("q4_0", M, N, K, 1, stationary=True) == "fp6"
         W = la.Weights(ol.Q4_0, A, M, K)
         W.matmul_torch(B, C, N)
         torch.cuda.synchronize()
@@ -924,13 +920,13 @@ def test_config3_repeated_calls_fresh_activations(act, monkeypatch):
     W.close()
 
 
-@pytest.mark.parametrize("engine", ["dq16", "fp6"])
+@pytest.mark.parametrize("engine", ["fp6", "dq16"])
 def test_config3_four_slice_batched_launch(engine, monkeypatch):
     """The 4-slice batched launch bench.py times (ne02 = ne12 = 4, stationary weights; the default
-    dq16 engine with 1024 tiles, or the exact fp6 engine with 256): every slice's sampled rows x
-    all columns vs the oracle."""
-    if engine == "fp6":
-        monkeypatch.setenv("LAMM_GEMM_PATH", "fp6")
+    fp6 engine with 256 tiles, or the dequantizing f16 engine forced, 1024 tiles): every slice's
+    sampled rows x all columns vs the oracle."""
+    if engine == "dq16":
+        monkeypatch.setenv("LAMM_GEMM_PATH", "dq16")
     M, N, K = 4096, 512, 4096
     As, Bs = _config3_operands(77, 4)
     arow, brow = la.row_bytes(ol.Q4_0, K), la.row_bytes(ol.Q8_0, K)

@@ -188,10 +188,12 @@ def test_engine_choice(monkeypatch):
     assert e("q2_k", 4096, 5, 4096) == "gemv" and e("q2_k", 4096, 6, 4096) == "superblock"
     assert e("q6_k", 4096, 4, 4096) == "gemv" and e("q6_k", 4096, 5, 4096) == "superblock"
     assert e("f16", 4096, 5, 4096) == "dense" and e("f32", 512, 512, 512) == "dense"
-    # BASELINE config 3: the fp6 engine's 128x64 K-group tiles fill the chip with stationary weights
+    # BASELINE config 3: the fp6 engine's 128x64 K-group tiles fill the chip with stationary weights;
+    # q5_1 / q8_0 prefill on the dequantizing f16 engine once its tiles fill half the chip, the
+    # exact MFMA-i8 engine (split-K) below that
     assert e("q4_0", 4096, 512, 4096, stationary=True) == "fp6"
-    assert e("q5_1", 4096, 512, 4096, stationary=True) == "i8"
-    assert e("q8_0", 4096, 512, 4096) == "i8"
+    assert e("q5_1", 4096, 512, 4096, stationary=True) == "dq16"
+    assert e("q8_0", 4096, 512, 4096) == "dq16" and e("q8_0", 4096, 64, 4096) == "i8"
     assert e("q4_0", 4096, 9, 4096) in ("fp6", "i8")
     assert e("q5_0", 4096, 512, 4096, b_f32=True) == e("q5_0", 4096, 512, 4096)
     assert e("q4_0", 4096, 8, 4096, b_f32=True) == "gemv"

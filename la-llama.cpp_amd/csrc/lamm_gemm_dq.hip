@@ -327,19 +327,22 @@ __global__ __launch_bounds__(DQ_NT) void gemm_dq_kernel(GemvArgs p) {
 // wave's private LDS image of the quad (rows at a 4*BPB-byte pitch: the lanes' pair windows read
 // back conflict-free, 18r + 9h / 34c + 17h dwords), and the NEXT quads are already in flight in
 // VGPRs while this one is unpacked and multiplied.
-template <int T, int V, int NBV>
-__global__ __launch_bounds__(DQ_NT) void gemm_dq2_kernel(GemvArgs p) {
+template <int T, int V, int NBV, int WH>
+__global__ __launch_bounds__(DQ_NT * WH) void gemm_dq2_kernel(GemvArgs p) {
+  // WH waves per K-group, each owning 128 / WH of the tile's weight rows (2: two waves per SIMD, the
+  // activation quad unpacked by both)
+  constexpr int NT = DQ_NT * WH, TIW = DQ_TI / WH, YW = 4 / WH;
   using FA = DqFmt<T>;
   using FB = DqFmt<V>;
   constexpr int NWA = FA::BPB / 2, NWB = FB::BPB / 2;
   constexpr int QA = 4 * FA::BPB, QB = 4 * FB::BPB;   // bytes of a row's / a column's quad
   constexpr int PA = QA / 8, PB = QB / 8;             // its 8-byte pieces
-  constexpr int LA = DQ_TI * PA / 64, LB = DQ_TJ * PB / 64;   // piece loads per lane per quad
-  static_assert((DQ_TI * PA) % 64 == 0 && (DQ_TJ * PB) % 64 == 0, "whole loads");
+  constexpr int LA = TIW * PA / 64, LB = DQ_TJ * PB / 64;   // piece loads per lane per quad
+  static_assert((TIW * PA) % 64 == 0 && (DQ_TJ * PB) % 64 == 0, "whole loads");
   constexpr int QBYTES = 8 * 64 * (LA + LB);          // a wave's LDS image of one quad
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int t = threadIdx.x, lane = t & 63, lr = lane & 31, h = lane >> 5;
-  const int g = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wid = __builtin_amdgcn_readfirstlane(t >> 6), g = wid / WH, mh = wid % WH;
   const int nsi = (p.M + DQ_TI - 1) / DQ_TI, nsj = (p.N + DQ_TJ - 1) / DQ_TJ;
   int ti, tj, z;
   {   // XCD-aware order (gemm_dq_kernel)
@@ -369,7 +372,7 @@ __global__ __launch_bounds__(DQ_NT) void gemm_dq2_kernel(GemvArgs p) {
 #pragma unroll
     for (int i = 0; i < LA; ++i) {
       const int pc = i * 64 + lane;
-      a_off[i] = (uint32_t)(pc / PA) * lda + (uint32_t)(pc % PA) * 8;
+      a_off[i] = (uint32_t)(mh * TIW + pc / PA) * lda + (uint32_t)(pc % PA) * 8;
     }
 #pragma unroll
     for (int i = 0; i < LB; ++i) {
@@ -377,7 +380,7 @@ __global__ __launch_bounds__(DQ_NT) void gemm_dq2_kernel(GemvArgs p) {
       b_off[i] = (uint32_t)(pc / PB) * ldb + (uint32_t)(pc % PB) * 8;
     }
   }
-  unsigned char* img = smem + g * QBYTES;   // rows [128][QA], then columns [64][QB]
+  unsigned char* img = smem + wid * QBYTES;   // rows [TIW][QA], then columns [64][QB]
   u32x2 st[NBV][LA + LB];
   auto issue = [&](int u, auto S_) __attribute__((always_inline)) {
     constexpr int S = decltype(S_)::value;
@@ -394,27 +397,27 @@ __global__ __launch_bounds__(DQ_NT) void gemm_dq2_kernel(GemvArgs p) {
     for (int i = 0; i < LA + LB; ++i) *reinterpret_cast<u32x2*>(img + 8 * (i * 64 + lane)) = st[S][i];
   };
 
-  f32x16 acc[2][4];
-  unroll<2>([&](auto X) __attribute__((always_inline)) { unroll<4>([&](auto Y) __attribute__((always_inline)) { acc[X][Y] = f32x16{}; }); });
+  f32x16 acc[2][YW];
+  unroll<2>([&](auto X) __attribute__((always_inline)) { unroll<YW>([&](auto Y) __attribute__((always_inline)) { acc[X][Y] = f32x16{}; }); });
 
   auto quad = [&](int u) __attribute__((always_inline)) {
     const int q = g + DQ_KG * u;
-    uint32_t wa[4][NWA], wb[2][NWB];   // this lane's pair windows, from the image
+    uint32_t wa[YW][NWA], wb[2][NWB];   // this lane's pair windows, from the image
 #pragma unroll
-    for (int y = 0; y < 4; ++y) {
+    for (int y = 0; y < YW; ++y) {
       const uint32_t* src = reinterpret_cast<const uint32_t*>(img + (32 * y + lr) * QA + h * 2 * FA::BPB);
 #pragma unroll
       for (int k = 0; k < NWA; ++k) wa[y][k] = src[k];
     }
 #pragma unroll
     for (int x = 0; x < 2; ++x) {
-      const uint32_t* src = reinterpret_cast<const uint32_t*>(img + DQ_TI * QA + (32 * x + lr) * QB + h * 2 * FB::BPB);
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(img + TIW * QA + (32 * x + lr) * QB + h * 2 * FB::BPB);
 #pragma unroll
       for (int k = 0; k < NWB; ++k) wb[x][k] = src[k];
     }
     if constexpr (DQ_AB == 1) {
 #pragma unroll
-      for (int y = 0; y < 4; ++y)
+      for (int y = 0; y < YW; ++y)
 #pragma unroll
         for (int i = 0; i < NWA; ++i) asm volatile("" ::"v"(wa[y][i]));
 #pragma unroll
@@ -426,14 +429,14 @@ __global__ __launch_bounds__(DQ_NT) void gemm_dq2_kernel(GemvArgs p) {
     unroll<2>([&](auto JB_) __attribute__((always_inline)) {
       constexpr int JB = JB_;
       const bool valid = 4 * q + 2 * h + JB < nblk;
-      uint32_t ad[4], am[4], aq[4], bd[2], bm[2], bq[2];
-      unroll<4>([&](auto Y) __attribute__((always_inline)) { dq_scalars<T, JB>(wa[Y], valid, (_Float16)DQ_ASCALE, ad[Y], am[Y], aq[Y]); });
+      uint32_t ad[YW], am[YW], aq[YW], bd[2], bm[2], bq[2];
+      unroll<YW>([&](auto Y) __attribute__((always_inline)) { dq_scalars<T, JB>(wa[Y], valid, (_Float16)DQ_ASCALE, ad[Y], am[Y], aq[Y]); });
       unroll<2>([&](auto X) __attribute__((always_inline)) { dq_scalars<V, JB>(wb[X], valid, (_Float16)1, bd[X], bm[X], bq[X]); });
       unroll<4>([&](auto CG_) __attribute__((always_inline)) {
         constexpr int CG = CG_;
         half8 bo[2];
         unroll<2>([&](auto X) __attribute__((always_inline)) { bo[X] = dq_operand<V, JB, CG>(wb[X], bd[X], 0u, 0u); });
-        unroll<4>([&](auto Y) __attribute__((always_inline)) {
+        unroll<YW>([&](auto Y) __attribute__((always_inline)) {
           const half8 ao = dq_operand<T, JB, CG>(wa[Y], ad[Y], am[Y], aq[Y]);
           unroll<2>([&](auto X) __attribute__((always_inline)) { acc[X][Y] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bo[X], ao, acc[X][Y], 0, 0, 0); });
         });
@@ -466,10 +469,10 @@ __global__ __launch_bounds__(DQ_NT) void gemm_dq2_kernel(GemvArgs p) {
   __syncthreads();   // every wave past its last image read: the partial tiles reuse the LDS
   float* red = reinterpret_cast<float*>(smem);
   unroll<2>([&](auto X) __attribute__((always_inline)) {
-    unroll<4>([&](auto Y) __attribute__((always_inline)) {
+    unroll<YW>([&](auto Y) __attribute__((always_inline)) {
       unroll<16>([&](auto E) __attribute__((always_inline)) {
         constexpr int e = E;
-        const int j = 32 * X + (e & 3) + 8 * (e >> 2) + 4 * h, i = 32 * Y + lr;
+        const int j = 32 * X + (e & 3) + 8 * (e >> 2) + 4 * h, i = TIW * mh + 32 * Y + lr;
         red[(g * DQ_TJ + j) * DQ_PI + i] = acc[X][Y][e];
       });
     });
@@ -478,8 +481,8 @@ __global__ __launch_bounds__(DQ_NT) void gemm_dq2_kernel(GemvArgs p) {
   float* C = p.C + (int64_t)i12 * p.sc2 + (int64_t)i13 * p.sc3;
   const bool pair = (p.ldc & 1) == 0 && ((uintptr_t)C & 7) == 0;
 #pragma unroll
-  for (int r = 0; r < DQ_TJ * DQ_TI / (2 * DQ_NT); ++r) {
-    const int idx = 2 * (r * DQ_NT + t), jl = idx / DQ_TI, il = idx % DQ_TI;
+  for (int r = 0; r < DQ_TJ * DQ_TI / (2 * NT); ++r) {
+    const int idx = 2 * (r * NT + t), jl = idx / DQ_TI, il = idx % DQ_TI;
     f32x2 v = *reinterpret_cast<const f32x2*>(&red[jl * DQ_PI + il]);
 #pragma unroll
     for (int g_ = 1; g_ < DQ_KG; ++g_) v += *reinterpret_cast<const f32x2*>(&red[(g_ * DQ_TJ + jl) * DQ_PI + il]);
@@ -695,14 +698,18 @@ __global__ __launch_bounds__(DQ_NT) void gemm_dq3_kernel(GemvArgs p, const _Floa
   }
 }
 
-template <int T, int V>
+template <int T, int V, int WH>
 constexpr size_t dq2_lds() {
-  constexpr size_t img = (size_t)8 * DQ_KG * (DQ_TI * (4 * DqFmt<T>::BPB / 8) + DQ_TJ * (4 * DqFmt<V>::BPB / 8));
+  constexpr size_t img =
+      (size_t)8 * DQ_KG * WH * (DQ_TI / WH * (4 * DqFmt<T>::BPB / 8) + DQ_TJ * (4 * DqFmt<V>::BPB / 8));
   return img > DQ_LDS ? img : DQ_LDS;
 }
 
 #ifndef DQ_FORM
 #define DQ_FORM 2   // 1: per-lane window loads into VGPRs (gemm_dq_kernel); 2: coalesced, LDS-staged; 3: + activations prepped to f16 once per call
+#endif
+#ifndef DQ_WH
+#define DQ_WH 1     // the LDS-staged form's waves per K-group (2: two waves per SIMD; measured no faster, profiles/r04/dq16/)
 #endif
 #ifndef DQ_NBV
 #define DQ_NBV 1    // the LDS-staged form's quads in flight in VGPRs
@@ -730,11 +737,11 @@ hipError_t launch_dq_t(const GemvArgs& p, void* ws, hipStream_t s) {
     set_max_lds((const void*)kern, (int)DQ_LDS);
     hipLaunchKernelGGL(kern, dim3((unsigned)tiles), dim3(DQ_NT), DQ_LDS, s, p);
   } else {
-    auto kern = gemm_dq2_kernel<T, V, DQ_NBV>;
-    constexpr size_t lds = dq2_lds<T, V>();
+    auto kern = gemm_dq2_kernel<T, V, DQ_NBV, DQ_WH>;
+    constexpr size_t lds = dq2_lds<T, V, DQ_WH>();
     static_assert(lds <= 160 * 1024, "LDS");
     set_max_lds((const void*)kern, (int)lds);
-    hipLaunchKernelGGL(kern, dim3((unsigned)tiles), dim3(DQ_NT), lds, s, p);
+    hipLaunchKernelGGL(kern, dim3((unsigned)tiles), dim3(DQ_NT * DQ_WH), lds, s, p);
   }
   return hipGetLastError();
 }

@@ -445,7 +445,17 @@ __global__ __launch_bounds__(DQ_NT * WH) void gemm_dq2_kernel(GemvArgs p) {
   };
 
   constexpr int LPQ = LA + LB;
-  if (mine > 0) {
+  if constexpr (DQ_AB == 2) {   // probe: unpack + MFMA only, on the first quad's image (no loads after it)
+    if (mine > 0) {
+      issue(0, std::integral_constant<int, 0>{});
+      wait_vm<0>();
+      stage(std::integral_constant<int, 0>{});
+      for (int u = 0; u < mine; ++u) {
+        asm volatile("" ::: "memory");
+        quad(u);
+      }
+    }
+  } else if (mine > 0) {
     unroll<NBV>([&](auto K) __attribute__((always_inline)) { issue(K, K); });
     int u0 = 0;
     for (; u0 + NBV <= mine; u0 += NBV) {

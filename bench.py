@@ -762,7 +762,9 @@ def main():
             devs = list(range(world)) if world > 1 and not ctx.rehearse else None
             e2e = {"note": "BASELINE config 5: llama.cpp-b2430's own llama_decode (integration/_build/llama_e2e_hip: "
                            "the reference's llama.cpp + ggml, LA_LLAMA hook -> liblamm_hip.so), synthetic "
-                           "Llama-7B-shaped Q4_0 GGUF (Q6_K output, F16 KV cache), pp512 then tg128 greedy; "
+                           "Llama-7B-shaped Q4_0 GGUF (Q6_K output, F16 KV cache), pp512 then tg128 greedy behind the "
+                           "prompt (tg_tok_s), and llama-bench's own tg128 from an empty cache "
+                           "(tg_from_empty_tok_s, examples/llama-bench/llama-bench.cpp:1234-1254); "
                            "weights device-resident after a warm-up pass; reference published (3A6000, 4 threads, "
                            "README.md:684,710): prompt 8.27 tok/s, text-gen 4.69 tok/s",
                    "devices": devs or [ctx.device],

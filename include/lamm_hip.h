@@ -128,6 +128,14 @@ int lamm_hip_matmul_ex(const lamm_matrix *A, const lamm_matrix *B, const lamm_ma
 int lamm_hip_quantize(int vec_type, int flavour, const float *x, int64_t ldx, void *y,
                       int64_t ldy, int K, int N, void *hip_stream);
 
+/* The same AVX2-flavour activation quantizer on the host (no device needed): one row of k
+ * floats (k a multiple of 32) -> k/32 q8_0 or q8_1 blocks, byte for byte what ggml's x86
+ * INIT writes (LC/ggml-quants.c:1277-1330 quantize_row_q8_0, :1505-1575 quantize_row_q8_1,
+ * AVX2 branches) and lamm_hip_quantize(.., flavour 1, ..) writes on the device.  The boundary
+ * runs it on ggml's pool threads for prefill-sized calls (LAMM_HIP_POOL).  Other vec types:
+ * LAMM_ERR_TYPE; k not a multiple of 32: LAMM_ERR_SHAPE. */
+int lamm_hip_quantize_host(int vec_type, const float *x, void *y, int64_t k);
+
 /* Weight-stationary form (weight residency).  Inference multiplies the
  * same weights by new activations on every call; a lamm_weights handle records A (whose
  * device blocks must stay valid and unchanged while the handle lives) and its ggml slice

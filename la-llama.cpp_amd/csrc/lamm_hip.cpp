@@ -801,9 +801,11 @@ class Runtime {
         }
         HIPCHK(hipHostFree(hbuf_[which]));
       }
-      const unsigned flags = hipHostMallocMapped | hipHostMallocPortable | (which == 0 ? hipHostMallocNonCoherent : 0u);
+      // 2: the prefill pool's upload image (DMA only, not mapped)
+      const unsigned flags = which == 2 ? hipHostMallocPortable
+                                        : hipHostMallocMapped | hipHostMallocPortable | (which == 0 ? hipHostMallocNonCoherent : 0u);
       HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&hbuf_[which]), bytes + 256, flags));
-      HIPCHK(hipHostGetDevicePointer(&hdev_[which], hbuf_[which], 0));
+      if (which != 2) HIPCHK(hipHostGetDevicePointer(&hdev_[which], hbuf_[which], 0));
       hcap_[which] = bytes;
     }
     return hbuf_[which];
@@ -842,9 +844,9 @@ class Runtime {
 
  private:
   size_t budget_ = 0;
-  unsigned char* hbuf_[2] = {nullptr, nullptr};
-  void* hdev_[2] = {nullptr, nullptr};
-  size_t hcap_[2] = {0, 0};
+  unsigned char* hbuf_[3] = {nullptr, nullptr, nullptr};
+  void* hdev_[3] = {nullptr, nullptr, nullptr};
+  size_t hcap_[3] = {0, 0, 0};
 };
 
 bool use_pinned(size_t bytes) {
@@ -1029,7 +1031,97 @@ void helper_wait(const void* dst, int mode) {
   }
 }
 
-void mul_mat_thread0(const ggml::compute_params* params, ggml::tensor* dst);
+// Prefill-sized calls put ggml's other pool threads to work (LAMM_HIP_POOL): they enter the same
+// COMPUTE call as thread 0 (LC/ggml.c:18404-18421), wait here instead of spinning in ggml's
+// barrier, and claim chunks of the row jobs thread 0 posts -- bit 1: quantize the F32 activation
+// rows to q8_0 / q8_1 in pinned memory (lamm_host_quant.cpp, the bytes ggml's AVX2 INIT and the
+// device quantizer write), so 2.2 MiB cross PCIe instead of 8 MiB of F32 (pageable: ~400 us per
+// 4096 x 512 call); bit 2: C down into pinned memory and scattered into dst by the pool (measured
+// slower than HIP's pageable download, profiles/r04/e2e_pool/: off).  Every thread decides from
+// the call's shapes alone (pool_call) whether the node is a pool node; a helper that arrives after
+// thread 0 has finished (or never sees it start within 2 s) returns, and thread 0 runs every chunk
+// nobody claimed -- the jobs are complete whoever does them.
+struct RowJob {   // rows r = (i3 * n2 + i2) * n1 + j: dst + off(r, d*) <- src + off(r, s*)
+  const unsigned char* src = nullptr;
+  unsigned char* dst = nullptr;
+  size_t bytes = 0, s1 = 0, s2 = 0, s3 = 0, d1 = 0, d2 = 0, d3 = 0;   // bytes: per row (a copy)
+  int64_t n1 = 1, n2 = 1, rows = 0, per_chunk = 1;
+  int qtype = -1;        // >= 0: quantize each F32 row to nblk blocks of qtype instead of copying
+  int64_t nblk = 0;
+};
+RowJob g_job;
+std::atomic<uint64_t> g_ctl{0};             // job sequence (24 bits) | chunks (20) | next chunk (20)
+std::atomic<int64_t> g_done{0};             // chunks of the current job completed
+std::atomic<const void*> g_pool_dst{nullptr};
+std::atomic<int> g_pool_finished{1};
+std::atomic<const void*> g_pool_last{nullptr};   // the node whose last job has been posted
+uint64_t g_pool_seq = 0;                    // thread 0's
+
+void run_rows(const RowJob& jb, int64_t c) {
+  const int64_t r1 = std::min(jb.rows, (c + 1) * jb.per_chunk);
+  for (int64_t r = c * jb.per_chunk; r < r1; ++r) {
+    const int64_t j = r % jb.n1, q = r / jb.n1, i2 = q % jb.n2, i3 = q / jb.n2;
+    unsigned char* y = jb.dst + j * jb.d1 + i2 * jb.d2 + i3 * jb.d3;
+    const unsigned char* x = jb.src + j * jb.s1 + i2 * jb.s2 + i3 * jb.s3;
+    if (jb.qtype >= 0) host_quantize_row(jb.qtype, reinterpret_cast<const float*>(x), y, jb.nblk);
+    else memcpy(y, x, jb.bytes);
+  }
+}
+
+void pool_work() {   // claim and run chunks of the posted job until none is left
+  for (;;) {
+    uint64_t v = g_ctl.load(std::memory_order_acquire);
+    if ((v & 0xFFFFF) >= ((v >> 20) & 0xFFFFF)) return;
+    if (!g_ctl.compare_exchange_weak(v, v + 1, std::memory_order_acq_rel)) continue;
+    run_rows(g_job, (int64_t)(v & 0xFFFFF));   // g_job is rewritten only after every chunk is done
+    g_done.fetch_add(1, std::memory_order_acq_rel);
+  }
+}
+
+void pool_run(const RowJob& jb, int nth) {   // thread 0: post, take part, wait for the stragglers
+  if (jb.rows <= 0) return;
+  RowJob j = jb;
+  const int64_t want = std::max<int64_t>(1, std::min<int64_t>(((int64_t)256 << 10) / (int64_t)std::max<size_t>(jb.bytes, 1),
+                                                              jb.rows / (2 * (int64_t)nth)));
+  j.per_chunk = std::max<int64_t>(want, (jb.rows + 0xFFFFE) / 0xFFFFF);
+  const uint64_t n = (uint64_t)((jb.rows + j.per_chunk - 1) / j.per_chunk);
+  g_job = j;
+  g_done.store(0, std::memory_order_relaxed);
+  ++g_pool_seq;
+  g_ctl.store(((g_pool_seq & 0xFFFFFF) << 40) | (n << 20), std::memory_order_release);
+  pool_work();
+  while ((uint64_t)g_done.load(std::memory_order_acquire) < n) __builtin_ia32_pause();
+}
+
+// sleep: once this call's last job is posted and claimed, wait asleep (futex) for thread 0 instead
+// of spinning (LAMM_HIP_HELPERS=2, or 3: asleep here only, decode nodes as with 0)
+void pool_help(const void* dst, bool sleep) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (unsigned it = 0;; ++it) {
+    const uint32_t gen = g_node_gen.load(std::memory_order_acquire);
+    if (g_pool_dst.load(std::memory_order_acquire) == dst) {
+      if (g_pool_finished.load(std::memory_order_acquire)) return;
+      pool_work();
+      if (sleep && g_pool_last.load(std::memory_order_acquire) == dst) {
+        const timespec ts{0, 500000};
+        syscall(SYS_futex, reinterpret_cast<uint32_t*>(&g_node_gen), FUTEX_WAIT_PRIVATE, gen, &ts, nullptr, 0);
+      }
+    }
+    if ((it & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) return;
+    __builtin_ia32_pause();
+  }
+}
+
+// Whether a COMPUTE call is a pool node -- the same answer in every thread (shapes and knobs only).
+constexpr size_t kPoolMin = (size_t)1 << 20;
+bool pool_call(const ggml::compute_params* params, const ggml::tensor* dst) {
+  if (!knobs().pool || params->nth < 2) return false;
+  const ggml::tensor* src1 = dst->src[1];
+  const int64_t rows = src1->ne[1] * src1->ne[2] * src1->ne[3];
+  return rows > 8 && (size_t)dst->ne[0] * rows * sizeof(float) >= kPoolMin;
+}
+
+void mul_mat_thread0(const ggml::compute_params* params, ggml::tensor* dst, bool pool);
 
 }  // namespace
 
@@ -1037,13 +1129,27 @@ extern "C" void lamm_mul_mat(const struct ggml_compute_params* vparams, struct g
   const auto* params = reinterpret_cast<const ggml::compute_params*>(vparams);
   auto* dst = reinterpret_cast<ggml::tensor*>(vdst);
   if (params->type != ggml::TASK_COMPUTE) return;  // INIT claimed for the GPU quantizer: nothing to do
-  const int helpers = knobs().helpers;
+  const bool pool = pool_call(params, dst);
+  const int helpers = pool || knobs().helpers == 3 ? 0 : knobs().helpers;   // 3: asleep in pool nodes only
   if (params->ith != 0) {   // thread 0 owns the device work; ggml's barrier follows
-    if (helpers > 0 && params->nth > 1) helper_wait(dst, helpers);
+    if (pool) pool_help(dst, knobs().helpers >= 2);
+    else if (helpers > 0 && params->nth > 1) helper_wait(dst, helpers);
     return;
   }
   if (helpers > 0) g_node_done.store(nullptr, std::memory_order_release);
-  mul_mat_thread0(params, dst);
+  if (pool) {
+    g_pool_finished.store(0, std::memory_order_release);
+    g_pool_last.store(nullptr, std::memory_order_release);
+    g_pool_dst.store(dst, std::memory_order_release);
+  }
+  mul_mat_thread0(params, dst, pool);
+  if (pool) {
+    g_pool_finished.store(1, std::memory_order_release);
+    if (knobs().helpers >= 2) {
+      g_node_gen.fetch_add(1, std::memory_order_acq_rel);
+      syscall(SYS_futex, reinterpret_cast<uint32_t*>(&g_node_gen), FUTEX_WAKE_PRIVATE, INT32_MAX, nullptr, nullptr, 0);
+    }
+  }
   if (helpers > 0) {
     g_node_done.store(dst, std::memory_order_release);
     g_node_gen.fetch_add(1, std::memory_order_acq_rel);
@@ -1053,7 +1159,7 @@ extern "C" void lamm_mul_mat(const struct ggml_compute_params* vparams, struct g
 
 namespace {
 
-void mul_mat_thread0(const ggml::compute_params* params, ggml::tensor* dst) {
+void mul_mat_thread0(const ggml::compute_params* params, ggml::tensor* dst, bool pool) {
 
   const ggml::tensor* src0 = dst->src[0];
   const ggml::tensor* src1 = dst->src[1];
@@ -1081,7 +1187,10 @@ void mul_mat_thread0(const ggml::compute_params* params, ggml::tensor* dst) {
   // activation bytes as the kernels read them: F32 rows (kFused, kGpuQuant; packed [slice][N][K])
   // or vec_dot_type rows (wdata / a vec_dot-typed src1)
   const int64_t ldx = (ne00 + 3) & ~int64_t(3);                 // the quantizer reads rows as float4
-  const size_t x_row = act == kCpuInit ? b_row : (size_t)ldx * sizeof(float);
+  // prefill q8_0 / q8_1 activations quantized by ggml's pool threads (LAMM_HIP_POOL bit 1): the
+  // kernels then read vdt rows, as after ggml's own INIT
+  const bool hostq = pool && (knobs().pool & 1) && act == kGpuQuant && host_quant_supported(vdt);
+  const size_t x_row = act == kCpuInit || hostq ? b_row : (size_t)ldx * sizeof(float);
   const size_t x_bytes = x_row * (size_t)(N * nslices);
   const size_t c_bytes = (size_t)M * N * nslices * sizeof(float);
   // zero copy on several devices (LAMM_HIP_ZERO_COPY_SPLIT=1): every device reads the one pinned
@@ -1092,6 +1201,7 @@ void mul_mat_thread0(const ggml::compute_params* params, ggml::tensor* dst) {
   const bool zc_in = zc_split && zero_copy(x_bytes, true) && act != kGpuQuant && (G == 1 || rt.pinned_shared(0, x_bytes));
   const bool zc_out = zc_split && zero_copy(c_bytes, false) && (G == 1 || rt.pinned_shared(1, c_bytes));
   const unsigned char* x_host = nullptr;   // the bytes every device uploads (or reads in place)
+  const bool c_pool = pool && (knobs().pool & 2) && !zc_out && G == 1;   // C: pinned + the pool's scatter
   auto gather_f32 = [&](unsigned char* out) {   // F32 src1 rows (any strides) -> [slice][N][ldx]
     for (int64_t i13 = 0; i13 < ne13; ++i13)
       for (int64_t i12 = 0; i12 < ne12; ++i12)
@@ -1107,6 +1217,19 @@ void mul_mat_thread0(const ggml::compute_params* params, ggml::tensor* dst) {
     else
       for (int64_t r = 0; r < N * nslices; ++r)
         memcpy(h + r * b_row, static_cast<const unsigned char*>(src1->data) + r * src1->nb[1], b_row);
+    x_host = h;
+  } else if (hostq) {   // the pool quantizes the F32 rows -> pinned [slice][N] vdt rows
+    unsigned char* h = rt.pinned(2, x_bytes);
+    RowJob jb;
+    jb.src = static_cast<const unsigned char*>(src1->data);
+    jb.dst = h;
+    jb.qtype = vdt, jb.nblk = kb;
+    jb.bytes = (size_t)ne00 * sizeof(float);
+    jb.s1 = src1->nb[1], jb.s2 = src1->nb[2], jb.s3 = src1->nb[3];
+    jb.d1 = b_row, jb.d2 = b_row * (size_t)N, jb.d3 = b_row * (size_t)(N * ne12);
+    jb.n1 = N, jb.n2 = ne12, jb.rows = N * nslices;
+    if (!c_pool) g_pool_last.store(dst, std::memory_order_release);   // no C job follows
+    pool_run(jb, params->nth);
     x_host = h;
   } else if (act == kCpuInit && use_wdata) {
     x_host = static_cast<const unsigned char*>(params->wdata);
@@ -1148,6 +1271,11 @@ void mul_mat_thread0(const ggml::compute_params* params, ggml::tensor* dst) {
     void* dB;
     if (zc_in) {
       dB = rt.pinned_dev(0);
+    } else if (hostq) {   // the pool's q8 rows
+      dB = d.scratch(0, x_bytes + 64);
+      HIPCHK(hipMemcpyAsync(dB, x_host, x_bytes, hipMemcpyHostToDevice, s));
+      if (knobs().stats_sync) HIPCHK(hipStreamSynchronize(s));
+      stat.phase(2);
     } else if (act == kFused || act == kGpuQuant) {
       float* dX = static_cast<float*>(d.scratch(2, x_bytes + 64));
       const bool dense = ldx == ne00 && src1->nb[1] == (size_t)ne00 * sizeof(float) &&
@@ -1184,7 +1312,7 @@ void mul_mat_thread0(const ggml::compute_params* params, ggml::tensor* dst) {
       HIPCHK(hipMemcpy2DAsync(dB, b_row, src1->data, src1->nb[1], b_row, (size_t)(N * nslices), hipMemcpyHostToDevice,
                               s));
     }
-    const bool b_f32 = act == kFused || (act == kGpuQuant && !ref && (vdt == kQ8_0 || vdt == kQ8_1));
+    const bool b_f32 = act == kFused || (act == kGpuQuant && !hostq && !ref && (vdt == kQ8_0 || vdt == kQ8_1));
     const size_t b_pitch = b_f32 ? x_row : b_row;
     // C: zero-copy = this device's rows [r0, r0 + rows) of the pinned [slice][N][M] image; else a
     // dense [slice][N][rows] scratch copied into dst below
@@ -1222,7 +1350,9 @@ void mul_mat_thread0(const ggml::compute_params* params, ggml::tensor* dst) {
       std::abort();
     }
     stat.phase(3);
-    if (!zc_out) {   // this device's rows straight into dst
+    if (c_pool) {   // C down into pinned memory; the pool scatters it into dst below
+      HIPCHK(hipMemcpyAsync(rt.pinned(1, c_bytes), dC, c_bytes, hipMemcpyDeviceToHost, s));
+    } else if (!zc_out) {   // this device's rows straight into dst
       const bool dense = rows == M && dst->nb[1] == (size_t)M * sizeof(float) &&
                          dst->nb[2] == dst->nb[1] * (size_t)N && dst->nb[3] == dst->nb[2] * (size_t)ne12;
       if (dense) {
@@ -1245,7 +1375,17 @@ void mul_mat_thread0(const ggml::compute_params* params, ggml::tensor* dst) {
     wait_device(rt.devs[g]);
   }
   stat.phase(5);
-  if (zc_out) {
+  if (c_pool) {
+    RowJob jb;
+    jb.src = rt.pinned(1, c_bytes);
+    jb.dst = static_cast<unsigned char*>(dst->data);
+    jb.bytes = (size_t)M * sizeof(float);
+    jb.s1 = jb.bytes, jb.s2 = jb.bytes * (size_t)N, jb.s3 = jb.s2 * (size_t)ne12;
+    jb.d1 = dst->nb[1], jb.d2 = dst->nb[2], jb.d3 = dst->nb[3];
+    jb.n1 = N, jb.n2 = ne12, jb.rows = N * nslices;
+    g_pool_last.store(dst, std::memory_order_release);
+    pool_run(jb, params->nth);
+  } else if (zc_out) {
     const unsigned char* hC = rt.pinned(1, c_bytes);
     const size_t c_slice = (size_t)M * N * sizeof(float);
     for (int64_t i13 = 0; i13 < ne13; ++i13)

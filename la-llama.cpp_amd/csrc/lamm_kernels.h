@@ -107,4 +107,8 @@ bool gemm_dq_supported(int type);
 bool gemm_dq_args_ok(const GemvArgs& p);
 int gemm_dq_tiles(const GemvArgs& p);   // its workgroups (128 x 64 output tiles over all slices)
 
+// host side: ggml's AVX2 from_float for q8_0 / q8_1 activations (lamm_host_quant.cpp)
+bool host_quant_supported(int type);
+void host_quantize_row(int type, const float* x, void* y, int64_t nblk);
+
 }  // namespace lamm

@@ -49,7 +49,8 @@ Knobs* read_env() {
   k->opt_level = env_int("LAMM_OPT_LEVEL", 3);
   k->device = env_int("LAMM_HIP_DEVICE", -1);
   if (const char* e = getenv("LAMM_HIP_DEVICES")) strncpy(k->devices, e, sizeof k->devices - 1);
-  k->stats = env_on("LAMM_HIP_STATS");
+  k->stats = env_int("LAMM_HIP_STATS", 0) > 0;
+  k->stats_sync = env_int("LAMM_HIP_STATS", 0) == 2;
   if (const char* e = getenv("LAMM_HIP_CACHE_GB")) k->cache_gb = atof(e);
   k->pinned = !env_off("LAMM_HIP_PINNED");
   k->views = env_on("LAMM_HIP_VIEWS") ? 1 : env_off("LAMM_HIP_VIEWS") ? 0 : -1;
@@ -63,6 +64,7 @@ Knobs* read_env() {
   k->zero_copy_split = env_on("LAMM_HIP_ZERO_COPY_SPLIT");
   k->ref_mfma = env_int("LAMM_REF_MFMA", -1);
   k->helpers = env_int("LAMM_HIP_HELPERS", 0);
+  k->pool = env_int("LAMM_HIP_POOL", 1);
   if (const char* e = getenv("LAMM_HIP_ORDER")) k->ref_order = strcmp(e, "fast") != 0;
   return k;
 }

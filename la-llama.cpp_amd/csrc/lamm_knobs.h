@@ -30,7 +30,8 @@ struct Knobs {
   int opt_level = 3;           // LAMM_OPT_LEVEL=0: lamm_can_mul_mat always false
   int device = -1;             // LAMM_HIP_DEVICE: the boundary's device (-1: first gfx950)
   char devices[256] = {0};     // LAMM_HIP_DEVICES: "all" or "0,1,2,3" (empty: one device)
-  bool stats = false;          // LAMM_HIP_STATS=1
+  bool stats = false;          // LAMM_HIP_STATS=1 (=2: also synchronise after each upload, so "B up"
+  bool stats_sync = false;     // holds the transfer itself, not only its issue)
   double cache_gb = 64.0;      // LAMM_HIP_CACHE_GB
   bool pinned = true;          // LAMM_HIP_PINNED=0: no pinned staging (and no zero copy)
   int views = -1;              // LAMM_HIP_VIEWS: 0 never, 1 always, -1 prefill only
@@ -40,13 +41,17 @@ struct Knobs {
   bool spin = true;            // LAMM_HIP_SPIN=0: hipStreamSynchronize instead of the flag spin
   bool kernel_signal = false;  // LAMM_HIP_KERNEL_SIGNAL=1: the GEMV writes the completion flag
   int zero_copy = 3;           // LAMM_HIP_ZERO_COPY: 0 off, 1 in, 2 out, 3 both
-  bool zero_copy_split = false;
+  bool zero_copy_split = false;   // LAMM_HIP_ZERO_COPY_SPLIT=1: zero copy also when rows split over devices
   int helpers = 0;             // LAMM_HIP_HELPERS: ggml's other pool threads during thread 0's device work:
                                // 0 return at once (ggml's barrier spins on them), 1 wait here yielding,
                                // 2 wait here asleep (futex)
   int ref_mfma = -1;           // LAMM_REF_MFMA: reference-order prefill kernel (1: ref_mfma_kernel, 2 / 4: ref_mfma2 G)
   bool ref_order = true;       // LAMM_HIP_ORDER=fast: the boundary runs the fast engines instead of the
-                               // reference's float order (lamm_ref.hip) for the formats that have both  // LAMM_HIP_ZERO_COPY_SPLIT=1: zero copy also when rows split over devices
+                               // reference's float order (lamm_ref.hip) for the formats that have both
+  int pool = 1;                // LAMM_HIP_POOL: what ggml's pool threads do for prefill-sized calls (bits):
+                               // 1 quantize the F32 activations to q8_0 / q8_1 rows in pinned memory (the
+                               // upload moves those instead of F32), 2 scatter C out of pinned memory
+                               // (else HIP's pageable copy); 0: thread 0 alone, as before
 };
 
 // The current switches (read from the environment at the first call).

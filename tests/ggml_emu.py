@@ -11,9 +11,13 @@ mul_mat node:
             what an x86 AVX2 build of ggml runs.  liblamm_hip claims INIT when it
             quantizes src1 on the GPU (LAMM_HIP_GPU_QUANT, default on): every worker
             calls the hook, which returns at once, and wdata stays untouched;
-  COMPUTE : every worker ith in [0, nth) calls the hook (LC/ggml.c:10858-10863).
+  COMPUTE : every worker ith in [0, nth) calls the hook (LC/ggml.c:10858-10863) -- one after
+            the other by default, or (threaded=True) from nth concurrent threads, as ggml's
+            pool does (LC/ggml.c:18404-18421): what the boundary's pool-parallel staging of
+            prefill calls (LAMM_HIP_POOL_COPY) needs to be exercised.
 """
 import ctypes
+import threading
 
 import numpy as np
 
@@ -46,9 +50,15 @@ class Tensor:
         self.ne, self.nb = ne, nb
 
 
-def mul_mat_node(src0, src1):
-    """dst = ggml_mul_mat(src0, src1): dst F32 [ne01, ne11, ne12, ne13]."""
-    dst = Tensor(ol.F32, [src0.ne[1], src1.ne[1], src1.ne[2], src1.ne[3]])
+def mul_mat_node(src0, src1, row_pad=0):
+    """dst = ggml_mul_mat(src0, src1): dst F32 [ne01, ne11, ne12, ne13] (row_pad: dst rows of
+    ne01 + row_pad floats, i.e. a view into a wider buffer)."""
+    ne = [src0.ne[1], src1.ne[1], src1.ne[2], src1.ne[3]]
+    nb = None
+    if row_pad:
+        nb = [4, 4 * (ne[0] + row_pad)]
+        nb += [nb[1] * ne[1], nb[1] * ne[1] * ne[2]]
+    dst = Tensor(ol.F32, ne, nb=nb)
     dst.t.op = la.OP_MUL_MAT
     dst.t.src[0] = ctypes.pointer(src0.t)
     dst.t.src[1] = ctypes.pointer(src1.t)
@@ -56,7 +66,26 @@ def mul_mat_node(src0, src1):
     return dst
 
 
-def compute(dst, nth=4, oracle=None, flavour=ol.QUANT_AVX):
+def _run_workers(params, dst, nth, threaded):
+    if not threaded:
+        for ith in range(nth):
+            params.ith = ith
+            la.mul_mat(params, dst.t)
+        return
+    la.can_mul_mat(params, dst.t)   # the environment is synced here, not in the workers
+    ps = []
+    for ith in range(nth):
+        p = la.GgmlComputeParams()
+        p.type, p.ith, p.nth, p.wsize, p.wdata = params.type, ith, params.nth, params.wsize, params.wdata
+        ps.append(p)
+    ths = [threading.Thread(target=la.lib.lamm_mul_mat, args=(ctypes.byref(p), ctypes.byref(dst.t))) for p in ps]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+
+
+def compute(dst, nth=4, oracle=None, flavour=ol.QUANT_AVX, threaded=False):
     """Replay INIT + COMPUTE.  Returns True if the lamm hook took the node."""
     oracle = oracle or ol.Oracle()
     src0, src1 = dst._keep
@@ -72,9 +101,7 @@ def compute(dst, nth=4, oracle=None, flavour=ol.QUANT_AVX):
 
     params.type = la.TASK_INIT
     if la.can_mul_mat(params, dst.t):   # GPU quantizes src1 in COMPUTE
-        for ith in range(nth):
-            params.ith = ith
-            la.mul_mat(params, dst.t)
+        _run_workers(params, dst, nth, threaded)
         params.ith = 0
         wdata[:] = 0xA5                  # poison: COMPUTE must not read wdata
     elif src1.t.type != vt:  # thread 0 quantizes src1 -> wdata (contiguous F32 src1 assumed)
@@ -84,7 +111,5 @@ def compute(dst, nth=4, oracle=None, flavour=ol.QUANT_AVX):
     params.type = la.TASK_COMPUTE
     if not la.can_mul_mat(params, dst.t):
         return False
-    for ith in range(nth):
-        params.ith = ith
-        la.mul_mat(params, dst.t)
+    _run_workers(params, dst, nth, threaded)
     return True

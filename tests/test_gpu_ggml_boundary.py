@@ -355,3 +355,47 @@ def test_decode_calls_fresh_every_call(t, monkeypatch):
     first = results["fused"].view(np.uint32)
     for mode, r in results.items():
         np.testing.assert_array_equal(r.view(np.uint32), first, err_msg=mode)
+
+
+@pytest.mark.parametrize("threaded", [True, False], ids=["pool_threads", "sequential"])
+@pytest.mark.parametrize("case", ["gpu_quant_strided", "cpu_init", "slices_padded_dst"])
+def test_pool_jobs(case, threaded, monkeypatch):
+    """Prefill-sized calls put ggml's pool threads to work (LAMM_HIP_POOL; lamm_hip.cpp pool_run /
+    pool_help): bit 1 quantizes the F32 src1 rows to q8_0 on the host (lamm_hip_quantize_host),
+    bit 2 scatters C out of pinned memory.  Driven from nth concurrent worker threads as ggml's
+    pool drives the hook -- or one worker after the other, when thread 0 finds no helper and runs
+    every chunk itself -- every mode is bit-identical to thread 0 alone with HIP's pageable copies
+    and the device quantizer (LAMM_HIP_POOL=0) and within the oracle's tolerance; strided src1
+    rows and padded dst rows exercise the row offsets."""
+    t, K = ol.Q4_0, 512
+    M, N, ne2, ne3, k_pad, row_pad = 2048, 160, (1, 1), (1, 1), 0, 0
+    if case == "gpu_quant_strided":
+        k_pad = 40
+    elif case == "slices_padded_dst":
+        M, N, ne2, ne3, row_pad = 1536, 72, (1, 2), (1, 2), 24
+    monkeypatch.setenv("LAMM_HIP_GPU_QUANT", "0" if case == "cpu_init" else "-1")
+    rng = np.random.default_rng(41)
+    n1 = ne2[1] * ne3[1]
+    a = rng.standard_normal((M, K), dtype=np.float32)
+    A_q = ORACLE.quantize(t, a)
+    b = rng.standard_normal((n1 * N, K), dtype=np.float32)
+    bp = np.zeros((n1 * N, K + k_pad), np.float32)
+    bp[:, :K] = b
+    nb1 = 4 * (K + k_pad)
+    src0 = ggml_emu.Tensor(t, [K, M, ne2[0], ne3[0]], data=A_q)
+    src1 = ggml_emu.Tensor(ol.F32, [K, N, ne2[1], ne3[1]], data=bp,
+                           nb=[4, nb1, nb1 * N, nb1 * N * ne2[1]])
+    want = expected(t, A_q, b, M, N, K, ne2, ne3)
+    outs = []
+    for pool in ("1", "2", "3", "0"):
+        monkeypatch.setenv("LAMM_HIP_POOL", pool)
+        dst = ggml_emu.mul_mat_node(src0, src1, row_pad=row_pad)
+        assert ggml_emu.compute(dst, nth=6, threaded=threaded)
+        got = dst.buf.view(np.float32).reshape(ne3[1], ne2[1], N, M + row_pad)
+        if row_pad:
+            assert not got[..., M:].any()          # nothing written between the rows
+            got = got[..., :M]
+        assert rel_err(got, want, np.abs(want) + 1.0).max() < 1e-3
+        outs.append(got.copy())
+    for o in outs[:-1]:
+        np.testing.assert_array_equal(o, outs[-1])

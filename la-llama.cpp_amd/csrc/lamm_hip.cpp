@@ -1064,7 +1064,7 @@ void run_rows(const RowJob& jb, int64_t c) {
     unsigned char* y = jb.dst + j * jb.d1 + i2 * jb.d2 + i3 * jb.d3;
     const unsigned char* x = jb.src + j * jb.s1 + i2 * jb.s2 + i3 * jb.s3;
     if (jb.qtype >= 0) host_quantize_row(jb.qtype, reinterpret_cast<const float*>(x), y, jb.nblk);
-    else memcpy(y, x, jb.bytes);
+    else host_stream_copy(y, x, jb.bytes);
   }
 }
 

@@ -8,8 +8,12 @@
 //   the int32 -> int8 pack saturation; q8_1 also stores s = fp16(d * sum q).
 // Used by prefill calls whose activations ggml's pool threads quantize in parallel before the
 // upload (lamm_hip.cpp pool jobs): 2.2 MiB of q8_0 rows cross PCIe instead of 8 MiB of F32.
+// host_stream_copy: the pool's C scatter (LAMM_HIP_POOL bit 2) with non-temporal stores.
 // Built with -ffp-contract=off: x * id must round before the rounding step, as the AVX2 code's
 // separate multiply does.
+#include <immintrin.h>
+
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -72,9 +76,37 @@ __attribute__((target_clones("arch=x86-64-v3", "default"))) void quant_q8(const 
   }
 }
 
+// n bytes with non-temporal stores where the destination is 32-byte aligned (no read for ownership
+// of lines the copy overwrites whole; ggml's dst is cold in the host caches)
+__attribute__((target("avx2"))) void stream_copy_avx2(unsigned char* __restrict d, const unsigned char* __restrict s,
+                                                        size_t n) {
+  const size_t head = std::min(n, (size_t)((32 - ((uintptr_t)d & 31)) & 31));
+  memcpy(d, s, head);
+  d += head, s += head, n -= head;
+  size_t i = 0;
+  for (; i + 128 <= n; i += 128) {
+    const __m256i a = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + i));
+    const __m256i b = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + i + 32));
+    const __m256i c = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + i + 64));
+    const __m256i e = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + i + 96));
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(d + i), a);
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(d + i + 32), b);
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(d + i + 64), c);
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(d + i + 96), e);
+  }
+  memcpy(d + i, s + i, n - i);
+  _mm_sfence();
+}
+
 }  // namespace
 
 namespace lamm {
+
+void host_stream_copy(void* dst, const void* src, size_t n) {
+  static const bool avx2 = __builtin_cpu_supports("avx2");
+  if (avx2) stream_copy_avx2(static_cast<unsigned char*>(dst), static_cast<const unsigned char*>(src), n);
+  else memcpy(dst, src, n);
+}
 
 bool host_quant_supported(int type) { return type == kQ8_0 || type == kQ8_1; }
 

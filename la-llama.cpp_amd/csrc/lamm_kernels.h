@@ -110,5 +110,6 @@ int gemm_dq_tiles(const GemvArgs& p);   // its workgroups (128 x 64 output tiles
 // host side: ggml's AVX2 from_float for q8_0 / q8_1 activations (lamm_host_quant.cpp)
 bool host_quant_supported(int type);
 void host_quantize_row(int type, const float* x, void* y, int64_t nblk);
+void host_stream_copy(void* dst, const void* src, size_t n);   // non-temporal stores (AVX2 hosts)
 
 }  // namespace lamm

@@ -563,6 +563,7 @@ __global__ __launch_bounds__(FNT) void ref_f16_kernel(GemvArgs p) {
 //   bytes; the activation columns converted to f16 once per workgroup)
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef _Float16 half2v __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 constexpr int MR = 64, MC = 32, MKB = 8, MNT = 256;   // rows, columns, blocks per chunk, threads
 
 // four unsigned bytes q (0 .. 255) -> f16 (q - OFF) pairs: {lo dword: q0, q1; hi dword: q2, q3}
@@ -908,10 +909,16 @@ __global__ __launch_bounds__(MNT) void ref_mfma2_kernel(GemvArgs p) {
         for (int c = 0; c < 4; ++c) {
           float d = da * sdb[k][nb + 2 * c + h];
           asm("" : "+v"(d));
+          // lanes e, e + 1 of a column share d: one packed fp32 fma per pair (v_pk_fma_f32, each
+          // element one IEEE fma -- the same bits as two v_fma_f32)
+          const f32x2 d2 = {d, d};
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            acc[g][0][4 * c + e] = __builtin_fmaf(d, S0[4 * c + e], acc[g][0][4 * c + e]);
-            acc[g][1][4 * c + e] = __builtin_fmaf(d, S1[4 * c + e], acc[g][1][4 * c + e]);
+          for (int e = 0; e < 4; e += 2) {
+            const int i = 4 * c + e;
+            const f32x2 r0 = __builtin_elementwise_fma(d2, f32x2{S0[i], S0[i + 1]}, f32x2{acc[g][0][i], acc[g][0][i + 1]});
+            const f32x2 r1 = __builtin_elementwise_fma(d2, f32x2{S1[i], S1[i + 1]}, f32x2{acc[g][1][i], acc[g][1][i + 1]});
+            acc[g][0][i] = r0[0], acc[g][0][i + 1] = r0[1];
+            acc[g][1][i] = r1[0], acc[g][1][i + 1] = r1[1];
           }
           if constexpr (AFF) {
             float pm = ma * ssb[k][nb + 2 * c + h];

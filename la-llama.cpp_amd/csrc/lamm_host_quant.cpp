@@ -36,6 +36,7 @@ typedef int8_t c8 __attribute__((ext_vector_type(8)));
 __attribute__((target_clones("arch=x86-64-v3", "default"))) void quant_q8(const float* __restrict x, unsigned char* __restrict y,
                                                                  int64_t nb, bool sum) {
   const int OFF = sum ? 4 : 2, BPB = sum ? 36 : 34;
+#pragma clang loop unroll_count(4)
   for (int64_t i = 0; i < nb; ++i, x += 32, y += BPB) {
     f8 v[4], a[4];
     for (int k = 0; k < 4; ++k) {
@@ -51,25 +52,28 @@ __attribute__((target_clones("arch=x86-64-v3", "default"))) void quant_q8(const 
     const float d = amax / 127.f;
     const float id = amax != 0.0f ? 127.f / amax : 0.0f;
     int8_t q[32];
+    int s = 0;
     if (finite) {   // |x id| <= 127 + 1 ulp: no saturation
+      i8 rs = 0;
       for (int k = 0; k < 4; ++k) {
         const f8 t = v[k] * id + 12582912.f;   // two roundings (-ffp-contract=off): the product, then the integer
         const i8 r = (__builtin_bit_cast(i8, t) & 0x007fffff) - 0x00400000;
+        rs += r;
         const c8 c = __builtin_convertvector(r, c8);
         memcpy(q + 8 * k, &c, 8);
       }
+      if (sum) s = __builtin_reduce_add(rs);
     } else {   // cvtps_epi32 gives INT_MIN for NaN; packs saturate
       for (int j = 0; j < 32; ++j) {
         const float r = std::nearbyint(x[j] * id);
         q[j] = r != r ? (int8_t)-128 : (int8_t)(r > 127.f ? 127 : r < -128.f ? -128 : (int)r);
+        s += q[j];
       }
     }
     const uint16_t dh = to_f16(d);
     memcpy(y, &dh, 2);
     memcpy(y + OFF, q, 32);
     if (sum) {
-      int s = 0;
-      for (int j = 0; j < 32; ++j) s += q[j];
       const uint16_t sh = to_f16(d * (float)s);
       memcpy(y + 2, &sh, 2);
     }

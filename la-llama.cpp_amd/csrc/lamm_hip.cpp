@@ -12,6 +12,7 @@
 #include <sys/syscall.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <climits>
@@ -550,12 +551,21 @@ uint64_t fingerprint(const unsigned char* p, size_t pitch, size_t row_bytes, int
 // LAMM_HIP_STATS=1: per-category count and wall time of lamm_mul_mat (thread 0, entry to
 // return: transfers, kernels, synchronisation), printed to stderr at exit -- how much of a
 // llama.cpp token the boundary accounts for.
+// Also the medians of a call's wall time and of the gap since thread 0 left the previous call
+// (ggml's barriers and CPU ops in between; gaps over 5 ms -- between passes -- left out).
 struct CallStats {
   const char* name;
   uint64_t calls = 0;
   double us = 0;
   double phase_us[7] = {0, 0, 0, 0, 0, 0, 0};
+  std::vector<float> call_us, gap_us;
 };
+std::chrono::steady_clock::time_point g_last_return{};
+double median(std::vector<float> v) {
+  if (v.empty()) return 0.0;
+  std::nth_element(v.begin(), v.begin() + v.size() / 2, v.end());
+  return v[v.size() / 2];
+}
 constexpr int kPhases = 7;
 const char* kPhase[kPhases] = {"host staging", "src0", "B up", "launch", "C down", "device sync", "C to dst"};
 CallStats g_stats[4] = {{"weights N<=8"}, {"weights N>8"}, {"views N<=8"}, {"views N>8"}};
@@ -567,13 +577,18 @@ void print_stats() {
       fprintf(stderr, "lamm_hip stats: %-13s %8llu calls %12.1f us total %8.2f us/call  (", c.name,
               (unsigned long long)c.calls, c.us, c.us / (double)c.calls);
       for (int k = 0; k < kPhases; ++k) fprintf(stderr, "%s%s %.2f", k ? ", " : "", kPhase[k], c.phase_us[k] / c.calls);
-      fprintf(stderr, ")\n");
+      fprintf(stderr, ")  median call %.2f us, median gap before it %.2f us\n", median(c.call_us), median(c.gap_us));
     }
 }
 struct StatScope {
   CallStats* c;
   std::chrono::steady_clock::time_point t0, tp;
-  explicit StatScope(CallStats* cs) : c(cs), t0(std::chrono::steady_clock::now()), tp(t0) {}
+  explicit StatScope(CallStats* cs) : c(cs), t0(std::chrono::steady_clock::now()), tp(t0) {
+    if (c && g_last_return.time_since_epoch().count()) {
+      const double gap = std::chrono::duration<double, std::micro>(t0 - g_last_return).count();
+      if (gap < 5000.0) c->gap_us.push_back((float)gap);
+    }
+  }
   void phase(int k) {   // time since the previous mark -> phase k
     if (!c) return;
     const auto now = std::chrono::steady_clock::now();
@@ -582,8 +597,11 @@ struct StatScope {
   }
   ~StatScope() {
     if (c) {
+      g_last_return = std::chrono::steady_clock::now();
+      const double us = std::chrono::duration<double, std::micro>(g_last_return - t0).count();
       c->calls++;
-      c->us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+      c->us += us;
+      c->call_us.push_back((float)us);
     }
   }
 };
@@ -597,6 +615,7 @@ struct StatScope {
 struct Dev {
   int id = 0;
   hipStream_t stream = nullptr;
+  hipStream_t stream2 = nullptr;  // the pipelined prefill's second column chunk (LAMM_HIP_POOL bit 4)
   unsigned* flag = nullptr;       // pinned, host-coherent completion word (lamm_signal.hip)
   unsigned* flag_dev = nullptr;   // its device address
   unsigned seq = 0;
@@ -727,6 +746,7 @@ class Runtime {
       devs[i].id = ids[i];
       HIPCHK(hipSetDevice(ids[i]));
       HIPCHK(hipStreamCreateWithFlags(&devs[i].stream, hipStreamNonBlocking));
+      HIPCHK(hipStreamCreateWithFlags(&devs[i].stream2, hipStreamNonBlocking));
       HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&devs[i].flag), 64, hipHostMallocCoherent | hipHostMallocMapped));
       HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&devs[i].flag_dev), devs[i].flag, 0));
       *(volatile unsigned*)devs[i].flag = 0;
@@ -833,6 +853,8 @@ class Runtime {
       (void)hipHostFree(d.flag);
       if (d.done_ctr) (void)hipFree(d.done_ctr);
       (void)hipStreamDestroy(d.stream);
+      (void)hipStreamSynchronize(d.stream2);
+      (void)hipStreamDestroy(d.stream2);
     }
     devs.clear();
   }
@@ -1201,6 +1223,12 @@ void mul_mat_thread0(const ggml::compute_params* params, ggml::tensor* dst, bool
   const bool zc_in = zc_split && zero_copy(x_bytes, true) && act != kGpuQuant && (G == 1 || rt.pinned_shared(0, x_bytes));
   const bool zc_out = zc_split && zero_copy(c_bytes, false) && (G == 1 || rt.pinned_shared(1, c_bytes));
   const unsigned char* x_host = nullptr;   // the bytes every device uploads (or reads in place)
+  // LAMM_HIP_POOL bit 4: a reference-order prefill call on one device runs as two column chunks on
+  // two streams -- the pool quantizes chunk 2 while chunk 1 uploads and multiplies, and chunk 1's C
+  // comes down while chunk 2 multiplies (the reference-order kernels compute every output in the
+  // same order whatever the chunking: the same bits)
+  const bool pipe = hostq && ref && weight && G == 1 && nslices == 1 && !zc_out && (knobs().pool & 4) &&
+                    !(knobs().pool & 2) && N >= 64 && dst->nb[1] == (size_t)M * sizeof(float);
   const bool c_pool = pool && (knobs().pool & 2) && !zc_out && G == 1;   // C: pinned + the pool's scatter
   auto gather_f32 = [&](unsigned char* out) {   // F32 src1 rows (any strides) -> [slice][N][ldx]
     for (int64_t i13 = 0; i13 < ne13; ++i13)
@@ -1218,6 +1246,51 @@ void mul_mat_thread0(const ggml::compute_params* params, ggml::tensor* dst, bool
       for (int64_t r = 0; r < N * nslices; ++r)
         memcpy(h + r * b_row, static_cast<const unsigned char*>(src1->data) + r * src1->nb[1], b_row);
     x_host = h;
+  } else if (pipe) {
+    Dev& d = rt.devs[0];
+    HIPCHK(hipSetDevice(d.id));
+    WeightEntry& w = rt.weights(d, WeightKey{src0->data, t0, M, kb, src0->nb[1], src0->nb[2], src0->nb[3]}, a_row, src0,
+                                0, M, fp);
+    stat.phase(1);
+    unsigned char* h = rt.pinned(2, x_bytes);
+    unsigned char* dB = static_cast<unsigned char*>(d.scratch(0, x_bytes + 64));
+    float* dC = static_cast<float*>(d.scratch(1, c_bytes + 64));
+    const int64_t per = ((N + 1) / 2 + 31) / 32 * 32;   // column chunks, whole 32-column tiles
+    const hipStream_t ss[2] = {d.stream, d.stream2};
+    const lamm_matrix A{w.dev, t0, (int)M, (int)kb, w.dev_pitch / (int64_t)block_bytes(t0)};
+    for (int c = 0; c < 2; ++c) {
+      const int64_t n0 = c * per, nc = std::min<int64_t>(per, N - n0);
+      if (nc <= 0) break;
+      RowJob jb;
+      jb.src = static_cast<const unsigned char*>(src1->data) + n0 * src1->nb[1];
+      jb.dst = h + n0 * b_row;
+      jb.qtype = vdt, jb.nblk = kb;
+      jb.bytes = (size_t)ne00 * sizeof(float);
+      jb.s1 = src1->nb[1], jb.d1 = b_row;
+      jb.n1 = nc, jb.rows = nc;
+      if (n0 + nc >= N) g_pool_last.store(dst, std::memory_order_release);
+      pool_run(jb, params->nth);
+      HIPCHK(hipMemcpyAsync(dB + n0 * b_row, jb.dst, (size_t)nc * b_row, hipMemcpyHostToDevice, ss[c]));
+      const lamm_matrix B{dB + n0 * b_row, vdt, (int)kb, (int)nc, (int64_t)kb};
+      const lamm_matrix C{dC + n0 * M, kF32, (int)M, (int)nc, M};
+      const int rc = lamm_hip_matmul_ex(&A, &B, &C, nullptr, LAMM_ORDER_REFERENCE, ss[c]);
+      if (rc != LAMM_OK) {
+        fprintf(stderr, "lamm_hip: lamm_hip_matmul_ex failed (%d): %s\n", rc, g_err.c_str());
+        std::abort();
+      }
+    }
+    stat.phase(3);
+    for (int c = 0; c < 2; ++c) {
+      const int64_t n0 = c * per, nc = std::min<int64_t>(per, N - n0);
+      if (nc <= 0) break;
+      HIPCHK(hipMemcpyAsync(static_cast<unsigned char*>(dst->data) + n0 * dst->nb[1], dC + n0 * M,
+                            (size_t)nc * M * sizeof(float), hipMemcpyDeviceToHost, ss[c]));
+    }
+    stat.phase(4);
+    HIPCHK(hipStreamSynchronize(d.stream2));
+    wait_device(d);
+    stat.phase(5);
+    return;
   } else if (hostq) {   // the pool quantizes the F32 rows -> pinned [slice][N] vdt rows
     unsigned char* h = rt.pinned(2, x_bytes);
     RowJob jb;

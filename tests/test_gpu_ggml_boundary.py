@@ -364,7 +364,8 @@ def test_pool_jobs(case, threaded, monkeypatch):
     pool_help): bit 1 quantizes the F32 src1 rows to q8_0 on the host (lamm_hip_quantize_host),
     bit 2 scatters C out of pinned memory.  Driven from nth concurrent worker threads as ggml's
     pool drives the hook -- or one worker after the other, when thread 0 finds no helper and runs
-    every chunk itself -- every mode is bit-identical to thread 0 alone with HIP's pageable copies
+    every chunk itself -- every mode (5: bit 1 plus bit 4, the reference-order call as two
+    pipelined column chunks on two streams) is bit-identical to thread 0 alone with HIP's pageable copies
     and the device quantizer (LAMM_HIP_POOL=0) and within the oracle's tolerance; strided src1
     rows and padded dst rows exercise the row offsets."""
     t, K = ol.Q4_0, 512
@@ -387,7 +388,7 @@ def test_pool_jobs(case, threaded, monkeypatch):
                            nb=[4, nb1, nb1 * N, nb1 * N * ne2[1]])
     want = expected(t, A_q, b, M, N, K, ne2, ne3)
     outs = []
-    for pool in ("1", "2", "3", "0"):
+    for pool in ("1", "2", "3", "5", "0"):
         monkeypatch.setenv("LAMM_HIP_POOL", pool)
         dst = ggml_emu.mul_mat_node(src0, src1, row_pad=row_pad)
         assert ggml_emu.compute(dst, nth=6, threaded=threaded)

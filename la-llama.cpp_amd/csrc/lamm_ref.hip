@@ -752,7 +752,13 @@ __global__ __launch_bounds__(MNT) void ref_mfma_kernel(GemvArgs p) {
 //     read a shared zero quad;
 //   * G groups of 8 columns per wave (G = 4: 64 columns per workgroup, the weight operand built
 //     once per block for 4 groups).
-template <int T, int G, bool ONE_SLICE>
+//   * SW (LAMM_REF_MFMA=5): the per-chunk image stores without bank conflicts -- a thread's
+//     (column, block) item puts columns 2 apart in each 16-lane group, and a block's 16 slots
+//     are XOR-swizzled by 4 k dwords, so the 8 blocks of a column land in distinct banks (the
+//     unswizzled stores hit 2 of the 64 banks' 16-dword groups: half the LDS cycles were
+//     conflicts, profiles/r04/ref_order/kernels/); the reads stay conflict-free (the swizzle
+//     only permutes a wave's 16-byte slots within each column).
+template <int T, int G, bool ONE_SLICE, bool SW = false>
 __global__ __launch_bounds__(MNT) void ref_mfma2_kernel(GemvArgs p) {
   using F = RefFmt<T>;
   static_assert(F::UE == 32, "32-element block formats");
@@ -797,6 +803,20 @@ __global__ __launch_bounds__(MNT) void ref_mfma2_kernel(GemvArgs p) {
   const auto rb = make_rsrc(Bz + (int64_t)n0 * p.ldb, (uint32_t)((bbytes + 3) & ~int64_t(3)));
   const int ml = 32 * wm + lr;
 
+  static_assert(!SW || (MKB == 8 && MC2 % 4 == 0), "the swizzled item order");
+  // item -> (column c, block k of the chunk)
+  auto item_ck = [](int item, int& c, int& k) __attribute__((always_inline)) {
+    if constexpr (SW) {
+      const int u = item >> 3;
+      k = item & 7;
+      c = (u & ~3) | ((u & 1) << 1) | ((u >> 1) & 1);   // lanes' columns 2 apart per 16-lane group
+    } else {
+      c = item / MKB;
+      k = item % MKB;
+    }
+  };
+  // dword of slot L (0 .. 63) of block k in a column's image
+  auto slot = [](int k, int L) __attribute__((always_inline)) { return k * 64 + (SW ? (L ^ (4 * k)) : L); };
   u32x4 pa[NA];
   uint32_t pb[NB][10];
   auto fetch = [&](int u0) {
@@ -809,7 +829,9 @@ __global__ __launch_bounds__(MNT) void ref_mfma2_kernel(GemvArgs p) {
     }
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
-      const int item = t + j * MNT, c = item / MKB, k = item % MKB;
+      const int item = t + j * MNT;
+      int c, k;
+      item_ck(item, c, k);
       const bool ok = item < NITEM && c < ncols && u0 + k < nunits;
       const uint32_t off = (uint32_t)((int64_t)c * p.ldb + (int64_t)(u0 + k) * F::VB);
       const uint32_t base = ok ? (off & ~3u) : 0x7ffffff0u;
@@ -828,7 +850,9 @@ __global__ __launch_bounds__(MNT) void ref_mfma2_kernel(GemvArgs p) {
     }
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
-      const int item = t + j * MNT, c = item / MKB, k = item % MKB;
+      const int item = t + j * MNT;
+      int c, k;
+      item_ck(item, c, k);
       if (item >= NITEM) break;
       const bool ok = c < ncols && u0 + k < nunits;
       const int sh = (int)((uint32_t)((int64_t)c * p.ldb + (int64_t)(u0 + k) * F::VB) & 3u) * 8;
@@ -842,7 +866,7 @@ __global__ __launch_bounds__(MNT) void ref_mfma2_kernel(GemvArgs p) {
         q4_to_f16<128>(qd ^ 0x80808080u, lo, hi);
         if (!ok) lo = hi = 0u;
         const u32x4 v = (q & 1) ? u32x4{0u, 0u, lo, hi} : u32x4{lo, hi, 0u, 0u};
-        *reinterpret_cast<u32x4*>(&sbp[c * NPC + ((k * 2 + (q >> 2)) * 2 + ((q & 3) >> 1)) * 16 + (q & 3) * 4]) = v;
+        *reinterpret_cast<u32x4*>(&sbp[c * NPC + slot(k, ((q >> 2) * 2 + ((q & 3) >> 1)) * 16 + (q & 3) * 4)]) = v;
       }
       sdb[k][c] = ok ? h2f(m[0] & 0xffffu) : 0.f;
       if constexpr (AFF) ssb[k][c] = ok ? h2f(m[0] >> 16) : 0.f;
@@ -864,10 +888,12 @@ __global__ __launch_bounds__(MNT) void ref_mfma2_kernel(GemvArgs p) {
   // group, K = 8h .. 8h + 7 of the half -- nonzero only when the slot's quad lies there
   const int lq = lr & 3;
   const uint32_t* arow = &sa[ml * SEGW];
-  const uint32_t* bl = &sbp[(8 * G * wn + (lr >> 2)) * NPC + h * 16 + lq * 4];   // + g, block, half offsets
+  const uint32_t* blc = &sbp[(8 * G * wn + (lr >> 2)) * NPC];   // + g, block, slot offsets
+  const int lb = h * 16 + lq * 4;                                  // this lane's slot in half 0
   for (int z = t; z < MC2 * MKB * 16; z += MNT) {   // the slots of the other k-group: zero for good
     const int c = z / (MKB * 16), rest = z % (MKB * 16), kh = rest >> 2, s = rest & 3;   // kh = (block, half, h)
-    if ((s >> 1) != (kh & 1)) *reinterpret_cast<u32x4*>(&sbp[c * NPC + kh * 16 + s * 4]) = u32x4{0u, 0u, 0u, 0u};
+    if ((s >> 1) != (kh & 1))
+      *reinterpret_cast<u32x4*>(&sbp[c * NPC + slot(kh >> 2, (kh & 3) * 16 + s * 4)]) = u32x4{0u, 0u, 0u, 0u};
   }
   fetch(0);
   for (int u0 = 0; u0 < nunits; u0 += MKB) {
@@ -900,8 +926,10 @@ __global__ __launch_bounds__(MNT) void ref_mfma2_kernel(GemvArgs p) {
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         const int nb = 8 * G * wn + 8 * g;
-        const u32x4 a0 = *reinterpret_cast<const u32x4*>(&bl[g * 8 * NPC + k * 64]);
-        const u32x4 a1 = *reinterpret_cast<const u32x4*>(&bl[g * 8 * NPC + k * 64 + 32]);
+        // half 1's slot is half 0's + 32: the swizzle (4 k < 32) leaves bit 5 alone
+        const uint32_t* bk = &blc[g * 8 * NPC + slot(k, lb)];
+        const u32x4 a0 = *reinterpret_cast<const u32x4*>(bk);
+        const u32x4 a1 = *reinterpret_cast<const u32x4*>(bk + 32);
         const f32x16 zero = {};
         const f32x16 S0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, a0), W0, zero, 0, 0, 0);
         const f32x16 S1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, a1), W1, zero, 0, 0, 0);
@@ -1197,7 +1225,7 @@ hipError_t launch_ref(int type, const GemvArgs& p, hipStream_t s) {
     // ref_mfma2_kernel, 2 column groups per wave (LAMM_REF_MFMA=4: 4 groups, one wave per SIMD; =1:
     // the unpipelined ref_mfma_kernel)
     const int sel = knobs().ref_mfma > 0 ? knobs().ref_mfma : 2;
-    const int mc = sel == 4 ? 64 : sel == 3 ? 16 : 32;
+    const int mc = sel == 4 ? 64 : sel == 3 ? 16 : 32;   // 5: the 2-group kernel, swizzled image
     const dim3 gm((unsigned)((p.M + MR - 1) / MR), (unsigned)((p.N + mc - 1) / mc), (unsigned)slices);
     auto gom = [&](auto tc) {
       constexpr int T = decltype(tc)::value;
@@ -1210,6 +1238,9 @@ hipError_t launch_ref(int type, const GemvArgs& p, hipStream_t s) {
       } else if (sel == 3) {   // one column group per wave (occupancy over reuse)
         if (slices == 1) hipLaunchKernelGGL((ref_mfma2_kernel<T, 1, true>), gm, dim3(MNT), 0, s, p);
         else hipLaunchKernelGGL((ref_mfma2_kernel<T, 1, false>), gm, dim3(MNT), 0, s, p);
+      } else if (sel == 5) {
+        if (slices == 1) hipLaunchKernelGGL((ref_mfma2_kernel<T, 2, true, true>), gm, dim3(MNT), 0, s, p);
+        else hipLaunchKernelGGL((ref_mfma2_kernel<T, 2, false, true>), gm, dim3(MNT), 0, s, p);
       } else {
         if (slices == 1) hipLaunchKernelGGL((ref_mfma2_kernel<T, 2, true>), gm, dim3(MNT), 0, s, p);
         else hipLaunchKernelGGL((ref_mfma2_kernel<T, 2, false>), gm, dim3(MNT), 0, s, p);

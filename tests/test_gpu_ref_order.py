@@ -223,3 +223,21 @@ def test_reference_order_rejects_other_types():
         C = torch.zeros(N * M, dtype=torch.float32, device="cuda")
         with pytest.raises(la.LammError):
             la.mul_mat_torch(t, A, B, C, M, N, K, flags=la.ORDER_REFERENCE)
+
+
+PREFILL_KERNELS = ["1", "2", "3", "4", "5"]   # LAMM_REF_MFMA: ref_mfma / ref_mfma2 G=2 / G=1 / G=4 / G=2 swizzled
+
+
+@pytest.mark.parametrize("variant", PREFILL_KERNELS)
+@pytest.mark.parametrize("t", [ol.Q4_0, ol.Q4_1, ol.Q5_0, ol.Q5_1], ids=["q4_0", "q4_1", "q5_0", "q5_1"])
+@pytest.mark.parametrize("shape", [(70, 40, 512), (128, 96, 1056), (64, 9, 256)], ids=["70x40x512", "128x96x1056", "64x9x256"])
+def test_reference_order_prefill_kernels_bit_exact(variant, t, shape, monkeypatch):
+    """Every reference-order prefill kernel (lamm_ref.hip; LAMM_REF_MFMA selects it) computes the
+    reference's lane order bit for bit: ragged row / column tiles, K not a multiple of the 8-block
+    chunk, and the swizzled activation image (=5)."""
+    monkeypatch.setenv("LAMM_REF_MFMA", variant)
+    M, N, K = shape
+    A_q, B_q = random_blocks(t, M, N, K, seed=M * 3 + N * 17 + K + int(variant))
+    c = ref_mul_mat(t, A_q, B_q, M, N, K)[:N * M].reshape(N, M)
+    want = ORACLE.mul_mat_avx(t, M, N, K, A_q, B_q)
+    assert np.array_equal(bits(c), bits(want)), f"{(c != want).sum()} of {c.size} differ"

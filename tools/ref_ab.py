@@ -69,7 +69,7 @@ for fmt, M, K in (("q4_0", 4096, 4096), ("q4_0", 11008, 4096), ("q4_0", 4096, 11
     B = torch.zeros(N * la.row_bytes(vt, K) + 64, dtype=torch.uint8, device="cuda")
     la.quantize_torch(vt, x, B, flavour=1)
     C = torch.zeros(N * M, dtype=torch.float32, device="cuda")
-    for v in (("1", "2", "3", "4") if fmt != "q6_k" else ("2",)):
+    for v in (("1", "2", "3", "4", "5") if fmt != "q6_k" else ("2",)):
         os.environ["LAMM_REF_MFMA"] = v
         out[f"gemm_{fmt}_{M}x{N}x{K}_ref_mfma{v}"] = events_us(
             lambda: la.mul_mat_torch(t, A, B, C, M, N, K, flags=la.ORDER_REFERENCE))

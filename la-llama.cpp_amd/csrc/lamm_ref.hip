@@ -804,6 +804,7 @@ __global__ __launch_bounds__(MNT) void ref_mfma2_kernel(GemvArgs p) {
   const int ml = 32 * wm + lr;
 
   static_assert(!SW || (MKB == 8 && MC2 % 4 == 0), "the swizzled item order");
+  constexpr bool PK = T == kQ4_0 || T == kQ5_1;   // packed chain steps where they cost no occupancy
   // item -> (column c, block k of the chunk)
   auto item_ck = [](int item, int& c, int& k) __attribute__((always_inline)) {
     if constexpr (SW) {
@@ -890,6 +891,7 @@ __global__ __launch_bounds__(MNT) void ref_mfma2_kernel(GemvArgs p) {
   const uint32_t* arow = &sa[ml * SEGW];
   const uint32_t* blc = &sbp[(8 * G * wn + (lr >> 2)) * NPC];   // + g, block, slot offsets
   const int lb = h * 16 + lq * 4;                                  // this lane's slot in half 0
+  const uint32_t* bl = blc + lb;                                   // (unswizzled: + g, block offsets)
   for (int z = t; z < MC2 * MKB * 16; z += MNT) {   // the slots of the other k-group: zero for good
     const int c = z / (MKB * 16), rest = z % (MKB * 16), kh = rest >> 2, s = rest & 3;   // kh = (block, half, h)
     if ((s >> 1) != (kh & 1))
@@ -902,6 +904,10 @@ __global__ __launch_bounds__(MNT) void ref_mfma2_kernel(GemvArgs p) {
     commit(u0);
     __syncthreads();
     if (u0 + MKB < nunits) fetch(u0 + MKB);   // the next chunk's bytes fly under this one's math
+    // swizzled: this lane's slot per block, recomputed every chunk (one v_xor per block) rather than
+    // eight hoisted addresses held across the loop (VGPRs past 256: occupancy 1)
+    int lbs = lb;
+    if constexpr (SW) asm volatile("" : "+v"(lbs));
     auto block = [&](int k) {
       const int ub = k * F::BPB;
       const float da = h2f(lds32(arow, ub) & 0xffffu);
@@ -927,7 +933,7 @@ __global__ __launch_bounds__(MNT) void ref_mfma2_kernel(GemvArgs p) {
       for (int g = 0; g < G; ++g) {
         const int nb = 8 * G * wn + 8 * g;
         // half 1's slot is half 0's + 32: the swizzle (4 k < 32) leaves bit 5 alone
-        const uint32_t* bk = &blc[g * 8 * NPC + slot(k, lb)];
+        const uint32_t* bk = SW ? &blc[g * 8 * NPC + k * 64 + (lbs ^ (4 * k))] : &bl[g * 8 * NPC + k * 64];
         const u32x4 a0 = *reinterpret_cast<const u32x4*>(bk);
         const u32x4 a1 = *reinterpret_cast<const u32x4*>(bk + 32);
         const f32x16 zero = {};
@@ -938,15 +944,24 @@ __global__ __launch_bounds__(MNT) void ref_mfma2_kernel(GemvArgs p) {
           float d = da * sdb[k][nb + 2 * c + h];
           asm("" : "+v"(d));
           // lanes e, e + 1 of a column share d: one packed fp32 fma per pair (v_pk_fma_f32, each
-          // element one IEEE fma -- the same bits as two v_fma_f32)
-          const f32x2 d2 = {d, d};
+          // element one IEEE fma -- the same bits as two v_fma_f32).  q4_1 / q5_0: single fmas
+          // (the packed form's register pairs push those kernels past 256 VGPRs: one wave per SIMD)
+          if constexpr (PK) {
+            const f32x2 d2 = {d, d};
 #pragma unroll
-          for (int e = 0; e < 4; e += 2) {
-            const int i = 4 * c + e;
-            const f32x2 r0 = __builtin_elementwise_fma(d2, f32x2{S0[i], S0[i + 1]}, f32x2{acc[g][0][i], acc[g][0][i + 1]});
-            const f32x2 r1 = __builtin_elementwise_fma(d2, f32x2{S1[i], S1[i + 1]}, f32x2{acc[g][1][i], acc[g][1][i + 1]});
-            acc[g][0][i] = r0[0], acc[g][0][i + 1] = r0[1];
-            acc[g][1][i] = r1[0], acc[g][1][i + 1] = r1[1];
+            for (int e = 0; e < 4; e += 2) {
+              const int i = 4 * c + e;
+              const f32x2 r0 = __builtin_elementwise_fma(d2, f32x2{S0[i], S0[i + 1]}, f32x2{acc[g][0][i], acc[g][0][i + 1]});
+              const f32x2 r1 = __builtin_elementwise_fma(d2, f32x2{S1[i], S1[i + 1]}, f32x2{acc[g][1][i], acc[g][1][i + 1]});
+              acc[g][0][i] = r0[0], acc[g][0][i + 1] = r0[1];
+              acc[g][1][i] = r1[0], acc[g][1][i + 1] = r1[1];
+            }
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              acc[g][0][4 * c + e] = __builtin_fmaf(d, S0[4 * c + e], acc[g][0][4 * c + e]);
+              acc[g][1][4 * c + e] = __builtin_fmaf(d, S1[4 * c + e], acc[g][1][4 * c + e]);
+            }
           }
           if constexpr (AFF) {
             float pm = ma * ssb[k][nb + 2 * c + h];

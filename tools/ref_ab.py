@@ -52,7 +52,8 @@ la.lib.lamm_hip_profile_next.argtypes = [__import__("ctypes").c_void_p] * 2
 gen = torch.Generator(device="cuda")
 gen.manual_seed(7)
 out = {"lib": os.environ.get("LAMM_HIP_LIB", "default")}
-for fmt, M, K in (("q4_0", 4096, 4096), ("q4_0", 11008, 4096), ("q4_0", 4096, 11008), ("q6_k", 32000, 4096)):
+for fmt, M, K in (("q4_0", 4096, 4096), ("q4_0", 11008, 4096), ("q4_0", 4096, 11008), ("q4_1", 4096, 4096),
+                  ("q5_0", 4096, 4096), ("q5_1", 4096, 4096), ("q6_k", 32000, 4096)):
     t = la.BY_NAME[fmt]
     vt = la.vec_dot_type(t)
     A, _ = bench.make_weights(torch, la, fmt, 1, M, K, gen)

@@ -1223,7 +1223,7 @@ void mul_mat_thread0(const ggml::compute_params* params, ggml::tensor* dst, bool
   const bool zc_in = zc_split && zero_copy(x_bytes, true) && act != kGpuQuant && (G == 1 || rt.pinned_shared(0, x_bytes));
   const bool zc_out = zc_split && zero_copy(c_bytes, false) && (G == 1 || rt.pinned_shared(1, c_bytes));
   const unsigned char* x_host = nullptr;   // the bytes every device uploads (or reads in place)
-  // LAMM_HIP_POOL bit 4: a reference-order prefill call on one device runs as two column chunks on
+  // LAMM_HIP_POOL bit 4 (default on): a reference-order prefill call on one device runs as two column chunks on
   // two streams -- the pool quantizes chunk 2 while chunk 1 uploads and multiplies, and chunk 1's C
   // comes down while chunk 2 multiplies (the reference-order kernels compute every output in the
   // same order whatever the chunking: the same bits)

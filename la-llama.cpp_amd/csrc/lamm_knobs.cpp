@@ -64,7 +64,7 @@ Knobs* read_env() {
   k->zero_copy_split = env_on("LAMM_HIP_ZERO_COPY_SPLIT");
   k->ref_mfma = env_int("LAMM_REF_MFMA", -1);
   k->helpers = env_int("LAMM_HIP_HELPERS", 0);
-  k->pool = env_int("LAMM_HIP_POOL", 1);
+  k->pool = env_int("LAMM_HIP_POOL", 5);
   if (const char* e = getenv("LAMM_HIP_ORDER")) k->ref_order = strcmp(e, "fast") != 0;
   return k;
 }

@@ -45,13 +45,15 @@ struct Knobs {
   int helpers = 0;             // LAMM_HIP_HELPERS: ggml's other pool threads during thread 0's device work:
                                // 0 return at once (ggml's barrier spins on them), 1 wait here yielding,
                                // 2 wait here asleep (futex)
-  int ref_mfma = -1;           // LAMM_REF_MFMA: reference-order prefill kernel (1: ref_mfma_kernel, 2 / 4: ref_mfma2 G)
+  int ref_mfma = -1;           // LAMM_REF_MFMA: reference-order prefill kernel (1: ref_mfma_kernel, 2 / 3 / 4: ref_mfma2
+                               // with 2 / 1 / 4 column groups, 5: 2 groups + swizzled image; unset: per format)
   bool ref_order = true;       // LAMM_HIP_ORDER=fast: the boundary runs the fast engines instead of the
                                // reference's float order (lamm_ref.hip) for the formats that have both
-  int pool = 1;                // LAMM_HIP_POOL: what ggml's pool threads do for prefill-sized calls (bits):
+  int pool = 5;                // LAMM_HIP_POOL: what ggml's pool threads do for prefill-sized calls (bits):
                                // 1 quantize the F32 activations to q8_0 / q8_1 rows in pinned memory (the
                                // upload moves those instead of F32), 2 scatter C out of pinned memory
-                               // (else HIP's pageable copy); 0: thread 0 alone, as before
+                               // (else HIP's pageable copy), 4 a reference-order call as two pipelined
+                               // column chunks on two streams; 0: thread 0 alone, as before
 };
 
 // The current switches (read from the environment at the first call).

@@ -804,7 +804,8 @@ __global__ __launch_bounds__(MNT) void ref_mfma2_kernel(GemvArgs p) {
   const int ml = 32 * wm + lr;
 
   static_assert(!SW || (MKB == 8 && MC2 % 4 == 0), "the swizzled item order");
-  constexpr bool PK = T == kQ4_0 || T == kQ5_1;   // packed chain steps where they cost no occupancy
+  // packed chain steps where they cost no occupancy (the swizzled q4_0 kernel with them: 265 VGPRs)
+  constexpr bool PK = (T == kQ4_0 || T == kQ5_1) && !SW;
   // item -> (column c, block k of the chunk)
   auto item_ck = [](int item, int& c, int& k) __attribute__((always_inline)) {
     if constexpr (SW) {
@@ -1239,7 +1240,10 @@ hipError_t launch_ref(int type, const GemvArgs& p, hipStream_t s) {
   if (p.N > 8 && type != kQ6_K) {
     // ref_mfma2_kernel, 2 column groups per wave (LAMM_REF_MFMA=4: 4 groups, one wave per SIMD; =1:
     // the unpipelined ref_mfma_kernel)
-    const int sel = knobs().ref_mfma > 0 ? knobs().ref_mfma : 2;
+    // default per format (tools/ref_ab.py, profiles/r04/ref_order/pk_fma/): the swizzled 2-group
+    // kernel for q4_0 / q4_1 / q5_0; q5_1's larger chunk keeps ref_mfma2 at one wave per SIMD, so
+    // it runs the unpipelined ref_mfma_kernel (205 vs 318 us at 4096 x 512 x 4096)
+    const int sel = knobs().ref_mfma > 0 ? knobs().ref_mfma : type == kQ5_1 ? 1 : 5;
     const int mc = sel == 4 ? 64 : sel == 3 ? 16 : 32;   // 5: the 2-group kernel, swizzled image
     const dim3 gm((unsigned)((p.M + MR - 1) / MR), (unsigned)((p.N + mc - 1) / mc), (unsigned)slices);
     auto gom = [&](auto tc) {

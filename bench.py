@@ -54,6 +54,7 @@ sys.path.insert(0, os.path.join(ROOT, "la-llama.cpp_amd"))
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 I8_DENSE_PEAK_TOPS = 5000.0    # dense MFMA-i8 = 2x the 2.5 PF dense bf16 rate (MI355X_MICROARCH.md)
+F32_VALU_PEAK_TFLOPS = 157.3   # f32 vector peak (v_pk_fma_f32; MI355X_MICROARCH.md F32 row)
 MALL_BYTES = 256 << 20
 ALIGN = 16                     # row-slab granularity of the GEMV split (one wave-group row tile)
 GEMM_ALIGN = 256               # fp6 GEMM row tile
@@ -238,8 +239,8 @@ def time_steps(ctx, step, steps, warmup, graph=True):
 _STEPS_LIB = None
 
 
-def isolated_launches(la, mats, R, Bm, Cm, n, sync_each=1):
-    """median duration (s) of n lamm_hip_matmul dispatches from their own timestamps
+def isolated_launches(la, mats, R, Bm, Cm, n, sync_each=1, flags=0):
+    """median duration (s) of n lamm_hip_matmul_ex dispatches from their own timestamps
     (lamm_hip_profile_next, tools/steps_loop.hip), each launched alone (sync_each) or back to back;
     None when the helper is not built or the kernel took no timestamps"""
     global _STEPS_LIB
@@ -249,16 +250,17 @@ def isolated_launches(la, mats, R, Bm, Cm, n, sync_each=1):
         if not os.path.exists(path):
             return None
         _STEPS_LIB = ctypes.CDLL(path)
-        _STEPS_LIB.lamm_steps_isolated.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(la.Matrix),
-                                                   ctypes.POINTER(la.Matrix), ctypes.c_int, ctypes.c_int,
-                                                   ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.c_int]
+        _STEPS_LIB.lamm_steps_isolated_ex.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(la.Matrix),
+                                                      ctypes.POINTER(la.Matrix), ctypes.c_int, ctypes.c_int,
+                                                      ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.c_int,
+                                                      ctypes.c_int]
     import torch
     arr = (la.Matrix * R)(*mats)
     out = (ctypes.c_float * n)()
     st = torch.cuda.Stream()
     torch.cuda.synchronize()
-    rc = _STEPS_LIB.lamm_steps_isolated(ctypes.cast(arr, ctypes.c_void_p), R, ctypes.byref(Bm), ctypes.byref(Cm), 0, n,
-                                        ctypes.c_void_p(st.cuda_stream), out, sync_each)
+    rc = _STEPS_LIB.lamm_steps_isolated_ex(ctypes.cast(arr, ctypes.c_void_p), R, ctypes.byref(Bm), ctypes.byref(Cm),
+                                           0, n, ctypes.c_void_p(st.cuda_stream), out, sync_each, flags)
     torch.cuda.synchronize()
     v = sorted(out)
     if rc != 0 or v[0] <= 0.0:
@@ -424,6 +426,53 @@ def config3_gemm(ctx, fmt, M, N, K, slices, steps):
     del A, B, C, slab, W
     torch.cuda.empty_cache()
     return per_step, kern, rows, sample
+
+
+def ref_order_kernels(ctx, fmt, M, N, K, steps):
+    """The kernels the ggml boundary runs by default (LAMM_HIP_ORDER=reference: the reference's own
+    AVX2 float order, bit for bit), at config 2 and config 3, each against its own bound:
+    ref_gemv_kernel against HBM (config 2's bytes, weights rotated > MALL, the dispatch's own
+    timestamps); the prefill kernel against the fp32 FMA-chain floor of that order -- per output and
+    32-element block 8 dependent lane FMAs, M*N*K/4 FMAs at the 157.3 TFLOP/s f32 VALU peak -- and,
+    for comparison with config 3, against the i8 MFMA peak."""
+    torch, la = ctx.torch, ctx.la
+    t = la.BY_NAME[fmt]
+    vt = la.vec_dot_type(t)
+    kb = K // la.blck_size(t)
+    arow, brow = la.row_bytes(t, K), la.row_bytes(vt, K)
+    out = {}
+    R = max(8, -(-int(1.15 * MALL_BYTES) // (M * arow)))
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(31)
+    A, _ = make_weights(torch, la, fmt, R, M, K, gen)
+    B = make_activations(torch, la, fmt, N, K, gen)
+    C = torch.zeros(N * M, dtype=torch.float32, device="cuda")
+    mats = [la.Matrix(A.data_ptr() + c * M * arow, t, M, kb, kb) for c in range(R)]
+    Bm1 = la.Matrix(B.data_ptr(), vt, kb, 1, kb)
+    Cm1 = la.Matrix(C.data_ptr(), la.F32, M, 1, M)
+    iso = isolated_launches(la, mats, R, Bm1, Cm1, 300, flags=la.ORDER_REFERENCE)
+    u = gemv_bytes(la, fmt, M, K)
+    if iso:
+        out["gemv"] = {"workload": f"{fmt.upper()}xQ8 GEMV M={M} N=1 K={K} (config 2), {R} weight copies rotated",
+                       "kernel": "lamm::ref_gemv_kernel (csrc/lamm_ref.hip)", "bound": "hbm",
+                       "per_launch_us": round(iso * 1e6, 3), "achieved_GBs": round(u / iso / 1e9, 1),
+                       "frac": round(u / iso / 1e9 / HBM_PEAK_GBS, 4)}
+    BmN = la.Matrix(B.data_ptr(), vt, kb, N, kb)
+    CmN = la.Matrix(C.data_ptr(), la.F32, M, N, M)
+    _, kern, _ = time_steps(ctx, lambda i: la.matmul_ex(mats[0], BmN, CmN, flags=la.ORDER_REFERENCE,
+                                                        stream=torch.cuda.current_stream().cuda_stream),
+                            max(steps, 100), 2)
+    floor = M * N * K / 4 * 2 / (F32_VALU_PEAK_TFLOPS * 1e12)
+    out["gemm"] = {"workload": f"{fmt.upper()}xQ8 GEMM M={M} N={N} K={K} (config 3), stationary weights",
+                   "kernel": "lamm::ref_mfma2_kernel<swizzled> (csrc/lamm_ref.hip)" if fmt in ("q4_0", "q4_1", "q5_0")
+                   else "lamm::ref_mfma_kernel (csrc/lamm_ref.hip)",
+                   "bound": "valu (the reference's fp32 lane chains)", "per_launch_us": round(kern * 1e6, 2),
+                   "floor_us": round(floor * 1e6, 2), "frac": round(floor / kern, 4),
+                   "floor": f"M*N*K/4 fp32 FMAs (8 lane chains per output and block) at {F32_VALU_PEAK_TFLOPS} TFLOP/s",
+                   "i8_frac": round(2.0 * M * N * K / kern / 1e12 / I8_DENSE_PEAK_TOPS, 4)}
+    del A, B, C
+    torch.cuda.empty_cache()
+    return out
 
 
 def config1_f32(ctx, steps):
@@ -605,6 +654,37 @@ def read_profile(kind, tag):
     return None
 
 
+def summary(out):
+    """The headline kernels in a few keys (per-launch us and roofline fraction), printed as the LAST key
+    of the JSON line so that a tail of the output still shows config 3 and the boundary's
+    reference-order kernels."""
+    s = {"config2_gemv": {"kernel": "gemv_flat1_kernel", "us": out["roofline"]["per_launch_us"],
+                          "frac_hbm": out["roofline"]["frac"], "value_GBs": out["value"]}}
+    gm = out.get("gemm", {}).get("slices1", {})
+    if "roofline" in gm:
+        s["config3_gemm"] = {"engine": gm["engine"], "us": gm["roofline"]["per_launch_us"],
+                             "frac_i8": gm["roofline"]["frac"], "scope": "whole launch"}
+    ro = out.get("ref_order", {})
+    if "gemv" in ro:
+        s["ref_order_gemv"] = {"kernel": "ref_gemv_kernel", "us": ro["gemv"]["per_launch_us"], "frac_hbm": ro["gemv"]["frac"]}
+    if "gemm" in ro:
+        s["ref_order_gemm"] = {"kernel": ro["gemm"]["kernel"].split(" ")[0].split("::")[-1], "us": ro["gemm"]["per_launch_us"],
+                               "frac_fma_floor": ro["gemm"]["frac"], "frac_i8": ro["gemm"]["i8_frac"]}
+    c4 = out.get("config4", {})
+    for f in ("q4_1", "q5_0", "q5_1", "q8_0", "q2_k"):
+        e = c4.get(f, {})
+        if "gemv_per_launch_us" in e:
+            s[f] = {"gemv_us": e["gemv_per_launch_us"], "gemv_frac": e["gemv_frac"]}
+            if "gemm_per_launch_us" in e:
+                s[f].update({"gemm": e["gemm_engine"], "gemm_us": e["gemm_per_launch_us"], "gemm_frac": e["gemm_frac"]})
+    e2e = out.get("llama7b_e2e", {})
+    for k in ("t16", "t8", "t16_fast_order"):
+        r = e2e.get(k, {})
+        if "pp_tok_s" in r:
+            s[f"config5_{k}"] = {kk: r.get(kk) for kk in ("pp_tok_s", "tg_tok_s", "tg_from_empty_tok_s")}
+    return s
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -714,6 +794,11 @@ def main():
             except Exception as e:  # noqa: BLE001
                 gm[f"slices{gslices}"] = {"error": str(e)[:300]}
         extras["gemm"] = gm
+        if world == 1:
+            try:
+                extras["ref_order"] = ref_order_kernels(ctx, fmt, M, gN, K, max(3, args.steps // 4))
+            except Exception as e:  # noqa: BLE001
+                extras["ref_order"] = {"error": str(e)[:300]}
     if world == 1 and not args.no_config1:
         try:
             extras["config1"] = config1_f32(ctx, args.steps)
@@ -834,6 +919,7 @@ def main():
             out["llama7b_e2e"]["parity_32_layers"] = par
     ctx.close()
     if rank == 0:
+        out["summary"] = summary(out)   # last key: what a tail of the line keeps
         print(json.dumps(out), flush=True)
 
 

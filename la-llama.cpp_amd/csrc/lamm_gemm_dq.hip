@@ -54,12 +54,9 @@ template <> struct DqFmt<kQ8_0> { static constexpr int BPB = 34, QS = 2, QH = -1
 // q8_1: its s = d * sum(q) is implied by the unpacked values (sum_k (d_a q_k + m_a) d_b b_k)
 template <> struct DqFmt<kQ8_1> { static constexpr int BPB = 36, QS = 4, QH = -1, MO = -1, C = 128; static constexpr bool NIB = false; };
 
-#ifndef DQ_NBUF
-#define DQ_NBUF 2   // quads of raw bytes in VGPRs (70 dwords each for q4_0)
-#endif
 #ifndef DQ_AB
 // probe builds only (tools/build_dq_var.sh): 1 loads only, 2 unpack + MFMA only (no loads after the
-// first quads), 3 production + the first workgroup's shader / real-time clock deltas in C[0], C[1]
+// first quads)
 #define DQ_AB 0
 #endif
 
@@ -67,9 +64,127 @@ constexpr int DQ_TI = 128, DQ_TJ = 64, DQ_KG = 4, DQ_NT = 256;
 constexpr int DQ_PI = DQ_TI + 8;   // LDS pitch of a parked partial row: the two half-waves' rows j, j + 4
                                    // fall on disjoint banks
 constexpr size_t DQ_LDS = (size_t)DQ_KG * DQ_TJ * DQ_PI * 4;
-// weights are pre-scaled by 2^8 (exact) so small block scales stay in f16's normal range; C is
-// scaled back by 2^-8 (exact) in the epilogue
-constexpr float DQ_ASCALE = 256.f, DQ_CSCALE = 1.f / 256.f;
+// weights are pre-scaled by 2^8 and activations by 2^4 (both exact) so the block scales of real
+// operands stay in f16's normal range; C is scaled back by 2^-12 (exact) in the epilogue.  The
+// window this leaves -- weight d in [2^-22, 2^8), activation d in [2^-18, 2^5) -- is enforced at run
+// time by the range guard below, not assumed.
+constexpr float DQ_ASCALE = 256.f, DQ_BSCALE = 16.f, DQ_CSCALE = 1.f / 4096.f;
+
+// ---------------------------------------------------------------- range guard
+// dq16 is exact to 2^-10 per product only while every unpacked f16 value is normal and finite.  Each
+// lane tracks the range of the pre-scaled block scales it unpacks (DqRange: a subnormal, inf or NaN
+// scale -> bad); an operand value that overflows f16 (|d * q| > 65504) turns its MFMA results into
+// inf / NaN, which the tile's final accumulators show.  A workgroup that sees either recomputes its
+// whole tile with exact int8 block dots (dq_exact_tile: d_a * d_b * S [+ m_a * s_b] in fp32, the
+// reference's lamm_kernel_q*.hpp arithmetic) -- slow, but only such tiles pay it, and the result is
+// finite wherever the reference's is (src/lamm_kernel_q8_0.hpp:50-117: any magnitude).
+constexpr int kDqNonFinite = 0x207;          // +-inf, NaN (v_cmp_class_f32 mask)
+
+// Scale tracking in VGPRs: per lane the largest |d| bits and the smallest nonzero |d| bits seen (the
+// packed u16 halves of a {d, d} pair; |d| - 1 wraps a zero to 0xffff): three packed ops per scale.
+// bad: an inf / NaN (>= 0x7c00) or a nonzero subnormal (< 0x0400) among them.
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+struct DqRange {
+  u16x2 hi = {0, 0}, lo = {0xffff, 0xffff};
+  __device__ __forceinline__ void see(uint32_t d2) {
+    const u16x2 a = __builtin_bit_cast(u16x2, d2 & 0x7fff7fffu);
+    hi = __builtin_elementwise_max(hi, a);
+    lo = __builtin_elementwise_min(lo, a - u16x2{1, 1});
+  }
+  __device__ __forceinline__ bool bad() const { return hi[0] >= 0x7c00 || lo[0] < 0x03ff; }
+};
+
+// the 16-bit word at byte offset o (even) of x
+__device__ __forceinline__ uint32_t ld16(const unsigned char* x, int o) {
+  return *reinterpret_cast<const uint16_t*>(x + o);
+}
+__device__ __forceinline__ uint32_t ld32(const unsigned char* x, int o) {   // o even
+  return ld16(x, o) | (ld16(x, o + 2) << 16);
+}
+
+// One weight block as 8 dwords of signed int8 values (q - c), d and m (0 unless affine)
+template <int T>
+__device__ __forceinline__ void exact_a(const unsigned char* a, uint32_t (&q)[8], float& d, float& m) {
+  using F = DqFmt<T>;
+  d = h2f(ld16(a, 0));
+  m = F::MO >= 0 ? h2f(ld16(a, F::MO >= 0 ? F::MO : 0)) : 0.f;
+  if constexpr (!F::NIB) {
+#pragma unroll
+    for (int w = 0; w < 8; ++w) q[w] = ld32(a, F::QS + 4 * w);
+  } else {
+    const uint32_t qh = F::QH >= 0 ? ld32(a, F::QH >= 0 ? F::QH : 0) : 0u;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const uint32_t x = ld32(a, F::QS + 4 * w);
+      uint32_t lo = x & 0x0f0f0f0fu, hi = (x >> 4) & 0x0f0f0f0fu;
+      if constexpr (F::QH >= 0) {
+        lo |= spread4_hi((qh >> (4 * w)) & 0xfu);
+        hi |= spread4_hi((qh >> (16 + 4 * w)) & 0xfu);
+      }
+      // bytes u in [0, 31] -> u - c as signed bytes (no borrow crosses a byte: u + 128 - c >= 0)
+      constexpr uint32_t cc = 0x01010101u * (uint32_t)F::C;
+      q[w] = ((lo | 0x80808080u) - cc) ^ 0x80808080u;
+      q[4 + w] = ((hi | 0x80808080u) - cc) ^ 0x80808080u;
+    }
+  }
+}
+
+// The tile [i0, i0 + arows) x [j0, j0 + bcols) with exact int8 block dots, every block in order:
+// per block the 64 activation blocks are staged in LDS (int8 quads, d, s), then each thread
+// accumulates its weight row against its columns.  NT threads, NT / DQ_TI columns each step.
+template <int T, int V, int NT>
+__device__ void dq_exact_tile(const unsigned char* A, int64_t lda, const unsigned char* B, int64_t ldb, float* C,
+                              int64_t ldc, int arows, int bcols, int nblk, unsigned char* smem) {
+  using FA = DqFmt<T>;
+  using FB = DqFmt<V>;
+  constexpr int CJ = NT / DQ_TI, NJ = DQ_TJ / CJ;
+  static_assert(NT % DQ_TI == 0 && DQ_TJ % CJ == 0, "tile split");
+  uint32_t* bq = reinterpret_cast<uint32_t*>(smem);    // [64][8] int8 quads
+  float* bd = reinterpret_cast<float*>(bq + DQ_TJ * 8);   // [64] d, then [64] s
+  const int t = threadIdx.x, i = t % DQ_TI, jc = t / DQ_TI;
+  float acc[NJ];
+#pragma unroll
+  for (int k = 0; k < NJ; ++k) acc[k] = 0.f;
+  for (int b = 0; b < nblk; ++b) {
+    __syncthreads();   // the previous block's LDS reads are done
+    if (t < DQ_TJ) {
+      uint32_t w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      float d = 0.f, sb = 0.f;
+      if (t < bcols) {
+        const unsigned char* x = B + (int64_t)t * ldb + (int64_t)b * FB::BPB;
+        d = h2f(ld16(x, 0));
+        if constexpr (FB::QS == 4) sb = h2f(ld16(x, 2));
+#pragma unroll
+        for (int k = 0; k < 8; ++k) w[k] = ld32(x, FB::QS + 4 * k);
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) bq[t * 8 + k] = w[k];
+      bd[t] = d;
+      bd[DQ_TJ + t] = sb;
+    }
+    __syncthreads();
+    if (i < arows) {
+      uint32_t qa[8];
+      float da, ma;
+      exact_a<T>(A + (int64_t)i * lda + (int64_t)b * FA::BPB, qa, da, ma);
+#pragma unroll
+      for (int k = 0; k < NJ; ++k) {
+        const int j = jc + CJ * k;
+        int sumi = 0;
+#pragma unroll
+        for (int w = 0; w < 8; ++w) sumi = dot4(qa[w], bq[j * 8 + w], sumi);
+        acc[k] += da * bd[j] * (float)sumi;
+        if constexpr (FA::MO >= 0) acc[k] += ma * bd[DQ_TJ + j];
+      }
+    }
+  }
+  if (i < arows)
+#pragma unroll
+    for (int k = 0; k < NJ; ++k) {
+      const int j = jc + CJ * k;
+      if (j < bcols) C[(int64_t)j * ldc + i] = acc[k];
+    }
+}
 
 // load_words' vector-memory instructions for NW dwords (b128s, then b64 / b32)
 [[maybe_unused]] constexpr int vm_ops(int nw) { return nw / 4 + (nw % 4 >= 2 ? 1 : 0) + (nw % 2 ? 1 : 0); }
@@ -158,167 +273,6 @@ __device__ __forceinline__ void dq_scalars(const uint32_t (&w)[NW], bool valid, 
   if constexpr (F::QH >= 0) qh = field32<O + F::QH>(w);
 }
 
-template <int T, int V, int NBUF>
-__global__ __launch_bounds__(DQ_NT) void gemm_dq_kernel(GemvArgs p) {
-  using FA = DqFmt<T>;
-  using FB = DqFmt<V>;
-  constexpr int NWA = FA::BPB / 2, NWB = FB::BPB / 2;   // dwords of a block pair (every BPB is even)
-  extern __shared__ __attribute__((aligned(16))) float red[];
-  const int t = threadIdx.x, lane = t & 63, lr = lane & 31, h = lane >> 5;
-  const int g = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int nsi = (p.M + DQ_TI - 1) / DQ_TI, nsj = (p.N + DQ_TJ - 1) / DQ_TJ;
-  int ti, tj, z;
-  {   // XCD-aware order: workgroup b runs on XCD b % 8; each XCD gets a contiguous run of tiles,
-      // row tiles outer, so an XCD's CUs share their weight rows and the activation rows in its L2
-    const int ntile = nsi * nsj * p.ne12 * p.ne13;
-    const int id = blockIdx.x, x = id & 7, k = id >> 3, q = ntile >> 3, rmd = ntile & 7;
-    const int wv = x < rmd ? x * (q + 1) + k : rmd * (q + 1) + (x - rmd) * q + k;
-    const int per = nsi * nsj;
-    z = wv / per;
-    ti = (wv % per) / nsj;
-    tj = (wv % per) % nsj;
-  }
-  const int i12 = z % p.ne12, i13 = z / p.ne12;
-  const int i02 = i12 / p.r2, i03 = i13 / p.r3;
-  const int64_t i0 = (int64_t)ti * DQ_TI, j0 = (int64_t)tj * DQ_TJ;
-  // resources from the tile's first row / column: rows past M and columns past N read zeros
-  const int64_t arows = min((int64_t)DQ_TI, (int64_t)p.M - i0), bcols = min((int64_t)DQ_TJ, (int64_t)p.N - j0);
-  const auto ra = make_rsrc(p.A + (int64_t)i02 * p.sa2 + (int64_t)i03 * p.sa3 + i0 * p.lda,
-                            (uint32_t)min(arows * p.lda, (int64_t)0x7fffffff));
-  const auto rb = make_rsrc(p.B + (int64_t)i12 * p.sb2 + (int64_t)i13 * p.sb3 + j0 * p.ldb,
-                            (uint32_t)min(bcols * p.ldb, (int64_t)0x7fffffff));
-  // (no lambda below captures p: a by-reference capture of the kernel argument puts it in scratch,
-  // and every value read back from there is a VGPR -- buffer loads through waterfall loops)
-  const int nblk = p.nblk;
-  const int nq = (nblk + 3) / 4;
-  const int mine = nq > g ? (nq - g + DQ_KG - 1) / DQ_KG : 0;   // this wave's quads
-  const uint32_t a_lane = (uint32_t)(lr * p.lda) + (uint32_t)(2 * h * FA::BPB);
-  const uint32_t b_lane = (uint32_t)(lr * p.ldb) + (uint32_t)(2 * h * FB::BPB);
-  const uint32_t a_sub = (uint32_t)(32 * p.lda), b_sub = (uint32_t)(32 * p.ldb);
-
-  uint32_t wa[NBUF][4][NWA], wb[NBUF][2][NWB];
-  // the raw pair windows of this wave's quad u into buffer S (past the end: its last quad again, so
-  // every buffer's wait count stays the same; never computed)
-  auto issue = [&](int u, auto S_) __attribute__((always_inline)) {
-    constexpr int S = decltype(S_)::value;
-    const int q = g + DQ_KG * min(u, mine - 1);
-    const uint32_t qa = (uint32_t)q * (4 * FA::BPB), qb = (uint32_t)q * (4 * FB::BPB);
-    unroll<4>([&](auto Y) __attribute__((always_inline)) { load_words<NWA, 0>(ra, a_lane + Y * a_sub + qa, wa[S][Y]); });
-    unroll<2>([&](auto X) __attribute__((always_inline)) { load_words<NWB, 0>(rb, b_lane + X * b_sub + qb, wb[S][X]); });
-  };
-  constexpr int LPQ = 4 * vm_ops(NWA) + 2 * vm_ops(NWB);   // vmem instructions per quad
-
-  f32x16 acc[2][4];
-  unroll<2>([&](auto X) __attribute__((always_inline)) { unroll<4>([&](auto Y) __attribute__((always_inline)) { acc[X][Y] = f32x16{}; }); });
-
-  auto quad = [&](int u, auto S_) __attribute__((always_inline)) {
-    constexpr int S = decltype(S_)::value;
-    if constexpr (DQ_AB == 1) {   // loads only: every raw dword consumed, nothing computed
-#pragma unroll
-      for (int y = 0; y < 4; ++y)
-#pragma unroll
-        for (int i = 0; i < NWA; ++i) asm volatile("" ::"v"(wa[S][y][i]));
-#pragma unroll
-      for (int x = 0; x < 2; ++x)
-#pragma unroll
-        for (int i = 0; i < NWB; ++i) asm volatile("" ::"v"(wb[S][x][i]));
-      return;
-    }
-    if constexpr (DQ_AB == 2) {   // compute only: the stale buffer, made opaque so nothing is hoisted
-#pragma unroll
-      for (int y = 0; y < 4; ++y)
-#pragma unroll
-        for (int i = 0; i < NWA; ++i) asm volatile("" : "+v"(wa[S][y][i]));
-#pragma unroll
-      for (int x = 0; x < 2; ++x)
-#pragma unroll
-        for (int i = 0; i < NWB; ++i) asm volatile("" : "+v"(wb[S][x][i]));
-    }
-    const int q = g + DQ_KG * u;
-    unroll<2>([&](auto JB_) __attribute__((always_inline)) {
-      constexpr int JB = JB_;
-      const bool valid = 4 * q + 2 * h + JB < nblk;   // the pair's block JB exists (ragged K)
-      uint32_t ad[4], am[4], aq[4], bd[2], bm[2], bq[2];
-      unroll<4>([&](auto Y) __attribute__((always_inline)) { dq_scalars<T, JB>(wa[S][Y], valid, (_Float16)DQ_ASCALE, ad[Y], am[Y], aq[Y]); });
-      unroll<2>([&](auto X) __attribute__((always_inline)) { dq_scalars<V, JB>(wb[S][X], valid, (_Float16)1, bd[X], bm[X], bq[X]); });
-      unroll<4>([&](auto CG_) __attribute__((always_inline)) {
-        constexpr int CG = CG_;
-        half8 bo[2];
-        unroll<2>([&](auto X) __attribute__((always_inline)) { bo[X] = dq_operand<V, JB, CG>(wb[S][X], bd[X], 0u, 0u); });
-        unroll<4>([&](auto Y) __attribute__((always_inline)) {
-          const half8 ao = dq_operand<T, JB, CG>(wa[S][Y], ad[Y], am[Y], aq[Y]);
-          unroll<2>([&](auto X) __attribute__((always_inline)) { acc[X][Y] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bo[X], ao, acc[X][Y], 0, 0, 0); });
-        });
-      });
-    });
-  };
-
-  [[maybe_unused]] uint64_t clk0 = 0, rt0 = 0;
-  if constexpr (DQ_AB == 3) {
-    clk0 = __builtin_amdgcn_s_memtime();
-    rt0 = __builtin_amdgcn_s_memrealtime();
-  }
-  if (mine > 0) {
-    unroll<NBUF>([&](auto K) __attribute__((always_inline)) { issue(K, K); });
-    int u0 = 0;
-    // whole rounds of the buffer ring (the wait counts stay compile-time), then the rest
-    for (; u0 + NBUF <= mine; u0 += NBUF) {
-      unroll<NBUF>([&](auto K) __attribute__((always_inline)) {
-        wait_vm<LPQ * (NBUF - 1)>();   // quad u0 + k landed; the NBUF - 1 younger ones may fly
-        quad(u0 + K, K);
-        if constexpr (DQ_AB != 2) issue(u0 + K + NBUF, K);
-      });
-    }
-    unroll<NBUF - 1>([&](auto K) __attribute__((always_inline)) {
-      if (u0 + (int)K < mine) {
-        wait_vm<LPQ * (NBUF - 1)>();
-        quad(u0 + K, K);
-        if constexpr (DQ_AB != 2) issue(u0 + K + NBUF, K);
-      }
-    });
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-
-  // the 4 partial tiles meet in LDS: [group][activation row j][weight row i]
-  unroll<2>([&](auto X) __attribute__((always_inline)) {
-    unroll<4>([&](auto Y) __attribute__((always_inline)) {
-      unroll<16>([&](auto E) __attribute__((always_inline)) {
-        constexpr int e = E;
-        const int j = 32 * X + (e & 3) + 8 * (e >> 2) + 4 * h, i = 32 * Y + lr;
-        red[(g * DQ_TJ + j) * DQ_PI + i] = acc[X][Y][e];
-      });
-    });
-  });
-  __syncthreads();
-  float* C = p.C + (int64_t)i12 * p.sc2 + (int64_t)i13 * p.sc3;
-  const bool pair = (p.ldc & 1) == 0 && ((uintptr_t)C & 7) == 0;
-#pragma unroll
-  for (int r = 0; r < DQ_TJ * DQ_TI / (2 * DQ_NT); ++r) {
-    const int idx = 2 * (r * DQ_NT + t), jl = idx / DQ_TI, il = idx % DQ_TI;
-    f32x2 v = *reinterpret_cast<const f32x2*>(&red[jl * DQ_PI + il]);
-#pragma unroll
-    for (int g_ = 1; g_ < DQ_KG; ++g_) v += *reinterpret_cast<const f32x2*>(&red[(g_ * DQ_TJ + jl) * DQ_PI + il]);
-    v *= DQ_CSCALE;
-    const int64_t j = j0 + jl, i = i0 + il;
-    if (j < p.N) {
-      float* c = C + j * p.ldc + i;
-      if (pair && i + 1 < p.M) {
-        __builtin_nontemporal_store(v, reinterpret_cast<f32x2*>(c));
-      } else {
-        if (i < p.M) c[0] = v[0];
-        if (i + 1 < p.M) c[1] = v[1];
-      }
-    }
-  }
-  if constexpr (DQ_AB == 3) {
-    if (blockIdx.x == 0 && t == 0) {
-      const uint64_t clk = __builtin_amdgcn_s_memtime() - clk0, rt = __builtin_amdgcn_s_memrealtime() - rt0;
-      p.C[0] = (float)clk;
-      p.C[1] = (float)rt;
-    }
-  }
-}
-
 // ---------------------------------------------------------------- LDS-staged form (v2)
 // The same unpacking and MFMA steps, but each wave's quad arrives by COALESCED loads: consecutive
 // lanes take consecutive 8-byte pieces of a row's (column's) quad -- 9 pieces of a q4_0 row, 17 of a
@@ -400,6 +354,7 @@ __global__ __launch_bounds__(DQ_NT * WH) void gemm_dq2_kernel(GemvArgs p) {
   f32x16 acc[2][YW];
   unroll<2>([&](auto X) __attribute__((always_inline)) { unroll<YW>([&](auto Y) __attribute__((always_inline)) { acc[X][Y] = f32x16{}; }); });
 
+  DqRange range;   // the range guard: the scales this lane unpacked
   auto quad = [&](int u) __attribute__((always_inline)) {
     const int q = g + DQ_KG * u;
     uint32_t wa[YW][NWA], wb[2][NWB];   // this lane's pair windows, from the image
@@ -431,7 +386,12 @@ __global__ __launch_bounds__(DQ_NT * WH) void gemm_dq2_kernel(GemvArgs p) {
       const bool valid = 4 * q + 2 * h + JB < nblk;
       uint32_t ad[YW], am[YW], aq[YW], bd[2], bm[2], bq[2];
       unroll<YW>([&](auto Y) __attribute__((always_inline)) { dq_scalars<T, JB>(wa[Y], valid, (_Float16)DQ_ASCALE, ad[Y], am[Y], aq[Y]); });
-      unroll<2>([&](auto X) __attribute__((always_inline)) { dq_scalars<V, JB>(wb[X], valid, (_Float16)1, bd[X], bm[X], bq[X]); });
+      unroll<2>([&](auto X) __attribute__((always_inline)) { dq_scalars<V, JB>(wb[X], valid, (_Float16)DQ_BSCALE, bd[X], bm[X], bq[X]); });
+      unroll<YW>([&](auto Y) __attribute__((always_inline)) {
+        range.see(ad[Y]);
+        if constexpr (FA::MO >= 0) range.see(am[Y]);
+      });
+      unroll<2>([&](auto X) __attribute__((always_inline)) { range.see(bd[X]); });
       unroll<4>([&](auto CG_) __attribute__((always_inline)) {
         constexpr int CG = CG_;
         half8 bo[2];
@@ -476,7 +436,28 @@ __global__ __launch_bounds__(DQ_NT * WH) void gemm_dq2_kernel(GemvArgs p) {
     });
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // range guard: any bad scale or non-finite accumulator in any wave -> the exact tile
+  bool bad = range.bad();
+  unroll<2>([&](auto X) __attribute__((always_inline)) {
+    unroll<YW>([&](auto Y) __attribute__((always_inline)) {
+      unroll<16>([&](auto E) __attribute__((always_inline)) { constexpr int e = E; bad |= __builtin_amdgcn_class(acc[X][Y][e], kDqNonFinite); });
+    });
+  });
+  __shared__ int wave_bad[NT / 64];
+  if (lane == 0) wave_bad[wid] = 0;
   __syncthreads();   // every wave past its last image read: the partial tiles reuse the LDS
+  if (bad) wave_bad[wid] = 1;   // (any lane; the same value)
+  __syncthreads();
+  int any_bad = 0;
+#pragma unroll
+  for (int w = 0; w < NT / 64; ++w) any_bad |= wave_bad[w];
+  if (any_bad) {
+    dq_exact_tile<T, V, NT>(p.A + (int64_t)i02 * p.sa2 + (int64_t)i03 * p.sa3 + i0 * p.lda, p.lda,
+                            p.B + (int64_t)i12 * p.sb2 + (int64_t)i13 * p.sb3 + j0 * p.ldb, p.ldb,
+                            p.C + (int64_t)i12 * p.sc2 + (int64_t)i13 * p.sc3 + j0 * p.ldc + i0, p.ldc, (int)arows,
+                            (int)bcols, nblk, smem);
+    return;
+  }
   float* red = reinterpret_cast<float*>(smem);
   unroll<2>([&](auto X) __attribute__((always_inline)) {
     unroll<YW>([&](auto Y) __attribute__((always_inline)) {
@@ -510,204 +491,6 @@ __global__ __launch_bounds__(DQ_NT * WH) void gemm_dq2_kernel(GemvArgs p) {
   }
 }
 
-// ---------------------------------------------------------------- activation-prepped form (v3)
-// The activations, shared by every row tile, are unpacked ONCE per call instead of once per CU:
-// dq_prep_b writes them as plain f16 rows d_b * b (zero past K, rows padded to whole quads), and
-// the main kernel reads each k-step's 8 activation values with one ds_read_b128 from its LDS image
-// (column pitch 4 * 64 + 16 bytes: conflict-free b128 reads) -- only the weights are unpacked.
-constexpr int DQ3_BP = 4 * 64 + 16;   // LDS pitch of a column's quad (256 bytes of f16 + pad)
-
-template <int V>
-__global__ __launch_bounds__(256) void dq_prep_b(GemvArgs p, _Float16* __restrict__ out, int64_t kpad) {
-  using F = DqFmt<V>;
-  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;   // (slice, row, block) of the padded image
-  const int64_t nbp = kpad / 32;
-  const int64_t per = (int64_t)p.N * nbp;
-  if (idx >= per * p.ne12 * p.ne13) return;
-  const int z = (int)(idx / per);
-  const int64_t r = idx % per, j = r / nbp, b = r % nbp;
-  const int i12 = z % p.ne12, i13 = z / p.ne12;
-  half8 v[4];
-  if (b < p.nblk) {
-    // the row through a buffer resource (nothing past its last block is read); the block sits at a
-    // 2- or 4-byte aligned offset: dwords from the one below, realigned
-    const unsigned char* row = p.B + (int64_t)i12 * p.sb2 + (int64_t)i13 * p.sb3 + j * p.ldb;
-    const auto rr = make_rsrc(row, (uint32_t)(p.nblk * F::BPB));
-    const uint32_t o = (uint32_t)(b * F::BPB), o4 = o & ~3u;
-    const int sh = (int)(o - o4) * 8;
-    uint32_t w[F::BPB / 4 + 1], raw[F::BPB / 4 + 2];
-#pragma unroll
-    for (int k = 0; k < F::BPB / 4 + 2; ++k) raw[k] = bload4(rr, o4 + 4 * k);
-#pragma unroll
-    for (int k = 0; k < F::BPB / 4 + 1; ++k) w[k] = __builtin_amdgcn_alignbit(raw[k + 1], raw[k], sh);
-    // the block now starts at byte 0 of w: reuse the pair unpacker with JB = 0
-    uint32_t d2, m2, qh;
-    dq_scalars<V, 0>(w, true, (_Float16)1, d2, m2, qh);
-    unroll<4>([&](auto CG) { v[CG] = dq_operand<V, 0, CG>(w, d2, 0u, 0u); });
-  } else {
-    unroll<4>([&](auto CG) { v[CG] = half8{}; });
-  }
-  half8* dst = reinterpret_cast<half8*>(out + ((int64_t)z * p.N + j) * kpad + b * 32);
-  unroll<4>([&](auto CG) { __builtin_nontemporal_store(v[CG], dst + CG); });
-}
-
-template <int T, int NBV>
-__global__ __launch_bounds__(DQ_NT) void gemm_dq3_kernel(GemvArgs p, const _Float16* __restrict__ bimg, int64_t kpad) {
-  using FA = DqFmt<T>;
-  constexpr int NWA = FA::BPB / 2;
-  constexpr int QA = 4 * FA::BPB, PA = QA / 8;
-  constexpr int LA = DQ_TI * PA / 64, LB = DQ_TJ * 16 / 64;   // b64 weight pieces, b128 activation pieces
-  constexpr int QBYTES = DQ_TI * QA + DQ_TJ * DQ3_BP;
-  static_assert((DQ_TI * PA) % 64 == 0, "whole loads");
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int t = threadIdx.x, lane = t & 63, lr = lane & 31, h = lane >> 5;
-  const int g = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int nsi = (p.M + DQ_TI - 1) / DQ_TI, nsj = (p.N + DQ_TJ - 1) / DQ_TJ;
-  int ti, tj, z;
-  {
-    const int ntile = nsi * nsj * p.ne12 * p.ne13;
-    const int id = blockIdx.x, x = id & 7, k = id >> 3, q = ntile >> 3, rmd = ntile & 7;
-    const int wv = x < rmd ? x * (q + 1) + k : rmd * (q + 1) + (x - rmd) * q + k;
-    const int per = nsi * nsj;
-    z = wv / per;
-    ti = (wv % per) / nsj;
-    tj = (wv % per) % nsj;
-  }
-  const int i12 = z % p.ne12, i13 = z / p.ne12;
-  const int i02 = i12 / p.r2, i03 = i13 / p.r3;
-  const int64_t i0 = (int64_t)ti * DQ_TI, j0 = (int64_t)tj * DQ_TJ;
-  const int64_t arows = min((int64_t)DQ_TI, (int64_t)p.M - i0), bcols = min((int64_t)DQ_TJ, (int64_t)p.N - j0);
-  const auto ra = make_rsrc(p.A + (int64_t)i02 * p.sa2 + (int64_t)i03 * p.sa3 + i0 * p.lda,
-                            (uint32_t)min(arows * p.lda, (int64_t)0x7fffffff));
-  const int64_t ldbb = kpad * 2;   // bytes of an f16 activation row
-  const auto rb = make_rsrc(bimg + ((int64_t)z * p.N + j0) * kpad, (uint32_t)min(bcols * ldbb, (int64_t)0x7fffffff));
-  const int nblk = p.nblk;
-  const int nq = (nblk + 3) / 4;
-  const int mine = nq > g ? (nq - g + DQ_KG - 1) / DQ_KG : 0;
-  uint32_t a_off[LA], b_off[LB];
-  {
-    const uint32_t lda = (uint32_t)p.lda;
-#pragma unroll
-    for (int i = 0; i < LA; ++i) {
-      const int pc = i * 64 + lane;
-      a_off[i] = (uint32_t)(pc / PA) * lda + (uint32_t)(pc % PA) * 8;
-    }
-#pragma unroll
-    for (int i = 0; i < LB; ++i) {
-      const int pc = i * 64 + lane;
-      b_off[i] = (uint32_t)(pc / 16) * (uint32_t)ldbb + (uint32_t)(pc % 16) * 16;
-    }
-  }
-  unsigned char* img = smem + g * QBYTES;   // weight rows [128][QA], then activation columns [64][DQ3_BP]
-  u32x2 sta[NBV][LA];
-  u32x4 stb[NBV][LB];
-  auto issue = [&](int u, auto S_) __attribute__((always_inline)) {
-    constexpr int S = decltype(S_)::value;
-    const int q = g + DQ_KG * min(u, mine - 1);
-    const uint32_t qa = (uint32_t)q * QA, qb = (uint32_t)q * 256;
-#pragma unroll
-    for (int i = 0; i < LA; ++i) sta[S][i] = __builtin_amdgcn_raw_buffer_load_b64(ra, a_off[i] + qa, 0, 0);
-#pragma unroll
-    for (int i = 0; i < LB; ++i) stb[S][i] = __builtin_amdgcn_raw_buffer_load_b128(rb, b_off[i] + qb, 0, 0);
-  };
-  auto stage = [&](auto S_) __attribute__((always_inline)) {
-    constexpr int S = decltype(S_)::value;
-#pragma unroll
-    for (int i = 0; i < LA; ++i) *reinterpret_cast<u32x2*>(img + 8 * (i * 64 + lane)) = sta[S][i];
-#pragma unroll
-    for (int i = 0; i < LB; ++i) {
-      const int pc = i * 64 + lane;
-      *reinterpret_cast<u32x4*>(img + DQ_TI * QA + (pc / 16) * DQ3_BP + (pc % 16) * 16) = stb[S][i];
-    }
-  };
-
-  f32x16 acc[2][4];
-  unroll<2>([&](auto X) __attribute__((always_inline)) { unroll<4>([&](auto Y) __attribute__((always_inline)) { acc[X][Y] = f32x16{}; }); });
-
-  auto quad = [&](int u) __attribute__((always_inline)) {
-    const int q = g + DQ_KG * u;
-    uint32_t wa[4][NWA];
-#pragma unroll
-    for (int y = 0; y < 4; ++y) {
-      const uint32_t* src = reinterpret_cast<const uint32_t*>(img + (32 * y + lr) * QA + h * 2 * FA::BPB);
-#pragma unroll
-      for (int k = 0; k < NWA; ++k) wa[y][k] = src[k];
-    }
-    unroll<2>([&](auto JB_) __attribute__((always_inline)) {
-      constexpr int JB = JB_;
-      const bool valid = 4 * q + 2 * h + JB < nblk;
-      uint32_t ad[4], am[4], aq[4];
-      unroll<4>([&](auto Y) __attribute__((always_inline)) { dq_scalars<T, JB>(wa[Y], valid, (_Float16)DQ_ASCALE, ad[Y], am[Y], aq[Y]); });
-      unroll<4>([&](auto CG_) __attribute__((always_inline)) {
-        constexpr int CG = CG_;
-        half8 bo[2];
-        unroll<2>([&](auto X) __attribute__((always_inline)) {
-          bo[X] = *reinterpret_cast<const half8*>(img + DQ_TI * QA + (32 * X + lr) * DQ3_BP + ((2 * h + JB) * 4 + CG) * 16);
-        });
-        unroll<4>([&](auto Y) __attribute__((always_inline)) {
-          const half8 ao = dq_operand<T, JB, CG>(wa[Y], ad[Y], am[Y], aq[Y]);
-          unroll<2>([&](auto X) __attribute__((always_inline)) { acc[X][Y] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bo[X], ao, acc[X][Y], 0, 0, 0); });
-        });
-      });
-    });
-  };
-
-  constexpr int LPQ = LA + LB;
-  if (mine > 0) {
-    unroll<NBV>([&](auto K) __attribute__((always_inline)) { issue(K, K); });
-    int u0 = 0;
-    for (; u0 + NBV <= mine; u0 += NBV) {
-      unroll<NBV>([&](auto K) __attribute__((always_inline)) {
-        wait_vm<LPQ * (NBV - 1)>();
-        stage(K);
-        issue(u0 + K + NBV, K);
-        quad(u0 + K);
-      });
-    }
-    unroll<NBV>([&](auto K) __attribute__((always_inline)) {
-      if (u0 + (int)K < mine) {
-        wait_vm<LPQ * (NBV - 1)>();
-        stage(K);
-        issue(u0 + K + NBV, K);
-        quad(u0 + K);
-      }
-    });
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  float* red = reinterpret_cast<float*>(smem);
-  unroll<2>([&](auto X) __attribute__((always_inline)) {
-    unroll<4>([&](auto Y) __attribute__((always_inline)) {
-      unroll<16>([&](auto E) __attribute__((always_inline)) {
-        constexpr int e = E;
-        const int j = 32 * X + (e & 3) + 8 * (e >> 2) + 4 * h, i = 32 * Y + lr;
-        red[(g * DQ_TJ + j) * DQ_PI + i] = acc[X][Y][e];
-      });
-    });
-  });
-  __syncthreads();
-  float* C = p.C + (int64_t)i12 * p.sc2 + (int64_t)i13 * p.sc3;
-  const bool pair = (p.ldc & 1) == 0 && ((uintptr_t)C & 7) == 0;
-#pragma unroll
-  for (int r = 0; r < DQ_TJ * DQ_TI / (2 * DQ_NT); ++r) {
-    const int idx = 2 * (r * DQ_NT + t), jl = idx / DQ_TI, il = idx % DQ_TI;
-    f32x2 v = *reinterpret_cast<const f32x2*>(&red[jl * DQ_PI + il]);
-#pragma unroll
-    for (int g_ = 1; g_ < DQ_KG; ++g_) v += *reinterpret_cast<const f32x2*>(&red[(g_ * DQ_TJ + jl) * DQ_PI + il]);
-    v *= DQ_CSCALE;
-    const int64_t j = j0 + jl, i = i0 + il;
-    if (j < p.N) {
-      float* c = C + j * p.ldc + i;
-      if (pair && i + 1 < p.M) {
-        __builtin_nontemporal_store(v, reinterpret_cast<f32x2*>(c));
-      } else {
-        if (i < p.M) c[0] = v[0];
-        if (i + 1 < p.M) c[1] = v[1];
-      }
-    }
-  }
-}
-
 template <int T, int V, int WH>
 constexpr size_t dq2_lds() {
   constexpr size_t img =
@@ -715,44 +498,21 @@ constexpr size_t dq2_lds() {
   return img > DQ_LDS ? img : DQ_LDS;
 }
 
-#ifndef DQ_FORM
-#define DQ_FORM 2   // 1: per-lane window loads into VGPRs (gemm_dq_kernel); 2: coalesced, LDS-staged; 3: + activations prepped to f16 once per call
-#endif
 #ifndef DQ_WH
-#define DQ_WH 1     // the LDS-staged form's waves per K-group (2: two waves per SIMD; measured no faster, profiles/r04/dq16/)
+#define DQ_WH 1     // waves per K-group (2: two waves per SIMD; measured no faster, profiles/r04/dq16/)
 #endif
 #ifndef DQ_NBV
-#define DQ_NBV 1    // the LDS-staged form's quads in flight in VGPRs
+#define DQ_NBV 1    // quads in flight in VGPRs
 #endif
 
-int64_t dq3_kpad(const GemvArgs& p) { return (int64_t)((p.nblk + 3) / 4) * 128; }
-
 template <int T, int V>
-hipError_t launch_dq_t(const GemvArgs& p, void* ws, hipStream_t s) {
+hipError_t launch_dq_t(const GemvArgs& p, hipStream_t s) {
   const int tiles = gemm_dq_tiles(p);
-  if constexpr (DQ_FORM == 3) {
-    const int64_t kpad = dq3_kpad(p), items = (int64_t)p.ne12 * p.ne13 * p.N * (kpad / 32);
-    auto* bimg = static_cast<_Float16*>(ws);
-    hipLaunchKernelGGL(dq_prep_b<V>, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, s, p, bimg, kpad);
-    auto kern = gemm_dq3_kernel<T, DQ_NBV>;
-    constexpr size_t img = (size_t)DQ_KG * (DQ_TI * 4 * DqFmt<T>::BPB + DQ_TJ * DQ3_BP);
-    constexpr size_t lds = img > DQ_LDS ? img : DQ_LDS;
-    static_assert(lds <= 160 * 1024, "LDS");
-    set_max_lds((const void*)kern, (int)lds);
-    hipLaunchKernelGGL(kern, dim3((unsigned)tiles), dim3(DQ_NT), lds, s, p, bimg, kpad);
-    return hipGetLastError();
-  }
-  if constexpr (DQ_FORM == 1) {
-    auto kern = gemm_dq_kernel<T, V, DQ_NBUF>;
-    set_max_lds((const void*)kern, (int)DQ_LDS);
-    hipLaunchKernelGGL(kern, dim3((unsigned)tiles), dim3(DQ_NT), DQ_LDS, s, p);
-  } else {
-    auto kern = gemm_dq2_kernel<T, V, DQ_NBV, DQ_WH>;
-    constexpr size_t lds = dq2_lds<T, V, DQ_WH>();
-    static_assert(lds <= 160 * 1024, "LDS");
-    set_max_lds((const void*)kern, (int)lds);
-    hipLaunchKernelGGL(kern, dim3((unsigned)tiles), dim3(DQ_NT * DQ_WH), lds, s, p);
-  }
+  auto kern = gemm_dq2_kernel<T, V, DQ_NBV, DQ_WH>;
+  constexpr size_t lds = dq2_lds<T, V, DQ_WH>();
+  static_assert(lds <= 160 * 1024, "LDS");
+  set_max_lds((const void*)kern, (int)lds);
+  hipLaunchKernelGGL(kern, dim3((unsigned)tiles), dim3(DQ_NT * DQ_WH), lds, s, p);
   return hipGetLastError();
 }
 
@@ -773,17 +533,15 @@ bool gemm_dq_args_ok(const GemvArgs& p) {
          (int64_t)DQ_TI * p.lda < 0x7fffffff && (int64_t)DQ_TJ * p.ldb < 0x7fffffff;
 }
 
-size_t gemm_dq_workspace_bytes(const GemvArgs& p) {
-  return DQ_FORM == 3 ? (size_t)p.ne12 * p.ne13 * p.N * dq3_kpad(p) * 2 + 256 : 0;
-}
+size_t gemm_dq_workspace_bytes(const GemvArgs&) { return 0; }
 
-hipError_t launch_gemm_dq(int type, const GemvArgs& p, void* ws, hipStream_t s) {
+hipError_t launch_gemm_dq(int type, const GemvArgs& p, void*, hipStream_t s) {
   switch (type) {
-    case kQ4_0: return launch_dq_t<kQ4_0, kQ8_0>(p, ws, s);
-    case kQ4_1: return launch_dq_t<kQ4_1, kQ8_1>(p, ws, s);
-    case kQ5_0: return launch_dq_t<kQ5_0, kQ8_0>(p, ws, s);
-    case kQ5_1: return launch_dq_t<kQ5_1, kQ8_1>(p, ws, s);
-    case kQ8_0: return launch_dq_t<kQ8_0, kQ8_0>(p, ws, s);
+    case kQ4_0: return launch_dq_t<kQ4_0, kQ8_0>(p, s);
+    case kQ4_1: return launch_dq_t<kQ4_1, kQ8_1>(p, s);
+    case kQ5_0: return launch_dq_t<kQ5_0, kQ8_0>(p, s);
+    case kQ5_1: return launch_dq_t<kQ5_1, kQ8_1>(p, s);
+    case kQ8_0: return launch_dq_t<kQ8_0, kQ8_0>(p, s);
     default: return hipErrorInvalidValue;
   }
 }

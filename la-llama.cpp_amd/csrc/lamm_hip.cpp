@@ -616,6 +616,7 @@ struct Dev {
   int id = 0;
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr;  // the pipelined prefill's second column chunk (LAMM_HIP_POOL bit 4)
+  hipEvent_t upload = nullptr;    // stream2 waits on it: the weight upload enqueued on stream
   unsigned* flag = nullptr;       // pinned, host-coherent completion word (lamm_signal.hip)
   unsigned* flag_dev = nullptr;   // its device address
   unsigned seq = 0;
@@ -747,6 +748,7 @@ class Runtime {
       HIPCHK(hipSetDevice(ids[i]));
       HIPCHK(hipStreamCreateWithFlags(&devs[i].stream, hipStreamNonBlocking));
       HIPCHK(hipStreamCreateWithFlags(&devs[i].stream2, hipStreamNonBlocking));
+      HIPCHK(hipEventCreateWithFlags(&devs[i].upload, hipEventDisableTiming));
       HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&devs[i].flag), 64, hipHostMallocCoherent | hipHostMallocMapped));
       HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&devs[i].flag_dev), devs[i].flag, 0));
       *(volatile unsigned*)devs[i].flag = 0;
@@ -855,6 +857,7 @@ class Runtime {
       (void)hipStreamDestroy(d.stream);
       (void)hipStreamSynchronize(d.stream2);
       (void)hipStreamDestroy(d.stream2);
+      (void)hipEventDestroy(d.upload);
     }
     devs.clear();
   }
@@ -1251,6 +1254,10 @@ void mul_mat_thread0(const ggml::compute_params* params, ggml::tensor* dst, bool
     HIPCHK(hipSetDevice(d.id));
     WeightEntry& w = rt.weights(d, WeightKey{src0->data, t0, M, kb, src0->nb[1], src0->nb[2], src0->nb[3]}, a_row, src0,
                                 0, M, fp);
+    // a cold weight's upload was enqueued on d.stream: chunk 2's kernel on stream2 must not start
+    // before it lands (a pageable H2D copy may still be in flight when hipMemcpy2DAsync returns)
+    HIPCHK(hipEventRecord(d.upload, d.stream));
+    HIPCHK(hipStreamWaitEvent(d.stream2, d.upload, 0));
     stat.phase(1);
     unsigned char* h = rt.pinned(2, x_bytes);
     unsigned char* dB = static_cast<unsigned char*>(d.scratch(0, x_bytes + 64));

@@ -388,7 +388,8 @@ def test_pool_jobs(case, threaded, monkeypatch):
                            nb=[4, nb1, nb1 * N, nb1 * N * ne2[1]])
     want = expected(t, A_q, b, M, N, K, ne2, ne3)
     outs = []
-    for pool in ("1", "2", "3", "5", "0"):
+    la.cache_clear()
+    for pool in ("5", "1", "2", "3", "5", "0"):
         monkeypatch.setenv("LAMM_HIP_POOL", pool)
         dst = ggml_emu.mul_mat_node(src0, src1, row_pad=row_pad)
         assert ggml_emu.compute(dst, nth=6, threaded=threaded)
@@ -400,3 +401,32 @@ def test_pool_jobs(case, threaded, monkeypatch):
         outs.append(got.copy())
     for o in outs[:-1]:
         np.testing.assert_array_equal(o, outs[-1])
+
+
+@pytest.mark.parametrize("t", [ol.Q5_1, ol.Q8_0], ids=["q5_1", "q8_0"])
+def test_boundary_prefill_value_range(t):
+    """A prefill-sized call through the boundary whose weights reach |w| = 300 and whose activation
+    rows reach |x| = 1e5 (half the rows) -- beyond the f16 range of the dequantizing engine the fast
+    order runs q8_0 / q5_1 prefill on; its range guard computes those tiles with exact block dots, so
+    the output is finite and within the bar, as the reference's is."""
+    M, N, K = 4096, 256, 512
+    rng = np.random.default_rng(17)
+    a = rng.standard_normal((M, K), dtype=np.float32)
+    a *= 300 / np.abs(a).max()
+    b = rng.standard_normal((N, K), dtype=np.float32)
+    b[::2] *= 1e5 / np.abs(b).max()
+    A_q = ORACLE.quantize(t, a)
+    src0 = ggml_emu.Tensor(t, [K, M], data=A_q)
+    src1 = ggml_emu.Tensor(ol.F32, [K, N], data=b)
+    dst = ggml_emu.mul_mat_node(src0, src1)
+    assert ggml_emu.compute(dst, nth=4)
+    got = dst.buf.view(np.float32).reshape(N, M)
+    want = expected(t, A_q, b, M, N, K, (1, 1), (1, 1))[0, 0]
+    vt = la.vec_dot_type(t)
+    B_q = ORACLE.quantize(vt, b, ol.QUANT_AVX)
+    absdot = np.abs(ORACLE.dequantize(vt, B_q, N, K).astype(np.float64)) @ \
+        np.abs(ORACLE.dequantize(t, A_q, M, K).astype(np.float64)).T
+    fin = np.isfinite(want)   # (q8_1's fp16 s overflows in the reference itself beyond |x| ~ 2e3)
+    assert fin.all() or t == ol.Q5_1
+    assert fin.any() and np.isfinite(got[fin]).all()
+    assert rel_err(got[fin], want[fin], absdot[fin]).max() < 1e-3

@@ -306,14 +306,23 @@ def test_gemm_dq16_rows_invariant(monkeypatch):
         assert np.array_equal(part, full[:, r0:r0 + rows]), (r0, rows)
 
 
-@pytest.mark.parametrize("case", ["tiny_scales", "large_activations", "extremes"])
+DQ_RANGE_CASES = ["tiny_scales", "large_activations", "huge_activations", "large_weights", "tiny_activations",
+                  "one_huge_column", "extremes"]
+
+
+@pytest.mark.parametrize("case", DQ_RANGE_CASES)
 def test_gemm_dq16_value_range(case, monkeypatch):
-    """dq16 folds the block scales into f16 operands: weights pre-scaled by 2^8 (exact) so block
-    scales down to ~1e-7 stay normal, activations as d_b * b (|x| < 65504, the f16 range).
-    tiny_scales: weight rows of magnitude 1e-5 (block scales ~1e-6); large_activations: rows
-    with |x| up to 3e4; extremes: all-max / all-min quants (q4 nibbles 0 / 15, q8 -127 / 127)."""
+    """dq16 folds the block scales into f16 operands (weights pre-scaled by 2^8, activations by 2^4).
+    Its range guard sends any tile whose scales leave f16's normal range, or whose
+    f16 operands overflow, to exact int8 block dots -- so every case stays finite and within the bar,
+    as the reference's exact kernels do (src/lamm_kernel_q8_0.hpp:50-117).
+    tiny_scales: weight rows of magnitude 1e-5 (block scales ~1e-6); large_activations: |x| up to 3e4;
+    huge_activations: |x| = 1e5 (d_b * b overflows f16); large_weights: |w| = 300 (q8_0 / q5_1
+    d_a * 2^8 * q overflows); tiny_activations: |x| ~ 1e-6 (d_b subnormal); one_huge_column: one
+    activation row of 1e5 among ordinary ones (only its tiles fall back); extremes: all-max / all-min
+    quants (q4 nibbles 0 / 15, q8 -127 / 127)."""
     monkeypatch.setenv("LAMM_GEMM_PATH", "dq16")
-    M, N, K = 128, 64, 1024
+    M, N, K = 256, 128, 1024
     rng = np.random.default_rng(3)
     a = rng.standard_normal((M, K), dtype=np.float32)
     b = rng.standard_normal((N, K), dtype=np.float32)
@@ -321,16 +330,55 @@ def test_gemm_dq16_value_range(case, monkeypatch):
         a *= 1e-5
     elif case == "large_activations":
         b *= 3e4 / np.abs(b).max()
+    elif case == "huge_activations":
+        b *= 1e5 / np.abs(b).max()
+    elif case == "large_weights":
+        a *= 300 / np.abs(a).max()
+    elif case == "tiny_activations":
+        b *= 1e-6
+    elif case == "one_huge_column":
+        b[70] *= 1e5 / np.abs(b[70]).max()
     else:
         a = np.where(np.arange(K) % 3 == 0, -1.0, 1.0).astype(np.float32) * np.ones((M, 1), np.float32)
         b = np.where(np.arange(K) % 2 == 0, 1.0, -1.0).astype(np.float32) * np.ones((N, 1), np.float32)
-    for t in (ol.Q4_0, ol.Q8_0):
+    for t in (ol.Q4_0, ol.Q5_1, ol.Q8_0):
+        vt = la.vec_dot_type(t)
         A_q = ORACLE.quantize(t, a, ol.QUANT_REF)
-        B_q = ORACLE.quantize(ol.Q8_0, b, ol.QUANT_AVX)
+        B_q = ORACLE.quantize(vt, b, ol.QUANT_AVX)
+        assert la.gemm_engine(t, M, N, K) == "dq16"
         c, _ = gpu_mul_mat(t, A_q, B_q, M, N, K)
         ref = ORACLE.mul_mat(t, M, N, K, A_q, B_q)
-        assert np.isfinite(c).all()
-        assert rel_err(c, ref, absdot(t, A_q, B_q, M, N, K)).max() < TOL, ol.NAMES[t]
+        # q8_1 keeps s = d * sum(q) as fp16: beyond |x| ~ 2e3 the reference's own q5_1 sums overflow there
+        fin = np.isfinite(ref)
+        assert fin.all() or vt == ol.Q8_1, ol.NAMES[t]
+        assert np.isfinite(c[fin]).all(), ol.NAMES[t]
+        if fin.any():
+            assert rel_err(c[fin], ref[fin], absdot(t, A_q, B_q, M, N, K)[fin]).max() < TOL, ol.NAMES[t]
+
+
+@pytest.mark.parametrize("t", [ol.Q5_1, ol.Q8_0], ids=["q5_1", "q8_0"])
+def test_gemm_default_engine_range(t):
+    """The DEFAULT engine of a q5_1 / q8_0 prefill call (dq16 at config-4 sizes) with weights of
+    magnitude 300 and activations of 1e5: finite and within the bar (its range guard's exact tiles)."""
+    M, N, K = 4096, 512, 1024
+    rng = np.random.default_rng(5)
+    a = rng.standard_normal((M, K), dtype=np.float32)
+    a *= 300 / np.abs(a).max()
+    b = rng.standard_normal((N, K), dtype=np.float32)
+    b[: N // 2] *= 1e5 / np.abs(b).max()
+    vt = la.vec_dot_type(t)
+    A_q = ORACLE.quantize(t, a, ol.QUANT_REF)
+    B_q = ORACLE.quantize(vt, b, ol.QUANT_AVX)
+    assert la.gemm_engine(t, M, N, K) == "dq16"
+    c, _ = gpu_mul_mat(t, A_q, B_q, M, N, K)
+    rows = np.random.default_rng(0).choice(M, 256, replace=False)
+    arow = la.row_bytes(t, K)
+    A_s = np.concatenate([A_q[r * arow:(r + 1) * arow] for r in rows])
+    ref = ORACLE.mul_mat(t, len(rows), N, K, A_s, B_q)
+    fin = np.isfinite(ref)   # (q8_1's fp16 s overflows in the reference itself beyond |x| ~ 2e3)
+    assert fin.all() or t == ol.Q5_1
+    assert fin.any() and np.isfinite(c[:, rows][fin]).all()
+    assert rel_err(c[:, rows][fin], ref[fin], absdot(t, A_s, B_q, len(rows), N, K)[fin]).max() < TOL
 
 
 @pytest.mark.parametrize("split", [1, 3, 8])

@@ -241,3 +241,26 @@ def test_reference_order_prefill_kernels_bit_exact(variant, t, shape, monkeypatc
     c = ref_mul_mat(t, A_q, B_q, M, N, K)[:N * M].reshape(N, M)
     want = ORACLE.mul_mat_avx(t, M, N, K, A_q, B_q)
     assert np.array_equal(bits(c), bits(want)), f"{(c != want).sum()} of {c.size} differ"
+
+
+FULL_SHAPES = [(4096, 512, 4096), (11008, 512, 4096)]
+
+
+@pytest.mark.parametrize("t", [ol.Q4_0, ol.Q4_1, ol.Q5_0, ol.Q5_1], ids=["q4_0", "q4_1", "q5_0", "q5_1"])
+@pytest.mark.parametrize("shape", FULL_SHAPES, ids=[f"{m}x{n}x{k}" for m, n, k in FULL_SHAPES])
+def test_reference_order_prefill_full_size(t, shape):
+    """The reference-order prefill kernel the boundary runs for a pp512 call (the swizzled ref_mfma2
+    for q4_0 / q4_1 / q5_0, ref_mfma for q5_1) at config 3's shape and at Llama-7B's ffn shape:
+    256 sampled weight rows x all 512 columns, bit for bit against the oracle's restatement of the
+    reference's AVX2 lane order."""
+    if t != ol.Q4_0 and shape[0] != 4096:
+        pytest.skip("the ffn shape runs for q4_0, Llama-7B's projection format")
+    M, N, K = shape
+    A_q, B_q = random_blocks(t, M, N, K, seed=M + N + K + t)
+    c = ref_mul_mat(t, A_q, B_q, M, N, K)[:N * M].reshape(N, M)
+    rows = np.sort(np.random.default_rng(M).choice(M, 256, replace=False))
+    arow = la.row_bytes(t, K)
+    A_s = np.concatenate([A_q[r * arow:(r + 1) * arow] for r in rows])
+    want = ORACLE.mul_mat_avx(t, len(rows), N, K, A_s, B_q)
+    got = c[:, rows]
+    assert np.array_equal(bits(got), bits(want)), f"{(got != want).sum()} of {got.size} differ"

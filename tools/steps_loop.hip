@@ -5,7 +5,7 @@
 //   lamm_steps_matmul_paced  : launches paced slower than the kernel, so a kernel tracer times
 //                              every dispatch on its own (no dispatch queued behind it to fold the
 //                              tracer's per-dispatch cost into)
-//   lamm_steps_isolated      : per-launch durations from the dispatches' own timestamps
+//   lamm_steps_isolated[_ex] : per-launch durations from the dispatches' own timestamps
 //                              (lamm_hip_profile_next), launches isolated or back to back --
 //                              what the kernel tracer reports for the same dispatch (bench.py's
 //                              roofline)
@@ -57,8 +57,8 @@ int lamm_steps_matmul_paced(const lamm_matrix* A, int nA, const lamm_matrix* B, 
 // out_us[i] = the dispatch's own duration (start / end timestamps of the kernel dispatch,
 // lamm_hip_profile_next -> hipExtLaunchKernel: what a kernel tracer reports) of launch i.
 // sync_each: each launch alone (completed before the next is issued); otherwise back to back.
-int lamm_steps_isolated(const lamm_matrix* A, int nA, const lamm_matrix* B, const lamm_matrix* C, int first,
-                        int launches, void* stream, float* out_us, int sync_each) {
+int lamm_steps_isolated_ex(const lamm_matrix* A, int nA, const lamm_matrix* B, const lamm_matrix* C, int first,
+                           int launches, void* stream, float* out_us, int sync_each, int flags) {
   const hipStream_t s = static_cast<hipStream_t>(stream);
   std::vector<hipEvent_t> e0(launches), e1(launches);
   int rc = LAMM_OK;
@@ -68,7 +68,7 @@ int lamm_steps_isolated(const lamm_matrix* A, int nA, const lamm_matrix* B, cons
   }
   for (int i = 0; i < launches && rc == LAMM_OK; ++i) {
     (void)lamm_hip_profile_next(e0[i], e1[i]);
-    rc = lamm_hip_matmul(&A[(first + i) % nA], B, C, stream);
+    rc = lamm_hip_matmul_ex(&A[(first + i) % nA], B, C, nullptr, flags, stream);
     if (sync_each && hipEventSynchronize(e1[i]) != hipSuccess) rc = -2;
   }
   if (hipStreamSynchronize(s) != hipSuccess && rc == LAMM_OK) rc = -2;
@@ -80,6 +80,12 @@ int lamm_steps_isolated(const lamm_matrix* A, int nA, const lamm_matrix* B, cons
     (void)hipEventDestroy(e1[i]);
   }
   return rc;
+}
+
+// the same with flags = 0 (lamm_hip_matmul)
+int lamm_steps_isolated(const lamm_matrix* A, int nA, const lamm_matrix* B, const lamm_matrix* C, int first,
+                        int launches, void* stream, float* out_us, int sync_each) {
+  return lamm_steps_isolated_ex(A, nA, B, C, first, launches, stream, out_us, sync_each, 0);
 }
 
 }  // extern "C"

@@ -456,6 +456,7 @@ struct ShardOpts {
   std::string comm_id;      // hex (2 * LAMM_COMM_ID_BYTES digits) or "auto" (world 1 only)
   std::string dump;
   std::string dump_q;       // the first projection's gathered output (identical inputs at any G)
+  bool graph = true;        // --no-graph: eager replays
 };
 
 int run_sharded(const ShardOpts& o, int type, int out_type, int N, int iters, int layers, bool stationary, bool tall) {
@@ -546,12 +547,12 @@ int run_sharded(const ShardOpts& o, int type, int out_type, int N, int iters, in
     hip_ok(hipSetDevice(r.dev), "hipSetDevice");
     hip_ok(hipStreamSynchronize(r.s), "warm-up");
   }
-  // one graph: the step on rank 0's stream, the other local ranks' streams forked from it.  More than
-  // 4 local ranks replay the step eagerly instead: capturing 8 streams joined by events at every
-  // all-gather sends the HIP runtime's graph code into unbounded recursion (one libamdhip64 frame
-  // calling itself until the stack is gone, with a 1 GiB stack as with 8 MiB; ROCm 7.2).  One
-  // process per GPU (--rank) always captures: it has one stream.
-  const bool graphed = R.size() <= 4;
+  // one graph: the step on rank 0's stream, the other local ranks' streams forked from it (any number
+  // of local ranks: the loopback all-gather joins the streams by fan-in / fan-out through rank 0's
+  // stream, every event waited on as soon as it is recorded -- round 4's all-pairs waits on reused
+  // events sent HIP's graph code into unbounded recursion at 8 ranks and forced eager replays there).
+  // --no-graph: eager replays.
+  const bool graphed = o.graph;
   if (!graphed) {
     printf("llama-matmul-bench: %zu local ranks: eager replays (no hipGraph)\n", R.size());
     step_sharded(R, comm, layers, N, tall);
@@ -720,7 +721,7 @@ int real_main(int argc, char** argv) {
     else if (a == "-i") iters = atoi(next());
     else if (a == "-l") layers = atoi(next());
     else if (a == "--output-type") out_type = parse_type(next());
-    else if (a == "--no-graph") graph = false;
+    else if (a == "--no-graph") graph = false, so.graph = false;
     else if (a == "-s") stationary = true;
     else if (a == "--unfused") g_fused = false;
     else if (a == "--batch-proj") batch_proj = true;

@@ -105,7 +105,7 @@ def _llama_logits(tmp_path, name, args):
 def test_llama_bench_sharded_decode_bitexact(tmp_path, tall):
     """Config 5 as north_star states it: every weight's rows sharded over the ranks
     (lamm_hip_shard_rows) with lamm_hip_allgather_rows after every projection, the whole step one
-    hipGraph.  Rehearsed on one GPU: 2, 3 and 8 local ranks on device 0 (the loopback exchange,
+    hipGraph (at every rank count).  Rehearsed on one GPU: 2, 3 and 8 local ranks on device 0 (the loopback exchange,
     event-ordered) and the RCCL path with one rank (--rank 0 --world 1): the decode step's logits
     must equal the one-rank run bit for bit (each output row is computed by the same kernel the
     same way whichever rank owns it)."""
@@ -116,6 +116,7 @@ def test_llama_bench_sharded_decode_bitexact(tmp_path, tall):
     for G in (2, 3, 8):
         dg, lg = _llama_logits(tmp_path, f"g{G}", ["--shard", str(G)] + extra)
         assert dg["world"] == G and dg["allgathers"] == d1["allgathers"]
+        assert dg["graph"] is True, f"{G} ranks: the step must be captured as one hipGraph (VERDICT r4 item 7)"
         np.testing.assert_array_equal(lg.view(np.uint32), l1.view(np.uint32), err_msg=f"{G} ranks")
     dr, lr = _llama_logits(tmp_path, "rccl1", ["--rank", "0", "--world", "1", "--comm-id", "auto"] + extra)
     np.testing.assert_array_equal(lr.view(np.uint32), l1.view(np.uint32), err_msg="RCCL, one rank")

@@ -157,8 +157,17 @@ void lamm_hip_weights_destroy(lamm_weights *W);
  * runs an M x N x K call of weight type `type` over `slices` A slices on, under the current
  * LAMM_* switches: "gemv" (decode GEMV), "gemv-groups" (GEMV launches of 8 columns), "dense"
  * (F32 / F16 GEMM), "superblock" (k-quant GEMM), "fp6" (block-scaled fp6 MFMA GEMM), "i8"
- * (MFMA-i8 GEMM); "" for an unsupported type or shape.  b_f32: B holds F32 rows (q8_0 / q8_1
- * activation types).  Host-only: no device is touched. */
+ * (MFMA-i8 GEMM), "dq16" (dequantizing f16 MFMA GEMM); "" for an unsupported type or shape.
+ * b_f32: B holds F32 rows (q8_0 / q8_1 activation types).  Host-only: no device is touched.
+ * The answer is for a call with flags = 0 (LAMM_ORDER_REFERENCE calls always run lamm_ref.hip's
+ * kernels), contiguous rows and a 4-byte aligned B (an unaligned q8_K B skips "superblock", an
+ * unaligned q8 B skips "dq16"): the engine an aligned, default-order call takes.
+ *
+ * Accuracy of the engines: every one computes each 32-element block dot exactly in integers and
+ * scales it in fp32 (the reference's arithmetic, its own order only under LAMM_ORDER_REFERENCE),
+ * except "dq16", which rounds each operand to f16 with its block scale folded in (<= 2^-10 relative
+ * per product, within the 1e-3 bar); its range guard recomputes, with exact block dots, every tile
+ * whose scales leave f16's normal range or whose operands overflow f16. */
 const char *lamm_hip_engine(int type, int64_t M, int N, int K, int slices, int stationary, int b_f32);
 
 /* Measurement hook: the next lamm_hip_matmul* call on this thread records the start and end of

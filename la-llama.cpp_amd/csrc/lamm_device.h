@@ -106,6 +106,13 @@ __device__ __forceinline__ float wave_sum(float x) {
   return (r0 + r1) + (r2 + r3);
 }
 
+// _mm256_cvtps_epi32 of an already rounded value: NaN and values outside int32 give INT_MIN (x86's
+// "integer indefinite"; v_cvt_i32_f32 would saturate instead) -- an id of inf (0 < amax < ~3.7e-37)
+// or NaN inputs then quantize to -128 after the packs, as on the reference's CPU
+__device__ __forceinline__ int avx_cvt_i32(float r) {
+  return (r >= -2147483648.f && r < 2147483648.f) ? (int)r : (int)0x80000000u;
+}
+
 // bit i (i<4) of x -> bit 4 of byte i  (the 5th quant bit of q5_0/q5_1)
 __device__ __forceinline__ uint32_t spread4_hi(uint32_t x4) {
   return ((x4 * 0x00204081u) & 0x01010101u) << 4;

@@ -108,7 +108,7 @@ __device__ __forceinline__ void stage_b_f32(SM& sm, const GemvArgs& p, const uns
       uint32_t qw = 0;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        int r = (int)__builtin_rintf(x[4 * k + e] * id);
+        int r = avx_cvt_i32(__builtin_rintf(x[4 * k + e] * id));
         r = r > 127 ? 127 : (r < -128 ? -128 : r);
         sum += r;
         qw |= (uint32_t)(r & 0xff) << (8 * e);

@@ -561,6 +561,13 @@ struct CallStats {
   std::vector<float> call_us, gap_us;
 };
 std::chrono::steady_clock::time_point g_last_return{};
+// per-call samples kept for the medians: the first kSamples, then a ring over them (bounded memory
+// in a long LAMM_HIP_STATS run)
+constexpr size_t kSamples = 1 << 16;
+void sample(std::vector<float>& v, uint64_t n, float x) {
+  if (v.size() < kSamples) v.push_back(x);
+  else v[n % kSamples] = x;
+}
 double median(std::vector<float> v) {
   if (v.empty()) return 0.0;
   std::nth_element(v.begin(), v.begin() + v.size() / 2, v.end());
@@ -586,7 +593,7 @@ struct StatScope {
   explicit StatScope(CallStats* cs) : c(cs), t0(std::chrono::steady_clock::now()), tp(t0) {
     if (c && g_last_return.time_since_epoch().count()) {
       const double gap = std::chrono::duration<double, std::micro>(t0 - g_last_return).count();
-      if (gap < 5000.0) c->gap_us.push_back((float)gap);
+      if (gap < 5000.0) sample(c->gap_us, c->calls, (float)gap);
     }
   }
   void phase(int k) {   // time since the previous mark -> phase k
@@ -599,9 +606,9 @@ struct StatScope {
     if (c) {
       g_last_return = std::chrono::steady_clock::now();
       const double us = std::chrono::duration<double, std::micro>(g_last_return - t0).count();
+      sample(c->call_us, c->calls, (float)us);
       c->calls++;
       c->us += us;
-      c->call_us.push_back((float)us);
     }
   }
 };
@@ -1139,11 +1146,20 @@ void pool_help(const void* dst, bool sleep) {
 
 // Whether a COMPUTE call is a pool node -- the same answer in every thread (shapes and knobs only).
 constexpr size_t kPoolMin = (size_t)1 << 20;
+// A pool node is one where thread 0 will post a job (every prefill-sized node used to
+// be one, and on nodes with no job -- ggml's own INIT, q8_K / F16 activations -- the helpers spun in
+// pool_help with LAMM_HIP_HELPERS' yield / sleep turned off): bit 1 with F32 rows the host
+// quantizer takes (the hostq condition of mul_mat_thread0), or bit 2 (the C scatter).
 bool pool_call(const ggml::compute_params* params, const ggml::tensor* dst) {
   if (!knobs().pool || params->nth < 2) return false;
+  const ggml::tensor* src0 = dst->src[0];
   const ggml::tensor* src1 = dst->src[1];
   const int64_t rows = src1->ne[1] * src1->ne[2] * src1->ne[3];
-  return rows > 8 && (size_t)dst->ne[0] * rows * sizeof(float) >= kPoolMin;
+  if (!(rows > 8 && (size_t)dst->ne[0] * rows * sizeof(float) >= kPoolMin)) return false;
+  const int vdt = vec_dot_type(src0->type);
+  const bool quant_job = (knobs().pool & 1) && src1->type != vdt && act_mode(src0, src1) == kGpuQuant &&
+                         host_quant_supported(vdt);
+  return quant_job || (knobs().pool & 2);
 }
 
 void mul_mat_thread0(const ggml::compute_params* params, ggml::tensor* dst, bool pool);

@@ -49,11 +49,11 @@ __attribute__((target_clones("arch=x86-64-v3", "default"))) void quant_q8(const 
     const i8 big = __builtin_elementwise_max(__builtin_elementwise_max(__builtin_bit_cast(i8, a[0]), __builtin_bit_cast(i8, a[1])),
                                              __builtin_elementwise_max(__builtin_bit_cast(i8, a[2]), __builtin_bit_cast(i8, a[3])));
     const bool finite = __builtin_reduce_max(big) < 0x7f800000;
-    const float d = amax / 127.f;
-    const float id = amax != 0.0f ? 127.f / amax : 0.0f;
+    float d = amax / 127.f;
+    float id = amax != 0.0f ? 127.f / amax : 0.0f;
     int8_t q[32];
     int s = 0;
-    if (finite) {   // |x id| <= 127 + 1 ulp: no saturation
+    if (finite && id < INFINITY) {   // |x id| <= 127 + 1 ulp: no saturation
       i8 rs = 0;
       for (int k = 0; k < 4; ++k) {
         const f8 t = v[k] * id + 12582912.f;   // two roundings (-ffp-contract=off): the product, then the integer
@@ -63,12 +63,34 @@ __attribute__((target_clones("arch=x86-64-v3", "default"))) void quant_q8(const 
         memcpy(q + 8 * k, &c, 8);
       }
       if (sum) s = __builtin_reduce_add(rs);
-    } else {   // cvtps_epi32 gives INT_MIN for NaN; packs saturate
+    } else {
+      // inf / NaN in the block, or 0 < amax < ~3.7e-37 (id = inf): the AVX2 code step by step
+      //  -- its amax reduction (_mm_max_ps(a, b) = a > b ? a : b, so a NaN's position
+      // decides), then _mm256_cvtps_epi32 (NaN / out of range -> INT_MIN) and the packs' saturation;
+      // q8_1's s sums the int32 values before the packs, wrapping (oracle/lamm_oracle.c quant_q8)
+      float mx[8], q4[4], r2[4];
+      for (int i = 0; i < 8; ++i) mx[i] = std::fabs(x[i]);
+      for (int u = 1; u < 4; ++u)
+        for (int i = 0; i < 8; ++i) {
+          const float b = std::fabs(x[8 * u + i]);
+          mx[i] = mx[i] > b ? mx[i] : b;
+        }
+      for (int i = 0; i < 4; ++i) q4[i] = mx[4 + i] > mx[i] ? mx[4 + i] : mx[i];
+      for (int i = 0; i < 4; ++i) {
+        const float b = q4[2 + (i & 1)];
+        r2[i] = q4[i] > b ? q4[i] : b;
+      }
+      const float am = r2[0] > r2[1] ? r2[0] : r2[1];
+      d = am / 127.f;
+      id = am != 0.0f ? 127.f / am : 0.0f;
+      uint32_t ws = 0;
       for (int j = 0; j < 32; ++j) {
         const float r = std::nearbyint(x[j] * id);
-        q[j] = r != r ? (int8_t)-128 : (int8_t)(r > 127.f ? 127 : r < -128.f ? -128 : (int)r);
-        s += q[j];
+        const int32_t iv = (r >= -2147483648.f && r < 2147483648.f) ? (int32_t)r : INT32_MIN;
+        ws += (uint32_t)iv;
+        q[j] = (int8_t)(iv > 127 ? 127 : iv < -128 ? -128 : iv);
       }
+      s = (int32_t)ws;
     }
     const uint16_t dh = to_f16(d);
     memcpy(y, &dh, 2);

@@ -52,7 +52,7 @@ __global__ __launch_bounds__(256) void quant_q8_32(const float* __restrict__ x, 
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const float s = v[k] * id;
-    int r = flavour == 1 ? (int)__builtin_rintf(s) : (int)roundf(s);
+    int r = flavour == 1 ? avx_cvt_i32(__builtin_rintf(s)) : (int)roundf(s);
     r = r > 127 ? 127 : (r < -128 ? -128 : r);
     q[k] = r;
     sum += r;

@@ -131,7 +131,7 @@ __device__ __forceinline__ void q8_from_f32(const uint32_t (&w)[32], uint32_t (&
     uint32_t qw = 0;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      int v = (int)__builtin_rintf(__builtin_bit_cast(float, w[4 * k + e]) * id);
+      int v = avx_cvt_i32(__builtin_rintf(__builtin_bit_cast(float, w[4 * k + e]) * id));
       v = v > 127 ? 127 : (v < -128 ? -128 : v);
       sum += v;
       qw |= (uint32_t)(v & 0xff) << (8 * e);
@@ -261,7 +261,7 @@ struct ActStageL {
       uint32_t qw = 0;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        int v = (int)__builtin_rintf(__builtin_bit_cast(float, w[4 * k + e]) * id);
+        int v = avx_cvt_i32(__builtin_rintf(__builtin_bit_cast(float, w[4 * k + e]) * id));
         v = v > 127 ? 127 : (v < -128 ? -128 : v);
         sum += v;
         qw |= (uint32_t)(v & 0xff) << (8 * e);

@@ -192,15 +192,34 @@ static void quant_q8(const float *x, uint8_t *blk, int flavour, int with_sum) {
   float d;
   int sum = 0;
   if (flavour == LO_QUANT_AVX) {
+    /* amax exactly as the AVX2 code reduces it (LC/ggml-quants.c:1286-1296): _mm_max_ps(a, b) is
+       a > b ? a : b per lane (the second operand when either is NaN), so a NaN block's amax
+       depends on where its NaNs sit -- restated step by step */
+    float m[8], q4[4], r[4];
+    for (int i = 0; i < 8; i++) m[i] = fabsf(x[i]);
+    for (int v = 1; v < 4; v++)
+      for (int i = 0; i < 8; i++) {
+        const float b = fabsf(x[8 * v + i]);
+        m[i] = m[i] > b ? m[i] : b;
+      }
+    for (int i = 0; i < 4; i++) q4[i] = m[4 + i] > m[i] ? m[4 + i] : m[i];   /* max(hi128, lo128) */
+    for (int i = 0; i < 4; i++) {                                           /* max(., movehl) */
+      const float b = q4[2 + (i & 1)];
+      r[i] = q4[i] > b ? q4[i] : b;
+    }
+    amax = r[0] > r[1] ? r[0] : r[1];                                       /* max_ss(., movehdup) */
     d = amax / 127.f;
     const float id = (amax != 0.0f) ? 127.f / amax : 0.0f;
+    uint32_t wsum = 0;   /* q8_1's s sums the int32 values before the packs, wrapping */
     for (int j = 0; j < 32; j++) {
-      int v = (int)rintf(x[j] * id);     /* _mm256_round_ps(_MM_ROUND_NEAREST) */
-      if (v > 127) v = 127;              /* packs saturation */
-      if (v < -128) v = -128;
-      qs[j] = (int8_t)v;
-      sum += v;
+      const float rv = rintf(x[j] * id);  /* _mm256_round_ps(_MM_ROUND_NEAREST) */
+      /* _mm256_cvtps_epi32: NaN and out-of-range values (an id of inf: amax below ~3.7e-37) give
+         INT_MIN, which the packs saturate to -128 */
+      const int32_t v = (rv >= -2147483648.f && rv < 2147483648.f) ? (int32_t)rv : INT32_MIN;
+      wsum += (uint32_t)v;
+      qs[j] = (int8_t)(v > 127 ? 127 : v < -128 ? -128 : v);   /* packs saturation */
     }
+    sum = (int32_t)wsum;
   } else {
     d = amax / ((1 << 7) - 1);
     const float id = d ? 1.0f / d : 0.0f;

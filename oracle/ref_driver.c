@@ -20,6 +20,10 @@
  * Usage:
  *   ref_driver gen   <type> <M> <N> <K> <nthreads> <A_f32.bin> <B_f32.bin> <out_prefix>
  *   ref_driver bench <type> <M> <N> <K> <nthreads> <iters> <budget_seconds>
+ *   ref_driver quant <type> <rows> <K> <x_f32.bin> <out.bin>
+ *         (quant: the type's from_float on each row -- the INIT quantizer of this build, e.g.
+ *         the AVX2 quantize_row_q8_0 / _q8_1 in the lamm3 build; pins the oracle's restatement
+ *         on edge inputs, tools/gen_golden_quant.py)
  * type is a ggml type name: f32 q4_0 q4_1 q5_0 q5_1 q8_0 q2_k (+ q4_k q5_k q6_k)
  */
 #include "ggml.h"
@@ -40,6 +44,7 @@ static enum ggml_type parse_type(const char *s) {
   if (!strcasecmp(s, "q5_0")) return GGML_TYPE_Q5_0;
   if (!strcasecmp(s, "q5_1")) return GGML_TYPE_Q5_1;
   if (!strcasecmp(s, "q8_0")) return GGML_TYPE_Q8_0;
+  if (!strcasecmp(s, "q8_1")) return GGML_TYPE_Q8_1;   /* activation type (quant mode) */
   if (!strcasecmp(s, "q2_k")) return GGML_TYPE_Q2_K;
   if (!strcasecmp(s, "q4_k")) return GGML_TYPE_Q4_K;   /* SURVEY §8f "next" formats */
   if (!strcasecmp(s, "q5_k")) return GGML_TYPE_Q5_K;
@@ -217,11 +222,27 @@ static int do_bench(int argc, char **argv) {
   return 0;
 }
 
+static int do_quant(int argc, char **argv) {
+  if (argc < 7) { fprintf(stderr, "quant: bad args\n"); return 2; }
+  enum ggml_type type = parse_type(argv[2]);
+  int rows = atoi(argv[3]), K = atoi(argv[4]);
+  float *x = read_file(argv[5], (size_t)rows * K * sizeof(float));
+  ggml_type_traits_t tr = ggml_internal_get_type_traits(type);
+  size_t row = ggml_row_size(type, K);
+  uint8_t *y = calloc((size_t)rows, row);
+  for (int r = 0; r < rows; r++) tr.from_float(x + (size_t)r * K, y + (size_t)r * row, K);
+  write_file(argv[6], "", y, (size_t)rows * row);
+  free(x);
+  free(y);
+  return 0;
+}
+
 int main(int argc, char **argv) {
   if (argc < 2) { fprintf(stderr, "usage: ref_driver gen|bench ...\n"); return 2; }
   ggml_time_init();
   if (!strcmp(argv[1], "gen")) return do_gen(argc, argv);
   if (!strcmp(argv[1], "bench")) return do_bench(argc, argv);
+  if (!strcmp(argv[1], "quant")) return do_quant(argc, argv);
   fprintf(stderr, "unknown mode %s\n", argv[1]);
   return 2;
 }

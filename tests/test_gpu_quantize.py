@@ -98,3 +98,18 @@ def test_weight_quantizer_kquants_constant_rows():
             q = gpu_quant(t, x, 0)
             d = o.dequantize(t, q, 2, K)
             assert np.allclose(d, c, rtol=2e-3, atol=0), (ol.NAMES[t], c, d[0, :4])
+
+
+@pytest.mark.parametrize("vt", [ol.Q8_0, ol.Q8_1], ids=["q8_0", "q8_1"])
+def test_quantizer_id_inf_blocks(vt):
+    """0 < amax < ~3.7e-37 makes the AVX2 flavour's id = 127 / amax infinite: x * id is inf (NaN
+    for zeros) and _mm256_cvtps_epi32 gives INT_MIN, -128 after the packs (v_cvt_i32_f32 would
+    saturate to INT_MAX instead) -- the device quantizer emulates the x86 conversion."""
+    o = ol.Oracle()
+    K = 1024
+    rng = np.random.default_rng(5)
+    x = (rng.standard_normal((3, K)) * 1e-38).astype(np.float32)
+    x[1, 32:64] = 0.0
+    x[1, 40] = 1e-39
+    x[2, ::3] = 0.0
+    assert np.array_equal(gpu_quant(vt, x, 1), o.quantize(vt, x, 1))

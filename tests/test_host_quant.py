@@ -3,6 +3,7 @@ the oracle's AVX2 from_float restatement (LC/ggml-quants.c:1277-1330 / :1505-157
 on the CPU (no device needed).  The prefill path (LAMM_HIP_POOL bit 1) uploads these bytes in
 place of ggml's INIT output / the device quantizer's, so they must be identical."""
 import ctypes
+import os
 import time
 
 import numpy as np
@@ -41,6 +42,19 @@ def cases(rng):
     yield "ties", t
     yield "tiny", (rng.standard_normal((4, k)) * 1e-30).astype(np.float32)   # subnormal d
     yield "huge", (rng.standard_normal((4, k)) * 1e35).astype(np.float32)
+    # 0 < amax < ~3.7e-37: id = 127 / amax is inf, x * id inf (or NaN for zeros) -> cvtps_epi32's
+    # INT_MIN -> -128 after the packs; q8_1's s from the wrapped int32 sum
+    u = (rng.standard_normal((4, k)) * 1e-38).astype(np.float32)
+    u[:, 32:64] = 0.0
+    u[:, 40] = 1e-39
+    yield "id_inf", u
+    # inf / NaN blocks: the AVX2 amax reduction's operand order decides where a NaN wins
+    n = rng.standard_normal((4, k), dtype=np.float32)
+    for blk in range(0, k // 32, 3):
+        n[blk % 4, 32 * blk + (blk * 7) % 32] = np.nan if blk % 2 else np.inf
+    n[1, 5] = -np.inf
+    n[2, 0:32] = np.nan
+    yield "nonfinite", n
 
 
 @pytest.mark.parametrize("t", Q8, ids=["q8_0", "q8_1"])
@@ -73,3 +87,17 @@ def test_host_quantize_rate():
         dt = min(dt, time.perf_counter() - t0)
         assert rc == 0
     print(f"host q8_0 quantize: {x.nbytes / dt / 1e9:.2f} GB/s of F32 on one thread")
+
+
+EDGE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "quant", "edge.npz")
+
+
+@pytest.mark.parametrize("t", Q8, ids=["q8_0", "q8_1"])
+def test_quantizers_match_reference_on_edge_inputs(t):
+    """The REAL reference's AVX2 from_float bytes (tools/gen_golden_quant.py: ref_driver_lamm3 quant)
+    on id = inf blocks, denormals, inf / NaN at every lane position: the oracle's restatement and the
+    host quantizer reproduce them byte for byte."""
+    z = np.load(EDGE, allow_pickle=False)
+    x, want = z["x"], z[ol.NAMES[t]]
+    assert np.array_equal(ORACLE.quantize(t, x, ol.QUANT_AVX), want)
+    assert np.array_equal(host_quant(t, x), want)

@@ -109,8 +109,8 @@ __device__ __forceinline__ void stage_b_f32(SM& sm, const GemvArgs& p, const uns
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         int r = avx_cvt_i32(__builtin_rintf(x[4 * k + e] * id));
+        sum = (int)((uint32_t)sum + (uint32_t)r);   // before the saturation, wrapping (AVX2 q8_1's s)
         r = r > 127 ? 127 : (r < -128 ? -128 : r);
-        sum += r;
         qw |= (uint32_t)(r & 0xff) << (8 * e);
       }
       sm.bq[j][swz(bi * 8 + k)] = qw;

@@ -53,14 +53,17 @@ __global__ __launch_bounds__(256) void quant_q8_32(const float* __restrict__ x, 
   for (int k = 0; k < 4; ++k) {
     const float s = v[k] * id;
     int r = flavour == 1 ? avx_cvt_i32(__builtin_rintf(s)) : (int)roundf(s);
+    const int raw = r;
     r = r > 127 ? 127 : (r < -128 ? -128 : r);
     q[k] = r;
-    sum += r;
+    // AVX2 q8_1: s sums the int32 values before the packs' saturation, wrapping (LC/ggml-quants.c
+    // :1562); the scalar reference sums the stored quants
+    sum = flavour == 1 ? (int)((uint32_t)sum + (uint32_t)raw) : sum + r;
   }
   if (Q81) {
-    sum += __shfl_xor(sum, 1);
-    sum += __shfl_xor(sum, 2);
-    sum += __shfl_xor(sum, 4);
+    sum = (int)((uint32_t)sum + (uint32_t)__shfl_xor(sum, 1));
+    sum = (int)((uint32_t)sum + (uint32_t)__shfl_xor(sum, 2));
+    sum = (int)((uint32_t)sum + (uint32_t)__shfl_xor(sum, 4));
   }
   if (!valid) return;
   unsigned char* blkp = y + j * ldy_bytes + b * (Q81 ? 36 : 34);

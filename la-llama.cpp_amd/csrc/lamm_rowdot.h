@@ -132,8 +132,8 @@ __device__ __forceinline__ void q8_from_f32(const uint32_t (&w)[32], uint32_t (&
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       int v = avx_cvt_i32(__builtin_rintf(__builtin_bit_cast(float, w[4 * k + e]) * id));
+      sum = (int)((uint32_t)sum + (uint32_t)v);   // before the saturation, wrapping (AVX2 q8_1's s)
       v = v > 127 ? 127 : (v < -128 ? -128 : v);
-      sum += v;
       qw |= (uint32_t)(v & 0xff) << (8 * e);
     }
     q[k] = qw;
@@ -262,8 +262,8 @@ struct ActStageL {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         int v = avx_cvt_i32(__builtin_rintf(__builtin_bit_cast(float, w[4 * k + e]) * id));
+        sum = (int)((uint32_t)sum + (uint32_t)v);   // before the saturation, wrapping (AVX2 q8_1's s)
         v = v > 127 ? 127 : (v < -128 ? -128 : v);
-        sum += v;
         qw |= (uint32_t)(v & 0xff) << (8 * e);
       }
       q[k] = qw;

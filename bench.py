@@ -464,7 +464,8 @@ def ref_order_kernels(ctx, fmt, M, N, K, steps):
                             max(steps, 100), 2)
     floor = M * N * K / 4 * 2 / (F32_VALU_PEAK_TFLOPS * 1e12)
     out["gemm"] = {"workload": f"{fmt.upper()}xQ8 GEMM M={M} N={N} K={K} (config 3), stationary weights",
-                   "kernel": "lamm::ref_mfma2_kernel<swizzled> (csrc/lamm_ref.hip)" if fmt in ("q4_0", "q4_1", "q5_0")
+                   "kernel": "lamm::ref_mfma2_kernel<swizzled, interleaved> (csrc/lamm_ref.hip)" if fmt in ("q4_0", "q5_0")
+                   else "lamm::ref_mfma2_kernel<swizzled> (csrc/lamm_ref.hip)" if fmt == "q4_1"
                    else "lamm::ref_mfma_kernel (csrc/lamm_ref.hip)",
                    "bound": "valu (the reference's fp32 lane chains)", "per_launch_us": round(kern * 1e6, 2),
                    "floor_us": round(floor * 1e6, 2), "frac": round(floor / kern, 4),

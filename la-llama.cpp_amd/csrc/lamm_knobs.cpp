@@ -63,6 +63,7 @@ Knobs* read_env() {
   k->zero_copy = !k->pinned || (zc && zc[0] == '0') ? 0 : zc && !strcmp(zc, "in") ? 1 : zc && !strcmp(zc, "out") ? 2 : 3;
   k->zero_copy_split = env_on("LAMM_HIP_ZERO_COPY_SPLIT");
   k->ref_mfma = env_int("LAMM_REF_MFMA", -1);
+  k->ref_gemv_bpt = env_int("LAMM_REF_GEMV_BPT", 2);
   k->helpers = env_int("LAMM_HIP_HELPERS", 0);
   k->pool = env_int("LAMM_HIP_POOL", 5);
   if (const char* e = getenv("LAMM_HIP_ORDER")) k->ref_order = strcmp(e, "fast") != 0;

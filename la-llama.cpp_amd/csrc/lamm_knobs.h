@@ -46,7 +46,10 @@ struct Knobs {
                                // 0 return at once (ggml's barrier spins on them), 1 wait here yielding,
                                // 2 wait here asleep (futex)
   int ref_mfma = -1;           // LAMM_REF_MFMA: reference-order prefill kernel (1: ref_mfma_kernel, 2 / 3 / 4: ref_mfma2
-                               // with 2 / 1 / 4 column groups, 5: 2 groups + swizzled image; unset: per format)
+                               // with 2 / 1 / 4 column groups, 5: 2 groups + swizzled image, 6: 5 with the chain
+                               // steps interleaved with the next group's MFMAs; unset: per format)
+  int ref_gemv_bpt = 2;        // LAMM_REF_GEMV_BPT: blocks per producer thread of ref_gemv_kernel (2: 512
+                               // threads per workgroup, 4: 256)
   bool ref_order = true;       // LAMM_HIP_ORDER=fast: the boundary runs the fast engines instead of the
                                // reference's float order (lamm_ref.hip) for the formats that have both
   int pool = 5;                // LAMM_HIP_POOL: what ggml's pool threads do for prefill-sized calls (bits):

@@ -273,7 +273,7 @@ __global__ __launch_bounds__(RR * 8) void ref_kernel(GemvArgs p) {
 // The activation column is staged once per workgroup (ActStage; F32 rows quantized there, ggml's
 // AVX2 from_float bit for bit -- the boundary's fused INIT).  The chunk's A loads for the next
 // chunk are in flight while the chains run.
-constexpr int GR = 8, GKC = 128, GNT = 256, GP = GKC + 4;   // rows, blocks per chunk, threads, LDS pitch
+constexpr int GR = 8, GKC = 128, GP = GKC + 4;   // rows, blocks per chunk, LDS pitch
 
 // dword at byte O of a register byte string, zero past its end (the last block's slack bytes)
 template <int O, int NW>
@@ -289,9 +289,22 @@ size_t ref_gemv_lds(int type, int nblk) {
   return (((size_t)nblk * 40 + 15) & ~size_t(15)) + sizeof(float) * GP * (GR * 8 + GR + (aff ? GR : 0));
 }
 
-template <int T, bool BF32, bool ONE_SLICE>
-__global__ __launch_bounds__(GNT) void ref_gemv_kernel(GemvArgs p) {
+#ifndef REF_GAB
+// probe builds only (ablations of ref_gemv_kernel): 1 no chains, 2 no producer arithmetic,
+// 3 no activation staging
+#define REF_GAB 0
+#endif
+template <int T, bool BF32, bool ONE_SLICE, int BPT = 4>
+__global__ __launch_bounds__(GR * GKC / BPT) void ref_gemv_kernel(GemvArgs p) {
   using F = RFmt<T>;
+  // BPT consecutive blocks of one row per producer thread (one wide load of BPT * BPB bytes, dword
+  // aligned: BPB is even); NT threads cover the chunk's GR x GKC blocks.  Config 2 (q4_0 4096 x 4096,
+  // F32 row, profiles/r05/ref_gemv/): BPT 2 (512 threads) 5.1-5.4 us, 4 (256) 5.9-6.0, 1 (1024
+  // threads, realigned 18-byte loads) 6.4-6.6 -- the producers' arithmetic runs after the one
+  // chunk's loads land, so more, shorter producer streams finish it sooner, until the realigning
+  // single-block loads cost more than they save
+  static_assert(BPT == 2 || BPT == 4, "blocks per producer thread");
+  constexpr int NT = GR * GKC / BPT, TPR = GKC / BPT;   // threads, threads per row
   constexpr bool AFF = T == kQ4_1 || T == kQ5_1;
   // -OFF as four int8: sum (q - OFF) b = sum q b + sum (-OFF) b, both exact
   constexpr uint32_t NEG = T == kQ4_0 ? 0xf8f8f8f8u : T == kQ5_0 ? 0xf0f0f0f0u : 0u;
@@ -319,25 +332,26 @@ __global__ __launch_bounds__(GNT) void ref_gemv_kernel(GemvArgs p) {
   const int nrows = p.M - row0 < GR ? p.M - row0 : GR;
   const auto ra = make_rsrc(Az + (int64_t)row0 * p.lda,
                             (uint32_t)(((int64_t)(nrows - 1) * p.lda + (int64_t)nb * F::BPB + 3) & ~int64_t(3)));
-  // producer: row pr, blocks 4 pg .. 4 pg + 3 of each chunk
-  const int pr = t >> 5, pg = t & 31;
-  uint32_t w[F::BPB];   // 4 blocks: 4 BPB bytes = BPB dwords, 16-byte aligned (4 BPB % 16 == 8 or 0)
+  // producer: row pr, blocks BPT pg .. BPT pg + BPT - 1 of each chunk
+  const int pr = t / TPR, pg = t % TPR;
+  uint32_t w[BPT * F::BPB / 4];   // BPT blocks: BPT BPB bytes
   auto issue = [&](int u0) {
-    const int u = u0 + 4 * pg;
+    const int u = u0 + BPT * pg;
     const uint32_t off = pr < nrows && u < nb ? (uint32_t)((int64_t)pr * p.lda + (int64_t)u * F::BPB) : 0x7ffffff0u;
-    load_words<F::BPB, 2>(ra, off, w);   // non-temporal: A is read once
+    load_words<BPT * F::BPB / 4, 2>(ra, off, w);   // non-temporal: A is read once
   };
   issue(0);
   // ---- the activation column, once per workgroup
   const auto rb = act_rsrc<T, 1, BF32>(p, Bz);
-  if constexpr (BF32) {
-    for (int it = t; it < 2 * nb; it += GNT) {   // two lanes per block (pairs stay together: GNT even)
+  if constexpr (REF_GAB == 3) {
+  } else if constexpr (BF32) {
+    for (int it = t; it < 2 * nb; it += NT) {   // two lanes per block (pairs stay together: NT even)
       ActStageL<T, 2> sl;
       sl.template load<1>(p, rb, it);
       sl.store(it, sq0, sq1, sbd, sbs);
     }
   } else {
-    for (int it = t; it < nb; it += GNT) {
+    for (int it = t; it < nb; it += NT) {
       ActStage<T, false> st;
       st.template load<1>(p, rb, it);
       st.store(it, sq0, sq1, sbd, sbs);
@@ -349,11 +363,19 @@ __global__ __launch_bounds__(GNT) void ref_gemv_kernel(GemvArgs p) {
   float chain = 0.f, summs = 0.f;
   for (int u0 = 0; u0 < nb; u0 += GKC) {
     // ---- producers: 4 blocks of row pr
-    {
-      f32x4 xv[8], dv, pv;
-      unroll<4>([&](auto J) {
+    typedef float fv __attribute__((ext_vector_type(BPT)));
+    if constexpr (REF_GAB == 2) {
+      fv xv;
+#pragma unroll
+      for (int j = 0; j < BPT; ++j) xv[j] = (float)w[j];
+#pragma unroll
+      for (int l = 0; l < 8; ++l) *reinterpret_cast<fv*>(&xs[(pr * 8 + l) * GP + BPT * pg]) = xv;
+      *reinterpret_cast<fv*>(&dsm[pr * GP + BPT * pg]) = xv;
+    } else {
+      fv xv[8], dv, pv;
+      unroll<BPT>([&](auto J) {
         constexpr int j = J;
-        const int u = u0 + 4 * pg + j;
+        const int u = u0 + BPT * pg + j;
         const bool ok = pr < nrows && u < nb;
         uint32_t m[F::BPB / 4 + 1];
         unroll<F::BPB / 4 + 1>([&](auto K) { m[K] = get32z<j * F::BPB + 4 * K>(w); });
@@ -378,15 +400,15 @@ __global__ __launch_bounds__(GNT) void ref_gemv_kernel(GemvArgs p) {
         }
       });
 #pragma unroll
-      for (int l = 0; l < 8; ++l) *reinterpret_cast<f32x4*>(&xs[(pr * 8 + l) * GP + 4 * pg]) = xv[l];
-      *reinterpret_cast<f32x4*>(&dsm[pr * GP + 4 * pg]) = dv;
-      if constexpr (AFF) *reinterpret_cast<f32x4*>(&pms[pr * GP + 4 * pg]) = pv;
+      for (int l = 0; l < 8; ++l) *reinterpret_cast<fv*>(&xs[(pr * 8 + l) * GP + BPT * pg]) = xv[l];
+      *reinterpret_cast<fv*>(&dsm[pr * GP + BPT * pg]) = dv;
+      if constexpr (AFF) *reinterpret_cast<fv*>(&pms[pr * GP + BPT * pg]) = pv;
     }
     if (u0 + GKC < nb) issue(u0 + GKC);   // the next chunk's A under the chains
     __syncthreads();
     // ---- chains: wave 0, the chunk's blocks in order (zeros past nb leave a chain unchanged:
     // fma(0, 0, acc) == acc, and no chain is ever -0)
-    if (t < 64) {
+    if (t < 64 && REF_GAB != 1) {
       // the whole chunk, always: the producers zero-filled it past nb, and a fixed trip count
       // lets the LDS reads run ahead of the chain instead of one wait per 4 blocks
       const float* xr = &xs[(cr * 8 + cl) * GP];
@@ -758,7 +780,12 @@ __global__ __launch_bounds__(MNT) void ref_mfma_kernel(GemvArgs p) {
 //     unswizzled stores hit 2 of the 64 banks' 16-dword groups: half the LDS cycles were
 //     conflicts, profiles/r04/ref_order/kernels/); the reads stay conflict-free (the swizzle
 //     only permutes a wave's 16-byte slots within each column).
-template <int T, int G, bool ONE_SLICE, bool SW = false>
+#ifndef REF_AB
+// probe builds only (ablations of the interleaved kernel, LAMM_REF_MFMA=6): 1 no chain steps, 2 no
+// weight unpacking, 3 no chunk refills after the first (every chunk computed from the first image)
+#define REF_AB 0
+#endif
+template <int T, int G, bool ONE_SLICE, bool SW = false, bool PIPE = false>
 __global__ __launch_bounds__(MNT) void ref_mfma2_kernel(GemvArgs p) {
   using F = RefFmt<T>;
   static_assert(F::UE == 32, "32-element block formats");
@@ -901,10 +928,12 @@ __global__ __launch_bounds__(MNT) void ref_mfma2_kernel(GemvArgs p) {
   fetch(0);
   for (int u0 = 0; u0 < nunits; u0 += MKB) {
     const int nu = nunits - u0 < MKB ? nunits - u0 : MKB;
-    if (u0 > 0) __syncthreads();   // every wave is done reading the previous chunk
-    commit(u0);
-    __syncthreads();
-    if (u0 + MKB < nunits) fetch(u0 + MKB);   // the next chunk's bytes fly under this one's math
+    if (!(PIPE && REF_AB == 3) || u0 == 0) {
+      if (u0 > 0) __syncthreads();   // every wave is done reading the previous chunk
+      commit(u0);
+      __syncthreads();
+      if (u0 + MKB < nunits) fetch(u0 + MKB);   // the next chunk's bytes fly under this one's math
+    }
     // swizzled: this lane's slot per block, recomputed every chunk (one v_xor per block) rather than
     // eight hoisted addresses held across the loop (VGPRs past 256: occupancy 1)
     int lbs = lb;
@@ -924,50 +953,106 @@ __global__ __launch_bounds__(MNT) void ref_mfma2_kernel(GemvArgs p) {
         whi[1] |= spread4_hi((qh >> (16 + 8 * h + 4)) & 0xfu);
       }
       uint32_t wf[2][4];
-      q4_to_f16<F::OFF>(wlo[0], wf[0][0], wf[0][1]);
-      q4_to_f16<F::OFF>(wlo[1], wf[0][2], wf[0][3]);
-      q4_to_f16<F::OFF>(whi[0], wf[1][0], wf[1][1]);
-      q4_to_f16<F::OFF>(whi[1], wf[1][2], wf[1][3]);
+      if constexpr (PIPE && REF_AB == 2) {
+        wf[0][0] = wf[0][1] = wlo[0]; wf[0][2] = wf[0][3] = wlo[1];
+        wf[1][0] = wf[1][1] = whi[0]; wf[1][2] = wf[1][3] = whi[1];
+      } else {
+        q4_to_f16<F::OFF>(wlo[0], wf[0][0], wf[0][1]);
+        q4_to_f16<F::OFF>(wlo[1], wf[0][2], wf[0][3]);
+        q4_to_f16<F::OFF>(whi[0], wf[1][0], wf[1][1]);
+        q4_to_f16<F::OFF>(whi[1], wf[1][2], wf[1][3]);
+      }
       const half8 W0 = __builtin_bit_cast(half8, u32x4{wf[0][0], wf[0][1], wf[0][2], wf[0][3]});
       const half8 W1 = __builtin_bit_cast(half8, u32x4{wf[1][0], wf[1][1], wf[1][2], wf[1][3]});
-#pragma unroll
-      for (int g = 0; g < G; ++g) {
-        const int nb = 8 * G * wn + 8 * g;
-        // half 1's slot is half 0's + 32: the swizzle (4 k < 32) leaves bit 5 alone
-        const uint32_t* bk = SW ? &blc[g * 8 * NPC + k * 64 + (lbs ^ (4 * k))] : &bl[g * 8 * NPC + k * 64];
-        const u32x4 a0 = *reinterpret_cast<const u32x4*>(bk);
-        const u32x4 a1 = *reinterpret_cast<const u32x4*>(bk + 32);
+      if constexpr (PIPE) {
+        // the chain steps of group g wait on that group's MFMAs; issue group g + 1's MFMAs between
+        // group g's two halves of chain steps so each half finds its MFMA result done (a half's
+        // results: 16 VGPRs; at most 3 halves live, +16 VGPRs over the plain order)
+        f32x16 S[G][2];
+        float d[G][4];
         const f32x16 zero = {};
-        const f32x16 S0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, a0), W0, zero, 0, 0, 0);
-        const f32x16 S1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, a1), W1, zero, 0, 0, 0);
+        auto issue = [&](int g, int q) {
+          const uint32_t* bk = SW ? &blc[g * 8 * NPC + k * 64 + (lbs ^ (4 * k))] : &bl[g * 8 * NPC + k * 64];
+          const u32x4 a = *reinterpret_cast<const u32x4*>(bk + 32 * q);
+          S[g][q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, a), q ? W1 : W0, zero, 0, 0, 0);
+        };
+        auto chains = [&](int g, int q) {
+          if constexpr (REF_AB == 1) {
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          float d = da * sdb[k][nb + 2 * c + h];
-          asm("" : "+v"(d));
-          // lanes e, e + 1 of a column share d: one packed fp32 fma per pair (v_pk_fma_f32, each
-          // element one IEEE fma -- the same bits as two v_fma_f32).  q4_1 / q5_0: single fmas
-          // (the packed form's register pairs push those kernels past 256 VGPRs: one wave per SIMD)
-          if constexpr (PK) {
-            const f32x2 d2 = {d, d};
+            for (int i = 0; i < 16; ++i) asm volatile("" ::"v"(S[g][q][i]));
+            return;
+          }
 #pragma unroll
-            for (int e = 0; e < 4; e += 2) {
-              const int i = 4 * c + e;
-              const f32x2 r0 = __builtin_elementwise_fma(d2, f32x2{S0[i], S0[i + 1]}, f32x2{acc[g][0][i], acc[g][0][i + 1]});
-              const f32x2 r1 = __builtin_elementwise_fma(d2, f32x2{S1[i], S1[i + 1]}, f32x2{acc[g][1][i], acc[g][1][i + 1]});
-              acc[g][0][i] = r0[0], acc[g][0][i + 1] = r0[1];
-              acc[g][1][i] = r1[0], acc[g][1][i + 1] = r1[1];
-            }
-          } else {
+          for (int c = 0; c < 4; ++c)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              acc[g][0][4 * c + e] = __builtin_fmaf(d, S0[4 * c + e], acc[g][0][4 * c + e]);
-              acc[g][1][4 * c + e] = __builtin_fmaf(d, S1[4 * c + e], acc[g][1][4 * c + e]);
+            for (int e = 0; e < 4; ++e)
+              acc[g][q][4 * c + e] = __builtin_fmaf(d[g][c], S[g][q][4 * c + e], acc[g][q][4 * c + e]);
+        };
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          const int nb = 8 * G * wn + 8 * g;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            d[g][c] = da * sdb[k][nb + 2 * c + h];
+            asm("" : "+v"(d[g][c]));
+            if constexpr (AFF) {
+              float pm = ma * ssb[k][nb + 2 * c + h];
+              asm("" : "+v"(pm));
+              summs[g][c] = summs[g][c] + pm;
             }
           }
-          if constexpr (AFF) {
-            float pm = ma * ssb[k][nb + 2 * c + h];
-            asm("" : "+v"(pm));
-            summs[g][c] = summs[g][c] + pm;
+        }
+        issue(0, 0);
+        issue(0, 1);
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          if (g + 1 < G) issue(g + 1, 0);
+          __builtin_amdgcn_sched_barrier(0);
+          chains(g, 0);
+          if (g + 1 < G) issue(g + 1, 1);
+          __builtin_amdgcn_sched_barrier(0);
+          chains(g, 1);
+        }
+      } else {
+  #pragma unroll
+        for (int g = 0; g < G; ++g) {
+          const int nb = 8 * G * wn + 8 * g;
+          // half 1's slot is half 0's + 32: the swizzle (4 k < 32) leaves bit 5 alone
+          const uint32_t* bk = SW ? &blc[g * 8 * NPC + k * 64 + (lbs ^ (4 * k))] : &bl[g * 8 * NPC + k * 64];
+          const u32x4 a0 = *reinterpret_cast<const u32x4*>(bk);
+          const u32x4 a1 = *reinterpret_cast<const u32x4*>(bk + 32);
+          const f32x16 zero = {};
+          const f32x16 S0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, a0), W0, zero, 0, 0, 0);
+          const f32x16 S1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, a1), W1, zero, 0, 0, 0);
+  #pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            float d = da * sdb[k][nb + 2 * c + h];
+            asm("" : "+v"(d));
+            // lanes e, e + 1 of a column share d: one packed fp32 fma per pair (v_pk_fma_f32, each
+            // element one IEEE fma -- the same bits as two v_fma_f32).  q4_1 / q5_0: single fmas
+            // (the packed form's register pairs push those kernels past 256 VGPRs: one wave per SIMD)
+            if constexpr (PK) {
+              const f32x2 d2 = {d, d};
+  #pragma unroll
+              for (int e = 0; e < 4; e += 2) {
+                const int i = 4 * c + e;
+                const f32x2 r0 = __builtin_elementwise_fma(d2, f32x2{S0[i], S0[i + 1]}, f32x2{acc[g][0][i], acc[g][0][i + 1]});
+                const f32x2 r1 = __builtin_elementwise_fma(d2, f32x2{S1[i], S1[i + 1]}, f32x2{acc[g][1][i], acc[g][1][i + 1]});
+                acc[g][0][i] = r0[0], acc[g][0][i + 1] = r0[1];
+                acc[g][1][i] = r1[0], acc[g][1][i + 1] = r1[1];
+              }
+            } else {
+  #pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                acc[g][0][4 * c + e] = __builtin_fmaf(d, S0[4 * c + e], acc[g][0][4 * c + e]);
+                acc[g][1][4 * c + e] = __builtin_fmaf(d, S1[4 * c + e], acc[g][1][4 * c + e]);
+              }
+            }
+            if constexpr (AFF) {
+              float pm = ma * ssb[k][nb + 2 * c + h];
+              asm("" : "+v"(pm));
+              summs[g][c] = summs[g][c] + pm;
+            }
           }
         }
       }
@@ -1195,17 +1280,22 @@ hipError_t launch_ref(int type, const GemvArgs& p, hipStream_t s) {
     const LaunchTiming tm = take_launch_timing();
     auto gov = [&](auto tc) {
       constexpr int T = decltype(tc)::value;
-      auto go3 = [&](auto kern) {
-        if (tm.start) hipExtLaunchKernelGGL(kern, g, dim3(GNT), lds, s, tm.start, tm.stop, 0, p);
-        else hipLaunchKernelGGL(kern, g, dim3(GNT), lds, s, p);
+      auto go3 = [&](auto kern, int nt) {
+        if (tm.start) hipExtLaunchKernelGGL(kern, g, dim3(nt), lds, s, tm.start, tm.stop, 0, p);
+        else hipLaunchKernelGGL(kern, g, dim3(nt), lds, s, p);
       };
-      if (p.b_f32) {
-        if (slices == 1) go3(ref_gemv_kernel<T, true, true>);
-        else go3(ref_gemv_kernel<T, true, false>);
-      } else {
-        if (slices == 1) go3(ref_gemv_kernel<T, false, true>);
-        else go3(ref_gemv_kernel<T, false, false>);
-      }
+      auto go2 = [&](auto bc) {
+        constexpr int BPT = decltype(bc)::value, nt = GR * GKC / BPT;
+        if (p.b_f32) {
+          if (slices == 1) go3(ref_gemv_kernel<T, true, true, BPT>, nt);
+          else go3(ref_gemv_kernel<T, true, false, BPT>, nt);
+        } else {
+          if (slices == 1) go3(ref_gemv_kernel<T, false, true, BPT>, nt);
+          else go3(ref_gemv_kernel<T, false, false, BPT>, nt);
+        }
+      };
+      if (knobs().ref_gemv_bpt == 4) go2(std::integral_constant<int, 4>{});
+      else go2(std::integral_constant<int, 2>{});
     };
     switch (type) {
       case kQ4_0: gov(std::integral_constant<int, kQ4_0>{}); break;
@@ -1240,10 +1330,11 @@ hipError_t launch_ref(int type, const GemvArgs& p, hipStream_t s) {
   if (p.N > 8 && type != kQ6_K) {
     // ref_mfma2_kernel, 2 column groups per wave (LAMM_REF_MFMA=4: 4 groups, one wave per SIMD; =1:
     // the unpipelined ref_mfma_kernel)
-    // default per format (tools/ref_ab.py, profiles/r04/ref_order/pk_fma/): the swizzled 2-group
-    // kernel for q4_0 / q4_1 / q5_0; q5_1's larger chunk keeps ref_mfma2 at one wave per SIMD, so
-    // it runs the unpipelined ref_mfma_kernel (205 vs 318 us at 4096 x 512 x 4096)
-    const int sel = knobs().ref_mfma > 0 ? knobs().ref_mfma : type == kQ5_1 ? 1 : 5;
+    // default per format (tools/ref_ab.py, profiles/r04/ref_order/pk_fma/, profiles/r05/ref_pipe/):
+    // the swizzled 2-group kernel with each group's chain steps behind the next group's MFMAs for
+    // q4_0 / q5_0 (6); q4_1 without that (its extra VGPRs cost a wave per SIMD: 5); q5_1's larger
+    // chunk keeps ref_mfma2 at one wave per SIMD, so it runs the unpipelined ref_mfma_kernel (1)
+    const int sel = knobs().ref_mfma > 0 ? knobs().ref_mfma : type == kQ5_1 ? 1 : type == kQ4_1 ? 5 : 6;
     const int mc = sel == 4 ? 64 : sel == 3 ? 16 : 32;   // 5: the 2-group kernel, swizzled image
     const dim3 gm((unsigned)((p.M + MR - 1) / MR), (unsigned)((p.N + mc - 1) / mc), (unsigned)slices);
     auto gom = [&](auto tc) {
@@ -1257,6 +1348,9 @@ hipError_t launch_ref(int type, const GemvArgs& p, hipStream_t s) {
       } else if (sel == 3) {   // one column group per wave (occupancy over reuse)
         if (slices == 1) hipLaunchKernelGGL((ref_mfma2_kernel<T, 1, true>), gm, dim3(MNT), 0, s, p);
         else hipLaunchKernelGGL((ref_mfma2_kernel<T, 1, false>), gm, dim3(MNT), 0, s, p);
+      } else if (sel == 6) {   // swizzled, chain steps interleaved with the next group's MFMAs
+        if (slices == 1) hipLaunchKernelGGL((ref_mfma2_kernel<T, 2, true, true, true>), gm, dim3(MNT), 0, s, p);
+        else hipLaunchKernelGGL((ref_mfma2_kernel<T, 2, false, true, true>), gm, dim3(MNT), 0, s, p);
       } else if (sel == 5) {
         if (slices == 1) hipLaunchKernelGGL((ref_mfma2_kernel<T, 2, true, true>), gm, dim3(MNT), 0, s, p);
         else hipLaunchKernelGGL((ref_mfma2_kernel<T, 2, false, true>), gm, dim3(MNT), 0, s, p);

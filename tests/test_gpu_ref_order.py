@@ -110,14 +110,18 @@ def test_reference_order_strides_and_slices(t):
 GEMV_TYPES = [ol.Q4_0, ol.Q4_1, ol.Q5_0, ol.Q5_1]
 
 
+@pytest.mark.parametrize("bpt", ["2", "4"])   # LAMM_REF_GEMV_BPT: blocks per producer thread
 @pytest.mark.parametrize("t", GEMV_TYPES, ids=[ol.NAMES[t] for t in GEMV_TYPES])
-@pytest.mark.parametrize("shape", [(1, 256), (67, 4096), (4096, 4096), (45, 11008), (9, 32 * 577)],
-                         ids=["1x256", "67x4096", "4096x4096", "45x11008", "9x18464"])
-def test_reference_order_gemv_f32_rows(t, shape):
+@pytest.mark.parametrize("shape", [(1, 256), (67, 4096), (4096, 4096), (45, 11008), (9, 32 * 577), (13, 4096 + 32 * 5)],
+                         ids=["1x256", "67x4096", "4096x4096", "45x11008", "9x18464", "13x4256"])
+def test_reference_order_gemv_f32_rows(t, shape, bpt, monkeypatch):
     """One F32 activation row (the boundary's decode calls, kFused): ref_gemv_kernel quantizes it
     in its staging the way ggml's AVX2 INIT does, then computes in the reference's order -- the
     same bits as quantizing with the oracle's AVX2 flavour and running mul_mat_avx.  Past 576
-    blocks the kernel declines F32 rows (LammError), as the boundary's routing expects."""
+    blocks the kernel declines F32 rows (LammError), as the boundary's routing expects.  Both
+    producer widths (2 or 4 blocks per thread: 512 / 256 threads per workgroup); 13x4256: an odd
+    block count (a partial last producer span)."""
+    monkeypatch.setenv("LAMM_REF_GEMV_BPT", bpt)
     M, K = shape
     rng = np.random.default_rng(M + K)
     A_q = ORACLE.quantize(t, rng.standard_normal((M, K), dtype=np.float32), ol.QUANT_REF)
@@ -225,7 +229,7 @@ def test_reference_order_rejects_other_types():
             la.mul_mat_torch(t, A, B, C, M, N, K, flags=la.ORDER_REFERENCE)
 
 
-PREFILL_KERNELS = ["1", "2", "3", "4", "5"]   # LAMM_REF_MFMA: ref_mfma / ref_mfma2 G=2 / G=1 / G=4 / G=2 swizzled
+PREFILL_KERNELS = ["1", "2", "3", "4", "5", "6"]   # LAMM_REF_MFMA: ref_mfma / ref_mfma2 G=2 / G=1 / G=4 / G=2 swizzled / + interleaved
 
 
 @pytest.mark.parametrize("variant", PREFILL_KERNELS)

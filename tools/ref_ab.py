@@ -52,8 +52,13 @@ la.lib.lamm_hip_profile_next.argtypes = [__import__("ctypes").c_void_p] * 2
 gen = torch.Generator(device="cuda")
 gen.manual_seed(7)
 out = {"lib": os.environ.get("LAMM_HIP_LIB", "default")}
+# REF_AB_ONLY=q4_0: only the 4096 x 4096 q4_0 shapes; REF_AB_SELS=5,6: only these prefill kernels
+ONLY = os.environ.get("REF_AB_ONLY")
+SELS = tuple(os.environ.get("REF_AB_SELS", "1,2,3,4,5,6").split(","))
 for fmt, M, K in (("q4_0", 4096, 4096), ("q4_0", 11008, 4096), ("q4_0", 4096, 11008), ("q4_1", 4096, 4096),
                   ("q5_0", 4096, 4096), ("q5_1", 4096, 4096), ("q6_k", 32000, 4096)):
+    if ONLY and (fmt != ONLY or M != 4096 or K != 4096):
+        continue
     t = la.BY_NAME[fmt]
     vt = la.vec_dot_type(t)
     A, _ = bench.make_weights(torch, la, fmt, 1, M, K, gen)
@@ -63,20 +68,24 @@ for fmt, M, K in (("q4_0", 4096, 4096), ("q4_0", 11008, 4096), ("q4_0", 4096, 11
         C = torch.zeros(M, dtype=torch.float32, device="cuda")
         Am, Bm, Cm = la.Matrix(A.data_ptr(), t, M, kb, kb), la.Matrix(x.data_ptr(), la.F32, K, 1, K), \
             la.Matrix(C.data_ptr(), la.F32, M, 1, M)
-        out[f"gemv_{fmt}_{M}x{K}_ref"] = dispatch_us(lambda: la.matmul_ex(Am, Bm, Cm, None, la.ORDER_REFERENCE, stream()))
+        for bpt in ("2", "4"):   # LAMM_REF_GEMV_BPT
+            os.environ["LAMM_REF_GEMV_BPT"] = bpt
+            out[f"gemv_{fmt}_{M}x{K}_ref{bpt}"] = dispatch_us(
+                lambda: la.matmul_ex(Am, Bm, Cm, None, la.ORDER_REFERENCE, stream()))
+        os.environ.pop("LAMM_REF_GEMV_BPT")
         out[f"gemv_{fmt}_{M}x{K}_fast"] = dispatch_us(lambda: la.matmul_ex(Am, Bm, Cm, None, 0, stream()))
     N = 512
     x = torch.randn(N, K, device="cuda", generator=gen)
     B = torch.zeros(N * la.row_bytes(vt, K) + 64, dtype=torch.uint8, device="cuda")
     la.quantize_torch(vt, x, B, flavour=1)
     C = torch.zeros(N * M, dtype=torch.float32, device="cuda")
-    for v in (("1", "2", "3", "4", "5") if fmt != "q6_k" else ("2",)):
+    for v in (SELS if fmt != "q6_k" else ("2",)):
         os.environ["LAMM_REF_MFMA"] = v
         out[f"gemm_{fmt}_{M}x{N}x{K}_ref_mfma{v}"] = events_us(
             lambda: la.mul_mat_torch(t, A, B, C, M, N, K, flags=la.ORDER_REFERENCE))
     os.environ.pop("LAMM_REF_MFMA")
     print(json.dumps(out), flush=True)
-for name, M, N, K in (("kq", 512, 512, 128), ("kqv", 128, 512, 512)):
+for name, M, N, K in (() if ONLY else (("kq", 512, 512, 128), ("kqv", 128, 512, 512))):
     H = 32
     A = (torch.randn(H * M * K, device="cuda", generator=gen) * 0.3).half().view(torch.uint8)
     Bh = torch.randn(H * N * K, device="cuda", generator=gen).half().view(torch.uint8)

@@ -830,9 +830,14 @@ class Runtime {
         }
         HIPCHK(hipHostFree(hbuf_[which]));
       }
-      // 2: the prefill pool's upload image (DMA only, not mapped)
+      // 2: the prefill pool's upload image (DMA only, not mapped); 0: activations, cached in the
+      // device's L2 (every launch's acquire drops stale lines); 1: C, non-coherent (written back
+      // by the kernel's end-of-kernel release) -- coherent under LAMM_HIP_C_WATCH=1, whose stores
+      // then go straight to host memory while watch_c spins on them
       const unsigned flags = which == 2 ? hipHostMallocPortable
-                                        : hipHostMallocMapped | hipHostMallocPortable | (which == 0 ? hipHostMallocNonCoherent : 0u);
+                                        : hipHostMallocMapped | hipHostMallocPortable |
+                                              (which == 0 || knobs().c_watch != 1 ? hipHostMallocNonCoherent
+                                                                                  : hipHostMallocCoherent);
       HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&hbuf_[which]), bytes + 256, flags));
       if (which != 2) HIPCHK(hipHostGetDevicePointer(&hdev_[which], hbuf_[which], 0));
       hcap_[which] = bytes;
@@ -935,8 +940,11 @@ bool boundary_ref_order(const ggml::tensor* src0) {
 //               lamm_gemv*.hip) -- no quantizer launch, no CPU INIT
 //   kGpuQuant : from 8 activation rows up: F32 rows up, lamm_hip_quantize (AVX2 flavour), then
 //               the GEMM engines (profiles/r01/e2e_gpu_quant.txt: Q4_0 4096x512x4096 528 -> 376 us)
-// LAMM_HIP_GPU_QUANT=0: always ggml's CPU INIT; =1: kGpuQuant for every row count;
-// LAMM_HIP_FUSED=0 turns kFused off (A/B).
+// LAMM_HIP_GPU_QUANT=0: always ggml's CPU INIT; =1: kGpuQuant for every row count.
+// kFused is opt-in since round 5 (LAMM_HIP_FUSED=1): through llama.cpp's decode every one of the
+// GEMV's 8 XCDs pulls the zero-copy F32 row (16 KiB) over PCIe into its own L2, where ggml's INIT
+// leaves 4.25 KiB of q8_0 -- the boundary call 24.4 -> 20.3 us in the reference order, 20.7 ->
+// 18.2 us in the fast order, tg +7 % (profiles/r05/decode_init/)
 enum ActMode { kCpuInit, kFused, kGpuQuant };
 ActMode act_mode(const ggml::tensor* src0, const ggml::tensor* src1) {
   const int vdt = vec_dot_type(src0->type);
@@ -1026,6 +1034,42 @@ void wait_device(Dev& d) {
     }
   }
   HIPCHK(hipStreamSynchronize(d.stream));
+}
+
+// Completion from C itself (LAMM_HIP_C_WATCH=1: coherent C, =2: non-coherent C, visible at the end-
+// of-kernel release; default 0: the signal launch): a decode-sized call whose C goes straight into
+// pinned host memory fills that C with a sentinel before the launch and spins until every word has
+// been overwritten -- no signal launch behind the matmul.  In llama.cpp's decode the one-lane signal
+// kernel shows 3.9 us of device time per call in the trace, but the boundary call measured the same
+// with either form (18.4-20.3 us, three alternating runs, profiles/r05/decode_init/): the flag lands
+// as soon as C does, so the signal is an A/B switch, not the default.  The sentinel is a
+// signalling NaN: every C word is the result of a float add (the kernels' final reduction), and
+// arithmetic never returns a signalling NaN, so no computed value can look unwritten.  Every word
+// is written exactly once, after the workgroup's reads of A and B (C depends on them), so the
+// activation buffer is free again when the last word lands.  After a second without progress the
+// stream is synchronised (which reports a fault) and C must then be complete.
+constexpr uint32_t kCSentinel = 0x7f80a5a5u;   // exponent all ones, quiet bit 0, payload != 0
+
+void watch_c(Dev& d, const unsigned char* c, size_t words) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(c);
+  const auto t0 = std::chrono::steady_clock::now();
+  size_t i = 0;
+  for (unsigned it = 0; i < words; ++it) {
+    if (__atomic_load_n(&w[i], __ATOMIC_ACQUIRE) != kCSentinel) {
+      ++i;
+      continue;
+    }
+    if ((it & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1)) {
+      HIPCHK(hipStreamSynchronize(d.stream));
+      for (; i < words; ++i)
+        if (__atomic_load_n(&w[i], __ATOMIC_ACQUIRE) == kCSentinel) {
+          fprintf(stderr, "lamm_hip: C word %zu of %zu was never written\n", i, words);
+          std::abort();
+        }
+      return;
+    }
+    __builtin_ia32_pause();
+  }
 }
 
 // Decode-sized calls read their activations from, and write C to, pinned host memory mapped into
@@ -1249,6 +1293,8 @@ void mul_mat_thread0(const ggml::compute_params* params, ggml::tensor* dst, bool
   const bool pipe = hostq && ref && weight && G == 1 && nslices == 1 && !zc_out && (knobs().pool & 4) &&
                     !(knobs().pool & 2) && N >= 64 && dst->nb[1] == (size_t)M * sizeof(float);
   const bool c_pool = pool && (knobs().pool & 2) && !zc_out && G == 1;   // C: pinned + the pool's scatter
+  // completion from C's own words (watch_c): one device, C zero-copy, decode-sized
+  const bool watch = zc_out && G == 1 && N <= 8 && spin_enabled() && knobs().c_watch;
   auto gather_f32 = [&](unsigned char* out) {   // F32 src1 rows (any strides) -> [slice][N][ldx]
     for (int64_t i13 = 0; i13 < ne13; ++i13)
       for (int64_t i12 = 0; i12 < ne12; ++i12)
@@ -1432,8 +1478,12 @@ void mul_mat_thread0(const ggml::compute_params* params, ggml::tensor* dst, bool
     const bool stationary = !ref && weight && N > gemv_max_n(t0) && (!b_f32 || N > 8) &&
                             ((gemm_fp6_supported(t0) && gemm_path(pa, true) == 0) ||
                              (gemm_kq_supported(t0) && knobs().kq_gemm));
+    if (watch) {   // the sentinel in every word of C before the launch (watch_c)
+      uint32_t* hc = reinterpret_cast<uint32_t*>(rt.pinned(1, c_bytes));
+      std::fill(hc, hc + c_bytes / sizeof(float), kCSentinel);
+    }
     Completion comp{d.done_ctr, d.flag_dev, 0, false};
-    if (zc_out && spin_enabled() && kernel_signal_enabled()) {   // nothing is queued behind the matmul
+    if (zc_out && spin_enabled() && kernel_signal_enabled() && !watch) {   // nothing is queued behind the matmul
       comp.seq = ++d.seq;
       g_completion = &comp;
     }
@@ -1466,9 +1516,13 @@ void mul_mat_thread0(const ggml::compute_params* params, ggml::tensor* dst, bool
     }
     stat.phase(4);
   }
-  for (int g = 0; g < G; ++g) {
-    HIPCHK(hipSetDevice(rt.devs[g].id));
-    wait_device(rt.devs[g]);
+  if (watch) {
+    watch_c(rt.devs[0], rt.pinned(1, c_bytes), c_bytes / sizeof(float));
+  } else {
+    for (int g = 0; g < G; ++g) {
+      HIPCHK(hipSetDevice(rt.devs[g].id));
+      wait_device(rt.devs[g]);
+    }
   }
   stat.phase(5);
   if (c_pool) {

@@ -56,9 +56,10 @@ Knobs* read_env() {
   k->views = env_on("LAMM_HIP_VIEWS") ? 1 : env_off("LAMM_HIP_VIEWS") ? 0 : -1;
   k->extra_types = !env_off("LAMM_HIP_EXTRA_TYPES");
   k->gpu_quant = env_on("LAMM_HIP_GPU_QUANT") ? 1 : env_off("LAMM_HIP_GPU_QUANT") ? 0 : -1;
-  k->fused = !env_off("LAMM_HIP_FUSED");
+  k->fused = env_on("LAMM_HIP_FUSED");
   k->spin = !env_off("LAMM_HIP_SPIN");
   k->kernel_signal = env_on("LAMM_HIP_KERNEL_SIGNAL");
+  k->c_watch = env_int("LAMM_HIP_C_WATCH", 0);
   const char* zc = getenv("LAMM_HIP_ZERO_COPY");
   k->zero_copy = !k->pinned || (zc && zc[0] == '0') ? 0 : zc && !strcmp(zc, "in") ? 1 : zc && !strcmp(zc, "out") ? 2 : 3;
   k->zero_copy_split = env_on("LAMM_HIP_ZERO_COPY_SPLIT");

@@ -37,8 +37,11 @@ struct Knobs {
   int views = -1;              // LAMM_HIP_VIEWS: 0 never, 1 always, -1 prefill only
   bool extra_types = true;     // LAMM_HIP_EXTRA_TYPES=0: only the reference's 7 pairs
   int gpu_quant = -1;          // LAMM_HIP_GPU_QUANT: 0 CPU INIT, 1 GPU for every row count
-  bool fused = true;           // LAMM_HIP_FUSED=0: no fused INIT in the decode GEMV
+  bool fused = false;          // LAMM_HIP_FUSED=1: the decode GEMV quantizes the F32 row itself (INIT claimed)
   bool spin = true;            // LAMM_HIP_SPIN=0: hipStreamSynchronize instead of the flag spin
+  int c_watch = 0;             // LAMM_HIP_C_WATCH=1|2: decode-sized zero-copy calls learn completion from
+                               // C's own words (lamm_hip.cpp watch_c; 1 coherent C, 2 non-coherent)
+                               // instead of from a signal launch behind the GEMV
   bool kernel_signal = false;  // LAMM_HIP_KERNEL_SIGNAL=1: the GEMV writes the completion flag
   int zero_copy = 3;           // LAMM_HIP_ZERO_COPY: 0 off, 1 in, 2 out, 3 both
   bool zero_copy_split = false;   // LAMM_HIP_ZERO_COPY_SPLIT=1: zero copy also when rows split over devices

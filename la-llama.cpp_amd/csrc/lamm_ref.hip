@@ -387,10 +387,12 @@ __global__ __launch_bounds__(GR * GKC / BPT) void ref_gemv_kernel(GemvArgs p) {
         const uint32_t bq[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
         float d = da * sbd[ub];
         asm("" : "+v"(d));   // rounded on its own: never contracted into the chain's fma
+        // past nb / nrows only d is zeroed: X is a finite integer whatever the (zero or clamped)
+        // operands, and fma(0, X, acc) == acc (no chain is ever -0)
 #pragma unroll
         for (int l = 0; l < 8; ++l) {
           const int c = NEG ? dot4(bq[l], NEG, 0) : 0;
-          xv[l][j] = ok ? (float)dot4(q[l], bq[l], c) : 0.f;
+          xv[l][j] = (float)dot4(q[l], bq[l], c);
         }
         dv[j] = ok ? d : 0.f;
         if constexpr (AFF) {

@@ -112,19 +112,22 @@ def test_non_compute_phases_and_unsupported(monkeypatch):
     p.type = la.TASK_FINALIZE
     assert not la.can_mul_mat(p, dst.t)
     p.type = la.TASK_INIT        # claimed whenever the GPU quantizes src1
-    # default (the reference's float order): a one-column call is quantized inside the
-    # one-column reference kernel (ggml's AVX2 INIT bytes), 2 .. 7 rows leave INIT to ggml as the
-    # reference does, and from 8 activation rows the GPU quantizer (the same bytes) takes it
-    assert la.can_mul_mat(p, dst.t)
+    # default: 1 .. 7 activation rows leave INIT to ggml as the reference does (decode: 4.25 KiB of
+    # q8_0 cross PCIe instead of the 16 KiB F32 row), and from 8 rows the GPU quantizer (the same
+    # bytes) takes it
+    assert not la.can_mul_mat(p, dst.t)
     src02, src12, _, _ = make_node(t, M, 2, K)
     assert not la.can_mul_mat(p, ggml_emu.mul_mat_node(src02, src12).t)
     src0r, src1r, _, _ = make_node(t, M, 8, K)
     assert la.can_mul_mat(p, ggml_emu.mul_mat_node(src0r, src1r).t)
-    monkeypatch.setenv("LAMM_HIP_ORDER", "fast")   # the fast engines: INIT fused into the GEMV
-    assert la.can_mul_mat(p, dst.t)              # decode-sized q4_0 -> fused into the GEMV
-    monkeypatch.setenv("LAMM_HIP_FUSED", "0")
-    assert not la.can_mul_mat(p, dst.t)          # N = 1 without fusion: ggml's CPU INIT
+    monkeypatch.setenv("LAMM_HIP_FUSED", "1")    # opt-in: the one-column GEMV quantizes the F32 row
+    assert la.can_mul_mat(p, dst.t)              # (reference order: ref_gemv_kernel's staging)
+    assert not la.can_mul_mat(p, ggml_emu.mul_mat_node(src02, src12).t)   # 2 rows: only the fast GEMVs
+    monkeypatch.setenv("LAMM_HIP_ORDER", "fast")
+    assert la.can_mul_mat(p, dst.t)
+    assert la.can_mul_mat(p, ggml_emu.mul_mat_node(src02, src12).t)
     monkeypatch.delenv("LAMM_HIP_FUSED")
+    assert not la.can_mul_mat(p, dst.t)          # N = 1 without fusion: ggml's CPU INIT
     monkeypatch.setenv("LAMM_HIP_GPU_QUANT", "1")
     assert la.can_mul_mat(p, dst.t)
     monkeypatch.setenv("LAMM_HIP_GPU_QUANT", "0")
@@ -302,8 +305,11 @@ def test_boundary_rows_split_over_devices(devices, t, M, N, K, quant, zc_split, 
         np.testing.assert_array_equal(d1.buf.view(np.float32).reshape(N, rows), got[:, r0:r0 + rows])
 
 
-DECODE_MODES = {"fused": {}, "cpu_init": {"LAMM_HIP_FUSED": "0"}, "device_copies": {"LAMM_HIP_ZERO_COPY": "0"},
-                "kernel_signal": {"LAMM_HIP_KERNEL_SIGNAL": "1"}, "no_spin": {"LAMM_HIP_SPIN": "0"}}
+DECODE_MODES = {"cpu_init": {}, "fused": {"LAMM_HIP_FUSED": "1"}, "device_copies": {"LAMM_HIP_ZERO_COPY": "0"},
+                "fused_watch": {"LAMM_HIP_FUSED": "1", "LAMM_HIP_C_WATCH": "1"},
+                "kernel_signal": {"LAMM_HIP_KERNEL_SIGNAL": "1"}, "watch_coherent": {"LAMM_HIP_C_WATCH": "1"},
+                "watch_noncoherent": {"LAMM_HIP_C_WATCH": "2"}, "no_spin": {"LAMM_HIP_SPIN": "0"}}
+DECODE_KEYS = ("LAMM_HIP_FUSED", "LAMM_HIP_ZERO_COPY", "LAMM_HIP_KERNEL_SIGNAL", "LAMM_HIP_SPIN", "LAMM_HIP_C_WATCH")
 
 
 @pytest.mark.parametrize("t", [ol.Q4_0, ol.Q4_1, ol.Q8_0, ol.Q6_K], ids=["q4_0", "q4_1", "q8_0", "q6_k"])
@@ -312,9 +318,10 @@ def test_decode_calls_fresh_every_call(t, monkeypatch):
     buffers with new contents every call (ggml's compute buffer is reused per token).  Modes:
     activations read in place from pinned host memory mapped into the device and C written back
     the same way (default), or copied by HIP (LAMM_HIP_ZERO_COPY=0); the activations quantized by
-    the GEMV (fused, default for q8_0 / q8_1 formats) or by ggml's CPU INIT (LAMM_HIP_FUSED=0);
-    completion by the signal launch (default), by the GEMV's own last workgroup
-    (LAMM_HIP_KERNEL_SIGNAL=1) or by hipStreamSynchronize (LAMM_HIP_SPIN=0).  The boundary re-reads
+    ggml's CPU INIT (default) or by the GEMV (LAMM_HIP_FUSED=1); completion by the signal launch
+    (default), seen in C's own words (LAMM_HIP_C_WATCH=1 coherent C / 2 non-coherent C), by the
+    GEMV's own last workgroup (LAMM_HIP_KERNEL_SIGNAL=1) or by hipStreamSynchronize
+    (LAMM_HIP_SPIN=0).  The boundary re-reads
     its switches at lamm_hip_boundary_reset (they used to be frozen at the first call).
     Every call must match the oracle, and every mode must give the same bits."""
     M, N, K = 4096, 1, 4096
@@ -329,7 +336,7 @@ def test_decode_calls_fresh_every_call(t, monkeypatch):
     results = {}
     try:
         for mode, env in DECODE_MODES.items():
-            for k in ("LAMM_HIP_FUSED", "LAMM_HIP_ZERO_COPY", "LAMM_HIP_KERNEL_SIGNAL", "LAMM_HIP_SPIN"):
+            for k in DECODE_KEYS:
                 monkeypatch.delenv(k, raising=False)
             for k, v in env.items():
                 monkeypatch.setenv(k, v)
@@ -349,10 +356,10 @@ def test_decode_calls_fresh_every_call(t, monkeypatch):
                 outs.append(got)
             results[mode] = np.stack(outs)
     finally:
-        for k in ("LAMM_HIP_FUSED", "LAMM_HIP_ZERO_COPY", "LAMM_HIP_KERNEL_SIGNAL", "LAMM_HIP_SPIN"):
+        for k in DECODE_KEYS:
             monkeypatch.delenv(k, raising=False)
         la.boundary_reset()
-    first = results["fused"].view(np.uint32)
+    first = results["cpu_init"].view(np.uint32)
     for mode, r in results.items():
         np.testing.assert_array_equal(r.view(np.uint32), first, err_msg=mode)
 

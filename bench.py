@@ -243,17 +243,9 @@ def isolated_launches(la, mats, R, Bm, Cm, n, sync_each=1, flags=0):
     """median duration (s) of n lamm_hip_matmul_ex dispatches from their own timestamps
     (lamm_hip_profile_next, tools/steps_loop.hip), each launched alone (sync_each) or back to back;
     None when the helper is not built or the kernel took no timestamps"""
-    global _STEPS_LIB
     import ctypes
-    path = os.path.join(ROOT, "tools", "libsteps_loop.so")
-    if _STEPS_LIB is None:
-        if not os.path.exists(path):
-            return None
-        _STEPS_LIB = ctypes.CDLL(path)
-        _STEPS_LIB.lamm_steps_isolated_ex.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(la.Matrix),
-                                                      ctypes.POINTER(la.Matrix), ctypes.c_int, ctypes.c_int,
-                                                      ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.c_int,
-                                                      ctypes.c_int]
+    if steps_lib(la) is None:
+        return None
     import torch
     arr = (la.Matrix * R)(*mats)
     out = (ctypes.c_float * n)()
@@ -267,6 +259,56 @@ def isolated_launches(la, mats, R, Bm, Cm, n, sync_each=1, flags=0):
         log("lamm_steps_isolated failed:", rc, v[:3])
         return None
     return v[n // 2] * 1e-6
+
+
+def steps_lib(la):
+    """tools/libsteps_loop.so (the C caller of the plug-in API), or None when it is not built"""
+    global _STEPS_LIB
+    import ctypes
+    path = os.path.join(ROOT, "tools", "libsteps_loop.so")
+    if _STEPS_LIB is None and os.path.exists(path):
+        _STEPS_LIB = ctypes.CDLL(path)
+        _STEPS_LIB.lamm_steps_isolated_ex.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(la.Matrix),
+                                                      ctypes.POINTER(la.Matrix), ctypes.c_int, ctypes.c_int,
+                                                      ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.c_int,
+                                                      ctypes.c_int]
+        _STEPS_LIB.lamm_steps_direct.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(la.Matrix),
+                                                 ctypes.POINTER(la.Matrix), ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                 ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
+    return _STEPS_LIB
+
+
+def time_direct(ctx, mats, R, Bm, Cm, steps, warmup, flags=0):
+    """The K steps on the library's own AQL queue (lamm_hip_direct_begin / end, tools/steps_loop.hip
+    lamm_steps_direct: K lamm_hip_matmul_ex calls from C in one direct region, returning once the
+    last kernel completed), between the same barrier + synchronize brackets as time_steps.  Returns
+    wall seconds per step (max over ranks), or None when a call did not dispatch directly."""
+    import ctypes
+    torch, la = ctx.torch, ctx.la
+    lib = steps_lib(la)
+    if lib is None:
+        return None
+    arr = (la.Matrix * R)(*mats)
+    dev = torch.cuda.current_device()
+    wall_us = ctypes.c_double()
+    torch.cuda.synchronize()
+    n = lib.lamm_steps_direct(ctypes.cast(arr, ctypes.c_void_p), R, ctypes.byref(Bm), ctypes.byref(Cm), 0,
+                              max(warmup, 1), dev, flags, ctypes.byref(wall_us))
+    if n != max(warmup, 1):
+        log("direct dispatch unavailable:", n, la.last_error())
+        return None
+    ctx.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    n = lib.lamm_steps_direct(ctypes.cast(arr, ctypes.c_void_p), R, ctypes.byref(Bm), ctypes.byref(Cm),
+                              max(warmup, 1), steps, dev, flags, ctypes.byref(wall_us))
+    torch.cuda.synchronize()
+    ctx.barrier()
+    wall = time.perf_counter() - t0
+    if n != steps:
+        log("direct dispatch: only", n, "of", steps, "steps dispatched directly")
+        return None
+    return ctx.max(wall / steps, 0.0)[0]
 
 
 def config2_gemv(ctx, fmt, M, K, steps, warmup):
@@ -305,6 +347,9 @@ def config2_gemv(ctx, fmt, M, K, steps, warmup):
         ctx.allgather_rows(C, M, 1, ALIGN, torch.cuda.current_stream().cuda_stream)
 
     per_step, ev_step, graphed = time_steps(ctx, step, steps, warmup, graph=not ctx.rehearse)
+    # one GPU: the same K steps dispatched on the library's own AQL queue (no collective to order
+    # against), reported beside the graph replay as value_direct
+    direct = time_direct(ctx, mats, R, Bm, Cm, steps, warmup) if ctx.world == 1 else None
     last = warmup + steps - 1
     torch.cuda.synchronize()
     gathered = C.clone()      # C after the last timed step (copy last % R)
@@ -341,7 +386,8 @@ def config2_gemv(ctx, fmt, M, K, steps, warmup):
     else:
         _, kern, _ = time_steps(ctx, gemv, max(steps, 1000), 3)
         kern_method = "HIP events over 1000 back-to-back hipGraph-replayed launches on their stream"
-    res = dict(per_step=per_step, ev_step=ev_step, kern=kern, kern_method=kern_method, kern_b2b=b2b, graphed=graphed,
+    res = dict(per_step=per_step, direct_step=direct, ev_step=ev_step, kern=kern,
+               kern_method=kern_method, kern_b2b=b2b, graphed=graphed,
                R=R, rows=rows,
                slab_bytes=slab_bytes + la.row_bytes(vt, K) + 4 * rows, gather_check=check, sample=sample)
     del A, B, C
@@ -736,6 +782,10 @@ def main():
                                   ((" + all-gather through gloo (one-GPU rehearsal)" if ctx.rehearse else
                                     " + lamm_hip_allgather_rows (RCCL)") if world > 1 else ""),
                    "timing": "hipGraph of the K steps, replayed" if g["graphed"] else "eager launches"},
+        # the same K steps as K calls from C on the library's own AQL queue (lamm_hip_direct_begin /
+        # end: one packet per call, one completion signal for the region), same brackets
+        "value_direct": round(unit / g["direct_step"] / 1e9, 2) if g["direct_step"] else None,
+        "ms_per_step_direct": round(g["direct_step"] * 1e3, 5) if g["direct_step"] else None,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic.get("bytes_per_launch") if traffic and traffic.get(

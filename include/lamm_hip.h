@@ -179,6 +179,21 @@ const char *lamm_hip_engine(int type, int64_t M, int N, int K, int slices, int s
  * stream around the call's launches.  The request expires with that call either way. */
 int lamm_hip_profile_next(void *start_event, void *stop_event);
 
+/* Direct dispatch (round 5): between lamm_hip_direct_begin(device) and lamm_hip_direct_end() the
+ * one-kernel decode GEMVs this thread launches (the block-format flat GEMV of config 2 and the
+ * reference-order GEMV) are written as AQL packets into the library's own user-mode queue on that
+ * device instead of going through HIP -- no hipLaunchKernel, no signal launch; the stream argument
+ * of the calls in between is not used for them, and any other kernel still goes to its stream.
+ * Inputs must be ready when the region opens (drain the streams that produced them).  end waits
+ * until every dispatched kernel completed (the command processor's completion signal) and returns
+ * how many were dispatched directly (0: every launch went through HIP); begin returns LAMM_OK,
+ * LAMM_ERR_NODEV for a device index out of range, or LAMM_ERR_HIP when the queue is not available
+ * (ROCr's loader extension missing, a region already open on this thread); end without an open
+ * region returns -LAMM_ERR_HIP.  The ggml boundary can use it for decode-sized calls
+ * (LAMM_HIP_DIRECT=1; off by default, it measured no faster there). */
+int lamm_hip_direct_begin(int device);
+int lamm_hip_direct_end(void);
+
 const char *lamm_hip_last_error(void);
 int lamm_hip_device_count(void);
 /* Provenance: hash (sha256, 16 hex digits) of the sources this library was built from. */

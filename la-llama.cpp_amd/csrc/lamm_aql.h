@@ -1,0 +1,20 @@
+// lamm_aql.h -- direct dispatch on the library's own AQL queue (lamm_aql.cpp)
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+namespace lamm {
+
+// Open a direct region on this thread for HIP device `device` (false: no queue, or one is open).
+bool direct_begin(int device);
+// Close it: wait until every kernel dispatched in it completed (abort after `seconds`); returns
+// the number of direct launches the region made (0: everything went through HIP).
+int direct_end(double seconds = 1.0);
+bool direct_active();
+// Dispatch kernel `fn` (its host stub) with explicit arguments [args, args + bytes) when a region
+// is open and the kernel's layout checks out; false: the caller launches through HIP.
+bool direct_launch(const void* fn, dim3 grid, dim3 block, uint32_t dyn_lds, const void* args, size_t bytes);
+
+}  // namespace lamm

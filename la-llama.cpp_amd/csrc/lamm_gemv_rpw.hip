@@ -16,6 +16,7 @@
 // Bytes per call are the algorithmic A + B + C (A streamed once, non-temporal).
 #include <hip/hip_ext.h>
 
+#include "lamm_aql.h"
 #include "lamm_rowdot.h"
 
 #include <cstdlib>
@@ -550,6 +551,18 @@ hipError_t launch_rpw_nc(const GemvArgs& p, hipStream_t s, int waves) {
                                      p.C, lda, p.M);
           return hipGetLastError();
         }
+        // direct region open (lamm_aql.cpp): the library's own queue; the explicit arguments as the
+        // kernel declares them
+        struct {
+          const unsigned char* A;
+          const unsigned char* B;
+          float* C;
+          uint32_t lda;
+          int M;
+        } a{p.A, p.B, p.C, lda, p.M};
+        const void* fn = bf ? reinterpret_cast<const void*>(gemv_flat1_kernel<T, true>)
+                            : reinterpret_cast<const void*>(gemv_flat1_kernel<T, false>);
+        if (direct_launch(fn, g, dim3(512), 0, &a, sizeof a)) return hipSuccess;
         if (bf) hipLaunchKernelGGL((gemv_flat1_kernel<T, true>), g, dim3(512), 0, s, p.A, p.B, p.C, lda, p.M);
         else hipLaunchKernelGGL((gemv_flat1_kernel<T, false>), g, dim3(512), 0, s, p.A, p.B, p.C, lda, p.M);
         return hipGetLastError();

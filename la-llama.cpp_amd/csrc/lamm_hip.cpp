@@ -28,6 +28,7 @@
 
 #include "../../include/lamm_hip.h"
 #include "ggml_b2430_abi.h"
+#include "lamm_aql.h"
 #include "lamm_formats.h"
 #include "lamm_kernels.h"
 #include "lamm_knobs.h"
@@ -393,6 +394,19 @@ extern "C" int lamm_hip_profile_next(void* start_event, void* stop_event) {
   return LAMM_OK;
 }
 
+extern "C" int lamm_hip_direct_begin(int device) {
+  const std::vector<int>& ids = probe().ids;
+  if (std::find(ids.begin(), ids.end(), device) == ids.end())
+    return fail(LAMM_ERR_NODEV, "lamm_hip_direct_begin: no gfx950 device %d", device);
+  if (!lamm::direct_begin(device)) return fail(LAMM_ERR_HIP, "lamm_hip_direct_begin: no direct queue on device %d", device);
+  return LAMM_OK;
+}
+
+extern "C" int lamm_hip_direct_end(void) {
+  if (!lamm::direct_active()) return -fail(LAMM_ERR_HIP, "lamm_hip_direct_end: no region open");
+  return lamm::direct_end();
+}
+
 extern "C" int lamm_hip_matmul_batched(const lamm_matrix* A, const lamm_matrix* B, const lamm_matrix* C,
                                        const lamm_batch* batch, void* hip_stream) {
   return matmul_impl(A, B, C, batch, hip_stream, nullptr);
@@ -629,6 +643,7 @@ struct Dev {
   unsigned seq = 0;
   unsigned* done_ctr = nullptr;   // device counter for the GEMV's own completion signal
   unsigned pending = 0;           // seq the last call's kernel signals itself (0: none)
+  bool enqueued = false;          // an upload went onto `stream` since the last direct region (lamm_aql.cpp)
   std::unordered_map<WeightKey, WeightEntry, WeightKeyHash> cache;
   std::list<WeightKey> lru;
   size_t cached = 0;
@@ -672,6 +687,7 @@ struct Transient {
   size_t s2, s3;
 };
 Transient upload_transient(Dev& d, const ggml::tensor* src0, size_t row_bytes) {
+  d.enqueued = true;
   const int64_t ne1 = src0->ne[1], ne2 = src0->ne[2], ne3 = src0->ne[3];
   const size_t nb1 = src0->nb[1], nb2 = src0->nb[2], nb3 = src0->nb[3];
   const auto* host = static_cast<const unsigned char*>(src0->data);
@@ -783,6 +799,7 @@ class Runtime {
       d.evict(it);
     }
     WeightEntry e;
+    d.enqueued = true;   // the upload below goes onto d.stream
     const size_t bpb = block_bytes(k.type);
     size_t pitch_blocks = (size_t)k.kb;
     while ((pitch_blocks * bpb) % 16) ++pitch_blocks;
@@ -1295,6 +1312,14 @@ void mul_mat_thread0(const ggml::compute_params* params, ggml::tensor* dst, bool
   const bool c_pool = pool && (knobs().pool & 2) && !zc_out && G == 1;   // C: pinned + the pool's scatter
   // completion from C's own words (watch_c): one device, C zero-copy, decode-sized
   const bool watch = zc_out && G == 1 && N <= 8 && spin_enabled() && knobs().c_watch;
+  // LAMM_HIP_DIRECT=1: decode-sized, everything in place in pinned memory, one device -- the GEMV
+  // goes onto the library's own AQL queue (lamm_aql.cpp), its completion signal replaces the signal
+  // launch.  Off by default: through llama.cpp's decode it measured 22.5-23 us per call against
+  // 20.3-21.1 through HIP (the host's launch cost drops 3 -> 0.6 us, the device wait grows by more;
+  // profiles/r05/direct/)
+  const bool direct = G == 1 && zc_in && zc_out && N <= 8 && act != kGpuQuant && spin_enabled() && knobs().direct &&
+                      !kernel_signal_enabled() && !watch;
+  bool in_direct = false;
   auto gather_f32 = [&](unsigned char* out) {   // F32 src1 rows (any strides) -> [slice][N][ldx]
     for (int64_t i13 = 0; i13 < ne13; ++i13)
       for (int64_t i12 = 0; i12 < ne12; ++i12)
@@ -1478,6 +1503,11 @@ void mul_mat_thread0(const ggml::compute_params* params, ggml::tensor* dst, bool
     const bool stationary = !ref && weight && N > gemv_max_n(t0) && (!b_f32 || N > 8) &&
                             ((gemm_fp6_supported(t0) && gemm_path(pa, true) == 0) ||
                              (gemm_kq_supported(t0) && knobs().kq_gemm));
+    if (direct) {   // the direct queue runs beside d.stream: nothing may still be in flight there
+      if (d.enqueued) HIPCHK(hipStreamSynchronize(s));
+      d.enqueued = false;
+      in_direct = lamm::direct_begin(d.id);
+    }
     if (watch) {   // the sentinel in every word of C before the launch (watch_c)
       uint32_t* hc = reinterpret_cast<uint32_t*>(rt.pinned(1, c_bytes));
       std::fill(hc, hc + c_bytes / sizeof(float), kCSentinel);
@@ -1516,7 +1546,9 @@ void mul_mat_thread0(const ggml::compute_params* params, ggml::tensor* dst, bool
     }
     stat.phase(4);
   }
-  if (watch) {
+  if (in_direct && lamm::direct_end() > 0) {
+    // completed on the direct queue (direct_end waited for its completion signal)
+  } else if (watch) {
     watch_c(rt.devs[0], rt.pinned(1, c_bytes), c_bytes / sizeof(float));
   } else {
     for (int g = 0; g < G; ++g) {

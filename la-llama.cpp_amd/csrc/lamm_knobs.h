@@ -39,6 +39,9 @@ struct Knobs {
   int gpu_quant = -1;          // LAMM_HIP_GPU_QUANT: 0 CPU INIT, 1 GPU for every row count
   bool fused = false;          // LAMM_HIP_FUSED=1: the decode GEMV quantizes the F32 row itself (INIT claimed)
   bool spin = true;            // LAMM_HIP_SPIN=0: hipStreamSynchronize instead of the flag spin
+  bool aql_host_karg = false;  // LAMM_AQL_HOSTKARG=1: the direct queue's kernargs in host memory (A/B)
+  bool direct = false;         // LAMM_HIP_DIRECT=1: decode-sized boundary calls dispatch on the library's
+                               // own AQL queue (lamm_aql.cpp) instead of launching through HIP
   int c_watch = 0;             // LAMM_HIP_C_WATCH=1|2: decode-sized zero-copy calls learn completion from
                                // C's own words (lamm_hip.cpp watch_c; 1 coherent C, 2 non-coherent)
                                // instead of from a signal launch behind the GEMV

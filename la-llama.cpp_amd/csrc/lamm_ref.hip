@@ -33,6 +33,7 @@
 // q - 16, q - 32) so each X_l is one v_dot4 -- integer, exact, any order.
 #include <hip/hip_ext.h>
 
+#include "lamm_aql.h"
 #include "lamm_device.h"
 #include "lamm_kernels.h"
 #include "lamm_rowdot.h"
@@ -1284,7 +1285,8 @@ hipError_t launch_ref(int type, const GemvArgs& p, hipStream_t s) {
       constexpr int T = decltype(tc)::value;
       auto go3 = [&](auto kern, int nt) {
         if (tm.start) hipExtLaunchKernelGGL(kern, g, dim3(nt), lds, s, tm.start, tm.stop, 0, p);
-        else hipLaunchKernelGGL(kern, g, dim3(nt), lds, s, p);
+        else if (!direct_launch(reinterpret_cast<const void*>(kern), g, dim3(nt), (uint32_t)lds, &p, sizeof p))
+          hipLaunchKernelGGL(kern, g, dim3(nt), lds, s, p);   // (direct: the library's own queue, lamm_aql.cpp)
       };
       auto go2 = [&](auto bc) {
         constexpr int BPT = decltype(bc)::value, nt = GR * GKC / BPT;

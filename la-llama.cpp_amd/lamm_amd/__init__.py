@@ -137,6 +137,9 @@ lib.lamm_hip_comm_last_error.restype = ctypes.c_char_p
 lib.lamm_hip_allgather_rows.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_int64),
                                         ctypes.POINTER(ctypes.c_void_p), ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
                                         ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
+lib.lamm_hip_direct_begin.restype = ctypes.c_int
+lib.lamm_hip_direct_begin.argtypes = [ctypes.c_int]
+lib.lamm_hip_direct_end.restype = ctypes.c_int
 lib.lamm_hip_cache_clear.restype = None
 lib.lamm_hip_cache_bytes.restype = ctypes.c_size_t
 lib.lamm_hip_boundary_reset.restype = None
@@ -227,6 +230,28 @@ def matmul_ex(A, B, C, batch=None, flags=0, stream=0):
     _check(lib.lamm_hip_matmul_ex(ctypes.byref(A), ctypes.byref(B), ctypes.byref(C),
                                   ctypes.byref(batch) if batch is not None else None, flags, ctypes.c_void_p(stream)),
            "lamm_hip_matmul_ex")
+
+
+class direct:
+    """Direct-dispatch region (lamm_hip_direct_begin / end): the one-kernel decode GEMVs launched
+    inside go onto the library's own AQL queue; on exit every one of them has completed, and
+    ``launches`` holds how many were dispatched that way."""
+
+    def __init__(self, device=0):
+        self.device = device
+        self.launches = None
+
+    def __enter__(self):
+        _sync_env()
+        _check(lib.lamm_hip_direct_begin(self.device), "lamm_hip_direct_begin")
+        return self
+
+    def __exit__(self, *exc):
+        n = lib.lamm_hip_direct_end()
+        if n < 0:
+            raise LammError(f"lamm_hip_direct_end failed ({n}): {last_error()}")
+        self.launches = n
+        return False
 
 
 def matmul_batched(A, B, C, batch, stream=0):

@@ -308,8 +308,10 @@ def test_boundary_rows_split_over_devices(devices, t, M, N, K, quant, zc_split, 
 DECODE_MODES = {"cpu_init": {}, "fused": {"LAMM_HIP_FUSED": "1"}, "device_copies": {"LAMM_HIP_ZERO_COPY": "0"},
                 "fused_watch": {"LAMM_HIP_FUSED": "1", "LAMM_HIP_C_WATCH": "1"},
                 "kernel_signal": {"LAMM_HIP_KERNEL_SIGNAL": "1"}, "watch_coherent": {"LAMM_HIP_C_WATCH": "1"},
-                "watch_noncoherent": {"LAMM_HIP_C_WATCH": "2"}, "no_spin": {"LAMM_HIP_SPIN": "0"}}
-DECODE_KEYS = ("LAMM_HIP_FUSED", "LAMM_HIP_ZERO_COPY", "LAMM_HIP_KERNEL_SIGNAL", "LAMM_HIP_SPIN", "LAMM_HIP_C_WATCH")
+                "watch_noncoherent": {"LAMM_HIP_C_WATCH": "2"}, "no_spin": {"LAMM_HIP_SPIN": "0"},
+                "direct": {"LAMM_HIP_DIRECT": "1"}, "fused_direct": {"LAMM_HIP_FUSED": "1", "LAMM_HIP_DIRECT": "1"}}
+DECODE_KEYS = ("LAMM_HIP_FUSED", "LAMM_HIP_ZERO_COPY", "LAMM_HIP_KERNEL_SIGNAL", "LAMM_HIP_SPIN", "LAMM_HIP_C_WATCH",
+               "LAMM_HIP_DIRECT")
 
 
 @pytest.mark.parametrize("t", [ol.Q4_0, ol.Q4_1, ol.Q8_0, ol.Q6_K], ids=["q4_0", "q4_1", "q8_0", "q6_k"])
@@ -318,10 +320,11 @@ def test_decode_calls_fresh_every_call(t, monkeypatch):
     buffers with new contents every call (ggml's compute buffer is reused per token).  Modes:
     activations read in place from pinned host memory mapped into the device and C written back
     the same way (default), or copied by HIP (LAMM_HIP_ZERO_COPY=0); the activations quantized by
-    ggml's CPU INIT (default) or by the GEMV (LAMM_HIP_FUSED=1); completion by the signal launch
-    (default), seen in C's own words (LAMM_HIP_C_WATCH=1 coherent C / 2 non-coherent C), by the
-    GEMV's own last workgroup (LAMM_HIP_KERNEL_SIGNAL=1) or by hipStreamSynchronize
-    (LAMM_HIP_SPIN=0).  The boundary re-reads
+    ggml's CPU INIT (default) or by the GEMV (LAMM_HIP_FUSED=1); the GEMV launched through HIP
+    (default) or dispatched on the library's own AQL queue with its completion signal
+    (LAMM_HIP_DIRECT=1, lamm_aql.cpp); completion by the signal launch (default), seen in C's own words
+    (LAMM_HIP_C_WATCH=1 coherent C / 2 non-coherent C), by the GEMV's own last workgroup
+    (LAMM_HIP_KERNEL_SIGNAL=1) or by hipStreamSynchronize (LAMM_HIP_SPIN=0).  The boundary re-reads
     its switches at lamm_hip_boundary_reset (they used to be frozen at the first call).
     Every call must match the oracle, and every mode must give the same bits."""
     M, N, K = 4096, 1, 4096

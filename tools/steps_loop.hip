@@ -9,6 +9,8 @@
 //                              (lamm_hip_profile_next), launches isolated or back to back --
 //                              what the kernel tracer reports for the same dispatch (bench.py's
 //                              roofline)
+//   lamm_steps_direct        : K calls inside one direct-dispatch region (lamm_hip_direct_begin /
+//                              end: the library's own AQL queue), completed before it returns
 // hipcc --offload-arch=gfx950 -O2 -shared -fPIC -I include tools/steps_loop.hip -L la-llama.cpp_amd -llamm_hip
 #include <hip/hip_runtime.h>
 
@@ -86,6 +88,20 @@ int lamm_steps_isolated_ex(const lamm_matrix* A, int nA, const lamm_matrix* B, c
 int lamm_steps_isolated(const lamm_matrix* A, int nA, const lamm_matrix* B, const lamm_matrix* C, int first,
                         int launches, void* stream, float* out_us, int sync_each) {
   return lamm_steps_isolated_ex(A, nA, B, C, first, launches, stream, out_us, sync_each, 0);
+}
+
+// K calls in one direct region on `device`: returns the number of direct dispatches (K when every
+// call's kernel went onto the library's queue), or a negative status; *wall_us = the region's
+// host wall time, from before the first call to the end of the wait for the last kernel
+int lamm_steps_direct(const lamm_matrix* A, int nA, const lamm_matrix* B, const lamm_matrix* C, int first, int steps,
+                      int device, int flags, double* wall_us) {
+  const double t0 = now_us();
+  if (lamm_hip_direct_begin(device) != LAMM_OK) return -1;
+  int rc = LAMM_OK;
+  for (int s = 0; s < steps && rc == LAMM_OK; ++s) rc = lamm_hip_matmul_ex(&A[(first + s) % nA], B, C, nullptr, flags, nullptr);
+  const int n = lamm_hip_direct_end();
+  if (wall_us) *wall_us = now_us() - t0;
+  return rc != LAMM_OK ? -100 - rc : n;
 }
 
 }  // extern "C"

@@ -380,12 +380,22 @@ __global__ __launch_bounds__(PB_NT) void prep_b_fp6_tile(GemvArgs p, unsigned ch
   const int64_t bbytes = nrow > 0 ? (nrow - 1) * p.ldb + (int64_t)p.nblk * VBPB : 0;
   const auto rs = make_rsrc(Bz + base, (uint32_t)min((bbytes + 3) & ~int64_t(3), (int64_t)0x7fffffff));
   const int t = threadIdx.x;
-  for (int idx = t; idx < PB_ROWS * PIECES; idx += PB_NT) {
-    const int r = idx / PIECES, o = idx % PIECES;
+  // every piece load of the thread issued before the first wait (round 5: a loop of load -> LDS
+  // store waited for each load in turn, three HBM round trips per thread)
+  constexpr int NPT = (PB_ROWS * PIECES + PB_NT - 1) / PB_NT;
+  u32x4 pc[NPT];
+#pragma unroll
+  for (int i = 0; i < NPT; ++i) {
+    const int idx = t + i * PB_NT, r = idx / PIECES, o = idx % PIECES;
     const uint32_t start = (uint32_t)((int64_t)r * p.ldb + (int64_t)kb0 * VBPB);
-    const uint32_t off = r < nrow && kb0 < p.nblk ? (start & ~3u) + 16 * o : 0x7ffffff0u;
-    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
-    *reinterpret_cast<u32x4*>(&raw[r * SEGW + 4 * o]) = v;
+    const uint32_t off =
+        idx < PB_ROWS * PIECES && r < nrow && kb0 < p.nblk ? (start & ~3u) + 16 * o : 0x7ffffff0u;
+    pc[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+  }
+#pragma unroll
+  for (int i = 0; i < NPT; ++i) {
+    const int idx = t + i * PB_NT, r = idx / PIECES, o = idx % PIECES;
+    if (idx < PB_ROWS * PIECES) *reinterpret_cast<u32x4*>(&raw[r * SEGW + 4 * o]) = pc[i];
   }
   __syncthreads();
   const int r = t % PB_ROWS, bl = t / PB_ROWS;

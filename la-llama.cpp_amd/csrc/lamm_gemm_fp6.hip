@@ -360,6 +360,11 @@ __device__ __forceinline__ void store_b_fp6(Put&& put, int b, int r, const uint3
   put(f6_boff(1, b, 1, r), u32x4{ol[4], ol[5], d, sv});
 }
 
+#ifndef F6_PREP_AB
+// probe builds only (tools/build_fp6_var.sh): 1 no plane stores, 2 no encoding (raw words stored),
+// 3 no loads (zero pieces)
+#define F6_PREP_AB 0
+#endif
 template <int T>
 __global__ __launch_bounds__(PB_NT) void prep_b_fp6_tile(GemvArgs p, unsigned char* ws) {
   using F = F6<T>;
@@ -389,7 +394,7 @@ __global__ __launch_bounds__(PB_NT) void prep_b_fp6_tile(GemvArgs p, unsigned ch
     const int idx = t + i * PB_NT, r = idx / PIECES, o = idx % PIECES;
     const uint32_t start = (uint32_t)((int64_t)r * p.ldb + (int64_t)kb0 * VBPB);
     const uint32_t off =
-        idx < PB_ROWS * PIECES && r < nrow && kb0 < p.nblk ? (start & ~3u) + 16 * o : 0x7ffffff0u;
+        idx < PB_ROWS * PIECES && r < nrow && kb0 < p.nblk && F6_PREP_AB != 3 ? (start & ~3u) + 16 * o : 0x7ffffff0u;
     pc[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
   }
 #pragma unroll
@@ -418,6 +423,22 @@ __global__ __launch_bounds__(PB_NT) void prep_b_fp6_tile(GemvArgs p, unsigned ch
   }
   unsigned char* wz = ws + (int64_t)z * L.b_slice;
   const int64_t ch = ((int64_t)(j / F6_TJ) * L.nsteps + kb / F6_KB) * F6_B_BYTES;
+  if constexpr (F6_PREP_AB == 1) {
+    uint32_t x = d ^ sv;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x ^= q[k];
+    asm volatile("" ::"v"(x));
+    return;
+  }
+  if constexpr (F6_PREP_AB == 2) {
+    const auto wr = make_rsrc(wz, (uint32_t)L.b_slice);
+    const int b_ = kb % F6_KB, r_ = (int)(j % F6_TJ);
+    bstore16_wt(wr, (uint32_t)(ch + f6_boff(0, b_, 0, r_)), u32x4{q[0], q[1], q[2], q[3]});
+    bstore16_wt(wr, (uint32_t)(ch + f6_boff(1, b_, 0, r_)), u32x4{q[4], q[5], d, sv});
+    bstore16_wt(wr, (uint32_t)(ch + f6_boff(0, b_, 1, r_)), u32x4{q[0], q[1], q[2], q[3]});
+    bstore16_wt(wr, (uint32_t)(ch + f6_boff(1, b_, 1, r_)), u32x4{q[4], q[5], d, sv});
+    return;
+  }
   if (L.b_slice <= 0x7fffffff) {   // write-through buffer stores from a wave-uniform base
     const auto wr = make_rsrc(wz, (uint32_t)L.b_slice);
     store_b_fp6([&](int o, u32x4 v) { bstore16_wt(wr, (uint32_t)(ch + o), v); }, kb % F6_KB, (int)(j % F6_TJ), q, d, sv);

@@ -314,8 +314,9 @@ DECODE_KEYS = ("LAMM_HIP_FUSED", "LAMM_HIP_ZERO_COPY", "LAMM_HIP_KERNEL_SIGNAL",
                "LAMM_HIP_DIRECT")
 
 
+@pytest.mark.parametrize("n", [1, 3], ids=["n1", "n3"])   # n3: the multi-column decode kernels
 @pytest.mark.parametrize("t", [ol.Q4_0, ol.Q4_1, ol.Q8_0, ol.Q6_K], ids=["q4_0", "q4_1", "q8_0", "q6_k"])
-def test_decode_calls_fresh_every_call(t, monkeypatch):
+def test_decode_calls_fresh_every_call(t, n, monkeypatch):
     """Decode-sized calls through the boundary, as llama.cpp makes them: the SAME src1 / dst
     buffers with new contents every call (ggml's compute buffer is reused per token).  Modes:
     activations read in place from pinned host memory mapped into the device and C written back
@@ -326,8 +327,9 @@ def test_decode_calls_fresh_every_call(t, monkeypatch):
     (LAMM_HIP_C_WATCH=1 coherent C / 2 non-coherent C), by the GEMV's own last workgroup
     (LAMM_HIP_KERNEL_SIGNAL=1) or by hipStreamSynchronize (LAMM_HIP_SPIN=0).  The boundary re-reads
     its switches at lamm_hip_boundary_reset (they used to be frozen at the first call).
-    Every call must match the oracle, and every mode must give the same bits."""
-    M, N, K = 4096, 1, 4096
+    Every call must match the oracle, and every mode must give the same bits (three columns: the
+    direct queue takes none of those kernels, so the region falls back to HIP and its completion)."""
+    M, N, K = 4096, n, 4096
     rng = np.random.default_rng(t)
     if t in ol.KQ_TYPES:
         A_q = ol.random_kq_blocks(t, M, K, rng)

@@ -305,7 +305,69 @@ Aql* queue_for(int device) {
   return q;
 }
 
+// HIP device -> its HSA GPU agent (PCI bus / device / domain) and the HDP flush register ROCr maps
+struct HdpEntry {
+  uint32_t* reg = nullptr;
+  bool host_access = false;   // the host can store into the agent's local memory (large BAR)
+};
+std::unordered_map<int, HdpEntry> g_hdp;
+
+uint32_t* hdp_register(int device) {
+  std::lock_guard<std::mutex> lock(g_mu);
+  auto it = g_hdp.find(device);
+  if (it != g_hdp.end()) return it->second.reg;
+  HdpEntry e;
+  int bus = -1, dev = -1, dom = -1;
+  if (hsa_init() == HSA_STATUS_SUCCESS && hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, device) == hipSuccess &&
+      hipDeviceGetAttribute(&dev, hipDeviceAttributePciDeviceId, device) == hipSuccess &&
+      hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainID, device) == hipSuccess) {
+    struct Want {
+      uint32_t bdf, dom;
+      hsa_agent_t gpu;
+    } w{(uint32_t)((bus << 8) | (dev << 3)), (uint32_t)dom, {0}};
+    hsa_iterate_agents(
+        [](hsa_agent_t a, void* d) {
+          Want* w = static_cast<Want*>(d);
+          hsa_device_type_t t;
+          hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t);
+          if (t != HSA_DEVICE_TYPE_GPU) return HSA_STATUS_SUCCESS;
+          uint32_t bdf = 0, dom = 0;
+          hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &bdf);
+          hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DOMAIN, &dom);
+          if ((bdf & ~7u) == w->bdf && dom == w->dom) w->gpu = a;
+          return HSA_STATUS_SUCCESS;
+        },
+        &w);
+    hsa_amd_hdp_flush_t h{};
+    if (w.gpu.handle && hsa_agent_get_info(w.gpu, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_HDP_FLUSH, &h) == HSA_STATUS_SUCCESS)
+      e.reg = h.HDP_MEM_FLUSH_CNTL;
+    bool direct = false;
+    if (w.gpu.handle &&
+        hsa_agent_get_info(w.gpu, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_SVM_DIRECT_HOST_ACCESS, &direct) == HSA_STATUS_SUCCESS)
+      e.host_access = direct;
+  }
+  g_hdp[device] = e;
+  return e.reg;
+}
+
 }  // namespace
+
+bool hdp_flush_available(int device) { return hdp_register(device) != nullptr; }
+
+bool vram_host_writable(int device) {
+  if (!hdp_register(device)) return false;
+  std::lock_guard<std::mutex> lock(g_mu);
+  return g_hdp[device].host_access;
+}
+
+void hdp_flush(int device, const void* last_written) {
+  uint32_t* r = hdp_register(device);
+  if (r) {
+    *r = 1u;
+    (void)*reinterpret_cast<volatile uint32_t*>(r);
+  }
+  if (last_written) (void)*reinterpret_cast<const volatile uint32_t*>(last_written);
+}
 
 bool direct_begin(int device) {
   if (t_direct) return false;

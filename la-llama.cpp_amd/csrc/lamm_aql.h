@@ -17,4 +17,11 @@ bool direct_active();
 // is open and the kernel's layout checks out; false: the caller launches through HIP.
 bool direct_launch(const void* fn, dim3 grid, dim3 block, uint32_t dyn_lds, const void* args, size_t bytes);
 
+// Host writes into device memory through the BAR reach it only through the HDP: flush it (ROCr's
+// mapped flush register) and read `last_written` back, so a kernel launched next sees the bytes.
+bool hdp_flush_available(int device);
+// the host can store straight into this device's memory (large BAR) and flush the HDP after it
+bool vram_host_writable(int device);
+void hdp_flush(int device, const void* last_written);
+
 }  // namespace lamm

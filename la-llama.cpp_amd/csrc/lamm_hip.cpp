@@ -644,6 +644,32 @@ struct Dev {
   unsigned* done_ctr = nullptr;   // device counter for the GEMV's own completion signal
   unsigned pending = 0;           // seq the last call's kernel signals itself (0: none)
   bool enqueued = false;          // an upload went onto `stream` since the last direct region (lamm_aql.cpp)
+  unsigned char* xv = nullptr;    // decode activations in fine-grained device memory, written by the host
+  size_t xv_cap = 0;              // through the BAR (LAMM_HIP_VRAM_X); xv_ok -1: not available here
+  int xv_ok = 0;
+
+  // the activation buffer in device memory the host writes directly (nullptr: not available)
+  unsigned char* vram_x(size_t bytes) {
+    if (xv_ok < 0) return nullptr;
+    if (xv_cap < bytes) {
+      if (xv) {
+        (void)hipSetDevice(id);
+        (void)hipStreamSynchronize(stream);
+        (void)hipFree(xv);
+        xv = nullptr;
+        xv_cap = 0;
+      }
+      void* p = nullptr;
+      if (!lamm::vram_host_writable(id) || hipExtMallocWithFlags(&p, bytes + 256, hipDeviceMallocFinegrained) != hipSuccess) {
+        xv_ok = -1;
+        return nullptr;
+      }
+      xv = static_cast<unsigned char*>(p);
+      xv_cap = bytes;
+      xv_ok = 1;
+    }
+    return xv;
+  }
   std::unordered_map<WeightKey, WeightEntry, WeightKeyHash> cache;
   std::list<WeightKey> lru;
   size_t cached = 0;
@@ -881,6 +907,7 @@ class Runtime {
       (void)hipStreamSynchronize(d.stream);
       for (void* b : d.buf)
         if (b) (void)hipFree(b);
+      if (d.xv) (void)hipFree(d.xv);
       (void)hipHostFree(d.flag);
       if (d.done_ctr) (void)hipFree(d.done_ctr);
       (void)hipStreamDestroy(d.stream);
@@ -1328,13 +1355,18 @@ void mul_mat_thread0(const ggml::compute_params* params, ggml::tensor* dst, bool
                  static_cast<const unsigned char*>(src1->data) + i12 * src1->nb[2] + i13 * src1->nb[3] + j * src1->nb[1],
                  (size_t)ne00 * sizeof(float));
   };
+  // one device: the decode activations go straight into device memory through the BAR (a kernel
+  // read them zero-copy from pinned host memory before, every XCD pulling them over PCIe;
+  // LAMM_HIP_VRAM_X=0 restores that)
+  unsigned char* xv = zc_in && G == 1 && knobs().vram_x ? rt.devs[0].vram_x(x_bytes) : nullptr;
   if (zc_in) {
-    unsigned char* h = rt.pinned(0, x_bytes);
+    unsigned char* h = xv ? xv : rt.pinned(0, x_bytes);
     if (act == kFused) gather_f32(h);
     else if (use_wdata) memcpy(h, params->wdata, x_bytes);
     else
       for (int64_t r = 0; r < N * nslices; ++r)
         memcpy(h + r * b_row, static_cast<const unsigned char*>(src1->data) + r * src1->nb[1], b_row);
+    if (xv) lamm::hdp_flush(rt.devs[0].id, xv + ((x_bytes - 4) & ~size_t(3)));
     x_host = h;
   } else if (pipe) {
     Dev& d = rt.devs[0];
@@ -1437,7 +1469,7 @@ void mul_mat_thread0(const ggml::compute_params* params, ggml::tensor* dst, bool
     // activations on (or mapped into) the device
     void* dB;
     if (zc_in) {
-      dB = rt.pinned_dev(0);
+      dB = xv ? static_cast<void*>(xv) : rt.pinned_dev(0);
     } else if (hostq) {   // the pool's q8 rows
       dB = d.scratch(0, x_bytes + 64);
       HIPCHK(hipMemcpyAsync(dB, x_host, x_bytes, hipMemcpyHostToDevice, s));

@@ -39,6 +39,8 @@ struct Knobs {
   int gpu_quant = -1;          // LAMM_HIP_GPU_QUANT: 0 CPU INIT, 1 GPU for every row count
   bool fused = false;          // LAMM_HIP_FUSED=1: the decode GEMV quantizes the F32 row itself (INIT claimed)
   bool spin = true;            // LAMM_HIP_SPIN=0: hipStreamSynchronize instead of the flag spin
+  bool vram_x = true;          // LAMM_HIP_VRAM_X=0: decode activations zero-copy from pinned host memory
+                               // instead of written into device memory through the BAR
   bool aql_host_karg = false;  // LAMM_AQL_HOSTKARG=1: the direct queue's kernargs in host memory (A/B)
   bool direct = false;         // LAMM_HIP_DIRECT=1: decode-sized boundary calls dispatch on the library's
                                // own AQL queue (lamm_aql.cpp) instead of launching through HIP

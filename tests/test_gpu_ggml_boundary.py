@@ -309,9 +309,10 @@ DECODE_MODES = {"cpu_init": {}, "fused": {"LAMM_HIP_FUSED": "1"}, "device_copies
                 "fused_watch": {"LAMM_HIP_FUSED": "1", "LAMM_HIP_C_WATCH": "1"},
                 "kernel_signal": {"LAMM_HIP_KERNEL_SIGNAL": "1"}, "watch_coherent": {"LAMM_HIP_C_WATCH": "1"},
                 "watch_noncoherent": {"LAMM_HIP_C_WATCH": "2"}, "no_spin": {"LAMM_HIP_SPIN": "0"},
-                "direct": {"LAMM_HIP_DIRECT": "1"}, "fused_direct": {"LAMM_HIP_FUSED": "1", "LAMM_HIP_DIRECT": "1"}}
+                "direct": {"LAMM_HIP_DIRECT": "1"}, "fused_direct": {"LAMM_HIP_FUSED": "1", "LAMM_HIP_DIRECT": "1"},
+                "pinned_in": {"LAMM_HIP_VRAM_X": "0"}, "fused_pinned_in": {"LAMM_HIP_FUSED": "1", "LAMM_HIP_VRAM_X": "0"}}
 DECODE_KEYS = ("LAMM_HIP_FUSED", "LAMM_HIP_ZERO_COPY", "LAMM_HIP_KERNEL_SIGNAL", "LAMM_HIP_SPIN", "LAMM_HIP_C_WATCH",
-               "LAMM_HIP_DIRECT")
+               "LAMM_HIP_DIRECT", "LAMM_HIP_VRAM_X")
 
 
 @pytest.mark.parametrize("n", [1, 3], ids=["n1", "n3"])   # n3: the multi-column decode kernels
@@ -319,8 +320,9 @@ DECODE_KEYS = ("LAMM_HIP_FUSED", "LAMM_HIP_ZERO_COPY", "LAMM_HIP_KERNEL_SIGNAL",
 def test_decode_calls_fresh_every_call(t, n, monkeypatch):
     """Decode-sized calls through the boundary, as llama.cpp makes them: the SAME src1 / dst
     buffers with new contents every call (ggml's compute buffer is reused per token).  Modes:
-    activations read in place from pinned host memory mapped into the device and C written back
-    the same way (default), or copied by HIP (LAMM_HIP_ZERO_COPY=0); the activations quantized by
+    activations written by the host into device memory through the BAR (default where the host can
+    reach it) or read in place from pinned host memory (LAMM_HIP_VRAM_X=0), C written back into pinned
+    host memory (default), or both copied by HIP (LAMM_HIP_ZERO_COPY=0); the activations quantized by
     ggml's CPU INIT (default) or by the GEMV (LAMM_HIP_FUSED=1); the GEMV launched through HIP
     (default) or dispatched on the library's own AQL queue with its completion signal
     (LAMM_HIP_DIRECT=1, lamm_aql.cpp); completion by the signal launch (default), seen in C's own words

@@ -2,8 +2,9 @@
 // row (16 KiB) per call, and every workgroup of the GEMV reads all of it.  Per strategy, median of
 // 300 calls of [host writes the row; kernel: 512 workgroups read it and write 8 floats of C each to
 // pinned host memory; signal kernel stores a flag into host-coherent memory; host spins on it]:
-//   pinned : the row in pinned host memory, read by the kernel over PCIe (zero copy, production)
-//   vram   : the row in fine-grained device memory the host writes through the BAR
+//   pinned : the row in coherent pinned host memory, read by the kernel over PCIe
+//   pinned_nc : the same in non-coherent pinned memory (cached in the device's L2; the boundary's form)
+//   vram   : the row in fine-grained device memory the host writes through the BAR (+ HDP flush)
 // plus each kernel's own duration by HIP events (row already written).
 // Usage: bar_probe [kib=16]
 #include <hip/hip_runtime.h>
@@ -54,9 +55,11 @@ int main(int argc, char** argv) {
   for (int i = 0; i < n; ++i) src[i] = (float)(i % 7);
   hipStream_t s;
   CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-  float *h_row, *d_row_h, *h_c, *d_c_h, *v_row;
-  CK(hipHostMalloc(&h_row, n * 4, hipHostMallocMapped));
+  float *h_row, *d_row_h, *h_c, *d_c_h, *v_row, *nc_row, *d_nc_row;
+  CK(hipHostMalloc(&h_row, n * 4, hipHostMallocMapped | hipHostMallocCoherent));
   CK(hipHostGetDevicePointer((void**)&d_row_h, h_row, 0));
+  CK(hipHostMalloc(&nc_row, n * 4, hipHostMallocMapped | hipHostMallocNonCoherent));
+  CK(hipHostGetDevicePointer((void**)&d_nc_row, nc_row, 0));
   CK(hipHostMalloc(&h_c, grid * 8 * 4, hipHostMallocMapped));
   CK(hipHostGetDevicePointer((void**)&d_c_h, h_c, 0));
   unsigned *h_flag, *d_flag;
@@ -72,9 +75,9 @@ int main(int argc, char** argv) {
   printf(", \"vram_host_write\": %s", chk == src[n - 1] ? "true" : "false");
   fflush(stdout);
   unsigned seq = 0;
-  for (int mode = 0; mode < 2; ++mode) {
-    float* dst_host = mode == 0 ? h_row : v_row;
-    const float* row_dev = mode == 0 ? d_row_h : v_row;
+  for (int mode = 0; mode < 3; ++mode) {
+    float* dst_host = mode == 0 ? h_row : mode == 1 ? v_row : nc_row;
+    const float* row_dev = mode == 0 ? d_row_h : mode == 1 ? v_row : d_nc_row;
     std::vector<double> call, write;
     for (int it = 0; it < 330; ++it) {
       const double t0 = now_us();
@@ -107,7 +110,8 @@ int main(int argc, char** argv) {
       kern.push_back(ms * 1e3);
     }
     std::sort(kern.begin(), kern.end());
-    printf(", \"%s\": {\"call_us\": %.2f, \"host_write_us\": %.2f, \"kernel_us\": %.2f}", mode == 0 ? "pinned" : "vram",
+    printf(", \"%s\": {\"call_us\": %.2f, \"host_write_us\": %.2f, \"kernel_us\": %.2f}",
+           mode == 0 ? "pinned" : mode == 1 ? "vram" : "pinned_nc",
            call[call.size() / 2], write[write.size() / 2], kern[kern.size() / 2]);
     fflush(stdout);
   }

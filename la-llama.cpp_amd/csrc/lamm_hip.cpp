@@ -1068,7 +1068,9 @@ void wait_device(Dev& d) {
     d.pending = 0;
     if (!seq) {
       seq = ++d.seq;
-      HIPCHK(launch_signal(d.flag_dev, seq, d.stream));
+      // LAMM_HIP_SIGNAL_WRITE=1 (A/B): HIP's stream write-value op instead of the one-lane kernel
+      if (knobs().signal_write) HIPCHK(hipStreamWriteValue32(d.stream, d.flag_dev, seq, 0));
+      else HIPCHK(launch_signal(d.flag_dev, seq, d.stream));
     }
     const auto t0 = std::chrono::steady_clock::now();
     for (unsigned it = 0;; ++it) {

@@ -194,6 +194,12 @@ int lamm_hip_profile_next(void *start_event, void *stop_event);
 int lamm_hip_direct_begin(int device);
 int lamm_hip_direct_end(void);
 
+/* ggml boundary diagnostics (round 5): how many sibling decode calls -- same activation row, another
+ * weight (llama.cpp's wq / wk / wv, ffn_gate / ffn_up) -- were computed ahead in an earlier call's
+ * device round trip, and how many of those results a later call took (its src1 bytes and weight
+ * fingerprint unchanged; LAMM_HIP_SIBLINGS=0 turns the prediction off).  Either pointer may be NULL. */
+void lamm_hip_sibling_stats(uint64_t *launched, uint64_t *taken);
+
 const char *lamm_hip_last_error(void);
 int lamm_hip_device_count(void);
 /* Provenance: hash (sha256, 16 hex digits) of the sources this library was built from. */

@@ -64,6 +64,7 @@ Knobs* read_env() {
   k->aql_host_karg = env_on("LAMM_AQL_HOSTKARG");
   k->vram_x = !env_off("LAMM_HIP_VRAM_X");
   k->signal_write = env_on("LAMM_HIP_SIGNAL_WRITE");
+  k->siblings = !env_off("LAMM_HIP_SIBLINGS");
   const char* zc = getenv("LAMM_HIP_ZERO_COPY");
   k->zero_copy = !k->pinned || (zc && zc[0] == '0') ? 0 : zc && !strcmp(zc, "in") ? 1 : zc && !strcmp(zc, "out") ? 2 : 3;
   k->zero_copy_split = env_on("LAMM_HIP_ZERO_COPY_SPLIT");

@@ -39,6 +39,7 @@ struct Knobs {
   int gpu_quant = -1;          // LAMM_HIP_GPU_QUANT: 0 CPU INIT, 1 GPU for every row count
   bool fused = false;          // LAMM_HIP_FUSED=1: the decode GEMV quantizes the F32 row itself (INIT claimed)
   bool spin = true;            // LAMM_HIP_SPIN=0: hipStreamSynchronize instead of the flag spin
+  bool siblings = true;        // LAMM_HIP_SIBLINGS=0: no sibling decode calls computed ahead (lamm_hip.cpp Siblings)
   bool signal_write = false;   // LAMM_HIP_SIGNAL_WRITE=1: completion flag by hipStreamWriteValue32 (A/B)
   bool vram_x = true;          // LAMM_HIP_VRAM_X=0: decode activations zero-copy from pinned host memory
                                // instead of written into device memory through the BAR

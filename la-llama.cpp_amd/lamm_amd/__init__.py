@@ -140,6 +140,8 @@ lib.lamm_hip_allgather_rows.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c
 lib.lamm_hip_direct_begin.restype = ctypes.c_int
 lib.lamm_hip_direct_begin.argtypes = [ctypes.c_int]
 lib.lamm_hip_direct_end.restype = ctypes.c_int
+lib.lamm_hip_sibling_stats.restype = None
+lib.lamm_hip_sibling_stats.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
 lib.lamm_hip_cache_clear.restype = None
 lib.lamm_hip_cache_bytes.restype = ctypes.c_size_t
 lib.lamm_hip_boundary_reset.restype = None
@@ -230,6 +232,13 @@ def matmul_ex(A, B, C, batch=None, flags=0, stream=0):
     _check(lib.lamm_hip_matmul_ex(ctypes.byref(A), ctypes.byref(B), ctypes.byref(C),
                                   ctypes.byref(batch) if batch is not None else None, flags, ctypes.c_void_p(stream)),
            "lamm_hip_matmul_ex")
+
+
+def sibling_stats():
+    """(launched, taken): sibling decode calls computed ahead / results taken (lamm_hip_sibling_stats)"""
+    a, b = ctypes.c_uint64(), ctypes.c_uint64()
+    lib.lamm_hip_sibling_stats(ctypes.byref(a), ctypes.byref(b))
+    return a.value, b.value
 
 
 class direct:

@@ -444,3 +444,55 @@ def test_boundary_prefill_value_range(t):
     assert fin.all() or t == ol.Q5_1
     assert fin.any() and np.isfinite(got[fin]).all()
     assert rel_err(got[fin], want[fin], absdot[fin]).max() < 1e-3
+
+
+def test_sibling_calls(monkeypatch):
+    """Sibling decode calls (lamm_hip.cpp Siblings): three weights multiplied by the same src1
+    tensor one after another, as llama.cpp's wq / wk / wv, over several tokens.  With the prediction
+    on, the first call of each token runs the other two GEMVs ahead and their calls take the kept
+    results; every output must be the bits of the prediction-off run.  Token 2 changes src1 between
+    the first and second call (the kept result must be discarded), token 3 rewrites the third
+    weight in place (its fingerprint changes: discarded, re-uploaded, recomputed)."""
+    M, K, t = 4096, 4096, ol.Q4_0
+    rng = np.random.default_rng(77)
+    As = [ORACLE.quantize(t, rng.standard_normal((M, K), dtype=np.float32)) for _ in range(3)]
+    A_new = ORACLE.quantize(t, rng.standard_normal((M, K), dtype=np.float32))
+    xs = [rng.standard_normal(K).astype(np.float32) for _ in range(6)]
+    x_alt = rng.standard_normal(K).astype(np.float32)
+
+    def run(siblings):
+        monkeypatch.setenv("LAMM_HIP_SIBLINGS", siblings)
+        la.boundary_reset()
+        srcs = [ggml_emu.Tensor(t, [K, M], data=a.copy()) for a in As]
+        x = ggml_emu.Tensor(ol.F32, [K, 1])
+        dsts = [ggml_emu.mul_mat_node(s0, x) for s0 in srcs]
+        l0, t0 = la.sibling_stats()
+        outs = []
+        for tok, xv in enumerate(xs):
+            if tok == 3:
+                srcs[2].buf[:] = A_new
+            for i, d in enumerate(dsts):
+                x.buf.view(np.float32)[:] = x_alt if (tok == 2 and i == 1) else xv
+                assert ggml_emu.compute(d, nth=2)
+                outs.append(d.buf.view(np.float32).reshape(M).copy())
+        l1, t1 = la.sibling_stats()
+        return outs, l1 - l0, t1 - t0
+
+    try:
+        off, l_off, t_off = run("0")
+        on, l_on, t_on = run("1")
+    finally:
+        monkeypatch.delenv("LAMM_HIP_SIBLINGS", raising=False)
+        la.boundary_reset()
+    assert (l_off, t_off) == (0, 0)
+    assert l_on >= 8 and t_on >= 6, (l_on, t_on)   # tokens 1..5 lead with 2 siblings each; 2 discarded
+    assert t_on < l_on
+    for i, (a, b) in enumerate(zip(off, on)):
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), f"call {i}"
+    # and against the oracle: the second call of token 2 used x_alt, the third of tokens >= 3 A_new
+    B = ORACLE.quantize(ol.Q8_0, x_alt.reshape(1, K), ol.QUANT_AVX)
+    want = ORACLE.mul_mat(t, M, 1, K, As[1], B)[0]
+    assert np.abs(on[2 * 3 + 1] - want).max() <= 1e-3 * (np.abs(want).max() + 1.0)
+    B = ORACLE.quantize(ol.Q8_0, xs[4].reshape(1, K), ol.QUANT_AVX)
+    want = ORACLE.mul_mat(t, M, 1, K, A_new, B)[0]
+    assert np.abs(on[4 * 3 + 2] - want).max() <= 1e-3 * (np.abs(want).max() + 1.0)

@@ -117,6 +117,17 @@ int lamm_hip_matmul_batched(const lamm_matrix *A, const lamm_matrix *B, const la
 int lamm_hip_matmul_ex(const lamm_matrix *A, const lamm_matrix *B, const lamm_matrix *C,
                        const lamm_batch *batch, int flags, void *hip_stream);
 
+/* n (1..LAMM_GROUP_MAX) weights times the same activation B: C[i] = A[i] * B, each exactly as
+ * lamm_hip_matmul_ex(&A[i], B, &C[i], NULL, flags, s) computes it (the same bits).  A one-column
+ * B with LAMM_ORDER_REFERENCE and weights of one 32-element type sharing col and ld runs as one
+ * launch (the reference-order GEMV over all of them); anything else as n calls.  No reference
+ * interface corresponds: llama.cpp multiplies wq / wk / wv (and ffn gate / up) by the same normed
+ * activation as separate mul_mat nodes (LC/llama.cpp:5738-5752 in build_llama), one lamm_mul_mat
+ * call each (LC/ggml.c:10858-10862); the ggml boundary's sibling calls batch them through here. */
+#define LAMM_GROUP_MAX 4
+int lamm_hip_matmul_group(const lamm_matrix *A, int n, const lamm_matrix *B, const lamm_matrix *C,
+                          int flags, void *hip_stream);
+
 /* Activation quantizer on device (ggml INIT phase, LC/ggml.c:10865-10887, run on
  * the GPU): x[N][K] f32 (row j at x + j*ldx floats) -> y, N rows of `vec_type`
  * blocks (row j at y + j*ldy blocks).  flavour 0 = *_reference rounding

@@ -327,6 +327,8 @@ int main(int argc, char** argv) {
   uint64_t seed = 1;
   bool regen = false, write_only = false;
   std::vector<llama_token> forced;
+  // llama.cpp's --numa (common/common.cpp): ggml pins its compute threads per strategy
+  ggml_numa_strategy numa = GGML_NUMA_STRATEGY_DISABLED;
   for (int i = 1; i < argc; ++i) {
     const std::string a = argv[i];
     auto next = [&]() -> const char* {
@@ -343,6 +345,13 @@ int main(int argc, char** argv) {
     else if (a == "--logits") logits_path = next();
     else if (a == "--regen") regen = true;
     else if (a == "--write-only") write_only = true;
+    else if (a == "--numa") {
+      const std::string v = next();
+      numa = v == "distribute" ? GGML_NUMA_STRATEGY_DISTRIBUTE
+           : v == "isolate"    ? GGML_NUMA_STRATEGY_ISOLATE
+           : v == "numactl"    ? GGML_NUMA_STRATEGY_NUMACTL
+                               : GGML_NUMA_STRATEGY_DISABLED;
+    }
     else if (a == "--dump") g_dump_dir = next();
     else if (a == "--dump-mm") g_mm_dir = next();
     else if (a == "--force") {
@@ -366,6 +375,7 @@ int main(int argc, char** argv) {
   if (write_only) return 0;
 
   llama_backend_init();
+  if (numa != GGML_NUMA_STRATEGY_DISABLED) llama_numa_init(numa);
   llama_model_params mp = llama_model_default_params();
   const double t_load0 = now_ms();
   llama_model* m = llama_load_model_from_file(model.c_str(), mp);

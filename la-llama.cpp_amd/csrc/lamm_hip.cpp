@@ -490,6 +490,50 @@ extern "C" int lamm_hip_matmul_ex(const lamm_matrix* A, const lamm_matrix* B, co
   return matmul_impl(A, B, C, batch, hip_stream, nullptr, flags);
 }
 
+extern "C" int lamm_hip_matmul_group(const lamm_matrix* A, int n, const lamm_matrix* B, const lamm_matrix* C,
+                                     int flags, void* hip_stream) {
+  if (!A || !B || !C) return fail(LAMM_ERR_SHAPE, "null matrix");
+  if (n < 1 || n > LAMM_GROUP_MAX) return fail(LAMM_ERR_SHAPE, "group of %d weights (1..%d)", n, LAMM_GROUP_MAX);
+  // one launch: the reference-order one-column kernel, every weight of one type and row length
+  bool one = (flags & LAMM_ORDER_REFERENCE) && n > 1 && B->col == 1;
+  for (int i = 0; i < n && one; ++i)
+    one = A[i].type == A[0].type && A[i].col == A[0].col && A[i].ld == A[0].ld && A[i].row > 0 &&
+          C[i].type == kF32 && C[i].row == A[i].row && C[i].col == 1 && ((uintptr_t)A[i].data & 15) == 0 &&
+          ((uintptr_t)C[i].data & 3) == 0;
+  if (one) {
+    const int t = A[0].type, vdt = vec_dot_type(t), Kb = A[0].col;
+    const bool b_f32 = B->type == kF32 && (vdt == kQ8_0 || vdt == kQ8_1);
+    const int64_t lda = A[0].ld * (int64_t)block_bytes(t);
+    one = is_weight_type(t) && ref_order_supported(t, vdt) && (B->type == vdt || b_f32) &&
+          B->row == (b_f32 ? Kb * block_elems(t) : Kb) && A[0].ld >= Kb && (lda & 15) == 0 &&
+          ((uintptr_t)B->data & (b_f32 ? 3 : 0)) == 0;
+    if (one) {
+      GemvArgs p{static_cast<const unsigned char*>(A[0].data), lda, static_cast<const unsigned char*>(B->data),
+                 B->ld * (int64_t)block_bytes(B->type), static_cast<float*>(C[0].data), C[0].ld, A[0].row, 1,
+                 Kb * block_elems(t), Kb};
+      p.b_f32 = b_f32 ? 1 : 0;
+      if (ref_gemv_supported(t, p) && probe().count > 0) {
+        RefSegs sg{};
+        for (int i = 0; i < n; ++i) {
+          sg.A[i] = static_cast<const unsigned char*>(A[i].data);
+          sg.C[i] = static_cast<float*>(C[i].data);
+          sg.M[i] = A[i].row;
+        }
+        g_timing = LaunchTiming{};
+        g_completion = nullptr;
+        const hipError_t e = launch_ref_group(t, p, sg, n, static_cast<hipStream_t>(hip_stream));
+        if (e != hipSuccess) return fail(LAMM_ERR_HIP, "kernel launch: %s", hipGetErrorString(e));
+        return LAMM_OK;
+      }
+    }
+  }
+  for (int i = 0; i < n; ++i) {   // anything else: one call per weight (the same kernels, the same bits)
+    const int rc = matmul_impl(&A[i], B, &C[i], nullptr, hip_stream, nullptr, flags);
+    if (rc != LAMM_OK) return rc;
+  }
+  return LAMM_OK;
+}
+
 extern "C" int lamm_hip_quantize(int vec_type, int flavour, const float* x, int64_t ldx, void* y,
                                  int64_t ldy, int K, int N, void* hip_stream) {
   const bool wq = quantize_weights_supported(vec_type);
@@ -1629,17 +1673,11 @@ void mul_mat_thread0(const ggml::compute_params* params, ggml::tensor* dst, bool
       comp.seq = ++d.seq;
       g_completion = &comp;
     }
-    const int rc = stationary ? lamm_hip_matmul_weights(rt.prepared(d, *w, A, ne02, ne03), &B, &C, &bt, s)
-                              : lamm_hip_matmul_ex(&A, &B, &C, &bt, ref ? LAMM_ORDER_REFERENCE : 0, s);
-    g_completion = nullptr;
-    d.pending = comp.signaled ? comp.seq : 0;
-    if (rc != LAMM_OK) {
-      fprintf(stderr, "lamm_hip: lamm_hip_matmul_batched failed (%d): %s\n", rc, g_err.c_str());
-      std::abort();
-    }
     // this call leads a learned group: its siblings' GEMVs on the same activation buffer, in the
-    // same round trip (their results wait in pinned memory for their own calls)
-    if (sib_form && !in_direct && !comp.signaled && zc_out) {
+    // same launch (lamm_hip_matmul_group) -- their results wait in pinned memory for their own calls
+    lamm_matrix gA[LAMM_GROUP_MAX], gC[LAMM_GROUP_MAX];
+    int ng = 0;
+    if (sib_form && !in_direct && !stationary && comp.seq == 0 && zc_out) {
       auto fit = g_sib.followers.find(wkey);
       if (fit != g_sib.followers.end() && !fit->second.empty()) {
         size_t total = 0;
@@ -1647,15 +1685,17 @@ void mul_mat_thread0(const ggml::compute_params* params, ggml::tensor* dst, bool
         g_sib.pending.clear();   // earlier results live in the buffer about to be rewritten (or regrown)
         rt.pinned(3, total * sizeof(float));
         float* dres = static_cast<float*>(rt.pinned_dev(3));
+        gA[0] = A;
+        gC[0] = C;
+        ng = 1;
         size_t off = 0;
         for (const SibKey& f : fit->second) {
           auto ce = d.cache.find(f.key);
-          if (ce == d.cache.end() || f.key.type != t0 || f.key.kb != kb) continue;   // same activation form
+          if (ce == d.cache.end() || f.key.type != t0 || f.key.kb != kb || ng == LAMM_GROUP_MAX) continue;
           const WeightEntry& we = ce->second;
-          lamm_matrix Af{we.dev, t0, (int)f.M, (int)kb, we.dev_pitch / (int64_t)block_bytes(t0)};
-          lamm_matrix Cf{dres + off, kF32, (int)f.M, 1, f.M};
-          const bool fref = boundary_ref_order(src0);
-          if (lamm_hip_matmul_ex(&Af, &B, &Cf, nullptr, fref ? LAMM_ORDER_REFERENCE : 0, s) != LAMM_OK) continue;
+          gA[ng] = lamm_matrix{we.dev, t0, (int)f.M, (int)kb, we.dev_pitch / (int64_t)block_bytes(t0)};
+          gC[ng] = lamm_matrix{dres + off, kF32, (int)f.M, 1, f.M};
+          ++ng;
           SibResult r;
           r.key = f.key;
           r.x = src1->data;
@@ -1668,6 +1708,16 @@ void mul_mat_thread0(const ggml::compute_params* params, ggml::tensor* dst, bool
           off += (size_t)f.M;
         }
       }
+    }
+    const int flags = ref ? LAMM_ORDER_REFERENCE : 0;
+    const int rc = ng > 1      ? lamm_hip_matmul_group(gA, ng, &B, gC, flags, s)
+                   : stationary ? lamm_hip_matmul_weights(rt.prepared(d, *w, A, ne02, ne03), &B, &C, &bt, s)
+                                : lamm_hip_matmul_ex(&A, &B, &C, &bt, flags, s);
+    g_completion = nullptr;
+    d.pending = comp.signaled ? comp.seq : 0;
+    if (rc != LAMM_OK) {
+      fprintf(stderr, "lamm_hip: lamm_hip_matmul_batched failed (%d): %s\n", rc, g_err.c_str());
+      std::abort();
     }
     stat.phase(3);
     if (c_pool) {   // C down into pinned memory; the pool scatters it into dst below

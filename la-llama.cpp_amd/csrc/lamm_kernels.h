@@ -81,6 +81,15 @@ hipError_t launch_signal(unsigned* flag_dev, unsigned seq, hipStream_t s);
 bool ref_order_supported(int type, int btype);
 bool ref_gemv_supported(int type, const GemvArgs& p);
 hipError_t launch_ref(int type, const GemvArgs& p, hipStream_t s);
+// up to kRefSegs weights of one type and row length times the same activation column in one launch
+// of ref_gemv_kernel's body (lamm_hip_matmul_group); entry 0 repeats p.A / p.C / p.M
+constexpr int kRefSegs = 4;
+struct RefSegs {
+  const unsigned char* A[kRefSegs];
+  float* C[kRefSegs];
+  int M[kRefSegs];
+};
+hipError_t launch_ref_group(int type, const GemvArgs& p, const RefSegs& sg, int nseg, hipStream_t s);
 
 hipError_t launch_gemm(int type, const GemvArgs& p, void* workspace, hipStream_t s);
 size_t gemm_workspace_bytes(int type, const GemvArgs& p);   // device scratch launch_gemm needs

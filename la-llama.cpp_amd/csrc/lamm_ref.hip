@@ -295,8 +295,10 @@ size_t ref_gemv_lds(int type, int nblk) {
 // 3 no activation staging
 #define REF_GAB 0
 #endif
-template <int T, bool BF32, bool ONE_SLICE, int BPT = 4>
-__global__ __launch_bounds__(GR * GKC / BPT) void ref_gemv_kernel(GemvArgs p) {
+// MODE 0: one slice; 1: ggml's batch slices over blockIdx.z; 2: blockIdx.z picks one of up to
+// kRefSegs weights sharing the activation column (lamm_hip_matmul_group)
+template <int T, bool BF32, int MODE, int BPT>
+__device__ __forceinline__ void ref_gemv_body(const GemvArgs& p, const RefSegs& sg) {
   using F = RFmt<T>;
   // BPT consecutive blocks of one row per producer thread (one wide load of BPT * BPB bytes, dword
   // aligned: BPB is even); NT threads cover the chunk's GR x GKC blocks.  Config 2 (q4_0 4096 x 4096,
@@ -322,15 +324,26 @@ __global__ __launch_bounds__(GR * GKC / BPT) void ref_gemv_kernel(GemvArgs p) {
   const unsigned char* Az = p.A;
   const unsigned char* Bz = p.B;
   float* Cz = p.C;
-  if constexpr (!ONE_SLICE) {
+  int Mz = p.M;
+  if constexpr (MODE == 1) {
     const int z = blockIdx.z, i12 = z % p.ne12, i13 = z / p.ne12;
     Az += (int64_t)(i12 / p.r2) * p.sa2 + (int64_t)(i13 / p.r3) * p.sa3;
     Bz += (int64_t)i12 * p.sb2 + (int64_t)i13 * p.sb3;
     Cz += (int64_t)i12 * p.sc2 + (int64_t)i13 * p.sc3;
+  } else if constexpr (MODE == 2) {   // uniform selects: no dynamic index into the kernargs
+    const int z = blockIdx.z;
+#pragma unroll
+    for (int i = 1; i < kRefSegs; ++i)
+      if (z == i) {
+        Az = sg.A[i];
+        Cz = sg.C[i];
+        Mz = sg.M[i];
+      }
   }
   const int t = threadIdx.x;
   const int row0 = blockIdx.x * GR;
-  const int nrows = p.M - row0 < GR ? p.M - row0 : GR;
+  if (MODE == 2 && row0 >= Mz) return;   // a shorter weight of the group (whole workgroup)
+  const int nrows = Mz - row0 < GR ? Mz - row0 : GR;
   const auto ra = make_rsrc(Az + (int64_t)row0 * p.lda,
                             (uint32_t)(((int64_t)(nrows - 1) * p.lda + (int64_t)nb * F::BPB + 3) & ~int64_t(3)));
   // producer: row pr, blocks BPT pg .. BPT pg + BPT - 1 of each chunk
@@ -446,7 +459,18 @@ __global__ __launch_bounds__(GR * GKC / BPT) void ref_gemv_kernel(GemvArgs p) {
     }
     if (cl == 0 && cr < nrows) Cz[row0 + cr] = v;
   }
-  if (p.flag) signal_done(p);
+  if (MODE != 2 && p.flag) signal_done(p);
+}
+
+template <int T, bool BF32, bool ONE_SLICE, int BPT = 4>
+__global__ __launch_bounds__(GR * GKC / BPT) void ref_gemv_kernel(GemvArgs p) {
+  ref_gemv_body<T, BF32, ONE_SLICE ? 0 : 1, BPT>(p, RefSegs{});
+}
+
+// several weights times one activation column in one launch (segment 0 in p.A / p.C / p.M)
+template <int T, bool BF32, int BPT = 4>
+__global__ __launch_bounds__(GR * GKC / BPT) void ref_gemv_group_kernel(GemvArgs p, RefSegs sg) {
+  ref_gemv_body<T, BF32, 2, BPT>(p, sg);
 }
 
 // ---------------------------------------------------------------- F16 x F16: ggml_vec_dot_f16's order
@@ -1397,6 +1421,33 @@ hipError_t launch_ref(int type, const GemvArgs& p, hipStream_t s) {
     case kQ5_0: go(std::integral_constant<int, kQ5_0>{}); break;
     case kQ5_1: go(std::integral_constant<int, kQ5_1>{}); break;
     case kQ6_K: go(std::integral_constant<int, kQ6_K>{}); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_ref_group(int type, const GemvArgs& p, const RefSegs& sg, int nseg, hipStream_t s) {
+  if (nseg < 1 || nseg > kRefSegs || !ref_gemv_supported(type, p) || p.ne12 * p.ne13 != 1 || p.flag)
+    return hipErrorInvalidValue;
+  int mmax = 0;
+  for (int i = 0; i < nseg; ++i) mmax = sg.M[i] > mmax ? sg.M[i] : mmax;
+  const dim3 g((unsigned)((mmax + GR - 1) / GR), 1, (unsigned)nseg);
+  const size_t lds = ref_gemv_lds(type, p.nblk);
+  auto gov = [&](auto tc) {
+    constexpr int T = decltype(tc)::value;
+    auto go2 = [&](auto bc) {
+      constexpr int BPT = decltype(bc)::value, nt = GR * GKC / BPT;
+      if (p.b_f32) hipLaunchKernelGGL((ref_gemv_group_kernel<T, true, BPT>), g, dim3(nt), lds, s, p, sg);
+      else hipLaunchKernelGGL((ref_gemv_group_kernel<T, false, BPT>), g, dim3(nt), lds, s, p, sg);
+    };
+    if (knobs().ref_gemv_bpt == 4) go2(std::integral_constant<int, 4>{});
+    else go2(std::integral_constant<int, 2>{});
+  };
+  switch (type) {
+    case kQ4_0: gov(std::integral_constant<int, kQ4_0>{}); break;
+    case kQ4_1: gov(std::integral_constant<int, kQ4_1>{}); break;
+    case kQ5_0: gov(std::integral_constant<int, kQ5_0>{}); break;
+    case kQ5_1: gov(std::integral_constant<int, kQ5_1>{}); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

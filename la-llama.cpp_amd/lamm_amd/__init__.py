@@ -96,6 +96,10 @@ lib.lamm_hip_matmul.restype = ctypes.c_int
 lib.lamm_hip_matmul.argtypes = [ctypes.POINTER(Matrix)] * 3 + [ctypes.c_void_p]
 lib.lamm_hip_matmul_ex.restype = ctypes.c_int
 lib.lamm_hip_matmul_ex.argtypes = [ctypes.POINTER(Matrix)] * 3 + [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+lib.lamm_hip_matmul_group.restype = ctypes.c_int
+lib.lamm_hip_matmul_group.argtypes = [ctypes.POINTER(Matrix), ctypes.c_int, ctypes.POINTER(Matrix),
+                                      ctypes.POINTER(Matrix), ctypes.c_int, ctypes.c_void_p]
+GROUP_MAX = 4         # LAMM_GROUP_MAX
 ORDER_REFERENCE = 1   # LAMM_ORDER_REFERENCE: the reference's x86 float order, bit for bit (lamm_ref.hip)
 lib.lamm_hip_matmul_batched.restype = ctypes.c_int
 lib.lamm_hip_matmul_batched.argtypes = [ctypes.POINTER(Matrix)] * 3 + [ctypes.POINTER(Batch), ctypes.c_void_p]
@@ -232,6 +236,19 @@ def matmul_ex(A, B, C, batch=None, flags=0, stream=0):
     _check(lib.lamm_hip_matmul_ex(ctypes.byref(A), ctypes.byref(B), ctypes.byref(C),
                                   ctypes.byref(batch) if batch is not None else None, flags, ctypes.c_void_p(stream)),
            "lamm_hip_matmul_ex")
+
+
+def matmul_group(As, B, Cs, flags=0, stream=0):
+    """lamm_hip_matmul_group: C[i] = A[i] * B for up to GROUP_MAX weights sharing the activation B
+    (one launch for a one-column reference-order call; the bits of one matmul_ex per weight)."""
+    _sync_env()
+    n = len(As)
+    if len(Cs) != n:
+        raise ValueError("one C per A")
+    arrA = (Matrix * max(n, 1))(*As)
+    arrC = (Matrix * max(n, 1))(*Cs)
+    _check(lib.lamm_hip_matmul_group(arrA, n, ctypes.byref(B), arrC, flags, ctypes.c_void_p(stream)),
+           "lamm_hip_matmul_group")
 
 
 def sibling_stats():

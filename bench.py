@@ -908,6 +908,11 @@ def main():
                    # the GPU build leaves ggml fewer CPU ops: 8 pool threads spin less against the
                    # boundary's thread (short-context decode 69 -> 97 tok/s, profiles/r03/boundary/)
                    "t8": llama_e2e(devs, threads=min(8, host_cores()[0])),
+                   # the reference's own headline thread count (4), ggml's threads kept on one NUMA node
+                   # (llama.cpp --numa isolate): with the matmuls on the GPU, ggml's per-node barriers
+                   # cost more than extra threads save (profiles/r05/decode_threads/)
+                   "t4_numa_isolate": llama_e2e(devs, threads=min(4, host_cores()[0]),
+                                                extra_args=("--numa", "isolate")),
                    # the boundary computes in the reference's own float order by default (bit-identical
                    # logits); the fast engines' order for comparison
                    "t16_fast_order": llama_e2e(devs, threads=min(16, host_cores()[0]),

@@ -80,9 +80,23 @@ constexpr int SCALE_W = 130, SCALE_HI = 134, SCALE_LO = 130;   // E8M0: 2^(s-127
 #endif
 
 template <int T> struct F6;
-template <> struct F6<kQ4_0> { static constexpr int ABPB = 18, VBPB = 34; static constexpr bool AFF = false; };
-template <> struct F6<kQ4_1> { static constexpr int ABPB = 20, VBPB = 36; static constexpr bool AFF = true; };
-template <> struct F6<kQ5_0> { static constexpr int ABPB = 22, VBPB = 34; static constexpr bool AFF = false; };
+// SH16 (q5_1): the quant q in [0, 31] is coded as n = q - 16 (|n| <= 16, exact in e2m3) and the
+// block's affine term carries the shift back: d q + m = d n + (m + 16 d), so sum_b (m_a + 16 d_a) s_b
+// -- both products in the m * s MFMA's spare k slots, f16 x f16 exact in fp32 (16 d_a is exact in f16
+// for d_a <= 4094: prepare_fp6_weights reports a weight with a larger block scale, which then stays
+// on the range-guarded dq16 engine)
+template <> struct F6<kQ4_0> { static constexpr int ABPB = 18, VBPB = 34; static constexpr bool AFF = false, SH16 = false; };
+template <> struct F6<kQ4_1> { static constexpr int ABPB = 20, VBPB = 36; static constexpr bool AFF = true, SH16 = false; };
+template <> struct F6<kQ5_0> { static constexpr int ABPB = 22, VBPB = 34; static constexpr bool AFF = false, SH16 = false; };
+template <> struct F6<kQ5_1> { static constexpr int ABPB = 24, VBPB = 36; static constexpr bool AFF = true, SH16 = true; };
+static_assert(F6_KB == 2, "q5_1's shift term uses the m * s MFMA's k slots 2..3");
+static_assert(!F6<kQ4_0>::SH16 && !F6<kQ4_1>::SH16 && !F6<kQ5_0>::SH16, "only q5_1 shifts its quants");
+
+// 16 * h for an f16 bit pattern h (exact below 4096); the f16 bits of the result
+__device__ __forceinline__ uint32_t f16_times16(uint32_t h) {
+  const _Float16 v = __builtin_bit_cast(_Float16, (uint16_t)(h & 0xffffu));
+  return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)(v * (_Float16)16.0f));
+}
 
 // A fragment = 8 dwords = two 16-byte planes: p0 = fp6 code dwords 0-3,
 // p1 = {code dwords 4-5, scale dword ({d, 0} fp16 pair), m (q4_1) / s (q8_1) fp16 or 0}.
@@ -158,7 +172,7 @@ constexpr int PREP_NT = 256;   // rows per prep workgroup
 constexpr int PW_ROWS = 64, PW_NB = 16, PW_NT = 256;
 
 template <int T>
-__global__ __launch_bounds__(PW_NT) void prep_w_fp6(GemvArgs p, unsigned char* ws) {
+__global__ __launch_bounds__(PW_NT) void prep_w_fp6(GemvArgs p, unsigned char* ws, unsigned* big_d) {
   using F = F6<T>;
   constexpr int SEG = PW_NB * F::ABPB;            // bytes per row segment (multiple of 16)
   constexpr int SEGW = SEG / 4 + 1;                // + 1 dword so unaligned block reads stay inside
@@ -206,17 +220,22 @@ __global__ __launch_bounds__(PW_NT) void prep_w_fp6(GemvArgs p, unsigned char* w
       for (int q = 0; q < NW; ++q) m[q] = __builtin_amdgcn_alignbit(src[q + 1], src[q], sh);
       d = m[0] & 0xffffu;
       if constexpr (F::AFF) mv = m[0] >> 16;
-      constexpr int QS = T == kQ4_0 ? 2 : T == kQ4_1 ? 4 : 6;
-      constexpr int OFF = T == kQ4_0 ? 8 : T == kQ5_0 ? 16 : 0;
+      constexpr int QS = T == kQ4_0 ? 2 : T == kQ4_1 ? 4 : T == kQ5_0 ? 6 : 8;
+      constexpr int OFF = T == kQ4_0 ? 8 : T == kQ4_1 ? 0 : 16;
+      constexpr bool Q5 = T == kQ5_0 || T == kQ5_1;
       uint32_t qh = 0;
       if constexpr (T == kQ5_0) qh = get32<2>(m);
+      if constexpr (T == kQ5_1) {
+        qh = get32<4>(m);
+        if ((d & 0x7fffu) > 0x6bffu) *big_d = 1u;   // |d| > 4094 (incl. inf / NaN): 16 d leaves f16
+      }
       uint32_t qs[4];
       unroll<4>([&](auto K) { qs[K] = get32<QS + 4 * K>(m); });
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const uint32_t byte = (qs[e >> 2] >> (8 * (e & 3))) & 0xffu;
         int lo = (int)(byte & 15u), hi = (int)(byte >> 4);
-        if constexpr (T == kQ5_0) {
+        if constexpr (Q5) {
           lo |= (int)((qh >> e) & 1u) << 4;
           hi |= (int)((qh >> (e + 16)) & 1u) << 4;
         }
@@ -681,6 +700,12 @@ __global__ __launch_bounds__((F6Waves<WJ, SI, SJ, KG>::NT)) void gemm_fp6_kernel
         for (int y = 0; y < 2; ++y) msA[y][b >> 1] |= ((uint32_t)fa[b & 1][y].v[7] & 0xffffu) << (16 * (b & 1));
 #pragma unroll
         for (int x = 0; x < WJ; ++x) msB[x][b >> 1] |= ((uint32_t)fb[b & 1][x].v[7] & 0xffffu) << (16 * (b & 1));
+        if constexpr (F::SH16) {   // k slots 2, 3: (16 d_a, s_b)
+#pragma unroll
+          for (int y = 0; y < 2; ++y) msA[y][1] |= f16_times16((uint32_t)fa[b & 1][y].v[6]) << (16 * (b & 1));
+#pragma unroll
+          for (int x = 0; x < WJ; ++x) msB[x][1] |= ((uint32_t)fb[b & 1][x].v[7] & 0xffffu) << (16 * (b & 1));
+        }
       }
     };
 
@@ -969,6 +994,7 @@ __global__ __launch_bounds__(512) void gemm_fp6_kv_kernel(GemvArgs p, const unsi
   F6Res rr[2];
   bool pend = false;
   uint32_t msA[2] = {0, 0}, msB[WJ] = {};   // q4_1: the K-step's m_a / s_b (16 bits per block)
+  uint32_t dsA[2] = {0, 0};                 // q5_1: the K-step's 16 d_a
   // a fragment's operands from its two 16-byte planes: the scale MFMA's six code dwords, the f16
   // MFMA's {d, 0, 0, 0} (q4_1: {d, m} -> {d, 0, 0, 0} too)
   auto codes = [](const u32x4& p0, const u32x4& p1) {
@@ -1070,18 +1096,24 @@ __global__ __launch_bounds__(512) void gemm_fp6_kv_kernel(GemvArgs p, const unsi
       for (int y = 0; y < 2; ++y) msA[y] |= ((uint32_t)wc.d[y][1] & 0xffffu) << (16 * bk);
 #pragma unroll
       for (int x = 0; x < WJ; ++x) msB[x] |= (rb_[S][x][1][3] & 0xffffu) << (16 * bk);
+      if constexpr (F::SH16) {
+#pragma unroll
+        for (int y = 0; y < 2; ++y) dsA[y] |= f16_times16((uint32_t)wc.d[y][0]) << (16 * bk);
+      }
       if (bk == F6_KB - 1) {
 #pragma unroll
         for (int x = 0; x < WJ; ++x) {
-          const half4 sf = __builtin_bit_cast(half4, uint2{msB[x], 0u});
+          // k slots 0, 1: (m_a, s_b) of the two blocks; q5_1 also 2, 3: (16 d_a, s_b)
+          const half4 sf = __builtin_bit_cast(half4, uint2{msB[x], F::SH16 ? msB[x] : 0u});
 #pragma unroll
           for (int y = 0; y < 2; ++y) {
-            const half4 mf = __builtin_bit_cast(half4, uint2{msA[y], 0u});
+            const half4 mf = __builtin_bit_cast(half4, uint2{msA[y], dsA[y]});
             acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x8f16(sf, mf, acc[x][y], 0, 0, 0);
           }
           msB[x] = 0;
         }
         msA[0] = msA[1] = 0;
+        dsA[0] = dsA[1] = 0;
       }
     }
     sb();
@@ -1246,11 +1278,11 @@ F6Plan f6_plan(const GemvArgs& p, const F6Layout& L) {
 int f6_nsplit(const GemvArgs& p, const F6Layout& L) { return f6_plan(p, L).nsplit; }
 
 template <int T>
-void launch_prep_w(const GemvArgs& p, unsigned char* wsA, hipStream_t s) {
+void launch_prep_w(const GemvArgs& p, unsigned char* wsA, hipStream_t s, unsigned* big_d = nullptr) {
   const F6Layout L = F6Layout::of(p);
   const int nkw = (L.nsteps * F6_KB + PW_NB - 1) / PW_NB;
   hipLaunchKernelGGL(prep_w_fp6<T>, dim3((unsigned)(((L.nit * F6_TI) / PW_ROWS) * nkw), (unsigned)L.na), dim3(PW_NT),
-                     0, s, p, wsA);
+                     0, s, p, wsA, big_d);
 }
 
 // Workspace: [packed A (unless prepared weights are given)] [packed B] [split-K partials]
@@ -1372,7 +1404,7 @@ hipError_t launch_fp6_t(const GemvArgs& p, const void* prepA, void* ws, hipStrea
 
 }  // namespace
 
-bool gemm_fp6_supported(int type) { return type == kQ4_0 || type == kQ4_1 || type == kQ5_0; }
+bool gemm_fp6_supported(int type) { return type == kQ4_0 || type == kQ4_1 || type == kQ5_0 || type == kQ5_1; }
 
 int gemm_fp6_tiles(const GemvArgs& p) {
   const F6Layout L = F6Layout::of(p);
@@ -1400,12 +1432,28 @@ size_t gemm_fp6_weight_bytes(int type, const GemvArgs& p) {
   return (size_t)F6Layout::of(p).a_bytes;
 }
 
-hipError_t prepare_fp6_weights(int type, const GemvArgs& p, void* wsA, hipStream_t s) {
+hipError_t prepare_fp6_weights(int type, const GemvArgs& p, void* wsA, hipStream_t s, bool* in_range) {
   auto* w = static_cast<unsigned char*>(wsA);
+  if (in_range) *in_range = true;
   switch (type) {
     case kQ4_0: launch_prep_w<kQ4_0>(p, w, s); break;
     case kQ4_1: launch_prep_w<kQ4_1>(p, w, s); break;
     case kQ5_0: launch_prep_w<kQ5_0>(p, w, s); break;
+    case kQ5_1: {   // reports block scales past 16 d's f16 range (the packed form is then unusable)
+      unsigned* flag = nullptr;
+      if (hipMalloc(&flag, sizeof(unsigned)) != hipSuccess) return hipErrorOutOfMemory;
+      unsigned h = 0;
+      hipError_t e = hipMemsetAsync(flag, 0, sizeof(unsigned), s);
+      if (e == hipSuccess) {
+        launch_prep_w<kQ5_1>(p, w, s, flag);
+        e = hipGetLastError();
+      }
+      if (e == hipSuccess) e = hipMemcpyAsync(&h, flag, sizeof(unsigned), hipMemcpyDeviceToHost, s);
+      if (e == hipSuccess) e = hipStreamSynchronize(s);
+      (void)hipFree(flag);
+      if (in_range) *in_range = h == 0;
+      return e;
+    }
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -1416,6 +1464,9 @@ hipError_t launch_gemm_fp6(int type, const GemvArgs& p, const void* prepA, void*
     case kQ4_0: return launch_fp6_t<kQ4_0>(p, prepA, ws, s);
     case kQ4_1: return launch_fp6_t<kQ4_1>(p, prepA, ws, s);
     case kQ5_0: return launch_fp6_t<kQ5_0>(p, prepA, ws, s);
+    case kQ5_1:   // prepared (range-checked) weights only: the per-call form has no range check
+      if (!prepA) return hipErrorInvalidValue;
+      return launch_fp6_t<kQ5_1>(p, prepA, ws, s);
     default: return hipErrorInvalidValue;
   }
 }

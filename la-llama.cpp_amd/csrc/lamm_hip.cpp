@@ -205,20 +205,23 @@ enum Engine { kEngGemv, kEngDense, kEngKq, kEngFp6, kEngI8, kEngGemvGroups, kEng
 // q5_1 / q8_0 prefill calls whose 128 x 64 tiles fill at least half the chip (it has no K-split):
 // there it beats the exact MFMA-i8 engine (config 4, 4096 x 512 x 4096: q5_1 37.7 vs 49.5 us, q8_0
 // 39.6 vs 47.3 us, profiles/r04/dq16/), while for q4_0 / q4_1 / q5_0 the exact fp6 engine stays ahead
-// (q4_0 28.5 vs 34.4 us).  LAMM_GEMM_PATH=dq16 forces it for every format, fp6 / i8 force the exact
-// engines.
+// (q4_0 28.5 vs 34.4 us).  q5_1 with prepared weights (lamm_weights) runs on the fp6 engine too
+// (F6<kQ5_1>: its quants shifted into e2m3's range, the shift carried by the affine term), its
+// per-call form stays here.  LAMM_GEMM_PATH=dq16 forces it for every format, fp6 / i8 force the
+// exact engines.
 constexpr int kDqMinTiles = 128;
-bool use_dq(int type, const GemvArgs& p) {
+bool use_dq(int type, const GemvArgs& p, bool stationary) {
   if (!gemm_dq_supported(type) || !gemm_dq_args_ok(p)) return false;
   if (knobs().gemm_path == 2) return true;
-  return knobs().gemm_path < 0 && (type == kQ5_1 || type == kQ8_0) && gemm_dq_tiles(p) >= kDqMinTiles;
+  return knobs().gemm_path < 0 && ((type == kQ5_1 && !stationary) || type == kQ8_0) &&
+         gemm_dq_tiles(p) >= kDqMinTiles;
 }
 Engine pick_engine(int type, const GemvArgs& p, bool stationary, bool b_al4) {
   if (p.N <= gemv_max_n(type) || (p.b_f32 && p.N <= 8)) return kEngGemv;
   if (gemm_dense_supported(type) && knobs().dense_gemm) return kEngDense;
   if (gemm_kq_supported(type) && knobs().kq_gemm && b_al4) return kEngKq;
-  if (use_dq(type, p)) return kEngDq;
-  if (gemm_fp6_supported(type) && gemm_path(p, stationary) == 0) return kEngFp6;
+  if (use_dq(type, p, stationary)) return kEngDq;
+  if (gemm_fp6_supported(type) && (type != kQ5_1 || stationary) && gemm_path(p, stationary) == 0) return kEngFp6;
   if (gemm_supported(type) && gemm_args_ok(type, p)) return kEngI8;
   return kEngGemvGroups;
 }
@@ -445,12 +448,18 @@ extern "C" int lamm_hip_weights_create(const lamm_matrix* A, int64_t ne02, int64
       delete W;
       return fail(LAMM_ERR_HIP, "hipMalloc of %zu packed weight bytes failed", nb);
     }
-    const hipError_t e = fp6 ? prepare_fp6_weights(A->type, p, W->packed, static_cast<hipStream_t>(hip_stream))
+    bool in_range = true;
+    const hipError_t e = fp6 ? prepare_fp6_weights(A->type, p, W->packed, static_cast<hipStream_t>(hip_stream), &in_range)
                              : prepare_kq_weights(A->type, p, W->packed, static_cast<hipStream_t>(hip_stream));
     if (e != hipSuccess) {
       (void)hipFree(W->packed);
       delete W;
       return fail(LAMM_ERR_HIP, "weight packing: %s", hipGetErrorString(e));
+    }
+    if (!in_range) {   // q5_1 block scales past the packed form's range: the unpacked engines take it
+      (void)hipFree(W->packed);
+      W->packed = nullptr;
+      W->packed_bytes = 0;
     }
   }
   *out = W;

@@ -96,14 +96,16 @@ size_t gemm_workspace_bytes(int type, const GemvArgs& p);   // device scratch la
 bool gemm_supported(int type);
 bool gemm_args_ok(int type, const GemvArgs& p);   // B pitch/alignment the GEMM staging needs
 
-// q4_0 / q4_1 / q5_0 prefill GEMM on the block-scaled fp6 matrix path (lamm_gemm_fp6.hip)
+// q4_0 / q4_1 / q5_0 (and q5_1 with prepared weights) prefill GEMM on the block-scaled fp6
+// matrix path (lamm_gemm_fp6.hip)
 // prepA: the weights' packed form from prepare_fp6_weights (weight-stationary callers), or
 // null to pack A into the workspace on every call
 hipError_t launch_gemm_fp6(int type, const GemvArgs& p, const void* prepA, void* workspace, hipStream_t s);
 size_t gemm_fp6_workspace_bytes(int type, const GemvArgs& p, bool prepared);
 // packed weights: depends on M, K and the A slices (p.ne12/p.r2 x p.ne13/p.r3), not on N or B
 size_t gemm_fp6_weight_bytes(int type, const GemvArgs& p);
-hipError_t prepare_fp6_weights(int type, const GemvArgs& p, void* wsA, hipStream_t s);
+// in_range (q5_1): false when a block scale is past what the packed form holds (use dq16)
+hipError_t prepare_fp6_weights(int type, const GemvArgs& p, void* wsA, hipStream_t s, bool* in_range = nullptr);
 bool gemm_fp6_supported(int type);
 int gemm_fp6_tiles(const GemvArgs& p);   // 256x128 output tiles of the fp6 GEMM (before K-splits)
 int gemm_fp6_grid(const GemvArgs& p);    // its main-kernel workgroups (tiles x K-splits)

@@ -192,7 +192,7 @@ def test_engine_choice(monkeypatch):
     # q5_1 / q8_0 prefill on the dequantizing f16 engine once its tiles fill half the chip, the
     # exact MFMA-i8 engine (split-K) below that
     assert e("q4_0", 4096, 512, 4096, stationary=True) == "fp6"
-    assert e("q5_1", 4096, 512, 4096, stationary=True) == "dq16"
+    assert e("q5_1", 4096, 512, 4096, stationary=True) == "fp6" and e("q5_1", 4096, 512, 4096) == "dq16"
     assert e("q8_0", 4096, 512, 4096) == "dq16" and e("q8_0", 4096, 64, 4096) == "i8"
     assert e("q4_0", 4096, 9, 4096) in ("fp6", "i8")
     assert e("q5_0", 4096, 512, 4096, b_f32=True) == e("q5_0", 4096, 512, 4096)

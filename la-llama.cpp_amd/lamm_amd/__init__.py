@@ -310,7 +310,7 @@ def mul_mat_torch(wtype, a, b, c, M, N, K, lda=None, ldb=None, ldc=None, stream=
 
 class Weights:
     """Weight-stationary handle (lamm_hip_weights_create): A stays where it is and must not
-    change; q4_0 / q4_1 / q5_0 additionally keep their packed prefill-GEMM form on device.
+    change; q4_0 / q4_1 / q5_0 / q5_1 additionally keep their packed prefill-GEMM form on device.
     ``a`` is a torch device tensor of A blocks; lda in blocks; slice strides in bytes."""
 
     def __init__(self, wtype, a, M, K, lda=None, ne02=1, ne03=1, nba2=0, nba3=0, stream=None):

@@ -725,7 +725,7 @@ def summary(out):
             if "gemm_per_launch_us" in e:
                 s[f].update({"gemm": e["gemm_engine"], "gemm_us": e["gemm_per_launch_us"], "gemm_frac": e["gemm_frac"]})
     e2e = out.get("llama7b_e2e", {})
-    for k in ("t16", "t8", "t16_fast_order"):
+    for k in ("t16", "t8", "t4_numa_isolate", "t16_fast_order"):
         r = e2e.get(k, {})
         if "pp_tok_s" in r:
             s[f"config5_{k}"] = {kk: r.get(kk) for kk in ("pp_tok_s", "tg_tok_s", "tg_from_empty_tok_s")}

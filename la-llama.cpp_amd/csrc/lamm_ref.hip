@@ -463,13 +463,21 @@ __device__ __forceinline__ void ref_gemv_body(const GemvArgs& p, const RefSegs& 
 }
 
 template <int T, bool BF32, bool ONE_SLICE, int BPT = 4>
-__global__ __launch_bounds__(GR * GKC / BPT) void ref_gemv_kernel(GemvArgs p) {
+#ifndef REF_GEMV_WPE
+#define REF_GEMV_WPE 6   // waves per SIMD the register budget is cut for (probe builds: 5 = unconstrained)
+#endif
+// 512-thread form (BPT 2): 86 -> <= 80 VGPRs, so three workgroups (24 waves) share a CU instead of
+// two -- a grouped launch (lamm_hip_matmul_group, 1536 / 2752 workgroups) runs in fewer rounds.  The
+// 256-thread form would spill under the same cut and keeps its budget.
+__global__ __launch_bounds__(GR * GKC / BPT) __attribute__((amdgpu_waves_per_eu(BPT == 2 ? REF_GEMV_WPE : 1)))
+void ref_gemv_kernel(GemvArgs p) {
   ref_gemv_body<T, BF32, ONE_SLICE ? 0 : 1, BPT>(p, RefSegs{});
 }
 
 // several weights times one activation column in one launch (segment 0 in p.A / p.C / p.M)
 template <int T, bool BF32, int BPT = 4>
-__global__ __launch_bounds__(GR * GKC / BPT) void ref_gemv_group_kernel(GemvArgs p, RefSegs sg) {
+__global__ __launch_bounds__(GR * GKC / BPT) __attribute__((amdgpu_waves_per_eu(BPT == 2 ? REF_GEMV_WPE : 1)))
+void ref_gemv_group_kernel(GemvArgs p, RefSegs sg) {
   ref_gemv_body<T, BF32, 2, BPT>(p, sg);
 }
 

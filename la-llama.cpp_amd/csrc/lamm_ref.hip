@@ -274,7 +274,12 @@ __global__ __launch_bounds__(RR * 8) void ref_kernel(GemvArgs p) {
 // The activation column is staged once per workgroup (ActStage; F32 rows quantized there, ggml's
 // AVX2 from_float bit for bit -- the boundary's fused INIT).  The chunk's A loads for the next
 // chunk are in flight while the chains run.
-constexpr int GR = 8, GKC = 128, GP = GKC + 4;   // rows, blocks per chunk, LDS pitch
+// GKC: blocks per chunk of a single-weight launch with K > 4096 (each workgroup's long chain then
+// runs over fewer, longer chunks); everything else takes chunks of GKC_S = 64 -- 256-thread
+// workgroups of a third of the LDS, so a grouped launch keeps ~2x the workgroups resident
+// (tools/ref_group_ab.py, profiles/r05/ref_gemv_occupancy/: q|k|v 9.1 -> 7.7 us, gate|up 16.4 -> 14.0,
+// wo 4.45 -> 4.33; down 8.6 at 128 vs 9.1 at 64)
+constexpr int GR = 8, GKC = 128, GKC_S = 64;   // rows, blocks per chunk (the LDS pitch is the chunk + 4)
 
 // dword at byte O of a register byte string, zero past its end (the last block's slack bytes)
 template <int O, int NW>
@@ -285,9 +290,9 @@ __device__ __forceinline__ uint32_t get32z(const uint32_t (&w)[NW]) {
   else return w[O >> 2] >> ((O & 3) * 8);
 }
 
-size_t ref_gemv_lds(int type, int nblk) {
+size_t ref_gemv_lds(int type, int nblk, int ck = GKC) {
   const bool aff = type == kQ4_1 || type == kQ5_1;
-  return (((size_t)nblk * 40 + 15) & ~size_t(15)) + sizeof(float) * GP * (GR * 8 + GR + (aff ? GR : 0));
+  return (((size_t)nblk * 40 + 15) & ~size_t(15)) + sizeof(float) * (ck + 4) * (GR * 8 + GR + (aff ? GR : 0));
 }
 
 #ifndef REF_GAB
@@ -297,9 +302,10 @@ size_t ref_gemv_lds(int type, int nblk) {
 #endif
 // MODE 0: one slice; 1: ggml's batch slices over blockIdx.z; 2: blockIdx.z picks one of up to
 // kRefSegs weights sharing the activation column (lamm_hip_matmul_group)
-template <int T, bool BF32, int MODE, int BPT>
+template <int T, bool BF32, int MODE, int BPT, int CK>
 __device__ __forceinline__ void ref_gemv_body(const GemvArgs& p, const RefSegs& sg) {
   using F = RFmt<T>;
+  constexpr int GKC = CK, GP = CK + 4;   // this instance's chunk (hides the namespace defaults)
   // BPT consecutive blocks of one row per producer thread (one wide load of BPT * BPB bytes, dword
   // aligned: BPB is even); NT threads cover the chunk's GR x GKC blocks.  Config 2 (q4_0 4096 x 4096,
   // F32 row, profiles/r05/ref_gemv/): BPT 2 (512 threads) 5.1-5.4 us, 4 (256) 5.9-6.0, 1 (1024
@@ -462,23 +468,23 @@ __device__ __forceinline__ void ref_gemv_body(const GemvArgs& p, const RefSegs& 
   if (MODE != 2 && p.flag) signal_done(p);
 }
 
-template <int T, bool BF32, bool ONE_SLICE, int BPT = 4>
+template <int T, bool BF32, bool ONE_SLICE, int BPT = 4, int CK = GKC>
 #ifndef REF_GEMV_WPE
 #define REF_GEMV_WPE 6   // waves per SIMD the register budget is cut for (probe builds: 5 = unconstrained)
 #endif
 // 512-thread form (BPT 2): 86 -> <= 80 VGPRs, so three workgroups (24 waves) share a CU instead of
 // two -- a grouped launch (lamm_hip_matmul_group, 1536 / 2752 workgroups) runs in fewer rounds.  The
 // 256-thread form would spill under the same cut and keeps its budget.
-__global__ __launch_bounds__(GR * GKC / BPT) __attribute__((amdgpu_waves_per_eu(BPT == 2 ? REF_GEMV_WPE : 1)))
+__global__ __launch_bounds__(GR * CK / BPT) __attribute__((amdgpu_waves_per_eu(BPT == 2 ? REF_GEMV_WPE : 1)))
 void ref_gemv_kernel(GemvArgs p) {
-  ref_gemv_body<T, BF32, ONE_SLICE ? 0 : 1, BPT>(p, RefSegs{});
+  ref_gemv_body<T, BF32, ONE_SLICE ? 0 : 1, BPT, CK>(p, RefSegs{});
 }
 
 // several weights times one activation column in one launch (segment 0 in p.A / p.C / p.M)
-template <int T, bool BF32, int BPT = 4>
-__global__ __launch_bounds__(GR * GKC / BPT) __attribute__((amdgpu_waves_per_eu(BPT == 2 ? REF_GEMV_WPE : 1)))
+template <int T, bool BF32, int BPT = 4, int CK = GKC_S>
+__global__ __launch_bounds__(GR * CK / BPT) __attribute__((amdgpu_waves_per_eu(BPT == 2 ? REF_GEMV_WPE : 1)))
 void ref_gemv_group_kernel(GemvArgs p, RefSegs sg) {
-  ref_gemv_body<T, BF32, 2, BPT>(p, sg);
+  ref_gemv_body<T, BF32, 2, BPT, CK>(p, sg);
 }
 
 // ---------------------------------------------------------------- F16 x F16: ggml_vec_dot_f16's order
@@ -1311,7 +1317,8 @@ hipError_t launch_ref(int type, const GemvArgs& p, hipStream_t s) {
   const int slices = p.ne12 * p.ne13;
   if (ref_gemv_supported(type, p)) {   // one column: ref_gemv_kernel (F32 rows quantized in its staging)
     const dim3 g((unsigned)((p.M + GR - 1) / GR), 1, (unsigned)slices);
-    const size_t lds = ref_gemv_lds(type, p.nblk);
+    const bool long_k = p.nblk > GKC;   // K > 4096: chunks of GKC, else GKC_S
+    const size_t lds = ref_gemv_lds(type, p.nblk, long_k ? GKC : GKC_S);
     const LaunchTiming tm = take_launch_timing();
     auto gov = [&](auto tc) {
       constexpr int T = decltype(tc)::value;
@@ -1320,15 +1327,19 @@ hipError_t launch_ref(int type, const GemvArgs& p, hipStream_t s) {
         else if (!direct_launch(reinterpret_cast<const void*>(kern), g, dim3(nt), (uint32_t)lds, &p, sizeof p))
           hipLaunchKernelGGL(kern, g, dim3(nt), lds, s, p);   // (direct: the library's own queue, lamm_aql.cpp)
       };
-      auto go2 = [&](auto bc) {
-        constexpr int BPT = decltype(bc)::value, nt = GR * GKC / BPT;
+      auto go1 = [&](auto bc, auto cc) {
+        constexpr int BPT = decltype(bc)::value, CK = decltype(cc)::value, nt = GR * CK / BPT;
         if (p.b_f32) {
-          if (slices == 1) go3(ref_gemv_kernel<T, true, true, BPT>, nt);
-          else go3(ref_gemv_kernel<T, true, false, BPT>, nt);
+          if (slices == 1) go3(ref_gemv_kernel<T, true, true, BPT, CK>, nt);
+          else go3(ref_gemv_kernel<T, true, false, BPT, CK>, nt);
         } else {
-          if (slices == 1) go3(ref_gemv_kernel<T, false, true, BPT>, nt);
-          else go3(ref_gemv_kernel<T, false, false, BPT>, nt);
+          if (slices == 1) go3(ref_gemv_kernel<T, false, true, BPT, CK>, nt);
+          else go3(ref_gemv_kernel<T, false, false, BPT, CK>, nt);
         }
+      };
+      auto go2 = [&](auto bc) {
+        if (long_k) go1(bc, std::integral_constant<int, GKC>{});
+        else go1(bc, std::integral_constant<int, GKC_S>{});
       };
       if (knobs().ref_gemv_bpt == 4) go2(std::integral_constant<int, 4>{});
       else go2(std::integral_constant<int, 2>{});
@@ -1440,11 +1451,11 @@ hipError_t launch_ref_group(int type, const GemvArgs& p, const RefSegs& sg, int 
   int mmax = 0;
   for (int i = 0; i < nseg; ++i) mmax = sg.M[i] > mmax ? sg.M[i] : mmax;
   const dim3 g((unsigned)((mmax + GR - 1) / GR), 1, (unsigned)nseg);
-  const size_t lds = ref_gemv_lds(type, p.nblk);
+  const size_t lds = ref_gemv_lds(type, p.nblk, GKC_S);
   auto gov = [&](auto tc) {
     constexpr int T = decltype(tc)::value;
     auto go2 = [&](auto bc) {
-      constexpr int BPT = decltype(bc)::value, nt = GR * GKC / BPT;
+      constexpr int BPT = decltype(bc)::value, nt = GR * GKC_S / BPT;
       if (p.b_f32) hipLaunchKernelGGL((ref_gemv_group_kernel<T, true, BPT>), g, dim3(nt), lds, s, p, sg);
       else hipLaunchKernelGGL((ref_gemv_group_kernel<T, false, BPT>), g, dim3(nt), lds, s, p, sg);
     };

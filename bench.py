@@ -503,6 +503,21 @@ def ref_order_kernels(ctx, fmt, M, N, K, steps):
                        "kernel": "lamm::ref_gemv_kernel (csrc/lamm_ref.hip)", "bound": "hbm",
                        "per_launch_us": round(iso * 1e6, 3), "achieved_GBs": round(u / iso / 1e9, 1),
                        "frac": round(u / iso / 1e9 / HBM_PEAK_GBS, 4)}
+    # llama.cpp's decode through the boundary runs wq / wk / wv as ONE grouped launch (sibling calls,
+    # lamm_hip_matmul_group -> ref_gemv_group_kernel): three config-2 weights per step,
+    # rotated over the copies, graph-replayed
+    if R >= 3 and t in (la.Q4_0, la.Q4_1, la.Q5_0, la.Q5_1):
+        C3 = torch.zeros(3 * M, dtype=torch.float32, device="cuda")
+        Cs3 = [la.Matrix(C3.data_ptr() + 4 * M * j, la.F32, M, 1, M) for j in range(3)]
+        _, kg, _ = time_steps(ctx, lambda i: la.matmul_group([mats[(3 * i + j) % R] for j in range(3)], Bm1, Cs3,
+                                                             la.ORDER_REFERENCE, torch.cuda.current_stream().cuda_stream),
+                              max(steps, 100), 2)
+        out["gemv_group3"] = {"workload": f"3 x {fmt.upper()}xQ8 GEMV M={M} N=1 K={K} in one launch (wq|wk|wv of a decode "
+                                          f"step), {R} weight copies rotated",
+                              "kernel": "lamm::ref_gemv_group_kernel (csrc/lamm_ref.hip)", "bound": "hbm",
+                              "per_launch_us": round(kg * 1e6, 3), "achieved_GBs": round(3 * u / kg / 1e9, 1),
+                              "frac": round(3 * u / kg / 1e9 / HBM_PEAK_GBS, 4)}
+        del C3
     BmN = la.Matrix(B.data_ptr(), vt, kb, N, kb)
     CmN = la.Matrix(C.data_ptr(), la.F32, M, N, M)
     _, kern, _ = time_steps(ctx, lambda i: la.matmul_ex(mats[0], BmN, CmN, flags=la.ORDER_REFERENCE,
@@ -714,6 +729,9 @@ def summary(out):
     ro = out.get("ref_order", {})
     if "gemv" in ro:
         s["ref_order_gemv"] = {"kernel": "ref_gemv_kernel", "us": ro["gemv"]["per_launch_us"], "frac_hbm": ro["gemv"]["frac"]}
+    if "gemv_group3" in ro:
+        s["ref_order_gemv_group3"] = {"kernel": "ref_gemv_group_kernel", "us": ro["gemv_group3"]["per_launch_us"],
+                                      "frac_hbm": ro["gemv_group3"]["frac"]}
     if "gemm" in ro:
         s["ref_order_gemm"] = {"kernel": ro["gemm"]["kernel"].split(" ")[0].split("::")[-1], "us": ro["gemm"]["per_launch_us"],
                                "frac_fma_floor": ro["gemm"]["frac"], "frac_i8": ro["gemm"]["i8_frac"]}

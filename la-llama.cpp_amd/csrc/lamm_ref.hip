@@ -290,10 +290,13 @@ __device__ __forceinline__ uint32_t get32z(const uint32_t (&w)[NW]) {
   else return w[O >> 2] >> ((O & 3) * 8);
 }
 
-size_t ref_gemv_lds(int type, int nblk, int ck = GKC) {
+size_t ref_gemv_lds(int type, int nblk, int ck = GKC, int rg = GR) {
   const bool aff = type == kQ4_1 || type == kQ5_1;
-  return (((size_t)nblk * 40 + 15) & ~size_t(15)) + sizeof(float) * (ck + 4) * (GR * 8 + GR + (aff ? GR : 0));
+  return (((size_t)nblk * 40 + 15) & ~size_t(15)) + sizeof(float) * (ck + 4) * (rg * 8 + rg + (aff ? rg : 0));
 }
+#ifndef REF_GROUP_RG
+#define REF_GROUP_RG 8   // rows per workgroup of the grouped launch (probe builds: 16)
+#endif
 
 #ifndef REF_GAB
 // probe builds only (ablations of ref_gemv_kernel): 1 no chains, 2 no producer arithmetic,
@@ -302,10 +305,10 @@ size_t ref_gemv_lds(int type, int nblk, int ck = GKC) {
 #endif
 // MODE 0: one slice; 1: ggml's batch slices over blockIdx.z; 2: blockIdx.z picks one of up to
 // kRefSegs weights sharing the activation column (lamm_hip_matmul_group)
-template <int T, bool BF32, int MODE, int BPT, int CK>
+template <int T, bool BF32, int MODE, int BPT, int CK, int RG = GR>
 __device__ __forceinline__ void ref_gemv_body(const GemvArgs& p, const RefSegs& sg) {
   using F = RFmt<T>;
-  constexpr int GKC = CK, GP = CK + 4;   // this instance's chunk (hides the namespace defaults)
+  constexpr int GKC = CK, GP = CK + 4, GR = RG;   // this instance's chunk and rows (hide the defaults)
   // BPT consecutive blocks of one row per producer thread (one wide load of BPT * BPB bytes, dword
   // aligned: BPB is even); NT threads cover the chunk's GR x GKC blocks.  Config 2 (q4_0 4096 x 4096,
   // F32 row, profiles/r05/ref_gemv/): BPT 2 (512 threads) 5.1-5.4 us, 4 (256) 5.9-6.0, 1 (1024
@@ -430,7 +433,7 @@ __device__ __forceinline__ void ref_gemv_body(const GemvArgs& p, const RefSegs& 
     __syncthreads();
     // ---- chains: wave 0, the chunk's blocks in order (zeros past nb leave a chain unchanged:
     // fma(0, 0, acc) == acc, and no chain is ever -0)
-    if (t < 64 && REF_GAB != 1) {
+    if (t < 8 * GR && REF_GAB != 1) {   // (GR / 8 chain waves)
       // the whole chunk, always: the producers zero-filled it past nb, and a fixed trip count
       // lets the LDS reads run ahead of the chain instead of one wait per 4 blocks
       const float* xr = &xs[(cr * 8 + cl) * GP];
@@ -454,7 +457,7 @@ __device__ __forceinline__ void ref_gemv_body(const GemvArgs& p, const RefSegs& 
     }
     __syncthreads();
   }
-  if (t < 64) {
+  if (t < 8 * GR) {
     float v = chain;
     {
 #pragma clang fp contract(off)
@@ -481,10 +484,10 @@ void ref_gemv_kernel(GemvArgs p) {
 }
 
 // several weights times one activation column in one launch (segment 0 in p.A / p.C / p.M)
-template <int T, bool BF32, int BPT = 4, int CK = GKC_S>
-__global__ __launch_bounds__(GR * CK / BPT) __attribute__((amdgpu_waves_per_eu(BPT == 2 ? REF_GEMV_WPE : 1)))
+template <int T, bool BF32, int BPT = 4, int CK = GKC_S, int RG = REF_GROUP_RG>
+__global__ __launch_bounds__(RG * CK / BPT) __attribute__((amdgpu_waves_per_eu(BPT == 2 ? REF_GEMV_WPE : 1)))
 void ref_gemv_group_kernel(GemvArgs p, RefSegs sg) {
-  ref_gemv_body<T, BF32, 2, BPT, CK>(p, sg);
+  ref_gemv_body<T, BF32, 2, BPT, CK, RG>(p, sg);
 }
 
 // ---------------------------------------------------------------- F16 x F16: ggml_vec_dot_f16's order
@@ -1450,12 +1453,12 @@ hipError_t launch_ref_group(int type, const GemvArgs& p, const RefSegs& sg, int 
     return hipErrorInvalidValue;
   int mmax = 0;
   for (int i = 0; i < nseg; ++i) mmax = sg.M[i] > mmax ? sg.M[i] : mmax;
-  const dim3 g((unsigned)((mmax + GR - 1) / GR), 1, (unsigned)nseg);
-  const size_t lds = ref_gemv_lds(type, p.nblk, GKC_S);
+  const dim3 g((unsigned)((mmax + REF_GROUP_RG - 1) / REF_GROUP_RG), 1, (unsigned)nseg);
+  const size_t lds = ref_gemv_lds(type, p.nblk, GKC_S, REF_GROUP_RG);
   auto gov = [&](auto tc) {
     constexpr int T = decltype(tc)::value;
     auto go2 = [&](auto bc) {
-      constexpr int BPT = decltype(bc)::value, nt = GR * GKC_S / BPT;
+      constexpr int BPT = decltype(bc)::value, nt = REF_GROUP_RG * GKC_S / BPT;
       if (p.b_f32) hipLaunchKernelGGL((ref_gemv_group_kernel<T, true, BPT>), g, dim3(nt), lds, s, p, sg);
       else hipLaunchKernelGGL((ref_gemv_group_kernel<T, false, BPT>), g, dim3(nt), lds, s, p, sg);
     };

@@ -290,9 +290,16 @@ __device__ __forceinline__ uint32_t get32z(const uint32_t (&w)[NW]) {
   else return w[O >> 2] >> ((O & 3) * 8);
 }
 
+#ifndef REF_NEG_LDS
+// probe builds: the q4_0 / q5_0 offset dots once per block in the staging instead of per row --
+// measured SLOWER (q|k|v 7.8 -> 9.2 us, wo 4.3 -> 4.7; the extra barrier and LDS reads cost more than
+// the 8 dot4 per block and row: the kernel is not VALU-bound, profiles/r05/ref_gemv_occupancy/)
+#define REF_NEG_LDS 0
+#endif
 size_t ref_gemv_lds(int type, int nblk, int ck = GKC, int rg = GR) {
   const bool aff = type == kQ4_1 || type == kQ5_1;
-  return (((size_t)nblk * 40 + 15) & ~size_t(15)) + sizeof(float) * (ck + 4) * (rg * 8 + rg + (aff ? rg : 0));
+  const size_t neg = REF_NEG_LDS && (type == kQ4_0 || type == kQ5_0) ? (size_t)nblk * 32 : 0;
+  return (((size_t)nblk * 40 + 15) & ~size_t(15)) + sizeof(float) * (ck + 4) * (rg * 8 + rg + (aff ? rg : 0)) + neg;
 }
 #ifndef REF_GROUP_RG
 #define REF_GROUP_RG 8   // rows per workgroup of the grouped launch (probe builds: 16)
@@ -381,6 +388,22 @@ __device__ __forceinline__ void ref_gemv_body(const GemvArgs& p, const RefSegs& 
     }
   }
   __syncthreads();
+  // the offset term's 8 lane dots depend on the activation only: once per block, not per row
+  u32x4* sng = reinterpret_cast<u32x4*>(pms);   // (q4_0 / q5_0 leave pms unused)
+  if constexpr (REF_NEG_LDS && NEG != 0) {
+    for (int it = t; it < nb; it += NT) {
+      const u32x4 b0 = sq0[it], b1 = sq1[it];
+      u32x4 n0, n1;
+#pragma unroll
+      for (int l = 0; l < 4; ++l) {
+        n0[l] = (uint32_t)dot4(b0[l], NEG, 0);
+        n1[l] = (uint32_t)dot4(b1[l], NEG, 0);
+      }
+      sng[2 * it] = n0;
+      sng[2 * it + 1] = n1;
+    }
+    __syncthreads();
+  }
 
   const int cl = t & 7, cr = t >> 3;   // chain lane (wave 0): row cr, lane cl
   float chain = 0.f, summs = 0.f;
@@ -408,13 +431,22 @@ __device__ __forceinline__ void ref_gemv_body(const GemvArgs& p, const RefSegs& 
         const int ub = ok ? u : 0;
         const u32x4 b0 = sq0[ub], b1 = sq1[ub];
         const uint32_t bq[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+        int negc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if constexpr (REF_NEG_LDS && NEG != 0) {
+          const u32x4 n0 = sng[2 * ub], n1 = sng[2 * ub + 1];
+#pragma unroll
+          for (int l = 0; l < 4; ++l) {
+            negc[l] = (int)n0[l];
+            negc[4 + l] = (int)n1[l];
+          }
+        }
         float d = da * sbd[ub];
         asm("" : "+v"(d));   // rounded on its own: never contracted into the chain's fma
         // past nb / nrows only d is zeroed: X is a finite integer whatever the (zero or clamped)
         // operands, and fma(0, X, acc) == acc (no chain is ever -0)
 #pragma unroll
         for (int l = 0; l < 8; ++l) {
-          const int c = NEG ? dot4(bq[l], NEG, 0) : 0;
+          const int c = REF_NEG_LDS ? negc[l] : NEG ? dot4(bq[l], NEG, 0) : 0;
           xv[l][j] = (float)dot4(q[l], bq[l], c);
         }
         dv[j] = ok ? d : 0.f;

@@ -346,10 +346,13 @@ template <> struct KQ<kQ4_K> { static constexpr int BPB = 144; };
 template <> struct KQ<kQ5_K> { static constexpr int BPB = 176; };
 template <> struct KQ<kQ6_K> { static constexpr int BPB = 210; };
 
+#ifndef KQ_WAVES
+#define KQ_WAVES 8   // rows (waves) per workgroup (probe builds: 4, 16)
+#endif
 template <int T, int ITER>
-__global__ __launch_bounds__(512) void gemv_kq_kernel(const unsigned char* A, int64_t lda, const unsigned char* B,
-                                                      float* C, int M, int nsb) {
-  constexpr int WAVES = 8, NSB = 16 * ITER, SBW = 80, SDW = NSB * 73, PASS = (SDW + 64 * WAVES - 1) / (64 * WAVES);
+__global__ __launch_bounds__(64 * KQ_WAVES) void gemv_kq_kernel(const unsigned char* A, int64_t lda, const unsigned char* B,
+                                                                float* C, int M, int nsb) {
+  constexpr int WAVES = KQ_WAVES, NSB = 16 * ITER, SBW = 80, SDW = NSB * 73, PASS = (SDW + 64 * WAVES - 1) / (64 * WAVES);
   constexpr int BPB = KQ<T>::BPB;
   __shared__ __attribute__((aligned(16))) uint32_t act[NSB * SBW];
   const int lane = threadIdx.x & 63, t0 = threadIdx.x, qq = lane & 3;
@@ -613,13 +616,14 @@ bool gemv_kq_supported(int type, const GemvArgs& p) {
 }
 
 hipError_t launch_gemv_kq(int type, const GemvArgs& p, hipStream_t s) {
-  const dim3 g((unsigned)((p.M + 7) / 8));
+  const dim3 g((unsigned)((p.M + KQ_WAVES - 1) / KQ_WAVES));
   auto go = [&](auto tc) {
     constexpr int T = decltype(tc)::value;
     const LaunchTiming tm = take_launch_timing();
     auto go = [&](auto kern) {
-      if (tm.start) hipExtLaunchKernelGGL(kern, g, dim3(512), 0, s, tm.start, tm.stop, 0, p.A, p.lda, p.B, p.C, p.M, p.nblk);
-      else hipLaunchKernelGGL(kern, g, dim3(512), 0, s, p.A, p.lda, p.B, p.C, p.M, p.nblk);
+      if (tm.start)
+        hipExtLaunchKernelGGL(kern, g, dim3(64 * KQ_WAVES), 0, s, tm.start, tm.stop, 0, p.A, p.lda, p.B, p.C, p.M, p.nblk);
+      else hipLaunchKernelGGL(kern, g, dim3(64 * KQ_WAVES), 0, s, p.A, p.lda, p.B, p.C, p.M, p.nblk);
     };
     if (p.nblk <= 16) go(gemv_kq_kernel<T, 1>);
     else if (p.nblk <= 32) go(gemv_kq_kernel<T, 2>);

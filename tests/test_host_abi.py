@@ -97,6 +97,27 @@ def test_validation_errors():
     assert _rc(A, B, C) in (la.LAMM_OK, la.LAMM_ERR_NODEV)
 
 
+def test_group_validation_errors():
+    """lamm_hip_matmul_group: 1..LAMM_GROUP_MAX weights; a group the one-launch form cannot take (two
+    columns, mixed types) goes through the per-weight calls and their own validation."""
+    A, B, C = _mats()
+    rc = la.lib.lamm_hip_matmul_group((la.Matrix * 5)(*([A] * 5)), 5, ctypes.byref(B), (la.Matrix * 5)(*([C] * 5)),
+                                      la.ORDER_REFERENCE, None)
+    assert rc == la.LAMM_ERR_SHAPE
+    rc = la.lib.lamm_hip_matmul_group((la.Matrix * 1)(A), 0, ctypes.byref(B), (la.Matrix * 1)(C), 0, None)
+    assert rc == la.LAMM_ERR_SHAPE
+    if not NO_GPU:   # the calls below reach the per-weight path with placeholder pointers
+        return
+    A2, B2, C2 = _mats()
+    B2.row = 64                       # a shape error in the second weight's call
+    rc = la.lib.lamm_hip_matmul_group((la.Matrix * 2)(A, A2), 2, ctypes.byref(B2), (la.Matrix * 2)(C, C2), 0, None)
+    assert rc in (la.LAMM_ERR_SHAPE, la.LAMM_ERR_NODEV)
+    A3, _, _ = _mats()
+    A3.type = 11                      # Q3_K: no kernel, even inside a group
+    rc = la.lib.lamm_hip_matmul_group((la.Matrix * 2)(A, A3), 2, ctypes.byref(B), (la.Matrix * 2)(C, C), 0, None)
+    assert rc in (la.LAMM_ERR_TYPE, la.LAMM_ERR_NODEV)
+
+
 @pytest.mark.skipif(not NO_GPU, reason="checks the no-GPU behaviour")
 def test_no_gpu_behaviour():
     A, B, C = _mats()

@@ -279,7 +279,10 @@ __global__ __launch_bounds__(RR * 8) void ref_kernel(GemvArgs p) {
 // workgroups of a third of the LDS, so a grouped launch keeps ~2x the workgroups resident
 // (tools/ref_group_ab.py, profiles/r05/ref_gemv_occupancy/: q|k|v 9.1 -> 7.7 us, gate|up 16.4 -> 14.0,
 // wo 4.45 -> 4.33; down 8.6 at 128 vs 9.1 at 64)
-constexpr int GR = 8, GKC = 128, GKC_S = 64;   // rows, blocks per chunk (the LDS pitch is the chunk + 4)
+#ifndef REF_GKC_S
+#define REF_GKC_S 64   // probe builds: the short chunk (a multiple of 4 and of 2 x blocks per producer)
+#endif
+constexpr int GR = 8, GKC = 128, GKC_S = REF_GKC_S;   // rows, blocks per chunk (the LDS pitch is the chunk + 4)
 
 // dword at byte O of a register byte string, zero past its end (the last block's slack bytes)
 template <int O, int NW>

@@ -182,7 +182,19 @@ class Ctx:
             self.dist.destroy_process_group()
 
 
-def time_steps(ctx, step, steps, warmup, graph=True):
+_SCRATCH = None
+
+
+def flush_caches(torch):
+    """Write a 512 MiB scratch buffer (2x the 256 MiB MALL, 128x an XCD's L2) so that weights an
+    untimed pass touched are not still cached when the timed pass starts."""
+    global _SCRATCH
+    if _SCRATCH is None:
+        _SCRATCH = torch.empty(512 << 20, dtype=torch.uint8, device="cuda")
+    _SCRATCH.fill_(1)
+
+
+def time_steps(ctx, step, steps, warmup, graph=True, flush=False):
     """Warm-up, then EXACTLY `steps` steps bracketed by barrier + synchronize on both sides;
     returns (wall seconds per step, event-timed seconds per step -- both max over ranks --,
     graph used).  graph: the steps are captured once as a hipGraph and replayed in the timed
@@ -218,6 +230,8 @@ def time_steps(ctx, step, steps, warmup, graph=True):
     # the timed region: nothing but the K steps between the barrier + synchronize brackets (the
     # events of the second pass cost host calls of their own: profiles/r04/roofline/)
     with torch.cuda.stream(st):
+        if flush:
+            flush_caches(torch)
         ctx.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -226,6 +240,8 @@ def time_steps(ctx, step, steps, warmup, graph=True):
         ctx.barrier()
         wall = time.perf_counter() - t0
         # the same K steps again, timed by HIP events on the stream they run on
+        if flush:
+            flush_caches(torch)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(st)
         run()
@@ -272,10 +288,53 @@ def steps_lib(la):
                                                       ctypes.POINTER(la.Matrix), ctypes.c_int, ctypes.c_int,
                                                       ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.c_int,
                                                       ctypes.c_int]
+        _STEPS_LIB.lamm_read_floor.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_size_t,
+                                               ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                               ctypes.POINTER(ctypes.c_float)]
+        _STEPS_LIB.lamm_empty_floor.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                                ctypes.POINTER(ctypes.c_float)]
         _STEPS_LIB.lamm_steps_direct.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(la.Matrix),
                                                  ctypes.POINTER(la.Matrix), ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                  ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
     return _STEPS_LIB
+
+
+def read_floor(la, base_ptr, stride, R, nbytes, n):
+    """median duration (s) of n isolated launches of a read-only kernel on the config-2 GEMV's grid over
+    the same rotated weight bytes (tools/steps_loop.hip lamm_read_floor, timed like isolated_launches):
+    what one launch of that size costs before any GEMV work -- the single-launch ceiling of DESIGN §3.1,
+    measured in the driver's own run"""
+    import ctypes
+    if steps_lib(la) is None:
+        return None
+    import torch
+    out = (ctypes.c_float * n)()
+    st = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    rc = _STEPS_LIB.lamm_read_floor(ctypes.c_void_p(base_ptr), stride, R, nbytes, 0, n, ctypes.c_void_p(st.cuda_stream),
+                                    out)
+    torch.cuda.synchronize()
+    v = sorted(out)
+    if rc != 0 or v[0] <= 0.0:
+        log("lamm_read_floor failed:", rc, v[:3])
+        return None
+    return v[n // 2] * 1e-6
+
+
+def empty_floor(la, grid, n):
+    """median duration (s) of n isolated launches of an EMPTY kernel on `grid` workgroups of 512 threads,
+    timed like isolated_launches: the dispatch's own cost, which every per-launch time above includes"""
+    import ctypes
+    if steps_lib(la) is None:
+        return None
+    import torch
+    out = (ctypes.c_float * n)()
+    st = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    rc = _STEPS_LIB.lamm_empty_floor(grid, n, ctypes.c_void_p(st.cuda_stream), out)
+    torch.cuda.synchronize()
+    v = sorted(out)
+    return v[n // 2] * 1e-6 if rc == 0 and v[0] > 0.0 else None
 
 
 def time_direct(ctx, mats, R, Bm, Cm, steps, warmup, flags=0):
@@ -292,11 +351,17 @@ def time_direct(ctx, mats, R, Bm, Cm, steps, warmup, flags=0):
     dev = torch.cuda.current_device()
     wall_us = ctypes.c_double()
     torch.cuda.synchronize()
-    n = lib.lamm_steps_direct(ctypes.cast(arr, ctypes.c_void_p), R, ctypes.byref(Bm), ctypes.byref(Cm), 0,
-                              max(warmup, 1), dev, flags, ctypes.byref(wall_us))
-    if n != max(warmup, 1):
-        log("direct dispatch unavailable:", n, la.last_error())
-        return None
+    # untimed: the warm-up calls, then the timed region's own K calls once (as time_steps replays its
+    # graph once untimed: the queue's cached kernarg slots then hold them, as in a decode loop's steady
+    # state); the caches are flushed before the timed pass, so the weights come from HBM
+    first = max(warmup, 1)
+    for f0, n0 in ((0, first), (first, steps)):
+        n = lib.lamm_steps_direct(ctypes.cast(arr, ctypes.c_void_p), R, ctypes.byref(Bm), ctypes.byref(Cm), f0,
+                                  n0, dev, flags, ctypes.byref(wall_us))
+        if n != n0:
+            log("direct dispatch unavailable:", n, la.last_error())
+            return None
+    flush_caches(torch)
     ctx.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -346,7 +411,7 @@ def config2_gemv(ctx, fmt, M, K, steps, warmup):
         gemv(i)
         ctx.allgather_rows(C, M, 1, ALIGN, torch.cuda.current_stream().cuda_stream)
 
-    per_step, ev_step, graphed = time_steps(ctx, step, steps, warmup, graph=not ctx.rehearse)
+    per_step, ev_step, graphed = time_steps(ctx, step, steps, warmup, graph=not ctx.rehearse, flush=True)
     # one GPU: the same K steps dispatched on the library's own AQL queue (no collective to order
     # against), reported beside the graph replay as value_direct
     direct = time_direct(ctx, mats, R, Bm, Cm, steps, warmup) if ctx.world == 1 else None
@@ -379,6 +444,8 @@ def config2_gemv(ctx, fmt, M, K, steps, warmup):
     # tracer are stretched by its own per-dispatch cost instead)
     iso = isolated_launches(la, mats, R, Bm, Cm, 300)
     b2b = isolated_launches(la, mats, R, Bm, Cm, 300, sync_each=0)
+    floor = read_floor(la, A.data_ptr(), slab_bytes, R, slab_bytes, 300)
+    empty = empty_floor(la, (rows + 7) // 8, 300)   # the GEMV's grid: 8 rows per 512-thread workgroup
     if iso is not None:
         kern = iso
         kern_method = ("median of 300 single launches, each completed before the next, timed by the dispatch's "
@@ -387,7 +454,7 @@ def config2_gemv(ctx, fmt, M, K, steps, warmup):
         _, kern, _ = time_steps(ctx, gemv, max(steps, 1000), 3)
         kern_method = "HIP events over 1000 back-to-back hipGraph-replayed launches on their stream"
     res = dict(per_step=per_step, direct_step=direct, ev_step=ev_step, kern=kern,
-               kern_method=kern_method, kern_b2b=b2b, graphed=graphed,
+               kern_method=kern_method, kern_b2b=b2b, floor=floor, empty=empty, graphed=graphed,
                R=R, rows=rows,
                slab_bytes=slab_bytes + la.row_bytes(vt, K) + 4 * rows, gather_check=check, sample=sample)
     del A, B, C
@@ -475,8 +542,9 @@ def config3_gemm(ctx, fmt, M, N, K, slices, steps):
 
 
 def ref_order_kernels(ctx, fmt, M, N, K, steps):
-    """The kernels the ggml boundary runs by default (LAMM_HIP_ORDER=reference: the reference's own
-    AVX2 float order, bit for bit), at config 2 and config 3, each against its own bound:
+    """The kernels the ggml boundary runs under LAMM_HIP_ORDER=reference (its default until round 5: the
+    reference's own AVX2 float order, bit for bit), at config 2 and config 3, each against
+    its own bound:
     ref_gemv_kernel against HBM (config 2's bytes, weights rotated > MALL, the dispatch's own
     timestamps); the prefill kernel against the fp32 FMA-chain floor of that order -- per output and
     32-element block 8 dependent lane FMAs, M*N*K/4 FMAs at the 157.3 TFLOP/s f32 VALU peak -- and,
@@ -703,6 +771,40 @@ def llama_step(fmt):
     return res
 
 
+def la_benchmark(dtype="q4_0", gpu_threads=4, iters=10):
+    """The reference's OWN benchmark, src/la-benchmark-matmult.cpp compiled unchanged (integration/Makefile
+    la-benchmark-matmult_hip: its ggml hook -> liblamm_hip.so), at its default shape (K=11008, M=4096,
+    N=128, la-benchmark-matmult.cpp:180-182), beside the same source built as the reference builds it
+    (oracle/_ref/la-benchmark-matmult_lamm3: lamm opt-3 AVX2) on this host's cores.  `Average` is the
+    reference's own figure (test/test_matmult_performance.py:42); the GPU's first iteration includes the
+    weight's upload into the device cache."""
+    import re
+    pat = re.compile(r"\nAverage\s*(\d+\.\d+)\n")
+    row = re.compile(r"^\s*\d+;\s*\d+;.*;\s*(\d+);\s*(\d+\.\d+)$", re.M)
+    out = {"workload": f"la-benchmark-matmult -d {dtype} -i {iters}: ggml_mul_mat of ({dtype} 4096 x 11008) x (F32 11008 "
+                       "x 128), ggml INIT quantization of src1 included, the binary's own Average GFLOPS"}
+    cores = host_cores()[0]
+    for name, exe, th in (("gpu", os.path.join(ROOT, "integration", "_build", "la-benchmark-matmult_hip"), gpu_threads),
+                          ("cpu_reference", os.path.join(ROOT, "oracle", "_ref", "la-benchmark-matmult_lamm3"), cores)):
+        if not os.path.exists(exe):
+            out[name] = {"error": f"{exe} missing"}
+            continue
+        try:
+            r = subprocess.run([exe, "-d", dtype, "-t", str(th), "-i", str(iters)], capture_output=True, text=True,
+                               timeout=300)
+            m = pat.search(r.stdout)
+            if r.returncode != 0 or not m:
+                out[name] = {"error": (r.stdout + r.stderr)[-300:]}
+                continue
+            us = sorted(int(u) for u, _ in row.findall(r.stdout))
+            out[name] = {"average_GFLOPS": float(m.group(1)), "threads": th,
+                         "median_iteration_us": us[len(us) // 2] if us else None,
+                         "binary": os.path.relpath(exe, ROOT)}
+        except Exception as e:  # noqa: BLE001
+            out[name] = {"error": str(e)[:300]}
+    return out
+
+
 def read_profile(kind, tag):
     """A committed per-launch measurement of config 2's kernel (profiles/<kind>_<tag>.json): the
     PMC traffic (tools/pmc_traffic_flat1.py) or the kernel tracer's paced durations
@@ -722,6 +824,10 @@ def summary(out):
     reference-order kernels."""
     s = {"config2_gemv": {"kernel": "gemv_flat1_kernel", "us": out["roofline"]["per_launch_us"],
                           "frac_hbm": out["roofline"]["frac"], "value_GBs": out["value"]}}
+    st = out.get("gemv_stacked", {})
+    if "per_launch_us" in st:   # the same GEMV, 33 weight slices in one launch: the streaming rate
+        s["config2_gemv_stacked"] = {"kernel": "gemv_stream_dma_kernel", "us": st["per_launch_us"],
+                                     "frac_hbm": st["frac"], "achieved_GBs": st["achieved_GBs"]}
     gm = out.get("gemm", {}).get("slices1", {})
     if "roofline" in gm:
         s["config3_gemm"] = {"engine": gm["engine"], "us": gm["roofline"]["per_launch_us"],
@@ -742,8 +848,12 @@ def summary(out):
             s[f] = {"gemv_us": e["gemv_per_launch_us"], "gemv_frac": e["gemv_frac"]}
             if "gemm_per_launch_us" in e:
                 s[f].update({"gemm": e["gemm_engine"], "gemm_us": e["gemm_per_launch_us"], "gemm_frac": e["gemm_frac"]})
+    lb = out.get("la_benchmark", {})
+    if "average_GFLOPS" in lb.get("gpu", {}):
+        s["la_benchmark_q4_0"] = {"gpu_GFLOPS": lb["gpu"]["average_GFLOPS"],
+                                  "cpu_reference_GFLOPS": lb.get("cpu_reference", {}).get("average_GFLOPS")}
     e2e = out.get("llama7b_e2e", {})
-    for k in ("t16", "t8", "t4_numa_isolate", "t16_fast_order"):
+    for k in ("t16", "t8", "t4_numa_isolate", "t16_reference_order"):
         r = e2e.get(k, {})
         if "pp_tok_s" in r:
             s[f"config5_{k}"] = {kk: r.get(kk) for kk in ("pp_tok_s", "tg_tok_s", "tg_from_empty_tok_s")}
@@ -816,6 +926,13 @@ def main():
                      "per_launch_us": round(g["kern"] * 1e6, 3),
                      "per_launch_method": g["kern_method"],
                      "per_launch_us_back_to_back": round(g["kern_b2b"] * 1e6, 3) if g["kern_b2b"] else None,
+                     # a read-only kernel on the same grid over the same weight bytes, timed the same way:
+                     # what a single launch of this size can reach (tools/steps_loop.hip read_floor_kernel)
+                     "single_launch_floor_us": round(g["floor"] * 1e6, 3) if g["floor"] else None,
+                     "single_launch_floor_frac": round(g["slab_bytes"] / g["floor"] / 1e9 / HBM_PEAK_GBS, 4)
+                     if g["floor"] else None,
+                     # an EMPTY kernel on the same grid, timed the same way: the dispatch's own cost
+                     "empty_launch_us": round(g["empty"] * 1e6, 3) if g["empty"] else None,
                      "algorithmic_bytes_per_launch": g["slab_bytes"]},
     }
     if trace and kname and trace.get("algorithmic_bytes_per_launch") == g["slab_bytes"]:
@@ -909,6 +1026,8 @@ def main():
             except Exception as e:  # noqa: BLE001
                 sw[f] = {"error": str(e)[:200]}
         extras["sweep"] = sw
+    if rank == 0 and world == 1:
+        extras["la_benchmark"] = la_benchmark(fmt)
     if not args.no_llama:
         extras["llama7b_matmul_step_sharded"] = llama_step_sharded(ctx, fmt)
         ctx.barrier()
@@ -931,11 +1050,12 @@ def main():
                    # cost more than extra threads save (profiles/r05/decode_threads/)
                    "t4_numa_isolate": llama_e2e(devs, threads=min(4, host_cores()[0]),
                                                 extra_args=("--numa", "isolate")),
-                   # the boundary computes in the reference's own float order by default (bit-identical
-                   # logits); the fast engines' order for comparison
-                   "t16_fast_order": llama_e2e(devs, threads=min(16, host_cores()[0]),
-                                               extra_env={"LAMM_HIP_ORDER": "fast"}),
-                   "float_order": "reference (LAMM_HIP_ORDER default): t16 / t8; t16_fast_order: LAMM_HIP_ORDER=fast"}
+                   # the boundary runs the fast engines by default (round 6); in the reference's own
+                   # float order (LAMM_HIP_ORDER=reference: bit-identical logits) for comparison
+                   "t16_reference_order": llama_e2e(devs, threads=min(16, host_cores()[0]),
+                                                    extra_env={"LAMM_HIP_ORDER": "reference"}),
+                   "float_order": "fast engines (the default): t16 / t8 / t4; t16_reference_order: "
+                                  "LAMM_HIP_ORDER=reference"}
             if world == 1:
                 extras["llama7b_matmul_step"] = llama_step(fmt)
             extras["llama7b_e2e"] = e2e
@@ -972,22 +1092,24 @@ def main():
                           "llama_e2e_hip teacher-forced with the reference's tokens (--force)"}
             if c.get("tokens"):
                 import numpy as np
-                g = llama_e2e(None, n_prompt=64, n_gen=16, threads=min(16, host_cores()[0]), keep_tokens=True,
-                              extra_args=("--logits", lg, "--force", ",".join(map(str, c["tokens"]))))
-                if g.get("argmax"):
-                    a = np.fromfile(lc, np.float32).reshape(-1, 32000)
-                    b = np.fromfile(lg, np.float32).reshape(-1, 32000)
-                    err = np.abs(b - a).max(axis=1) / np.abs(a).max(axis=1)
-                    par.update({"tokens_reference": c["tokens"], "argmax_reference": c["argmax"],
-                                "argmax_gpu": g["argmax"],
-                                "argmax_agree": sum(x == y for x, y in zip(g["argmax"], c["argmax"])),
-                                "rows": len(c["argmax"]),
-                                "max_rel_dlogit_per_row": [round(float(e), 4) for e in err],
-                                "reference_own_spread": "scalar vs AVX2 lamm builds of the reference, same forced "
-                                                        "run: max 0.0949 per row, argmax agree 15 of 17 "
-                                                        "(profiles/r03/e2e_32_layers.txt)"})
-                else:
-                    par["error"] = g.get("error")
+                a = np.fromfile(lc, np.float32).reshape(-1, 32000)
+                par.update({"tokens_reference": c["tokens"], "argmax_reference": c["argmax"], "rows": len(c["argmax"]),
+                            "reference_own_spread": "scalar vs AVX2 lamm builds of the reference, same forced run: "
+                                                    "max 0.0949 per row, argmax agree 15 of 17 "
+                                                    "(profiles/r03/e2e_32_layers.txt)"})
+                # the default build (fast engines) and LAMM_HIP_ORDER=reference (bit-identical expected)
+                for key, env in (("default_fast_order", None), ("reference_order", {"LAMM_HIP_ORDER": "reference"})):
+                    g = llama_e2e(None, n_prompt=64, n_gen=16, threads=min(16, host_cores()[0]), keep_tokens=True,
+                                  extra_env=env, extra_args=("--logits", lg, "--force", ",".join(map(str, c["tokens"]))))
+                    if g.get("argmax"):
+                        b = np.fromfile(lg, np.float32).reshape(-1, 32000)
+                        err = np.abs(b - a).max(axis=1) / np.abs(a).max(axis=1)
+                        par[key] = {"argmax_gpu": g["argmax"],
+                                    "argmax_agree": sum(x == y for x, y in zip(g["argmax"], c["argmax"])),
+                                    "max_rel_dlogit_per_row": [round(float(e), 4) for e in err],
+                                    "bit_identical_logits": bool(np.array_equal(a.view(np.uint32), b.view(np.uint32)))}
+                    else:
+                        par[key] = {"error": g.get("error")}
             else:
                 par["error"] = c.get("error")
             out["llama7b_e2e"]["parity_32_layers"] = par

@@ -112,7 +112,8 @@ int lamm_hip_matmul_batched(const lamm_matrix *A, const lamm_matrix *B, const la
  * AVX2 ggml_vec_dot_q6_K_q8_K for q6_K (LC/ggml-quants.c:8305-8385) -- so C is bit-identical to
  * the reference's CPU build on the same blocks (VALU kernels, slower than the default engines).
  * Supported: q4_0 / q5_0 with q8_0 B, q4_1 / q5_1 with q8_1 B, q6_K with q8_K B (quantized B
- * only); others return LAMM_ERR_TYPE.  The ggml boundary uses it by default (LAMM_HIP_ORDER). */
+ * only); others return LAMM_ERR_TYPE.  The ggml boundary uses it under LAMM_HIP_ORDER=reference (its
+ * default until round 5; since round 6 the boundary runs the fast engines unless asked). */
 #define LAMM_ORDER_REFERENCE 1
 int lamm_hip_matmul_ex(const lamm_matrix *A, const lamm_matrix *B, const lamm_matrix *C,
                        const lamm_batch *batch, int flags, void *hip_stream);
@@ -203,7 +204,10 @@ int lamm_hip_profile_next(void *start_event, void *stop_event);
  * LAMM_ERR_NODEV for a device index out of range, or LAMM_ERR_HIP when the queue is not available
  * (ROCr's loader extension missing, a region already open on this thread); end without an open
  * region returns -LAMM_ERR_HIP.  The ggml boundary can use it for decode-sized calls
- * (LAMM_HIP_DIRECT=1; off by default, it measured no faster there). */
+ * (LAMM_HIP_DIRECT=1; off by default, it measured no faster there).  Round 6: a region in which
+ * some calls had to launch through HIP sets lamm_hip_last_error() to the reason (as a failed begin
+ * does), and a kernarg block the queue has written before (same kernel, arguments and grid) is
+ * dispatched from its cached slot without rewriting it. */
 int lamm_hip_direct_begin(int device);
 int lamm_hip_direct_end(void);
 

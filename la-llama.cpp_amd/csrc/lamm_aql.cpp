@@ -15,6 +15,18 @@
 // here as HIP fills it.  Anything that does not check out (no ROCr entry, name not found, another
 // kernarg size) leaves the call on HIP's launch path: direct_launch returns false.
 //
+// Kernarg blocks are content-addressed (round 6): a block whose bytes were written before (the same
+// kernel, arguments and grid: a decode step's call on the same weight, every step of a benchmark that
+// rotates over a fixed set of weights) is dispatched from its cached slot -- immutable once written,
+// so any packet may point at it at any time -- with no BAR writes and no HDP flush + read-back (two
+// PCIe round trips that set the host's cost per dispatch).  Blocks the cache cannot hold go through
+// the ring of reusable slots as before.
+//
+// Every reason the queue or a kernel is unusable is recorded (Aql::why, direct_reason()): round 5's
+// driver box dispatched nothing directly and said nothing about why.  Several GPU agents can share
+// one PCI function's address (a partitioned device); the queue is created on the agent the library's
+// kernels were loaded for, found when the first kernel is looked up.
+//
 // Ordering: the queue is a second queue beside the HIP stream.  A direct region (lamm_hip_direct_
 // begin / end, or the boundary's decode call) must not mix with work on the HIP stream: callers
 // drain the stream before it (cold weight uploads) and the region ends with every packet complete.
@@ -42,6 +54,7 @@ constexpr uint32_t kQueueSize = 256;       // packets
 constexpr uint32_t kSlots = 2 * kQueueSize;  // kernarg slots (a slot is reused only once its packet completed)
 constexpr uint32_t kSlotBytes = 1024;
 constexpr uint32_t kImplicitBytes = 256;   // code object v5 implicit kernarg block
+constexpr uint32_t kCached = 512;          // content-addressed kernarg slots (never rewritten)
 
 struct AqlKernel {
   uint64_t object = 0;
@@ -59,13 +72,13 @@ void queue_error(hsa_status_t st, hsa_queue_t*, void*) {
 class Aql {
  public:
   bool init(int device) {
-    if (hsa_init() != HSA_STATUS_SUCCESS) return false;
+    if (hsa_init() != HSA_STATUS_SUCCESS) return no("hsa_init failed");
     hsa_inited_ = true;
     int bus = -1, dev = -1, dom = -1;
     if (hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, device) != hipSuccess ||
         hipDeviceGetAttribute(&dev, hipDeviceAttributePciDeviceId, device) != hipSuccess ||
         hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainID, device) != hipSuccess)
-      return false;
+      return no("HIP reports no PCI address for the device");
     want_bdf_ = (uint32_t)((bus << 8) | (dev << 3));
     want_dom_ = (uint32_t)dom;
     hsa_iterate_agents(
@@ -78,12 +91,17 @@ class Aql {
             uint32_t bdf = 0, dom = 0;
             hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &bdf);
             hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DOMAIN, &dom);
-            if ((bdf & ~7u) == self->want_bdf_ && dom == self->want_dom_) self->gpu_ = a;
+            if ((bdf & ~7u) == self->want_bdf_ && dom == self->want_dom_) self->cands_.push_back(a);
           }
           return HSA_STATUS_SUCCESS;
         },
         this);
-    if (!gpu_.handle || !cpu_.handle) return false;
+    if (cands_.empty()) {
+      char b[96];
+      snprintf(b, sizeof b, "no HSA GPU agent at PCI %04x:%02x:%02x", want_dom_, (unsigned)bus, (unsigned)dev);
+      return no(b);
+    }
+    if (!cpu_.handle) return no("no HSA CPU agent");
     // kernarg memory: the host pool that carries the kernarg flag
     hsa_amd_agent_iterate_memory_pools(
         cpu_,
@@ -97,7 +115,17 @@ class Aql {
           return HSA_STATUS_SUCCESS;
         },
         &karg_pool_);
-    if (!karg_pool_.handle) return false;
+    if (!karg_pool_.handle) return no("no host kernarg memory pool");
+    if (hsa_system_get_major_extension_table(HSA_EXTENSION_AMD_LOADER, 1, sizeof(loader_), &loader_) !=
+        HSA_STATUS_SUCCESS)
+      return no("no ROCr loader extension");
+    return true;
+  }
+
+  // the queue, its kernarg memory and completion signal on agent `gpu` (the agent the first kernel
+  // looked up was loaded for)
+  bool create_queue(hsa_agent_t gpu) {
+    gpu_ = gpu;
     // The kernarg ring in the GPU's fine-grained memory, written by the host through the BAR and
     // made visible by an HDP flush + read-back before the doorbell (as HIP does for its device
     // kernargs): the kernels' scalar loads of their arguments stay on the device.  With the ring in
@@ -124,20 +152,19 @@ class Aql {
       }
     }
     void* k = nullptr;
-    if (hsa_amd_memory_pool_allocate(karg_pool_, (size_t)kSlots * kSlotBytes, 0, &k) != HSA_STATUS_SUCCESS) return false;
+    const size_t bytes = (size_t)(kSlots + kCached) * kSlotBytes;
+    if (hsa_amd_memory_pool_allocate(karg_pool_, bytes, 0, &k) != HSA_STATUS_SUCCESS)
+      return no(dev_karg_ ? "kernarg allocation in device fine-grained memory failed" : "kernarg allocation failed");
     karg_ = static_cast<unsigned char*>(k);
     const hsa_agent_t both[2] = {gpu_, cpu_};
-    if (hsa_amd_agents_allow_access(2, both, nullptr, karg_) != HSA_STATUS_SUCCESS) return false;
-    memset(karg_, 0, (size_t)kSlots * kSlotBytes);
+    if (hsa_amd_agents_allow_access(2, both, nullptr, karg_) != HSA_STATUS_SUCCESS) return no("kernarg access grant failed");
+    memset(karg_, 0, bytes);
     if (hsa_queue_create(gpu_, kQueueSize, HSA_QUEUE_TYPE_SINGLE, queue_error, nullptr, UINT32_MAX, UINT32_MAX, &q_) !=
         HSA_STATUS_SUCCESS)
-      return false;
+      return no("hsa_queue_create failed");
     // a busy-wait completion signal (no interrupt behind each completion: the host spins anyway)
     if (hsa_amd_signal_create(0, 0, nullptr, HSA_AMD_SIGNAL_AMD_GPU_ONLY, &done_) != HSA_STATUS_SUCCESS)
-      return false;
-    if (hsa_system_get_major_extension_table(HSA_EXTENSION_AMD_LOADER, 1, sizeof(loader_), &loader_) !=
-        HSA_STATUS_SUCCESS)
-      return false;
+      return no("completion signal creation failed");
     return true;
   }
 
@@ -147,49 +174,76 @@ class Aql {
     AqlKernel k;
     hipFuncAttributes fa;
     const char* name = hipFuncGetAttributes(&fa, fn) == hipSuccess ? hipKernelNameRefByPtr(fn, nullptr) : nullptr;
-    if (name) {
+    hsa_agent_t found{0};
+    if (!name) {
+      no("HIP gives no name for a kernel");
+    } else {
       struct Find {
         Aql* self;
         std::string name;
         AqlKernel* k;
-      } f{this, name, &k};
+        hsa_agent_t* found;
+      } f{this, name, &k, &found};
       loader_.hsa_ven_amd_loader_iterate_executables(
           [](hsa_executable_t ex, void* d) {
             Find* f = static_cast<Find*>(d);
             if (f->k->object) return HSA_STATUS_SUCCESS;
-            for (const std::string& n : {f->name, f->name + ".kd"}) {
-              hsa_executable_symbol_t sym;
-              if (hsa_executable_get_symbol_by_name(ex, n.c_str(), &f->self->gpu_, &sym) != HSA_STATUS_SUCCESS) continue;
-              hsa_symbol_kind_t kind;
-              hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_TYPE, &kind);
-              if (kind != HSA_SYMBOL_KIND_KERNEL) continue;
-              hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT, &f->k->object);
-              hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_KERNARG_SEGMENT_SIZE, &f->k->kernarg);
-              hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_GROUP_SEGMENT_SIZE, &f->k->group);
-              hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_PRIVATE_SEGMENT_SIZE, &f->k->priv);
-              break;
-            }
+            // the queue's agent once there is one, else every agent at the device's PCI address
+            std::vector<hsa_agent_t> agents = f->self->q_ ? std::vector<hsa_agent_t>{f->self->gpu_} : f->self->cands_;
+            for (hsa_agent_t a : agents)
+              for (const std::string& n : {f->name, f->name + ".kd"}) {
+                hsa_executable_symbol_t sym;
+                if (hsa_executable_get_symbol_by_name(ex, n.c_str(), &a, &sym) != HSA_STATUS_SUCCESS) continue;
+                hsa_symbol_kind_t kind;
+                hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_TYPE, &kind);
+                if (kind != HSA_SYMBOL_KIND_KERNEL) continue;
+                hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT, &f->k->object);
+                hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_KERNARG_SEGMENT_SIZE, &f->k->kernarg);
+                hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_GROUP_SEGMENT_SIZE, &f->k->group);
+                hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_PRIVATE_SEGMENT_SIZE, &f->k->priv);
+                *f->found = a;
+                return HSA_STATUS_SUCCESS;
+              }
             return HSA_STATUS_SUCCESS;
           },
           &f);
+      // the code object v5 layout this file fills: explicit args, then the implicit block at the next
+      // 8-byte boundary; any other size (an older code object, a kernel whose hidden args differ)
+      // stays on HIP's launch path
+      const size_t want = ((explicit_bytes + 7) & ~size_t(7)) + kImplicitBytes;
+      char b[256];
+      if (!k.object) {
+        snprintf(b, sizeof b, "kernel %.120s not found in any loaded executable for the device's %zu agent(s)", name,
+                 cands_.size());
+        no(b);
+      } else if (k.priv) {
+        snprintf(b, sizeof b, "kernel %.120s needs %u B of scratch", name, k.priv);
+        no(b);
+      } else if (k.kernarg != want || k.kernarg > kSlotBytes) {
+        snprintf(b, sizeof b, "kernel %.120s: kernarg segment %u B, expected %zu", name, k.kernarg, want);
+        no(b);
+      } else if (!q_ && !create_queue(found)) {
+        // (create_queue recorded why)
+      } else {
+        k.ok = true;
+      }
     }
-    // the code object v5 layout this file fills: explicit args, then the implicit block at the next
-    // 8-byte boundary; any other size (an older code object, a kernel whose hidden args differ)
-    // stays on HIP's launch path
-    k.ok = k.object && k.priv == 0 && k.kernarg == ((explicit_bytes + 7) & ~size_t(7)) + kImplicitBytes &&
-           k.kernarg <= kSlotBytes;
     return cache_.emplace(fn, k).first->second;
   }
 
-  // A packet is written at once but published (header + doorbell) only when the next one arrives or
+  // Round 6 (default, eager_): every packet is published as soon as it is written, the region's
+  // first with a system-scope acquire, all with agent-scope releases, and the region ends with a
+  // barrier packet carrying the completion signal and the system-scope release -- the first kernel
+  // no longer waits for the second call.  Round 5 (LAMM_AQL_EAGER=0):
+  // a packet is written at once but published (header + doorbell) only when the next one arrives or
   // the region ends, so the last packet of a region is known when it is published: only it carries
   // the completion signal and a system-scope release; the first carries a system-scope acquire
   // (inputs the host wrote), the others agent scope on both sides (probe, profiles/r05/direct/:
   // system fences and a signal on every packet cost 1.5-3 us per kernel back to back).
   bool dispatch(const AqlKernel& k, dim3 g, dim3 b, uint32_t dyn_lds, const void* args, size_t bytes) {
     const uint64_t idx = hsa_queue_add_write_index_relaxed(q_, 1);
-    // queue space (and with it the kernarg slot: packets run in order behind their barrier bits, so
-    // packet idx - kSlots completed before packet idx - kSlots + 1 was launched)
+    // queue space (and with it the ring's kernarg slot: packets run in order behind their barrier
+    // bits, so packet idx - kSlots completed before packet idx - kSlots + 1 was launched)
     const auto t0 = std::chrono::steady_clock::now();
     while (idx - hsa_queue_load_read_index_scacquire(q_) >= kQueueSize) {
       if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
@@ -198,10 +252,12 @@ class Aql {
       }
       __builtin_ia32_pause();
     }
-    unsigned char* ka = karg_ + (idx % kSlots) * kSlotBytes;
-    memcpy(ka, args, bytes);
-    unsigned char* im = ka + ((bytes + 7) & ~size_t(7));
-    memset(im, 0, kImplicitBytes);
+    // the whole kernarg block, explicit arguments + implicit block, built on the host first
+    const size_t ibase = (bytes + 7) & ~size_t(7), total = ibase + kImplicitBytes;
+    unsigned char blk[kSlotBytes];
+    memset(blk, 0, total);
+    memcpy(blk, args, bytes);
+    unsigned char* im = blk + ibase;
     const uint32_t bc[3] = {g.x, g.y, g.z};
     const uint16_t gs[3] = {(uint16_t)b.x, (uint16_t)b.y, (uint16_t)b.z};
     memcpy(im + 0, bc, 12);    // hidden_block_count_x/y/z
@@ -209,6 +265,27 @@ class Aql {
     const uint16_t dims = g.z > 1 ? 3 : g.y > 1 ? 2 : 1;
     memcpy(im + 64, &dims, 2);       // hidden_grid_dims
     memcpy(im + 120, &dyn_lds, 4);   // hidden_dynamic_lds_size
+    // a block written before: its cached slot; a new one: a fresh cached slot while there are any,
+    // else the ring
+    std::string key(reinterpret_cast<const char*>(blk), total);
+    key.append(reinterpret_cast<const char*>(&k.object), sizeof k.object);
+    unsigned char* ka;
+    bool written = false;
+    auto hit = slots_.find(key);
+    if (hit != slots_.end()) {
+      ka = karg_ + (size_t)(kSlots + hit->second) * kSlotBytes;
+      ++hits_;
+    } else {
+      if (slots_.size() < kCached) {
+        const uint32_t c = (uint32_t)slots_.size();
+        slots_.emplace(std::move(key), c);
+        ka = karg_ + (size_t)(kSlots + c) * kSlotBytes;
+      } else {
+        ka = karg_ + (idx % kSlots) * kSlotBytes;
+      }
+      memcpy(ka, blk, total);
+      written = true;
+    }
     hsa_kernel_dispatch_packet_t* p = packet(idx);
     p->workgroup_size_x = (uint16_t)b.x;
     p->workgroup_size_y = (uint16_t)b.y;
@@ -222,10 +299,10 @@ class Aql {
     p->kernel_object = k.object;
     p->kernarg_address = ka;
     p->reserved2 = 0;
-    if (dev_karg_) {   // the BAR writes above reach device memory before the packet can be read
+    if (dev_karg_ && written) {   // the BAR writes above reach device memory before the packet can be read
       *hdp_.HDP_MEM_FLUSH_CNTL = 1u;
       (void)*reinterpret_cast<volatile uint32_t*>(hdp_.HDP_MEM_FLUSH_CNTL);
-      (void)*reinterpret_cast<volatile uint32_t*>(im + 120);
+      (void)*reinterpret_cast<volatile uint32_t*>(ka + ibase + 120);
     }
     if (pending_) publish(false);
     pending_ = true;
@@ -233,6 +310,10 @@ class Aql {
     pend_setup_ = (uint16_t)(dims << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS);
     pend_first_ = first_;
     first_ = false;
+    if (eager_) {   // published at once; the region's end adds a barrier packet for completion
+      publish(false);
+      dispatched_ = true;
+    }
     return true;
   }
 
@@ -240,6 +321,10 @@ class Aql {
   // packet opens a new region (system-scope acquire).
   bool wait(double seconds) {
     if (pending_) publish(true);
+    if (dispatched_) {   // eager packets: a barrier-AND packet behind them carries the completion
+      barrier_packet();
+      dispatched_ = false;
+    }
     first_ = true;
     const auto t0 = std::chrono::steady_clock::now();
     for (unsigned it = 0;; ++it) {
@@ -252,8 +337,14 @@ class Aql {
   }
 
   std::mutex mu;
+  std::string why;        // the first reason this queue (or a kernel on it) cannot dispatch
+  uint64_t hits_ = 0;     // dispatches from a cached kernarg slot
 
  private:
+  bool no(const char* reason) {
+    if (why.empty()) why = reason;
+    return false;
+  }
   hsa_kernel_dispatch_packet_t* packet(uint64_t idx) {
     return static_cast<hsa_kernel_dispatch_packet_t*>(q_->base_address) + (idx % kQueueSize);
   }
@@ -271,6 +362,31 @@ class Aql {
     pending_ = false;
   }
 
+  // a barrier-AND packet (no dependencies) behind the region's kernels: it completes once they have
+  // (barrier bit), then its system-scope release makes their stores visible to the host and it
+  // decrements the completion signal
+  void barrier_packet() {
+    const uint64_t idx = hsa_queue_add_write_index_relaxed(q_, 1);
+    while (idx - hsa_queue_load_read_index_scacquire(q_) >= kQueueSize) __builtin_ia32_pause();
+    hsa_barrier_and_packet_t* p = reinterpret_cast<hsa_barrier_and_packet_t*>(packet(idx));
+    p->reserved0 = 0;
+    p->reserved1 = 0;
+    for (auto& d : p->dep_signal) d = hsa_signal_t{0};
+    p->reserved2 = 0;
+    hsa_signal_add_relaxed(done_, 1);
+    p->completion_signal = done_;
+    const uint16_t header = (uint16_t)((HSA_PACKET_TYPE_BARRIER_AND << HSA_PACKET_HEADER_TYPE) |
+                                       (1u << HSA_PACKET_HEADER_BARRIER) |
+                                       (HSA_FENCE_SCOPE_NONE << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+                                       (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
+    __atomic_store_n(reinterpret_cast<uint32_t*>(p), (uint32_t)header, __ATOMIC_RELEASE);
+    hsa_signal_store_screlease(q_->doorbell_signal, (hsa_signal_value_t)idx);
+  }
+
+  // LAMM_AQL_EAGER (default 1): publish every kernel packet as it is written (agent-scope release) and
+  // close the region with a barrier packet; 0: hold each packet until the next arrives (round 5)
+  const bool eager_ = knobs().aql_eager;
+  bool dispatched_ = false;
   bool hsa_inited_ = false, dev_karg_ = false;
   hsa_amd_hdp_flush_t hdp_{};
   bool pending_ = false, pend_first_ = false, first_ = true;
@@ -278,19 +394,23 @@ class Aql {
   uint16_t pend_setup_ = 0;
   uint32_t want_bdf_ = 0, want_dom_ = 0;
   hsa_agent_t gpu_{0}, cpu_{0};
+  std::vector<hsa_agent_t> cands_;   // GPU agents at the device's PCI address
   hsa_amd_memory_pool_t karg_pool_{0};
   unsigned char* karg_ = nullptr;
   hsa_queue_t* q_ = nullptr;
   hsa_signal_t done_{0};
   hsa_ven_amd_loader_1_03_pfn_t loader_{};
   std::unordered_map<const void*, AqlKernel> cache_;
+  std::unordered_map<std::string, uint32_t> slots_;   // kernarg block bytes -> cached slot
 };
 
 std::mutex g_mu;
 std::unordered_map<int, Aql*> g_queues;   // per HIP device; nullptr: unavailable
+std::unordered_map<int, std::string> g_unavailable;   // why a device has no queue
 
 thread_local Aql* t_direct = nullptr;
-thread_local int t_launches = 0;
+thread_local int t_launches = 0, t_fallbacks = 0;
+thread_local std::string t_reason;
 
 Aql* queue_for(int device) {
   std::lock_guard<std::mutex> lock(g_mu);
@@ -298,7 +418,8 @@ Aql* queue_for(int device) {
   if (it != g_queues.end()) return it->second;
   Aql* q = new Aql();
   if (!q->init(device)) {
-    delete q;   // (a half-initialised queue is leaked rather than torn down: never on this path)
+    g_unavailable[device] = q->why;
+    delete q;   // (init creates no queue: nothing to tear down)
     q = nullptr;
   }
   g_queues[device] = q;
@@ -370,12 +491,20 @@ void hdp_flush(int device, const void* last_written) {
 }
 
 bool direct_begin(int device) {
-  if (t_direct) return false;
+  t_reason.clear();
+  if (t_direct) {
+    t_reason = "a direct region is already open on this thread";
+    return false;
+  }
   Aql* q = queue_for(device);
-  if (!q) return false;
+  if (!q) {
+    std::lock_guard<std::mutex> lock(g_mu);
+    t_reason = g_unavailable[device];
+    return false;
+  }
   q->mu.lock();
   t_direct = q;
-  t_launches = 0;
+  t_launches = t_fallbacks = 0;
   return true;
 }
 
@@ -394,11 +523,25 @@ int direct_end(double seconds) {
 
 bool direct_active() { return t_direct != nullptr; }
 
+int direct_fallbacks() { return t_fallbacks; }
+
+const std::string& direct_reason() { return t_reason; }
+
+uint64_t direct_cache_hits(int device) {
+  std::lock_guard<std::mutex> lock(g_mu);
+  auto it = g_queues.find(device);
+  return it != g_queues.end() && it->second ? it->second->hits_ : 0;
+}
+
 bool direct_launch(const void* fn, dim3 grid, dim3 block, uint32_t dyn_lds, const void* args, size_t bytes) {
   Aql* q = t_direct;
   if (!q) return false;
   const AqlKernel& k = q->kernel(fn, bytes);
-  if (!k.ok) return false;
+  if (!k.ok) {
+    ++t_fallbacks;
+    t_reason = q->why;
+    return false;
+  }
   q->dispatch(k, grid, block, dyn_lds, args, bytes);
   ++t_launches;
   return true;

@@ -4,6 +4,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <string>
 
 namespace lamm {
 
@@ -13,6 +14,12 @@ bool direct_begin(int device);
 // the number of direct launches the region made (0: everything went through HIP).
 int direct_end(double seconds = 1.0);
 bool direct_active();
+// calls of the open (or last) region that fell back to HIP, and why the last fallback, or the last
+// direct_begin, could not use the queue
+int direct_fallbacks();
+const std::string& direct_reason();
+// dispatches that found their kernarg block already in a cached slot (this device's queue)
+uint64_t direct_cache_hits(int device);
 // Dispatch kernel `fn` (its host stub) with explicit arguments [args, args + bytes) when a region
 // is open and the kernel's layout checks out; false: the caller launches through HIP.
 bool direct_launch(const void* fn, dim3 grid, dim3 block, uint32_t dyn_lds, const void* args, size_t bytes);

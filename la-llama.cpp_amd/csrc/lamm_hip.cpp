@@ -401,13 +401,21 @@ extern "C" int lamm_hip_direct_begin(int device) {
   const std::vector<int>& ids = probe().ids;
   if (std::find(ids.begin(), ids.end(), device) == ids.end())
     return fail(LAMM_ERR_NODEV, "lamm_hip_direct_begin: no gfx950 device %d", device);
-  if (!lamm::direct_begin(device)) return fail(LAMM_ERR_HIP, "lamm_hip_direct_begin: no direct queue on device %d", device);
+  if (!lamm::direct_begin(device))
+    return fail(LAMM_ERR_HIP, "lamm_hip_direct_begin: no direct queue on device %d: %s", device,
+                lamm::direct_reason().c_str());
   return LAMM_OK;
 }
 
 extern "C" int lamm_hip_direct_end(void) {
   if (!lamm::direct_active()) return -fail(LAMM_ERR_HIP, "lamm_hip_direct_end: no region open");
-  return lamm::direct_end();
+  const int n = lamm::direct_end();
+  // calls whose kernel could not go onto the queue ran through HIP: say why (round 5's driver box
+  // dispatched nothing directly with no reason given)
+  if (lamm::direct_fallbacks() > 0)
+    fail(LAMM_ERR_HIP, "lamm_hip_direct_end: %d call(s) launched through HIP: %s", lamm::direct_fallbacks(),
+         lamm::direct_reason().c_str());
+  return n;
 }
 
 extern "C" int lamm_hip_matmul_batched(const lamm_matrix* A, const lamm_matrix* B, const lamm_matrix* C,
@@ -1686,7 +1694,9 @@ void mul_mat_thread0(const ggml::compute_params* params, ggml::tensor* dst, bool
     // same launch (lamm_hip_matmul_group) -- their results wait in pinned memory for their own calls
     lamm_matrix gA[LAMM_GROUP_MAX], gC[LAMM_GROUP_MAX];
     int ng = 0;
-    if (sib_form && !in_direct && !stationary && comp.seq == 0 && zc_out) {
+    if (sib_form && !in_direct && !stationary && comp.seq == 0 && zc_out && !watch) {
+      // (not with a C watch: watch_c returns once the LEADER's words land, while the group's other
+      // segments may still read the activations and write their pinned results -- ADVICE r5)
       auto fit = g_sib.followers.find(wkey);
       if (fit != g_sib.followers.end() && !fit->second.empty()) {
         size_t total = 0;

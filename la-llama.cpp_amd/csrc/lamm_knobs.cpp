@@ -62,6 +62,7 @@ Knobs* read_env() {
   k->c_watch = env_int("LAMM_HIP_C_WATCH", 0);
   k->direct = env_on("LAMM_HIP_DIRECT");
   k->aql_host_karg = env_on("LAMM_AQL_HOSTKARG");
+  k->aql_eager = !env_off("LAMM_AQL_EAGER");
   k->vram_x = !env_off("LAMM_HIP_VRAM_X");
   k->signal_write = env_on("LAMM_HIP_SIGNAL_WRITE");
   k->siblings = !env_off("LAMM_HIP_SIBLINGS");
@@ -72,7 +73,7 @@ Knobs* read_env() {
   k->ref_gemv_bpt = env_int("LAMM_REF_GEMV_BPT", 2);
   k->helpers = env_int("LAMM_HIP_HELPERS", 0);
   k->pool = env_int("LAMM_HIP_POOL", 5);
-  if (const char* e = getenv("LAMM_HIP_ORDER")) k->ref_order = strcmp(e, "fast") != 0;
+  if (const char* e = getenv("LAMM_HIP_ORDER")) k->ref_order = !strcmp(e, "reference") || !strcmp(e, "ref");
   return k;
 }
 

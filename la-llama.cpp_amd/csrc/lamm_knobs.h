@@ -60,8 +60,11 @@ struct Knobs {
                                // steps interleaved with the next group's MFMAs; unset: per format)
   int ref_gemv_bpt = 2;        // LAMM_REF_GEMV_BPT: blocks per producer thread of ref_gemv_kernel (2: 512
                                // threads per workgroup, 4: 256)
-  bool ref_order = true;       // LAMM_HIP_ORDER=fast: the boundary runs the fast engines instead of the
-                               // reference's float order (lamm_ref.hip) for the formats that have both
+  bool aql_eager = true;       // LAMM_AQL_EAGER=0: direct-dispatch packets held until the next call (round 5)
+  bool ref_order = false;      // LAMM_HIP_ORDER=reference: the boundary computes in the reference's own float
+                               // order (lamm_ref.hip, bit-identical to the lamm opt-3 AVX2 build) instead of
+                               // the fast engines (the default since round 6: within the north star's 1e-3
+                               // per node)
   int pool = 5;                // LAMM_HIP_POOL: what ggml's pool threads do for prefill-sized calls (bits):
                                // 1 quantize the F32 activations to q8_0 / q8_1 rows in pinned memory (the
                                // upload moves those instead of F32), 2 scatter C out of pinned memory

@@ -121,9 +121,10 @@ def test_non_compute_phases_and_unsupported(monkeypatch):
     src0r, src1r, _, _ = make_node(t, M, 8, K)
     assert la.can_mul_mat(p, ggml_emu.mul_mat_node(src0r, src1r).t)
     monkeypatch.setenv("LAMM_HIP_FUSED", "1")    # opt-in: the one-column GEMV quantizes the F32 row
+    monkeypatch.setenv("LAMM_HIP_ORDER", "reference")
     assert la.can_mul_mat(p, dst.t)              # (reference order: ref_gemv_kernel's staging)
     assert not la.can_mul_mat(p, ggml_emu.mul_mat_node(src02, src12).t)   # 2 rows: only the fast GEMVs
-    monkeypatch.setenv("LAMM_HIP_ORDER", "fast")
+    monkeypatch.delenv("LAMM_HIP_ORDER")         # the default since round 6: the fast engines
     assert la.can_mul_mat(p, dst.t)
     assert la.can_mul_mat(p, ggml_emu.mul_mat_node(src02, src12).t)
     monkeypatch.delenv("LAMM_HIP_FUSED")
@@ -173,8 +174,9 @@ def test_f16_policy(monkeypatch):
     # them in ggml_vec_dot_f16's AVX2 order, ref_f16_kernel), decode-sized ones stay
     assert la.can_mul_mat(p, dstb.t)
     assert not la.can_mul_mat(p, dst.t)
-    monkeypatch.setenv("LAMM_HIP_ORDER", "fast")
+    monkeypatch.setenv("LAMM_HIP_ORDER", "reference")
     assert la.can_mul_mat(p, dstb.t)
+    assert not la.can_mul_mat(p, dst.t)
 
 
 GGML_OP_VIEW = 31   # LC/ggml.h enum ggml_op (b2430)

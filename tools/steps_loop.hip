@@ -11,8 +11,13 @@
 //                              roofline)
 //   lamm_steps_direct        : K calls inside one direct-dispatch region (lamm_hip_direct_begin /
 //                              end: the library's own AQL queue), completed before it returns
+//   lamm_read_floor          : the single-launch floor of config 2: a read-only
+//                              kernel on the GEMV's grid (512 workgroups of 512 threads, 36 bytes per
+//                              thread as the GEMV's two 18-byte blocks per lane) over the same bytes,
+//                              timed per isolated launch like lamm_steps_isolated
 // hipcc --offload-arch=gfx950 -O2 -shared -fPIC -I include tools/steps_loop.hip -L la-llama.cpp_amd -llamm_hip
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <chrono>
 #include <vector>
@@ -20,6 +25,26 @@
 #include "lamm_hip.h"
 
 namespace {
+
+// 512 threads x 36 B per workgroup, coalesced: b128 at [t], b128 at [512 + t], b32 at 16 KiB + 4 t
+constexpr uint32_t kFloorWgBytes = 512 * 36;
+__global__ __launch_bounds__(512) void read_floor_kernel(const unsigned char* A, uint32_t bytes, uint32_t* sink) {
+  const uint32_t base = blockIdx.x * kFloorWgBytes, t = threadIdx.x;
+  const uint32_t o0 = base + 16 * t, o1 = base + 8192 + 16 * t, o2 = base + 16384 + 4 * t;
+  uint32_t x = 0;
+  if (o0 + 16 <= bytes) {
+    const uint4 v = *reinterpret_cast<const uint4*>(A + o0);
+    x ^= v.x ^ v.y ^ v.z ^ v.w;
+  }
+  if (o1 + 16 <= bytes) {
+    const uint4 v = *reinterpret_cast<const uint4*>(A + o1);
+    x ^= v.x ^ v.y ^ v.z ^ v.w;
+  }
+  if (o2 + 4 <= bytes) x ^= *reinterpret_cast<const uint32_t*>(A + o2);
+  if (x == 0x9e3779b9u) sink[blockIdx.x] = x;   // (never in practice: keeps the loads)
+}
+
+__global__ __launch_bounds__(512) void empty_floor_kernel(uint32_t*) {}
 
 double now_us() {
   return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -102,6 +127,54 @@ int lamm_steps_direct(const lamm_matrix* A, int nA, const lamm_matrix* B, const 
   const int n = lamm_hip_direct_end();
   if (wall_us) *wall_us = now_us() - t0;
   return rc != LAMM_OK ? -100 - rc : n;
+}
+
+// out_us[i] = the dispatch's own duration of an EMPTY kernel on `grid` workgroups of 512 threads, each
+// launch completed before the next: what the timestamps report for a dispatch that does nothing
+int lamm_empty_floor(int grid, int launches, void* stream, float* out_us) {
+  const hipStream_t s = static_cast<hipStream_t>(stream);
+  int rc = LAMM_OK;
+  for (int i = 0; i < launches && rc == LAMM_OK; ++i) {
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    hipExtLaunchKernelGGL(empty_floor_kernel, dim3(grid), dim3(512), 0, s, e0, e1, 0, nullptr);
+    float ms = 0.f;
+    if (hipGetLastError() != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
+        hipEventElapsedTime(&ms, e0, e1) != hipSuccess)
+      rc = -2;
+    out_us[i] = ms * 1e3f;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+  }
+  return rc;
+}
+
+// out_us[i] = the dispatch's own duration of read_floor_kernel over [A + ((first + i) % nA) * stride,
+// + bytes), each launch completed before the next (as lamm_steps_isolated with sync_each)
+int lamm_read_floor(const unsigned char* A, size_t stride, int nA, size_t bytes, int first, int launches, void* stream,
+                    float* out_us) {
+  const hipStream_t s = static_cast<hipStream_t>(stream);
+  uint32_t* sink = nullptr;
+  const unsigned grid = (unsigned)((bytes + kFloorWgBytes - 1) / kFloorWgBytes);
+  if (bytes >= (1ull << 32) || hipMalloc(&sink, grid * sizeof(uint32_t)) != hipSuccess) return -2;
+  int rc = LAMM_OK;
+  for (int i = 0; i < launches && rc == LAMM_OK; ++i) {
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    hipExtLaunchKernelGGL(read_floor_kernel, dim3(grid), dim3(512), 0, s, e0, e1, 0,
+                          A + (size_t)((first + i) % nA) * stride, (uint32_t)bytes, sink);
+    float ms = 0.f;
+    if (hipGetLastError() != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
+        hipEventElapsedTime(&ms, e0, e1) != hipSuccess)
+      rc = -2;
+    out_us[i] = ms * 1e3f;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+  }
+  (void)hipFree(sink);
+  return rc;
 }
 
 }  // extern "C"

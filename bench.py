@@ -489,6 +489,44 @@ def stacked_gemv(ctx, fmt, M, K, steps):
             "achieved_GBs": round(sl * u / kern / 1e9, 1), "frac": round(sl * u / kern / 1e9 / HBM_PEAK_GBS, 4)}
 
 
+def group3_fast(ctx, fmt, M, K, steps):
+    """wq|wk|wv of a decode step as the ggml boundary's sibling calls run them in the default (fast)
+    order: three config-2 weights times one activation in ONE launch (lamm_hip_matmul_group ->
+    gemv_flat_group_kernel), weights rotated > MALL, graph-replayed, against three single calls."""
+    torch, la = ctx.torch, ctx.la
+    t = la.BY_NAME[fmt]
+    vt = la.vec_dot_type(t)
+    kb = K // la.blck_size(t)
+    arow = la.row_bytes(t, K)
+    R = max(9, -(-int(1.15 * MALL_BYTES) // (M * arow)))
+    R -= R % 3
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(41)
+    A, _ = make_weights(torch, la, fmt, R, M, K, gen)
+    B = make_activations(torch, la, fmt, 1, K, gen)
+    C3 = torch.zeros(3 * M, dtype=torch.float32, device="cuda")
+    mats = [la.Matrix(A.data_ptr() + c * M * arow, t, M, kb, kb) for c in range(R)]
+    Bm = la.Matrix(B.data_ptr(), vt, kb, 1, kb)
+    Cs = [la.Matrix(C3.data_ptr() + 4 * M * j, la.F32, M, 1, M) for j in range(3)]
+    st = lambda: torch.cuda.current_stream().cuda_stream  # noqa: E731
+    _, kg, _ = time_steps(ctx, lambda i: la.matmul_group([mats[(3 * i + j) % R] for j in range(3)], Bm, Cs, 0, st()),
+                          max(steps, 100), 2, flush=True)
+
+    def three(i):
+        for j in range(3):
+            la.matmul(mats[(3 * i + j) % R], Bm, Cs[j], st())
+    _, k3, _ = time_steps(ctx, three, max(steps, 100), 2, flush=True)
+    u = gemv_bytes(la, fmt, M, K)
+    del A, B, C3
+    torch.cuda.empty_cache()
+    return {"workload": f"3 x {fmt.upper()}xQ8 GEMV M={M} N=1 K={K} per step (wq|wk|wv of a decode step), {R} weight "
+                        "copies rotated, graph-replayed",
+            "kernel": "lamm::gemv_flat_group_kernel (csrc/lamm_gemv_rpw.hip)", "bound": "hbm",
+            "per_launch_us": round(kg * 1e6, 3), "achieved_GBs": round(3 * u / kg / 1e9, 1),
+            "frac": round(3 * u / kg / 1e9 / HBM_PEAK_GBS, 4),
+            "three_single_calls_us": round(k3 * 1e6, 3)}
+
+
 def config3_gemm(ctx, fmt, M, N, K, slices, steps):
     """BASELINE config 3 with stationary weights: `slices` independent M x K weight slices, each
     against its own N activation rows, per launch.  N GPUs: each slice's rows split over the
@@ -828,6 +866,10 @@ def summary(out):
     if "per_launch_us" in st:   # the same GEMV, 33 weight slices in one launch: the streaming rate
         s["config2_gemv_stacked"] = {"kernel": "gemv_stream_dma_kernel", "us": st["per_launch_us"],
                                      "frac_hbm": st["frac"], "achieved_GBs": st["achieved_GBs"]}
+    g3 = out.get("gemv_group3", {})
+    if "per_launch_us" in g3:
+        s["gemv_group3"] = {"kernel": "gemv_flat_group_kernel", "us": g3["per_launch_us"], "frac_hbm": g3["frac"],
+                            "three_single_calls_us": g3["three_single_calls_us"]}
     gm = out.get("gemm", {}).get("slices1", {})
     if "roofline" in gm:
         s["config3_gemm"] = {"engine": gm["engine"], "us": gm["roofline"]["per_launch_us"],
@@ -952,6 +994,11 @@ def main():
             extras["gemv_stacked"] = stacked_gemv(ctx, fmt, M, K, max(5, args.steps // 2))
     except Exception as e:  # noqa: BLE001
         extras["gemv_stacked"] = {"error": str(e)[:300]}
+    try:
+        if world == 1:
+            extras["gemv_group3"] = group3_fast(ctx, fmt, M, K, args.steps)
+    except Exception as e:  # noqa: BLE001
+        extras["gemv_group3"] = {"error": str(e)[:300]}
     if not args.no_gemm:
         gN = args.gemm_N
         gm = {}

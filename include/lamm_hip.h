@@ -154,7 +154,8 @@ int lamm_hip_quantize_host(int vec_type, const float *x, void *y, int64_t k);
  * dims, and for the formats the prefill GEMM repacks (q4_0 / q4_1 / q5_0 / q5_1) keeps that
  * packed form device-resident (lamm_hip_weights_bytes), so a call skips the per-call weight
  * repack.  q5_1 is packed (and then runs on the fp6 engine) only while every block scale is
- * <= 4094; creation synchronises hip_stream for that check, and a tensor past it keeps no packed
+ * <= 2047 and every block min <= 32752 in magnitude (round 6: 32 d and 2 m must stay exact in fp16);
+ * creation synchronises hip_stream for that check, and a tensor past it keeps no packed
  * form (lamm_hip_weights_bytes 0).  lamm_hip_matmul_weights(W, B, C, batch, s) computes exactly what
  * lamm_hip_matmul_batched(&A, B, C, batch, s) computes; batch may be NULL (one slice per A
  * slice) and, if given, must repeat W's ne02 / ne03 / nba2 / nba3.  Creation runs on

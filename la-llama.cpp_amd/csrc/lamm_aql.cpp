@@ -525,6 +525,13 @@ bool direct_active() { return t_direct != nullptr; }
 
 int direct_fallbacks() { return t_fallbacks; }
 
+int direct_launches() { return t_launches; }
+
+void direct_note(const std::string& why) {
+  ++t_fallbacks;
+  if (t_reason.empty()) t_reason = why;
+}
+
 const std::string& direct_reason() { return t_reason; }
 
 uint64_t direct_cache_hits(int device) {

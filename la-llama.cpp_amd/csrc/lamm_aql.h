@@ -17,6 +17,10 @@ bool direct_active();
 // calls of the open (or last) region that fell back to HIP, and why the last fallback, or the last
 // direct_begin, could not use the queue
 int direct_fallbacks();
+// direct launches so far in the open region; a call made in the region whose kernel did not go onto
+// the queue for a reason of the caller's (another engine, a pending profiling request) notes why
+int direct_launches();
+void direct_note(const std::string& why);
 const std::string& direct_reason();
 // dispatches that found their kernarg block already in a cached slot (this device's queue)
 uint64_t direct_cache_hits(int device);

@@ -81,10 +81,17 @@ constexpr int SCALE_W = 130, SCALE_HI = 134, SCALE_LO = 130;   // E8M0: 2^(s-127
 
 template <int T> struct F6;
 // SH16 (q5_1): the quant q in [0, 31] is coded as n = q - 16 (|n| <= 16, exact in e2m3) and the
-// block's affine term carries the shift back: d q + m = d n + (m + 16 d), so sum_b (m_a + 16 d_a) s_b
-// -- both products in the m * s MFMA's spare k slots, f16 x f16 exact in fp32 (16 d_a is exact in f16
-// for d_a <= 4094: prepare_fp6_weights reports a weight with a larger block scale, which then stays
-// on the range-guarded dq16 engine)
+// block's affine term carries the shift back: d q + m = d n + (m + 16 d).  The reference multiplies
+// d_a d_b sum q b, so the shift's share is 16 d_a (d_b sum q_b) -- the activation block's fp16 s_b
+// is that product ROUNDED (and from ggml's fp32 d), off by up to ~2^-10 of s_b, which at small K with
+// activations that do not cancel reached 1.1e-3 of sum |a b|.  So the activation prep
+// also stores the residual r_b = d_b sum q_b - s_b (exact in fp32, kept as fp16 -- its own rounding is
+// ~2^-11 of a residual that is ~2^-11 of s_b) and the m * s MFMA adds, per block,
+//   2 m_a s_b + 32 d_a s_b + 32 d_a r_b = 2 (m_a s_b + 16 d_a d_b sum q_b)
+// over its eight k slots (lanes 0-31: {2 m_a, 32 d_a} x {s_b, s_b}, lanes 32-63: {32 d_a} x {r_b}; the
+// x2 matches the P-MFMA's 2 d_a d_b), each product f16 x f16 exact in fp32.  32 d_a and 2 m_a are
+// exact in f16 for |d_a| <= 2047 and |m_a| <= 32752: prepare_fp6_weights reports a weight outside
+// that range, which then stays on the range-guarded dq16 engine.
 template <> struct F6<kQ4_0> { static constexpr int ABPB = 18, VBPB = 34; static constexpr bool AFF = false, SH16 = false; };
 template <> struct F6<kQ4_1> { static constexpr int ABPB = 20, VBPB = 36; static constexpr bool AFF = true, SH16 = false; };
 template <> struct F6<kQ5_0> { static constexpr int ABPB = 22, VBPB = 34; static constexpr bool AFF = false, SH16 = false; };
@@ -98,8 +105,27 @@ __device__ __forceinline__ uint32_t f16_times16(uint32_t h) {
   return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)(v * (_Float16)16.0f));
 }
 
+__device__ __forceinline__ uint32_t f16_times2(uint32_t h) {   // 2 * h (exact below 32768)
+  const _Float16 v = __builtin_bit_cast(_Float16, (uint16_t)(h & 0xffffu));
+  return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)(v * (_Float16)2.0f));
+}
+
+// q8_1 activation blocks (d, s fp16 bits, the 32 int8 quants as 8 dwords): the fp16 bits of the residual
+// r = d * sum q - s (SH16 above), 0 when s or the product is not finite (the term then falls back to
+// 16 d_a s_b, as the reference's own s overflows there)
+__device__ __forceinline__ uint32_t s_residual(uint32_t dbits, uint32_t sbits, const uint32_t (&q)[8]) {
+  int sum = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) sum = __builtin_amdgcn_sdot4((int)q[k], 0x01010101, sum, false);
+  const float e = h2f(dbits & 0xffffu) * (float)sum;   // 11 x 12 significant bits: exact
+  const float r = e - h2f(sbits & 0xffffu);             // within a factor 2 of each other: exact
+  if (!__builtin_isfinite(r)) return 0u;
+  return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)r);
+}
+
 // A fragment = 8 dwords = two 16-byte planes: p0 = fp6 code dwords 0-3,
-// p1 = {code dwords 4-5, scale dword ({d, 0} fp16 pair), m (q4_1) / s (q8_1) fp16 or 0}.
+// p1 = {code dwords 4-5, scale dword ({d, 0} fp16 pair), m (q4_1) / s (q8_1) fp16 or 0; q8_1 B planes
+// carry s's residual r (SH16) in the upper half of that last dword}.
 // Chunk = one K-step of one tile, exactly the GEMM's LDS image:
 //   A chunk: [p 2][b KB][r TI] x 16 B            B chunk: [p 2][b KB][h 2][r TJ] x 16 B
 // (h = k-group: 0 = hi codes, 1 = lo codes; both copies carry d_b and s_b)
@@ -227,7 +253,8 @@ __global__ __launch_bounds__(PW_NT) void prep_w_fp6(GemvArgs p, unsigned char* w
       if constexpr (T == kQ5_0) qh = get32<2>(m);
       if constexpr (T == kQ5_1) {
         qh = get32<4>(m);
-        if ((d & 0x7fffu) > 0x6bffu) *big_d = 1u;   // |d| > 4094 (incl. inf / NaN): 16 d leaves f16
+        // |d| > 2047 or |m| > 32752 (incl. inf / NaN): 32 d or 2 m leaves f16
+        if ((d & 0x7fffu) > 0x67ffu || ((m[0] >> 16) & 0x7fffu) > 0x77ffu) *big_d = 1u;
       }
       uint32_t qs[4];
       unroll<4>([&](auto K) { qs[K] = get32<QS + 4 * K>(m); });
@@ -293,6 +320,7 @@ __global__ __launch_bounds__(PREP_NT) void prep_b_fp6(GemvArgs p, unsigned char*
         q8_from_f32<VBPB == 36>(x, q8, dh, sh);
         d = dh;
         sv = sh;
+        if constexpr (VBPB == 36) sv |= s_residual(d, sv, q8) << 16;
 #pragma unroll
         for (int e = 0; e < 32; ++e) {
           const int q = (int)(int8_t)((q8[e >> 2] >> (8 * (e & 3))) & 0xffu);
@@ -303,7 +331,13 @@ __global__ __launch_bounds__(PREP_NT) void prep_b_fp6(GemvArgs p, unsigned char*
         uint32_t m[9];
         load_block<9>(rs, (uint32_t)((j - jw) * p.ldb + (int64_t)kb * VBPB), m);
         d = m[0] & 0xffffu;
-        if constexpr (VBPB == 36) sv = m[0] >> 16;
+        if constexpr (VBPB == 36) {
+          sv = m[0] >> 16;
+          uint32_t q8[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) q8[k] = m[1 + k];   // q8_1: the quants from byte 4
+          sv |= s_residual(d, sv, q8) << 16;
+        }
 #pragma unroll
         for (int e = 0; e < 32; ++e) {
           const int q = (int)(int8_t)((m[(VQS + e) >> 2] >> (8 * ((VQS + e) & 3))) & 0xffu);
@@ -439,6 +473,7 @@ __global__ __launch_bounds__(PB_NT) void prep_b_fp6_tile(GemvArgs p, unsigned ch
     d = m[0] & 0xffffu;
     if constexpr (VBPB == 36) sv = m[0] >> 16;
     unroll<8>([&](auto K) { q[K] = get32<VQS + 4 * K>(m); });
+    if constexpr (VBPB == 36) sv |= s_residual(d, sv, q) << 16;
   }
   unsigned char* wz = ws + (int64_t)z * L.b_slice;
   const int64_t ch = ((int64_t)(j / F6_TJ) * L.nsteps + kb / F6_KB) * F6_B_BYTES;
@@ -700,11 +735,15 @@ __global__ __launch_bounds__((F6Waves<WJ, SI, SJ, KG>::NT)) void gemm_fp6_kernel
         for (int y = 0; y < 2; ++y) msA[y][b >> 1] |= ((uint32_t)fa[b & 1][y].v[7] & 0xffffu) << (16 * (b & 1));
 #pragma unroll
         for (int x = 0; x < WJ; ++x) msB[x][b >> 1] |= ((uint32_t)fb[b & 1][x].v[7] & 0xffffu) << (16 * (b & 1));
-        if constexpr (F::SH16) {   // k slots 2, 3: (16 d_a, s_b)
+        if constexpr (F::SH16) {   // [0]: 2 m_a / s_b, [1]: 32 d_a / s's residual r_b (SH16 above)
 #pragma unroll
-          for (int y = 0; y < 2; ++y) msA[y][1] |= f16_times16((uint32_t)fa[b & 1][y].v[6]) << (16 * (b & 1));
+          for (int y = 0; y < 2; ++y) {
+            msA[y][0] = (msA[y][0] & ~(0xffffu << (16 * (b & 1)))) |
+                        f16_times2((uint32_t)fa[b & 1][y].v[7]) << (16 * (b & 1));
+            msA[y][1] |= f16_times2(f16_times16((uint32_t)fa[b & 1][y].v[6])) << (16 * (b & 1));
+          }
 #pragma unroll
-          for (int x = 0; x < WJ; ++x) msB[x][1] |= ((uint32_t)fb[b & 1][x].v[7] & 0xffffu) << (16 * (b & 1));
+          for (int x = 0; x < WJ; ++x) msB[x][1] |= ((uint32_t)fb[b & 1][x].v[7] >> 16) << (16 * (b & 1));
         }
       }
     };
@@ -732,10 +771,13 @@ __global__ __launch_bounds__((F6Waves<WJ, SI, SJ, KG>::NT)) void gemm_fp6_kernel
     if constexpr (AFF) {   // sum_b m_a * s_b: rank-KB per K-step, both k halves carry it (x2 like P)
 #pragma unroll
       for (int x = 0; x < WJ; ++x) {
-        const half4 sf = __builtin_bit_cast(half4, uint2{msB[x][0], msB[x][1]});
+        // SH16: lanes 0-31 {s_b, s_b} x {2 m_a, 32 d_a}, lanes 32-63 {r_b, 0} x {32 d_a, 0}
+        const half4 sf = F::SH16 ? __builtin_bit_cast(half4, uint2{h ? msB[x][1] : msB[x][0], h ? 0u : msB[x][0]})
+                                 : __builtin_bit_cast(half4, uint2{msB[x][0], msB[x][1]});
 #pragma unroll
         for (int y = 0; y < 2; ++y) {
-          const half4 mf = __builtin_bit_cast(half4, uint2{msA[y][0], msA[y][1]});
+          const half4 mf = F::SH16 ? __builtin_bit_cast(half4, uint2{h ? msA[y][1] : msA[y][0], h ? 0u : msA[y][1]})
+                                   : __builtin_bit_cast(half4, uint2{msA[y][0], msA[y][1]});
           acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x8f16(sf, mf, acc[x][y], 0, 0, 0);
         }
       }
@@ -994,7 +1036,8 @@ __global__ __launch_bounds__(512) void gemm_fp6_kv_kernel(GemvArgs p, const unsi
   F6Res rr[2];
   bool pend = false;
   uint32_t msA[2] = {0, 0}, msB[WJ] = {};   // q4_1: the K-step's m_a / s_b (16 bits per block)
-  uint32_t dsA[2] = {0, 0};                 // q5_1: the K-step's 16 d_a
+  uint32_t dsA[2] = {0, 0};                 // q5_1: the K-step's 32 d_a
+  uint32_t rsB[WJ] = {};                    // q5_1: the K-step's residuals r_b of s_b
   // a fragment's operands from its two 16-byte planes: the scale MFMA's six code dwords, the f16
   // MFMA's {d, 0, 0, 0} (q4_1: {d, m} -> {d, 0, 0, 0} too)
   auto codes = [](const u32x4& p0, const u32x4& p1) {
@@ -1096,21 +1139,30 @@ __global__ __launch_bounds__(512) void gemm_fp6_kv_kernel(GemvArgs p, const unsi
       for (int y = 0; y < 2; ++y) msA[y] |= ((uint32_t)wc.d[y][1] & 0xffffu) << (16 * bk);
 #pragma unroll
       for (int x = 0; x < WJ; ++x) msB[x] |= (rb_[S][x][1][3] & 0xffffu) << (16 * bk);
-      if constexpr (F::SH16) {
+      if constexpr (F::SH16) {   // 2 m_a (in msA), 32 d_a, s's residual r_b (SH16 above)
 #pragma unroll
-        for (int y = 0; y < 2; ++y) dsA[y] |= f16_times16((uint32_t)wc.d[y][0]) << (16 * bk);
+        for (int y = 0; y < 2; ++y) {
+          msA[y] = (msA[y] & ~(0xffffu << (16 * bk))) | f16_times2((uint32_t)wc.d[y][1]) << (16 * bk);
+          dsA[y] |= f16_times2(f16_times16((uint32_t)wc.d[y][0])) << (16 * bk);
+        }
+#pragma unroll
+        for (int x = 0; x < WJ; ++x) rsB[x] |= (rb_[S][x][1][3] >> 16) << (16 * bk);
       }
       if (bk == F6_KB - 1) {
 #pragma unroll
         for (int x = 0; x < WJ; ++x) {
-          // k slots 0, 1: (m_a, s_b) of the two blocks; q5_1 also 2, 3: (16 d_a, s_b)
-          const half4 sf = __builtin_bit_cast(half4, uint2{msB[x], F::SH16 ? msB[x] : 0u});
+          // k slots 0, 1: (m_a, s_b) of the two blocks, both k halves (x2 like P); q5_1: lanes 0-31
+          // {s_b, s_b} x {2 m_a, 32 d_a}, lanes 32-63 {r_b, 0} x {32 d_a, 0}
+          const half4 sf = F::SH16 ? __builtin_bit_cast(half4, uint2{h ? rsB[x] : msB[x], h ? 0u : msB[x]})
+                                   : __builtin_bit_cast(half4, uint2{msB[x], 0u});
 #pragma unroll
           for (int y = 0; y < 2; ++y) {
-            const half4 mf = __builtin_bit_cast(half4, uint2{msA[y], dsA[y]});
+            const half4 mf = F::SH16 ? __builtin_bit_cast(half4, uint2{h ? dsA[y] : msA[y], h ? 0u : dsA[y]})
+                                     : __builtin_bit_cast(half4, uint2{msA[y], dsA[y]});
             acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x8f16(sf, mf, acc[x][y], 0, 0, 0);
           }
           msB[x] = 0;
+          rsB[x] = 0;
         }
         msA[0] = msA[1] = 0;
         dsA[0] = dsA[1] = 0;

@@ -326,6 +326,20 @@ __global__ __launch_bounds__(512) void gemv_flat1_kernel(const unsigned char* A,
   flat_body<T, 8, BF32, 2>(A, lda, B, C, M, 128, group);
 }
 
+// Several weights times the same activation column in one launch (lamm_hip_matmul_group in the fast
+// order: llama.cpp's wq / wk / wv and ffn gate / up decode calls, the ggml boundary's sibling calls):
+// blockIdx.y picks the weight, blockIdx.x its 8-row group in gemv_flat1_kernel's XCD-aware order over
+// the longest weight's groups (groups past a shorter weight's rows return at once).  Each row runs
+// flat_body exactly as in gemv_flat1_kernel, so every C[i] has the bits of its own single call.
+template <int T, bool BF32>
+__global__ __launch_bounds__(512) void gemv_flat_group_kernel(RefSegs sg, const unsigned char* B, uint32_t lda) {
+  const int z = blockIdx.y, M = sg.M[z];
+  const int n = gridDim.x, x = blockIdx.x & 7, k = blockIdx.x >> 3, q = n >> 3, r = n & 7;
+  const int group = x < r ? x * (q + 1) + k : r * (q + 1) + (x - r) * q + k;
+  if (group * 8 >= M) return;
+  flat_body<T, 8, BF32, 2>(sg.A[z], lda, B, sg.C[z], M, 128, group);
+}
+
 // The k-quant formats against q8_K, one column, K <= 12288 (the reference's Q2_K kernel,
 // src/lamm_kernel_q2_k.hpp, whose block dot is LC/ggml-quants.c ggml_vec_dot_q2_K_q8_K; q4_K /
 // q5_K, SURVEY §8f: ggml_vec_dot_q4_K_q8_K / _q5_K_q8_K): one wave per row, lane l on super-block
@@ -634,6 +648,40 @@ hipError_t launch_gemv_kq(int type, const GemvArgs& p, hipStream_t s) {
     case kQ4_K: go(std::integral_constant<int, kQ4_K>{}); break;
     case kQ5_K: go(std::integral_constant<int, kQ5_K>{}); break;
     case kQ6_K: go(std::integral_constant<int, kQ6_K>{}); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+bool gemv_group_supported(int type, const GemvArgs& p, const RefSegs& sg, int nseg) {
+  if (nseg < 1 || nseg > kRefSegs || p.N != 1 || p.nblk != 128 || p.ne12 * p.ne13 != 1 || p.flag ||
+      (p.lda & 15) || p.lda >= (1 << 16) || !gemv_rpw_supported(type, p) || knobs().gemv_rpw >= 0 || knobs().gemv_laneb)
+    return false;
+  for (int i = 0; i < nseg; ++i) {   // the rows whose single calls are gemv_flat1_kernel (rpw_waves: 8 waves)
+    GemvArgs q = p;
+    q.M = sg.M[i];
+    if (sg.M[i] < 2048 || rpw_waves(q) != 8) return false;
+  }
+  return true;
+}
+
+hipError_t launch_gemv_group(int type, const GemvArgs& p, const RefSegs& sg, int nseg, hipStream_t s) {
+  if (!gemv_group_supported(type, p, sg, nseg)) return hipErrorInvalidValue;
+  int mmax = 0;
+  for (int i = 0; i < nseg; ++i) mmax = sg.M[i] > mmax ? sg.M[i] : mmax;
+  const dim3 g((unsigned)((mmax + 7) / 8), (unsigned)nseg);
+  const bool bf = p.b_f32 != 0;
+  auto go = [&](auto tc) {
+    constexpr int T = decltype(tc)::value;
+    if (bf) hipLaunchKernelGGL((gemv_flat_group_kernel<T, true>), g, dim3(512), 0, s, sg, p.B, (uint32_t)p.lda);
+    else hipLaunchKernelGGL((gemv_flat_group_kernel<T, false>), g, dim3(512), 0, s, sg, p.B, (uint32_t)p.lda);
+  };
+  switch (type) {
+    case kQ4_0: go(std::integral_constant<int, kQ4_0>{}); break;
+    case kQ4_1: go(std::integral_constant<int, kQ4_1>{}); break;
+    case kQ5_0: go(std::integral_constant<int, kQ5_0>{}); break;
+    case kQ5_1: go(std::integral_constant<int, kQ5_1>{}); break;
+    case kQ8_0: go(std::integral_constant<int, kQ8_0>{}); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

@@ -249,7 +249,15 @@ int matmul_impl(const lamm_matrix* A, const lamm_matrix* B, const lamm_matrix* C
   // two events bracket the call's launches on the stream instead
   const LaunchTiming tm = g_timing;
   if (tm.start) (void)hipEventRecord(tm.start, static_cast<hipStream_t>(hip_stream));
+  const int direct0 = lamm::direct_active() ? lamm::direct_launches() : -1;
   const int rc = matmul_impl_(A, B, C, batch, hip_stream, W, flags);
+  if (direct0 >= 0 && rc == LAMM_OK && lamm::direct_launches() == direct0) {
+    // a call in a direct region that launched through HIP: say which one and why it could
+    char why[160];
+    snprintf(why, sizeof why, "A type %d, %d x %d x %d%s%s: its kernel is not one the queue takes", A->type, A->row,
+             B->col, A->col, tm.start ? ", with a profiling request pending" : "", flags ? ", flags set" : "");
+    lamm::direct_note(why);
+  }
   if (g_timing.start) (void)hipEventRecord(tm.stop, static_cast<hipStream_t>(hip_stream));
   g_timing = LaunchTiming{};
   return rc;
@@ -415,6 +423,8 @@ extern "C" int lamm_hip_direct_end(void) {
   if (lamm::direct_fallbacks() > 0)
     fail(LAMM_ERR_HIP, "lamm_hip_direct_end: %d call(s) launched through HIP: %s", lamm::direct_fallbacks(),
          lamm::direct_reason().c_str());
+  else if (n == 0)
+    fail(LAMM_ERR_HIP, "lamm_hip_direct_end: no call was made in the region");
   return n;
 }
 
@@ -511,8 +521,11 @@ extern "C" int lamm_hip_matmul_group(const lamm_matrix* A, int n, const lamm_mat
                                      int flags, void* hip_stream) {
   if (!A || !B || !C) return fail(LAMM_ERR_SHAPE, "null matrix");
   if (n < 1 || n > LAMM_GROUP_MAX) return fail(LAMM_ERR_SHAPE, "group of %d weights (1..%d)", n, LAMM_GROUP_MAX);
-  // one launch: the reference-order one-column kernel, every weight of one type and row length
-  bool one = (flags & LAMM_ORDER_REFERENCE) && n > 1 && B->col == 1;
+  // one launch: the one-column kernel of the call's order over every weight of one type and row
+  // length (the reference order: ref_gemv_group_kernel; the fast engines: gemv_flat_group_kernel for
+  // the K = 4096 weights their single calls run on gemv_flat1_kernel)
+  const bool ref = (flags & LAMM_ORDER_REFERENCE) != 0;
+  bool one = n > 1 && B->col == 1;
   for (int i = 0; i < n && one; ++i)
     one = A[i].type == A[0].type && A[i].col == A[0].col && A[i].ld == A[0].ld && A[i].row > 0 &&
           C[i].type == kF32 && C[i].row == A[i].row && C[i].col == 1 && ((uintptr_t)A[i].data & 15) == 0 &&
@@ -521,7 +534,7 @@ extern "C" int lamm_hip_matmul_group(const lamm_matrix* A, int n, const lamm_mat
     const int t = A[0].type, vdt = vec_dot_type(t), Kb = A[0].col;
     const bool b_f32 = B->type == kF32 && (vdt == kQ8_0 || vdt == kQ8_1);
     const int64_t lda = A[0].ld * (int64_t)block_bytes(t);
-    one = is_weight_type(t) && ref_order_supported(t, vdt) && (B->type == vdt || b_f32) &&
+    one = is_weight_type(t) && (!ref || ref_order_supported(t, vdt)) && (B->type == vdt || b_f32) &&
           B->row == (b_f32 ? Kb * block_elems(t) : Kb) && A[0].ld >= Kb && (lda & 15) == 0 &&
           ((uintptr_t)B->data & (b_f32 ? 3 : 0)) == 0;
     if (one) {
@@ -529,16 +542,22 @@ extern "C" int lamm_hip_matmul_group(const lamm_matrix* A, int n, const lamm_mat
                  B->ld * (int64_t)block_bytes(B->type), static_cast<float*>(C[0].data), C[0].ld, A[0].row, 1,
                  Kb * block_elems(t), Kb};
       p.b_f32 = b_f32 ? 1 : 0;
-      if (ref_gemv_supported(t, p) && probe().count > 0) {
-        RefSegs sg{};
-        for (int i = 0; i < n; ++i) {
-          sg.A[i] = static_cast<const unsigned char*>(A[i].data);
-          sg.C[i] = static_cast<float*>(C[i].data);
-          sg.M[i] = A[i].row;
-        }
+      RefSegs sg{};
+      for (int i = 0; i < n; ++i) {
+        sg.A[i] = static_cast<const unsigned char*>(A[i].data);
+        sg.C[i] = static_cast<float*>(C[i].data);
+        sg.M[i] = A[i].row;
+      }
+      if ((ref ? ref_gemv_supported(t, p) : gemv_group_supported(t, p, sg, n)) && probe().count > 0) {
+        // a lamm_hip_profile_next request brackets the one launch, as matmul_impl brackets its
+        // launches (it used to be dropped here)
+        const LaunchTiming tm = g_timing;
         g_timing = LaunchTiming{};
         g_completion = nullptr;
-        const hipError_t e = launch_ref_group(t, p, sg, n, static_cast<hipStream_t>(hip_stream));
+        const hipStream_t s = static_cast<hipStream_t>(hip_stream);
+        if (tm.start) (void)hipEventRecord(tm.start, s);
+        const hipError_t e = ref ? launch_ref_group(t, p, sg, n, s) : launch_gemv_group(t, p, sg, n, s);
+        if (tm.start) (void)hipEventRecord(tm.stop, s);
         if (e != hipSuccess) return fail(LAMM_ERR_HIP, "kernel launch: %s", hipGetErrorString(e));
         return LAMM_OK;
       }
@@ -715,8 +734,10 @@ struct Dev {
   unsigned char* vram_x(size_t bytes) {
     if (xv_ok < 0) return nullptr;
     if (xv_cap < bytes) {
+      // on this device, the first allocation too (the caller's current device can be
+      // another one, and the buffer and its HDP flush must be this device's)
+      (void)hipSetDevice(id);
       if (xv) {
-        (void)hipSetDevice(id);
         (void)hipStreamSynchronize(stream);
         (void)hipFree(xv);
         xv = nullptr;

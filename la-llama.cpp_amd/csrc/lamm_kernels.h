@@ -90,6 +90,11 @@ struct RefSegs {
   int M[kRefSegs];
 };
 hipError_t launch_ref_group(int type, const GemvArgs& p, const RefSegs& sg, int nseg, hipStream_t s);
+// the same group in the fast engines' order (lamm_gemv_rpw.hip gemv_flat_group_kernel): one column,
+// K = 4096, every weight >= 2048 rows -- the weights whose single calls run gemv_flat1_kernel, whose
+// per-row arithmetic the group kernel repeats, so each C[i] has its single call's bits
+bool gemv_group_supported(int type, const GemvArgs& p, const RefSegs& sg, int nseg);
+hipError_t launch_gemv_group(int type, const GemvArgs& p, const RefSegs& sg, int nseg, hipStream_t s);
 
 hipError_t launch_gemm(int type, const GemvArgs& p, void* workspace, hipStream_t s);
 size_t gemm_workspace_bytes(int type, const GemvArgs& p);   // device scratch launch_gemm needs

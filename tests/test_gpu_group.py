@@ -1,8 +1,9 @@
-"""lamm_hip_matmul_group (csrc/lamm_hip.cpp, ref_gemv_group_kernel in csrc/lamm_ref.hip): several
-weights times one activation column -- wq / wk / wv, ffn gate / up (LC/llama.cpp:5738-5752) -- must
-give every C[i] the bits of its own lamm_hip_matmul_ex call, in one launch for reference-order calls
-and through the per-weight fallback for anything else; and the reference-order results are the
-oracle's AVX2-order bits."""
+"""lamm_hip_matmul_group (csrc/lamm_hip.cpp; ref_gemv_group_kernel in csrc/lamm_ref.hip,
+gemv_flat_group_kernel in csrc/lamm_gemv_rpw.hip): several weights times one activation column -- wq /
+wk / wv, ffn gate / up (LC/llama.cpp:5738-5752) -- must give every C[i] the bits of its own
+lamm_hip_matmul_ex call, in one launch for reference-order calls and for fast-order K = 4096 weights of
+>= 2048 rows, and through the per-weight fallback for anything else; the reference-order results are
+the oracle's AVX2-order bits, the fast-order ones within the north star's 1e-3."""
 import numpy as np
 import pytest
 
@@ -67,11 +68,14 @@ def run(Ams, Bm, Ms, flags, group):
 
 
 @pytest.mark.parametrize("t", REF_TYPES, ids=[ol.NAMES[t] for t in REF_TYPES])
-@pytest.mark.parametrize("Ms", [(4096, 4096, 4096), (11008, 11008), (4096, 1024, 67, 13)],
-                         ids=["qkv", "gate_up", "ragged4"])
+@pytest.mark.parametrize("Ms,K", [((4096, 4096, 4096), 4096), ((11008, 11008), 4096), ((4096, 1024, 67, 13), 4096),
+                                  ((5120, 5120, 5120), 5120), ((4096, 2048), 8192)],
+                         ids=["qkv", "gate_up", "ragged4", "qkv_k5120", "k8192"])
 @pytest.mark.parametrize("f32_rows", [False, True], ids=["q8_rows", "f32_rows"])
-def test_group_reference_order_bitwise(t, Ms, f32_rows):
-    K = 4096
+def test_group_reference_order_bitwise(t, Ms, K, f32_rows):
+    """K = 5120 / 8192 (13B / 70B hidden sizes): the single reference-order launch switches
+    to 128-block chunks beyond K = 4096 while the group kernel keeps 64-block chunks -- the chained
+    lane order must not depend on the chunking."""
     qs, keep, Ams = weights(t, Ms, K, seed=len(Ms) * 100 + t)
     B, Bm, Bq = activation(t, K, f32_rows, seed=t + 3)
     one = run(Ams, Bm, Ms, la.ORDER_REFERENCE, False)
@@ -82,6 +86,30 @@ def test_group_reference_order_bitwise(t, Ms, f32_rows):
     i = int(np.argmin(Ms))
     want = ORACLE.mul_mat_avx(t, Ms[i], 1, K, qs[i], Bq)[0]
     assert np.array_equal(bits(grp[i]), bits(want))
+
+
+FAST_TYPES = [ol.Q4_0, ol.Q4_1, ol.Q5_0, ol.Q5_1, ol.Q8_0]
+
+
+@pytest.mark.parametrize("t", FAST_TYPES, ids=[ol.NAMES[t] for t in FAST_TYPES])
+@pytest.mark.parametrize("Ms", [(4096, 4096, 4096), (11008, 11008), (4096, 2048, 3000, 11008)],
+                         ids=["qkv", "gate_up", "ragged4"])
+@pytest.mark.parametrize("f32_rows", [False, True], ids=["q8_rows", "f32_rows"])
+def test_group_fast_order_bitwise(t, Ms, f32_rows):
+    """The fast order (the ggml boundary's default since round 6): one gemv_flat_group_kernel launch,
+    every weight's C the bits of its single call (gemv_flat1_kernel), and within 1e-3 of the oracle."""
+    K = 4096
+    qs, keep, Ams = weights(t, Ms, K, seed=len(Ms) * 10 + t)
+    B, Bm, Bq = activation(t, K, f32_rows, seed=t + 5)
+    one = run(Ams, Bm, Ms, 0, False)
+    grp = run(Ams, Bm, Ms, 0, True)
+    for i, (a, b) in enumerate(zip(one, grp)):
+        assert np.array_equal(bits(a), bits(b)), f"weight {i}"
+    for i in range(len(Ms)):
+        want = ORACLE.mul_mat(t, Ms[i], 1, K, qs[i], Bq)[0]
+        Ad = ORACLE.dequantize(t, qs[i], Ms[i], K).astype(np.float64)
+        absdot = np.abs(Ad) @ np.abs(ORACLE.dequantize(la.vec_dot_type(t), Bq, 1, K).astype(np.float64))[0]
+        assert (np.abs(grp[i] - want) / np.maximum(absdot, 1e-30)).max() < 1e-3
 
 
 def test_group_fallbacks_and_errors():

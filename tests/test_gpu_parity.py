@@ -1094,9 +1094,10 @@ def _config4_operands(t):
 @pytest.mark.parametrize("t", CONFIG4_TYPES, ids=[ol.NAMES[t] for t in CONFIG4_TYPES])
 def test_config4_full_size_gemm(t, mode):
     """BASELINE config 4 at its real size: every sweep format at M=4096 N=512 K=4096 on its
-    default prefill engine (q4_1 / q5_0: fp6, q5_1 / q8_0: MFMA-i8, q2_K: the super-block
-    engine), through the weight-stationary handle (the ggml boundary's and bench.py's path) and
-    the per-call API.  >= 256 sampled rows x all 512 columns vs the oracle."""
+    default prefill engine (q4_1 / q5_0: fp6; q5_1: fp6 with prepared weights, dq16 per call; q8_0:
+    dq16, range-guarded; q2_K: the super-block engine), through the weight-stationary handle (the
+    ggml boundary's and bench.py's path) and the per-call API.  >= 256 sampled rows x all 512
+    columns vs the oracle."""
     M, N, K = 4096, 512, 4096
     A_q, B_q = _config4_operands(t)
     A = dev_bytes(np.concatenate([A_q, np.zeros(64, np.uint8)]))

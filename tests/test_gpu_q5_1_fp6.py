@@ -1,7 +1,8 @@
 """q5_1 prefill on the block-scaled fp6 engine (lamm_gemm_fp6.hip F6<kQ5_1>): its quants are coded as
-q - 16 (exact in e2m3) and the shift rides on the affine term, sum_b (m_a + 16 d_a) s_b, in the m * s
-MFMA's spare k slots.  Only weight-stationary calls take it (lamm_hip_weights_create packs and range-
-checks the weights once); a tensor with a block scale past 4094 (16 d leaves f16) keeps no packed form
+q - 16 (exact in e2m3) and the shift rides on the affine term in the m * s MFMA's spare k slots:
+sum_b (m_a s_b + 16 d_a (s_b + r_b)), r_b the activation prep's residual of the block's rounded s_b
+(round 6, lamm_gemm_fp6.hip SH16), so the shift's share is 16 d_a d_b sum q_b as in the reference.  Only weight-stationary calls take it (lamm_hip_weights_create packs and range-
+checks the weights once); a tensor with a block scale past 2047 (32 d leaves f16; round 6) keeps no packed form
 and runs on the range-guarded dq16 engine.  Checked against the oracle (the reference's lamm q5_1
 block kernel, src/lamm_kernel_q5_1.hpp) at the usual bar."""
 import numpy as np
@@ -64,6 +65,32 @@ def test_q5_1_fp6_stationary_vs_oracle(shape, monkeypatch):
     assert err < TOL
 
 
+POS_SHAPES = [(300, 40, 96), (257, 64, 1024), (4096, 512, 1024)]
+
+
+@pytest.mark.parametrize("shape", POS_SHAPES, ids=[f"{m}x{n}x{k}" for m, n, k in POS_SHAPES])
+def test_q5_1_fp6_positive_activations(shape, monkeypatch):
+    """the shift's affine term uses the activation block's rounded fp16 s = d_b sum q_b, so
+    sum_b 16 d_a s_b differs from the reference's 16 d_a d_b sum q_b by 16 d_a (s_b - d_b sum q_b) per
+    block.  Activations that never cancel (all positive: s_b large) and centred weights (|w| << 16 d,
+    small sum |a b|) make that margin largest, most at small K.  Still within the bar."""
+    M, N, K = shape
+    if M * N < 4096 * 512:
+        monkeypatch.setenv("LAMM_GEMM_PATH", "fp6")
+    assert la.gemm_engine(T, M, N, K, 1, stationary=True) == "fp6"
+    rng = np.random.default_rng(M * 7 + K)
+    a = rng.standard_normal((M, K), dtype=np.float32) * 0.1   # centred: m ~ -16 d
+    b = rng.random((N, K), dtype=np.float32) + 0.5            # all positive, no cancellation
+    A_q = ORACLE.quantize(T, a, ol.QUANT_REF)
+    B_q = ORACLE.quantize(ol.Q8_1, b, ol.QUANT_AVX)
+    c, packed = stationary(A_q, B_q, M, N, K)
+    assert packed > 0
+    rows = np.arange(M) if M <= 512 else np.unique(np.r_[np.arange(0, M, 16), [1, 255, 256, M - 1]])
+    err = check(c, A_q, B_q, M, N, K, rows)
+    print(f"q5_1 fp6 positive activations {M}x{N}x{K}: max rel err {err:.2e}")
+    assert err < TOL
+
+
 def test_q5_1_per_call_stays_off_fp6(monkeypatch):
     """Without prepared weights q5_1 never reaches the fp6 engine (no range check per call): dq16 by
     default, the exact i8 engine when fp6 is forced."""
@@ -84,7 +111,7 @@ def test_q5_1_per_call_stays_off_fp6(monkeypatch):
 
 
 def test_q5_1_large_block_scale_falls_back():
-    """A weight tensor with one block scale past 4094 (a block spanning -65000 .. 65000: d = 4193,
+    """A weight tensor with one block scale past 2047 (a block spanning -65000 .. 65000: d = 4193,
     m still inside f16): no packed form is kept and the call runs, finite and within the bar, on
     the range-guarded dq16 engine."""
     M, N, K = 4096, 512, 1024

@@ -21,6 +21,8 @@ unit = bench.gemv_bytes(la, "q4_0", 4096, 4096)
 lib = bench.steps_lib(la)
 lib.lamm_steps_matmul.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(la.Matrix), ctypes.POINTER(la.Matrix),
                                   ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+lib.lamm_steps_graph.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(la.Matrix), ctypes.POINTER(la.Matrix),
+                                 ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_float)]
 for K in (20, 200, 20, 200):
     g = bench.config2_gemv(ctx, "q4_0", 4096, 4096, K, 5)
     row = {"K": K, "graph_us": round(g["per_step"] * 1e6, 3),
@@ -45,7 +47,11 @@ for K in (20, 200, 20, 200):
                           ctypes.c_void_p(st.cuda_stream))
     torch.cuda.synchronize()
     row["cloop_us"] = round((time.perf_counter() - t0) / K * 1e6, 3)
-    row["value_best_GBs"] = round(unit / min(v for k, v in row.items() if k in ("graph_us", "direct_us", "cloop_us")
-                                            and v) / 1e3, 1)
+    # the same K calls as a hipGraph captured, instantiated and uploaded from C, replayed from C
+    out = (ctypes.c_float * 7)()
+    rc = lib.lamm_steps_graph(ctypes.cast(mats, ctypes.c_void_p), R, ctypes.byref(Bm), ctypes.byref(Cm), 5, K, 7, out)
+    row["cgraph_us"] = round(sorted(out)[3] / K, 3) if rc == 0 else f"rc {rc}"
+    row["value_best_GBs"] = round(unit / min(v for k, v in row.items() if k in ("graph_us", "direct_us", "cloop_us", "cgraph_us")
+                                            and isinstance(v, float)) / 1e3, 1)
     print(json.dumps(row), flush=True)
     del A, Bq, C

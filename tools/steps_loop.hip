@@ -11,6 +11,8 @@
 //                              roofline)
 //   lamm_steps_direct        : K calls inside one direct-dispatch region (lamm_hip_direct_begin /
 //                              end: the library's own AQL queue), completed before it returns
+//   lamm_steps_graph         : the K calls captured from C as one hipGraph (instantiated, uploaded),
+//                              replayed; wall time of launch -> synchronize per replay
 //   lamm_read_floor          : the single-launch floor of config 2: a read-only
 //                              kernel on the GEMV's grid (512 workgroups of 512 threads, 36 bytes per
 //                              thread as the GEMV's two 18-byte blocks per lane) over the same bytes,
@@ -127,6 +129,39 @@ int lamm_steps_direct(const lamm_matrix* A, int nA, const lamm_matrix* B, const 
   const int n = lamm_hip_direct_end();
   if (wall_us) *wall_us = now_us() - t0;
   return rc != LAMM_OK ? -100 - rc : n;
+}
+
+// K = steps calls A[(first + s) % nA] * B -> C captured on a fresh stream as one hipGraph, instantiated and
+// uploaded; one untimed replay, then `reps` replays each timed on the host from hipGraphLaunch to the
+// end of hipStreamSynchronize (out_us[r]).  Returns LAMM_OK or a negative status.
+int lamm_steps_graph(const lamm_matrix* A, int nA, const lamm_matrix* B, const lamm_matrix* C, int first, int steps,
+                     int reps, float* out_us) {
+  hipStream_t s;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return -2;
+  int rc = LAMM_OK;
+  // warm: every kernel of the steps launched once, outside the capture
+  for (int i = 0; i < steps && rc == LAMM_OK; ++i) rc = lamm_hip_matmul(&A[(first + i) % nA], B, C, s);
+  if (rc != LAMM_OK || hipStreamSynchronize(s) != hipSuccess) {
+    (void)hipStreamDestroy(s);
+    return rc != LAMM_OK ? rc : -2;
+  }
+  hipGraph_t g = nullptr;
+  hipGraphExec_t ge = nullptr;
+  if (hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) != hipSuccess) rc = -3;
+  for (int i = 0; i < steps && rc == LAMM_OK; ++i) rc = lamm_hip_matmul(&A[(first + i) % nA], B, C, s);
+  if (hipStreamEndCapture(s, &g) != hipSuccess && rc == LAMM_OK) rc = -4;
+  if (rc == LAMM_OK && hipGraphInstantiate(&ge, g, nullptr, nullptr, 0) != hipSuccess) rc = -5;
+  if (rc == LAMM_OK && hipGraphUpload(ge, s) != hipSuccess) rc = -6;
+  if (rc == LAMM_OK && (hipGraphLaunch(ge, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)) rc = -7;
+  for (int r = 0; r < reps && rc == LAMM_OK; ++r) {
+    const double t0 = now_us();
+    if (hipGraphLaunch(ge, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess) rc = -8;
+    out_us[r] = (float)(now_us() - t0);
+  }
+  if (ge) (void)hipGraphExecDestroy(ge);
+  if (g) (void)hipGraphDestroy(g);
+  (void)hipStreamDestroy(s);
+  return rc;
 }
 
 // out_us[i] = the dispatch's own duration of an EMPTY kernel on `grid` workgroups of 512 threads, each

@@ -92,12 +92,19 @@ template <int T> struct F6;
 // x2 matches the P-MFMA's 2 d_a d_b), each product f16 x f16 exact in fp32.  32 d_a and 2 m_a are
 // exact in f16 for |d_a| <= 2047 and |m_a| <= 32752: prepare_fp6_weights reports a weight outside
 // that range, which then stays on the range-guarded dq16 engine.
-template <> struct F6<kQ4_0> { static constexpr int ABPB = 18, VBPB = 34; static constexpr bool AFF = false, SH16 = false; };
-template <> struct F6<kQ4_1> { static constexpr int ABPB = 20, VBPB = 36; static constexpr bool AFF = true, SH16 = false; };
-template <> struct F6<kQ5_0> { static constexpr int ABPB = 22, VBPB = 34; static constexpr bool AFF = false, SH16 = false; };
-template <> struct F6<kQ5_1> { static constexpr int ABPB = 24, VBPB = 36; static constexpr bool AFF = true, SH16 = true; };
+// WP: weight code planes per block.  q8_0 (round 6): its quants q in [-127, 127] do not
+// fit e2m3, so the weight is split like the activations, q = 16 h + l (h = q >> 4 in [-8, 7], l = q & 15),
+// into a hi and a lo code plane; the S of a unit is then two chained scale MFMAs, the hi one with its
+// weight scale x16 (E8M0 +4) accumulating into the lo one -- S = sum (16 h + l) b, every partial an
+// integer below 2^24, exact in fp32.  Only the 128 x 64 K-group plan (gemm_fp6_kv_kernel) takes it, and
+// only with prepared weights; other q8_0 calls stay on dq16.
+template <> struct F6<kQ4_0> { static constexpr int ABPB = 18, VBPB = 34, WP = 1; static constexpr bool AFF = false, SH16 = false; };
+template <> struct F6<kQ4_1> { static constexpr int ABPB = 20, VBPB = 36, WP = 1; static constexpr bool AFF = true, SH16 = false; };
+template <> struct F6<kQ5_0> { static constexpr int ABPB = 22, VBPB = 34, WP = 1; static constexpr bool AFF = false, SH16 = false; };
+template <> struct F6<kQ5_1> { static constexpr int ABPB = 24, VBPB = 36, WP = 1; static constexpr bool AFF = true, SH16 = true; };
+template <> struct F6<kQ8_0> { static constexpr int ABPB = 34, VBPB = 34, WP = 2; static constexpr bool AFF = false, SH16 = false; };
 static_assert(F6_KB == 2, "q5_1's shift term uses the m * s MFMA's k slots 2..3");
-static_assert(!F6<kQ4_0>::SH16 && !F6<kQ4_1>::SH16 && !F6<kQ5_0>::SH16, "only q5_1 shifts its quants");
+static_assert(!F6<kQ4_0>::SH16 && !F6<kQ4_1>::SH16 && !F6<kQ5_0>::SH16 && !F6<kQ8_0>::SH16, "only q5_1 shifts its quants");
 
 // 16 * h for an f16 bit pattern h (exact below 4096); the f16 bits of the result
 __device__ __forceinline__ uint32_t f16_times16(uint32_t h) {
@@ -144,13 +151,14 @@ __host__ __device__ constexpr int f6_boff(int p, int b, int h, int r) {
 struct F6Layout {
   int nsteps, nit, njt, na;
   int64_t a_slice, b_slice, a_bytes;
-  __host__ __device__ static F6Layout of(const GemvArgs& p) {
+  // wp: weight code planes (F6<T>::WP): a K-step's A chunk is wp x F6_A_BYTES (q8_0: hi then lo)
+  __host__ __device__ static F6Layout of(const GemvArgs& p, int wp = 1) {
     F6Layout L;
     L.nsteps = (p.nblk + F6_KB - 1) / F6_KB;
     L.nit = (p.M + F6_TI - 1) / F6_TI;
     L.njt = (p.N + F6_TJ - 1) / F6_TJ;
     L.na = (p.ne12 / p.r2) * (p.ne13 / p.r3);
-    L.a_slice = (int64_t)L.nit * L.nsteps * F6_A_BYTES;
+    L.a_slice = (int64_t)L.nit * L.nsteps * F6_A_BYTES * wp;
     L.b_slice = (int64_t)L.njt * L.nsteps * F6_B_BYTES;
     L.a_bytes = (int64_t)L.na * L.a_slice;
     return L;
@@ -203,7 +211,7 @@ __global__ __launch_bounds__(PW_NT) void prep_w_fp6(GemvArgs p, unsigned char* w
   constexpr int SEG = PW_NB * F::ABPB;            // bytes per row segment (multiple of 16)
   constexpr int SEGW = SEG / 4 + 1;                // + 1 dword so unaligned block reads stay inside
   __shared__ uint32_t raw[PW_ROWS * SEGW];
-  const F6Layout L = F6Layout::of(p);
+  const F6Layout L = F6Layout::of(p, F::WP);
   const int nkg = (L.nsteps * F6_KB + PW_NB - 1) / PW_NB;
   const int64_t i0 = (int64_t)(blockIdx.x / nkg) * PW_ROWS;
   const int kb0 = (blockIdx.x % nkg) * PW_NB;
@@ -234,9 +242,23 @@ __global__ __launch_bounds__(PW_NT) void prep_w_fp6(GemvArgs p, unsigned char* w
     const int64_t i = i0 + r;
     const int kb = kb0 + bl;
     if (i >= (int64_t)L.nit * F6_TI || kb >= L.nsteps * F6_KB) continue;
-    uint32_t code[32];
+    uint32_t code[32], code2[32];   // code2: q8_0's lo plane
     uint32_t d = 0, mv = 0;
-    if (i < p.M && kb < p.nblk) {
+    if (T == kQ8_0 && i < p.M && kb < p.nblk) {
+      uint32_t m[9];
+      const int bo = bl * F::ABPB;
+      const uint32_t* src = &raw[r * SEGW + (bo >> 2)];
+      const int sh = (bo & 3) * 8;
+#pragma unroll
+      for (int q = 0; q < 9; ++q) m[q] = __builtin_amdgcn_alignbit(src[q + 1], src[q], sh);
+      d = m[0] & 0xffffu;
+#pragma unroll
+      for (int e = 0; e < 32; ++e) {
+        const int q = (int)(int8_t)((m[(2 + e) >> 2] >> (8 * ((2 + e) & 3))) & 0xffu);
+        code[e] = sm_code(q >> 4);          // h = floor(q / 16) in [-8, 7]
+        code2[e] = (uint32_t)(q & 15);      // l in [0, 15]
+      }
+    } else if (T != kQ8_0 && i < p.M && kb < p.nblk) {
       constexpr int NW = (F::ABPB + 3) / 4;
       uint32_t m[NW];
       const int bo = bl * F::ABPB;
@@ -271,15 +293,20 @@ __global__ __launch_bounds__(PW_NT) void prep_w_fp6(GemvArgs p, unsigned char* w
       }
     } else {
 #pragma unroll
-      for (int e = 0; e < 32; ++e) code[e] = 0;
+      for (int e = 0; e < 32; ++e) code[e] = code2[e] = 0;
     }
     uint32_t o[6];
     pack_fp6(code, o);
     const int it = (int)(i / F6_TI), rr = (int)(i % F6_TI);
-    unsigned char* ch = ws + (int64_t)a * L.a_slice + ((int64_t)it * L.nsteps + kb / F6_KB) * F6_A_BYTES;
+    unsigned char* ch = ws + (int64_t)a * L.a_slice + ((int64_t)it * L.nsteps + kb / F6_KB) * (F6_A_BYTES * F::WP);
     const int b = kb % F6_KB;
     *(u32x4*)(ch + f6_aoff(0, b, rr)) = u32x4{o[0], o[1], o[2], o[3]};
     *(u32x4*)(ch + f6_aoff(1, b, rr)) = u32x4{o[4], o[5], d, mv};
+    if constexpr (F::WP == 2) {   // the lo plane: the second half of the K-step's chunk
+      pack_fp6(code2, o);
+      *(u32x4*)(ch + F6_A_BYTES + f6_aoff(0, b, rr)) = u32x4{o[0], o[1], o[2], o[3]};
+      *(u32x4*)(ch + F6_A_BYTES + f6_aoff(1, b, rr)) = u32x4{o[4], o[5], d, mv};
+    }
   }
 }
 
@@ -966,13 +993,15 @@ __global__ __launch_bounds__(512) void gemm_fp6_kv_kernel(GemvArgs p, const unsi
                                                           const unsigned char* wsB) {
   using F = F6<T>;
   constexpr bool AFF = F::AFF;
+  constexpr int WP = F::WP;   // weight code planes (q8_0: hi, lo)
   constexpr int KG = 4, TI = 128, TJ = 64, NW = 8, WJ = 2, UPB = 2 * WJ;
-  constexpr int LPB = 2 + 2 * WJ;   // vmem ops per block: 2 weight DMA pieces, WJ x 2 activation loads
-  constexpr int RING = P * 2 * F6_PIECE;   // bytes of a wave's weight ring
+  constexpr int LPB = 2 * WP + 2 * WJ;   // vmem ops per block: 2 weight DMA pieces per plane, WJ x 2 activation loads
+  constexpr int RING = P * 2 * WP * F6_PIECE;   // bytes of a wave's weight ring
+  constexpr int ABY = WP * F6_A_BYTES;          // bytes of a K-step's A chunk
   static_assert(P >= 2 && P <= 6, "blocks in flight");
   static_assert(NW * RING <= 4 * 64 * (128 + 8) * 4, "the rings live under the epilogue's LDS");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const F6Layout L = F6Layout::of(p);
+  const F6Layout L = F6Layout::of(p, WP);
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int lr = lane & 31, h = lane >> 5;
@@ -993,11 +1022,11 @@ __global__ __launch_bounds__(512) void gemm_fp6_kv_kernel(GemvArgs p, const unsi
   const int it = ti / 2, jt = tj / 2, ri0 = (ti % 2) * TI, rj0 = (tj % 2) * TJ;
   const int i12 = z % p.ne12, i13 = z / p.ne12;
   const int ne02 = p.ne12 / p.r2, a = (i12 / p.r2) + (i13 / p.r3) * ne02;
-  const unsigned char* wa = wsA + (int64_t)a * L.a_slice + (int64_t)it * L.nsteps * F6_A_BYTES;
+  const unsigned char* wa = wsA + (int64_t)a * L.a_slice + (int64_t)it * L.nsteps * ABY;
   const unsigned char* wb = wsB + (int64_t)z * L.b_slice + (int64_t)jt * L.nsteps * F6_B_BYTES;
   const int nsteps = L.nsteps;
   const int nbw = nsteps > g ? (nsteps - g + KG - 1) / KG * F6_KB : 0;   // this wave's blocks
-  const auto ra = make_rsrc(wa, (uint32_t)(nsteps * F6_A_BYTES));
+  const auto ra = make_rsrc(wa, (uint32_t)(nsteps * ABY));
   const auto rb = make_rsrc(wb, (uint32_t)(nsteps * F6_B_BYTES));
   const int a0 = (ri0 + 64 * wi) * 16;                         // f6_aoff(0, 0, first row)
   const uint32_t b0 = (uint32_t)(h * F6_TJ + rj0 + lr) * 16;   // f6_boff(0, 0, h, row)
@@ -1010,11 +1039,12 @@ __global__ __launch_bounds__(512) void gemm_fp6_kv_kernel(GemvArgs p, const unsi
     constexpr int S = decltype(S_)::value;
     const int uu = min(u, nbw - 1);
     const int ks = g + KG * (uu / F6_KB), b = uu % F6_KB;
-    const int ka = ks * F6_A_BYTES, kb = ks * F6_B_BYTES;
+    const int ka = ks * ABY, kb = ks * F6_B_BYTES;
 #pragma unroll
-    for (int pl = 0; pl < 2; ++pl) {
-      auto* d = (__attribute__((address_space(3))) void*)(ring + (S * 2 + pl) * F6_PIECE);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, d, 16, lane * 16, ka + a0 + (pl * F6_KB + b) * F6_TI * 16, 0, 0);
+    for (int pl = 0; pl < 2 * WP; ++pl) {   // (code plane pl / 2) x (16-byte plane pl % 2)
+      auto* d = (__attribute__((address_space(3))) void*)(ring + (S * 2 * WP + pl) * F6_PIECE);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, d, 16, lane * 16,
+                                               ka + (pl / 2) * F6_A_BYTES + a0 + ((pl % 2) * F6_KB + b) * F6_TI * 16, 0, 0);
     }
 #pragma unroll
     for (int x = 0; x < WJ; ++x)
@@ -1050,10 +1080,10 @@ __global__ __launch_bounds__(512) void gemm_fp6_kv_kernel(GemvArgs p, const unsi
 
   // a block's weight fragments from its ring slot: per sub-tile y (rows 32 y + lr in both half-waves)
   // the scale MFMA's six code dwords and the f16 MFMA's {d, m} pair
-  struct WFrag { i32x8 c[2]; i32x2 d[2]; };
+  struct WFrag { i32x8 c[2]; i32x2 d[2]; i32x8 c2[WP == 2 ? 2 : 1]; };   // c2: q8_0's lo codes
   const int lo = (32 * 0 + lr) * 16;
   auto wread = [&](int slot, WFrag& f) {
-    const unsigned char* r0 = ring + slot * 2 * F6_PIECE;
+    const unsigned char* r0 = ring + slot * 2 * WP * F6_PIECE;
 #pragma unroll
     for (int y = 0; y < 2; ++y) {
       const int o = lo + 32 * y * 16;
@@ -1061,6 +1091,11 @@ __global__ __launch_bounds__(512) void gemm_fp6_kv_kernel(GemvArgs p, const unsi
       const i32x4 q1 = *reinterpret_cast<const i32x4*>(r0 + F6_PIECE + o);
       f.d[y] = i32x2{q1[2], q1[3]};
       f.c[y] = i32x8{q0[0], q0[1], q0[2], q0[3], q1[0], q1[1], 0, 0};
+      if constexpr (WP == 2) {
+        const i32x4 q2 = *reinterpret_cast<const i32x4*>(r0 + 2 * F6_PIECE + o);
+        const i32x4 q3 = *reinterpret_cast<const i32x4*>(r0 + 3 * F6_PIECE + o);
+        f.c2[y] = i32x8{q2[0], q2[1], q2[2], q2[3], q3[0], q3[1], 0, 0};
+      }
     }
   };
   WFrag wc;   // the current block's weight fragments (read during the block before)
@@ -1087,8 +1122,14 @@ __global__ __launch_bounds__(512) void gemm_fp6_kv_kernel(GemvArgs p, const unsi
     // cycles in the matrix pipe covered by 8 FMAs (32 issue cycles) of the unit before
     auto mfma_s = [&](int n, F6Res& R) {
       const int x = (n / 2) % WJ, y = n & 1;
-      R.s = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(codes(rb_[S][x][0], rb_[S][x][1]), wc.c[y], fz, 2, 2, 0,
-                                                            sc_a, 0, SCALE_W);
+      if constexpr (WP == 2) {   // q8_0: S = sum 16 h b (hi codes, weight scale x16) + sum l b
+        const i32x8 bc = codes(rb_[S][x][0], rb_[S][x][1]);
+        R.s = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(bc, wc.c[y], fz, 2, 2, 0, sc_a, 0, SCALE_W + 4);
+        R.s = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(bc, wc.c2[y], R.s, 2, 2, 0, sc_a, 0, SCALE_W);
+      } else {
+        R.s = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(codes(rb_[S][x][0], rb_[S][x][1]), wc.c[y], fz, 2, 2, 0,
+                                                              sc_a, 0, SCALE_W);
+      }
     };
     auto mfma_p = [&](int n, F6Res& R) {
       const int x = (n / 2) % WJ, y = n & 1;
@@ -1393,11 +1434,14 @@ hipError_t launch_fp6_t(const GemvArgs& p, const void* prepA, void* ws, hipStrea
 #endif
   if (plan.sub == 1 && knobs().fp6_av) {   // LAMM_FP6_AV=0: the LDS-staged form below
     constexpr size_t lds = (size_t)4 * 64 * (128 + 8) * 4;   // the epilogue's parked tiles
-    auto kern = gemm_fp6_kv_kernel<T, F6<T>::AFF ? 2 : 3>;   // more in flight spills
+    auto kern = gemm_fp6_kv_kernel<T, F6<T>::AFF || F6<T>::WP == 2 ? 2 : 3>;   // more in flight spills
     set_max_lds((const void*)kern, (int)lds);
     hipLaunchKernelGGL(kern, dim3((unsigned)plan.grid), dim3(512), lds, s, p, kA, static_cast<const unsigned char*>(wsB));
     return hipGetLastError();
   }
+  if constexpr (F6<T>::WP == 2) {
+    return hipErrorInvalidValue;   // q8_0: the K-group plan only (f6_kv_plan)
+  } else {
   if (plan.sub == 1) {
     using WK = F6Waves<2, 2, 2, 4>;
 #ifdef LAMM_AB_VARIANTS
@@ -1452,11 +1496,19 @@ hipError_t launch_fp6_t(const GemvArgs& p, const void* prepA, void* ws, hipStrea
   }
   if (nsplit > 1 && !ctr) launch_splitk_reduce(p, nsplit, part, s);
   return hipGetLastError();
+  }
 }
 
 }  // namespace
 
-bool gemm_fp6_supported(int type) { return type == kQ4_0 || type == kQ4_1 || type == kQ5_0 || type == kQ5_1; }
+bool gemm_fp6_kv_plan(const GemvArgs& p) {
+  const F6Plan plan = f6_plan(p, F6Layout::of(p));
+  return plan.sub == 1 && knobs().fp6_av;
+}
+
+bool gemm_fp6_supported(int type) {
+  return type == kQ4_0 || type == kQ4_1 || type == kQ5_0 || type == kQ5_1 || type == kQ8_0;
+}
 
 int gemm_fp6_tiles(const GemvArgs& p) {
   const F6Layout L = F6Layout::of(p);
@@ -1469,8 +1521,7 @@ int gemm_fp6_grid(const GemvArgs& p) {
 }
 
 size_t gemm_fp6_workspace_bytes(int type, const GemvArgs& p, bool prepared) {
-  (void)type;
-  const F6Layout L = F6Layout::of(p);
+  const F6Layout L = F6Layout::of(p, type == kQ8_0 ? 2 : 1);
   const int nsplit = f6_nsplit(p, L);
   // split-K partials: C-shaped for f6_reduce, or whole 256 x 128 tiles for the in-launch fixup
   const size_t tiles = (size_t)L.nit * L.njt * p.ne12 * p.ne13;
@@ -1480,8 +1531,7 @@ size_t gemm_fp6_workspace_bytes(int type, const GemvArgs& p, bool prepared) {
 }
 
 size_t gemm_fp6_weight_bytes(int type, const GemvArgs& p) {
-  (void)type;
-  return (size_t)F6Layout::of(p).a_bytes;
+  return (size_t)F6Layout::of(p, type == kQ8_0 ? 2 : 1).a_bytes;
 }
 
 hipError_t prepare_fp6_weights(int type, const GemvArgs& p, void* wsA, hipStream_t s, bool* in_range) {
@@ -1491,6 +1541,7 @@ hipError_t prepare_fp6_weights(int type, const GemvArgs& p, void* wsA, hipStream
     case kQ4_0: launch_prep_w<kQ4_0>(p, w, s); break;
     case kQ4_1: launch_prep_w<kQ4_1>(p, w, s); break;
     case kQ5_0: launch_prep_w<kQ5_0>(p, w, s); break;
+    case kQ8_0: launch_prep_w<kQ8_0>(p, w, s); break;
     case kQ5_1: {   // reports block scales past 16 d's f16 range (the packed form is then unusable)
       unsigned* flag = nullptr;
       if (hipMalloc(&flag, sizeof(unsigned)) != hipSuccess) return hipErrorOutOfMemory;
@@ -1519,6 +1570,9 @@ hipError_t launch_gemm_fp6(int type, const GemvArgs& p, const void* prepA, void*
     case kQ5_1:   // prepared (range-checked) weights only: the per-call form has no range check
       if (!prepA) return hipErrorInvalidValue;
       return launch_fp6_t<kQ5_1>(p, prepA, ws, s);
+    case kQ8_0:   // prepared weights (the two code planes) and the K-group plan only
+      if (!prepA || !gemm_fp6_kv_plan(p)) return hipErrorInvalidValue;
+      return launch_fp6_t<kQ8_0>(p, prepA, ws, s);
     default: return hipErrorInvalidValue;
   }
 }

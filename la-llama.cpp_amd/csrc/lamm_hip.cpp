@@ -213,7 +213,9 @@ constexpr int kDqMinTiles = 128;
 bool use_dq(int type, const GemvArgs& p, bool stationary) {
   if (!gemm_dq_supported(type) || !gemm_dq_args_ok(p)) return false;
   if (knobs().gemm_path == 2) return true;
-  return knobs().gemm_path < 0 && ((type == kQ5_1 && !stationary) || type == kQ8_0) &&
+  // q8_0 with prepared weights on the K-group plan: the exact fp6 engine's two-plane form (round 6)
+  const bool q8_fp6 = type == kQ8_0 && stationary && gemm_fp6_kv_plan(p);
+  return knobs().gemm_path < 0 && ((type == kQ5_1 && !stationary) || (type == kQ8_0 && !q8_fp6)) &&
          gemm_dq_tiles(p) >= kDqMinTiles;
 }
 Engine pick_engine(int type, const GemvArgs& p, bool stationary, bool b_al4) {
@@ -221,7 +223,9 @@ Engine pick_engine(int type, const GemvArgs& p, bool stationary, bool b_al4) {
   if (gemm_dense_supported(type) && knobs().dense_gemm) return kEngDense;
   if (gemm_kq_supported(type) && knobs().kq_gemm && b_al4) return kEngKq;
   if (use_dq(type, p, stationary)) return kEngDq;
-  if (gemm_fp6_supported(type) && (type != kQ5_1 || stationary) && gemm_path(p, stationary) == 0) return kEngFp6;
+  if (gemm_fp6_supported(type) && (type != kQ5_1 || stationary) && gemm_path(p, stationary) == 0 &&
+      (type != kQ8_0 || (stationary && gemm_fp6_kv_plan(p))))
+    return kEngFp6;
   if (gemm_supported(type) && gemm_args_ok(type, p)) return kEngI8;
   return kEngGemvGroups;
 }

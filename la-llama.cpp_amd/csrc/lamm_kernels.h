@@ -111,7 +111,10 @@ size_t gemm_fp6_workspace_bytes(int type, const GemvArgs& p, bool prepared);
 size_t gemm_fp6_weight_bytes(int type, const GemvArgs& p);
 // in_range (q5_1): false when a block scale is past what the packed form holds (use dq16)
 hipError_t prepare_fp6_weights(int type, const GemvArgs& p, void* wsA, hipStream_t s, bool* in_range = nullptr);
-bool gemm_fp6_supported(int type);
+bool gemm_fp6_supported(int type);   // q4_0 / q4_1 / q5_0 / q5_1 / q8_0 (q5_1, q8_0: prepared weights only)
+// the call runs on the 128 x 64 K-group plan (gemm_fp6_kv_kernel) -- the only one q8_0's two weight
+// code planes have
+bool gemm_fp6_kv_plan(const GemvArgs& p);
 int gemm_fp6_tiles(const GemvArgs& p);   // 256x128 output tiles of the fp6 GEMM (before K-splits)
 int gemm_fp6_grid(const GemvArgs& p);    // its main-kernel workgroups (tiles x K-splits)
 

@@ -665,7 +665,7 @@ def test_weights_stationary_matches_per_call(t, monkeypatch):
     B = dev_bytes(np.concatenate([np.ascontiguousarray(b).view(np.uint8).reshape(-1)[:bbytes] for b in Bs]))
     bt = la.Batch(2, 1, 4, 1, abytes, 2 * abytes, bbytes, 4 * bbytes, 4 * M * N, 4 * M * N * 4)
     W = la.Weights(t, A, M, K, lda=lda, ne02=2, ne03=1, nba2=abytes, nba3=2 * abytes)
-    assert (W.packed_bytes > 0) == (t in FP6_TYPES)
+    assert (W.packed_bytes > 0) == (t in FP6_TYPES or t == ol.Q8_0)   # (q8_0: two code planes, round 6)
     for n in (N, 3):   # GEMM and GEMV
         C0 = torch.full((4 * n * M,), float("nan"), dtype=torch.float32, device="cuda")
         C1 = torch.full_like(C0, float("nan"))

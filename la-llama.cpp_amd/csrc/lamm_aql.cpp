@@ -352,8 +352,9 @@ class Aql {
     hsa_kernel_dispatch_packet_t* p = packet(pend_idx_);
     if (last) hsa_signal_add_relaxed(done_, 1);
     p->completion_signal = last ? done_ : hsa_signal_t{0};
-    const uint32_t acq = pend_first_ ? HSA_FENCE_SCOPE_SYSTEM : HSA_FENCE_SCOPE_AGENT;
-    const uint32_t rel = last ? HSA_FENCE_SCOPE_SYSTEM : HSA_FENCE_SCOPE_AGENT;
+    const uint32_t inner = knobs().aql_fence_none ? HSA_FENCE_SCOPE_NONE : HSA_FENCE_SCOPE_AGENT;
+    const uint32_t acq = pend_first_ ? HSA_FENCE_SCOPE_SYSTEM : inner;
+    const uint32_t rel = last ? HSA_FENCE_SCOPE_SYSTEM : inner;
     const uint16_t header = (uint16_t)((HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
                                        (1u << HSA_PACKET_HEADER_BARRIER) | (acq << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
                                        (rel << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));

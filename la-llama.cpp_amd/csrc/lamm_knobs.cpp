@@ -63,6 +63,10 @@ Knobs* read_env() {
   k->direct = env_on("LAMM_HIP_DIRECT");
   k->aql_host_karg = env_on("LAMM_AQL_HOSTKARG");
   k->aql_eager = !env_off("LAMM_AQL_EAGER");
+  {
+    const char* f = getenv("LAMM_AQL_FENCE");
+    k->aql_fence_none = f && !strcmp(f, "none");
+  }
   k->vram_x = !env_off("LAMM_HIP_VRAM_X");
   k->signal_write = env_on("LAMM_HIP_SIGNAL_WRITE");
   k->siblings = !env_off("LAMM_HIP_SIBLINGS");

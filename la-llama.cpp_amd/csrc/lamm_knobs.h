@@ -61,6 +61,8 @@ struct Knobs {
   int ref_gemv_bpt = 2;        // LAMM_REF_GEMV_BPT: blocks per producer thread of ref_gemv_kernel (2: 512
                                // threads per workgroup, 4: 256)
   bool aql_eager = true;       // LAMM_AQL_EAGER=0: direct-dispatch packets held until the next call (round 5)
+  bool aql_fence_none = false; // LAMM_AQL_FENCE=none: a region's inner packets carry no acquire / release fence
+                               // (probe: what the agent-scope fences between back-to-back kernels cost)
   bool ref_order = false;      // LAMM_HIP_ORDER=reference: the boundary computes in the reference's own float
                                // order (lamm_ref.hip, bit-identical to the lamm opt-3 AVX2 build) instead of
                                // the fast engines (the default since round 6: within the north star's 1e-3

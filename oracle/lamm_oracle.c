@@ -642,8 +642,9 @@ void lo_mul_mat(int type, int M, int N, int K, const void *A, size_t lda_bytes,
 
 /* --------------------------------------------------------- the AVX2 float order
  * The reference's CPU path on x86 (the lamm opt-3 AVX2 kernels, src/lamm_kernel_q*.hpp
- * lamm_simd_block_kernel / lamm_simd_kernel with src/lamm_simd_avx2.h; for q6_K, which lamm
- * declines, ggml's AVX2 ggml_vec_dot_q6_K_q8_K, LC/ggml-quants.c:8305-8385) keeps EIGHT fp32
+ * lamm_simd_block_kernel / lamm_simd_kernel with src/lamm_simd_avx2.h, q2_K among them; for q4_K /
+ * q5_K / q6_K, which lamm declines, ggml's AVX2 ggml_vec_dot_q*_K_q8_K, LC/ggml-quants.c:7082-7145,
+ * :7696-7777, :8305-8385 -- their min terms are restated beside the lanes below) keeps EIGHT fp32
  * accumulators per output -- one per 32-bit lane of an __m256 -- and for every block / super-block
  * adds d * (float)X_l into lane l with a fused multiply-add (_mm256_fmadd_ps), where X_l is the
  * exact int32 sum of the 4 products (block formats: elements 4l..4l+3, through
@@ -725,6 +726,68 @@ float lo_vec_dot_avx(int type, int k, const void *va, const void *vb) {
       for (int l = 0; l < 8; ++l) acc[l] = fmaf(d, (float)X[l], acc[l]);
     }
     return tree8(acc);
+  }
+  if (type == LO_Q2_K) {
+    /* lamm's AVX2 q2_K block kernel (src/lamm_kernel_q2_k.hpp:163-307, the opt-3 tier's kernel for
+     * every tile, src/lamm_impl.hpp:124-143): per super-block, lane l of sumi is the exact int sum over
+     * the 8 32-element groups h of (scale nibble sc[2h + (l >= 4)]) * (the 4-element dot of q2 (0..3)
+     * and q8 at positions 4l .. 4l+3 of group h) -- maddubs pairs, madd_epi16 with the shuffled
+     * scales (:212-233); lane l of prod is mins[2l] bsums[2l] + mins[2l+1] bsums[2l+1] (madd_epi16,
+     * :247); then acc = fma(fp32(d_a) * d_b, sumi, acc) and acc = fma(-fp32(dmin_a) * d_b, prod, acc)
+     * (:245-248), in that order; reduce_sum's tree at the end */
+    for (int i = 0; i < k / 256; ++i, a += ab, b += bb) {
+      float yd; memcpy(&yd, b, 4);
+      const int8_t *q8 = (const int8_t *)(b + 4);
+      const float d1 = H2F(rd16(a + 80)) * yd;
+      const float d2 = -H2F(rd16(a + 82)) * yd;
+      int32_t X[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (int h = 0; h < 8; ++h)          /* group h: elements 32 h .. 32 h + 31 */
+        for (int e = 0; e < 32; ++e) {
+          const int q = (a[16 + 32 * (h / 4) + e] >> (2 * (h % 4))) & 3;
+          X[e / 4] += (a[2 * h + (e >= 16)] & 0xF) * q * q8[32 * h + e];
+        }
+      for (int l = 0; l < 8; ++l) {
+        int16_t s0, s1;
+        memcpy(&s0, b + 260 + 4 * l, 2);
+        memcpy(&s1, b + 262 + 4 * l, 2);
+        const int32_t Y = (a[2 * l] >> 4) * s0 + (a[2 * l + 1] >> 4) * s1;
+        acc[l] = fmaf(d1, (float)X[l], acc[l]);
+        acc[l] = fmaf(d2, (float)Y, acc[l]);
+      }
+    }
+    return tree8(acc);
+  }
+  if (type == LO_Q4_K || type == LO_Q5_K) {
+    /* ggml's AVX2 ggml_vec_dot_q4_K_q8_K (LC/ggml-quants.c:7082-7145) / q5_K (:7696-7777), which lamm
+     * declines: per super-block lane l of sumi = sum over the 8 32-element groups g of sc[g] * (the
+     * 4-element dot at positions 4l .. 4l+3 of group g), acc_l = fma(d_b * fp32(d_a), sumi_l, acc_l);
+     * the mins: q8s = hadd(bsums) (pairs), prod_k = mn[2k] q8s[2k] + mn[2k+1] q8s[2k+1] (k = 0..3);
+     * q4_K keeps them in a 4-lane fma chain reduced (m0 + m2) + (m1 + m3), q5_K adds dmin * (the int
+     * sum of the four) into a scalar per super-block (product and sum rounded separately);
+     * then hsum_float_8(acc) + that */
+    float acc_m[4] = {0, 0, 0, 0}, summs = 0.0f;
+    for (int i = 0; i < k / 256; ++i, a += ab, b += bb) {
+      float yd; memcpy(&yd, b, 4);
+      const int8_t *q8 = (const int8_t *)(b + 4);
+      const float d = yd * H2F(rd16(a)), dmin = -yd * H2F(rd16(a + 2));
+      uint8_t sc[8], mn[8];
+      kq_scale_min(a + 4, sc, mn);
+      int16_t bs[16];
+      memcpy(bs, b + 260, 32);
+      int32_t prod[4];
+      for (int q = 0; q < 4; ++q)
+        prod[q] = mn[2 * q] * (int16_t)(bs[4 * q] + bs[4 * q + 1]) + mn[2 * q + 1] * (int16_t)(bs[4 * q + 2] + bs[4 * q + 3]);
+      if (type == LO_Q4_K) {
+        for (int q = 0; q < 4; ++q) acc_m[q] = fmaf(dmin, (float)prod[q], acc_m[q]);
+      } else {
+        summs = summs + dmin * (float)((prod[0] + prod[1]) + (prod[2] + prod[3]));
+      }
+      int32_t X[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (int e = 0; e < 256; ++e) X[(e % 32) / 4] += sc[e / 32] * kq_nibble(a, type, e) * q8[e];
+      for (int l = 0; l < 8; ++l) acc[l] = fmaf(d, (float)X[l], acc[l]);
+    }
+    if (type == LO_Q4_K) return tree8(acc) + ((acc_m[0] + acc_m[2]) + (acc_m[1] + acc_m[3]));
+    return tree8(acc) + summs;
   }
   if (type != LO_Q4_0 && type != LO_Q4_1 && type != LO_Q5_0 && type != LO_Q5_1) return 0.0f;
   const int aff = type == LO_Q4_1 || type == LO_Q5_1;

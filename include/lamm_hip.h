@@ -108,11 +108,13 @@ int lamm_hip_matmul_batched(const lamm_matrix *A, const lamm_matrix *B, const la
 
 /* lamm_hip_matmul_batched with flags.  LAMM_ORDER_REFERENCE: compute every output in the
  * reference's own x86 float order -- the lamm opt-3 AVX2 kernels' eight fp32 FMA lanes per output
- * and reduce_sum's tree (src/lamm_kernel_q4_0.hpp:59-128, src/lamm_simd_avx2.h:117-127), ggml's
- * AVX2 ggml_vec_dot_q6_K_q8_K for q6_K (LC/ggml-quants.c:8305-8385) -- so C is bit-identical to
- * the reference's CPU build on the same blocks (VALU kernels, slower than the default engines).
- * Supported: q4_0 / q5_0 with q8_0 B, q4_1 / q5_1 with q8_1 B, q6_K with q8_K B (quantized B
- * only); others return LAMM_ERR_TYPE.  The ggml boundary uses it under LAMM_HIP_ORDER=reference (its
+ * and reduce_sum's tree (src/lamm_kernel_q4_0.hpp:59-128, src/lamm_simd_avx2.h:117-127; q2_K's
+ * block kernel src/lamm_kernel_q2_k.hpp:163-307 with its mins term), ggml's AVX2
+ * ggml_vec_dot_q{4,5,6}_K_q8_K for q4_K / q5_K / q6_K (LC/ggml-quants.c:7082-7145, :7696-7777,
+ * :8305-8385) -- so C is bit-identical to the reference's CPU build on the same blocks (VALU
+ * kernels, slower than the default engines).  Supported: q4_0 / q5_0 with q8_0 B, q4_1 / q5_1 with
+ * q8_1 B, q2_K / q4_K / q5_K / q6_K with q8_K B (quantized B only); others (q8_0: SURVEY §8a
+ * defect 2's order) return LAMM_ERR_TYPE.  The ggml boundary uses it under LAMM_HIP_ORDER=reference (its
  * default until round 5; since round 6 the boundary runs the fast engines unless asked). */
 #define LAMM_ORDER_REFERENCE 1
 int lamm_hip_matmul_ex(const lamm_matrix *A, const lamm_matrix *B, const lamm_matrix *C,

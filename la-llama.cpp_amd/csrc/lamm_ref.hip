@@ -46,12 +46,19 @@ constexpr int RR = 32;           // rows per workgroup (16 for decode calls: lau
 
 template <int T> struct RefFmt;
 // BPB: A block bytes; QS / QH / M: byte offsets of the quants, the 5th bits, m (-1: none);
-// OFF: the signed-byte offset of the quants (their unsigned maximum + 1, halved); UE: elements per unit
-template <> struct RefFmt<kQ4_0> { static constexpr int BPB = 18, QS = 2, QH = -1, M = -1, OFF = 8, UE = 32, VB = 34; };
-template <> struct RefFmt<kQ4_1> { static constexpr int BPB = 20, QS = 4, QH = -1, M = 2, OFF = 0, UE = 32, VB = 36; };
-template <> struct RefFmt<kQ5_0> { static constexpr int BPB = 22, QS = 6, QH = 2, M = -1, OFF = 16, UE = 32, VB = 34; };
-template <> struct RefFmt<kQ5_1> { static constexpr int BPB = 24, QS = 8, QH = 4, M = 2, OFF = 0, UE = 32, VB = 36; };
-template <> struct RefFmt<kQ6_K> { static constexpr int BPB = 210, QS = 0, QH = 128, M = -1, OFF = 32, UE = 256, VB = 292; };
+// OFF: the signed-byte offset of the quants (their unsigned maximum + 1, halved); UE: elements per unit;
+// D / DM: byte offsets of the (super-)block's d and dmin (-1: none)
+template <> struct RefFmt<kQ4_0> { static constexpr int BPB = 18, QS = 2, QH = -1, M = -1, OFF = 8, UE = 32, VB = 34, D = 0, DM = -1; };
+template <> struct RefFmt<kQ4_1> { static constexpr int BPB = 20, QS = 4, QH = -1, M = 2, OFF = 0, UE = 32, VB = 36, D = 0, DM = -1; };
+template <> struct RefFmt<kQ5_0> { static constexpr int BPB = 22, QS = 6, QH = 2, M = -1, OFF = 16, UE = 32, VB = 34, D = 0, DM = -1; };
+template <> struct RefFmt<kQ5_1> { static constexpr int BPB = 24, QS = 8, QH = 4, M = 2, OFF = 0, UE = 32, VB = 36, D = 0, DM = -1; };
+template <> struct RefFmt<kQ6_K> { static constexpr int BPB = 210, QS = 0, QH = 128, M = -1, OFF = 32, UE = 256, VB = 292, D = 208, DM = -1; };
+// the super-block formats with mins (round 6): q2_K in lamm's AVX2 block kernel's order
+// (src/lamm_kernel_q2_k.hpp:163-307), q4_K / q5_K in ggml's AVX2 vec_dot's (LC/ggml-quants.c:7082-7145,
+// :7696-7777); their quants are unsigned (0..3 / 0..15 / 0..31), every dot4 stays exact as is
+template <> struct RefFmt<kQ2_K> { static constexpr int BPB = 84, QS = 16, QH = -1, M = -1, OFF = 0, UE = 256, VB = 292, D = 80, DM = 82; };
+template <> struct RefFmt<kQ4_K> { static constexpr int BPB = 144, QS = 16, QH = -1, M = -1, OFF = 0, UE = 256, VB = 292, D = 0, DM = 2; };
+template <> struct RefFmt<kQ5_K> { static constexpr int BPB = 176, QS = 48, QH = 16, M = -1, OFF = 0, UE = 256, VB = 292, D = 0, DM = 2; };
 
 // units of K per LDS chunk, and the dwords of quads one (column, lane, unit) holds
 template <int T> constexpr int ref_kch() { return RefFmt<T>::UE == 256 ? 8 : 64; }
@@ -85,6 +92,11 @@ __global__ __launch_bounds__(RR * 8) void ref_kernel(GemvArgs p) {
   constexpr int U = QW == 1 ? 4 : 1;                 // units per batch of LDS reads
   constexpr bool AFF = F::M >= 0;
   constexpr bool KQ = F::UE == 256;
+  // mins terms: q2_K a second fma per super-block on the lane chains (Y_l = mins[2l] bsums[2l] +
+  // mins[2l+1] bsums[2l+1]); q4_K a 4-lane fma chain of prod_q = mn[2q] q8s[2q] + mn[2q+1] q8s[2q+1]
+  // (q8s = pairwise sums of the bsums) reduced (m0 + m2) + (m1 + m3); q5_K one scalar sum of dmin * the
+  // four prods' int sum, product and sum rounded separately -- each added after the lane tree
+  constexpr bool K2 = T == kQ2_K, K45 = T == kQ4_K || T == kQ5_K, MINS = K2 || K45;
   constexpr int SEG = KCH * F::BPB;                  // bytes of a row's chunk (a multiple of 16)
   constexpr int SEGW = SEG / 4 + 1;                  // dwords per LDS row (+1: realignment reads)
   static_assert(SEG % 16 == 0, "chunks start 16-byte aligned");
@@ -92,6 +104,7 @@ __global__ __launch_bounds__(RR * 8) void ref_kernel(GemvArgs p) {
   __shared__ __attribute__((aligned(16))) uint32_t sq[NCOL * 8 * KCH * QW];   // [col][lane][unit][group]
   __shared__ __attribute__((aligned(16))) float sd[NCOL * KCH];               // d_b     [col][unit]
   __shared__ __attribute__((aligned(16))) float ss[AFF ? NCOL * KCH : 1];     // s_b (q8_1)
+  __shared__ __attribute__((aligned(16))) uint32_t sbs[MINS ? NCOL * KCH * 8 : 1];   // q8_K bsums [col][unit]
 
   const unsigned char* Az = p.A;
   const unsigned char* Bz = p.B;
@@ -116,11 +129,11 @@ __global__ __launch_bounds__(RR * 8) void ref_kernel(GemvArgs p) {
 
   // the reference's lane l of each column's __m256 accumulator: one fp32 chain per column here
   // (the 8 lanes of a row sit in 8 threads)
-  float chain[NCOL], summs[AFF ? NCOL : 1];
+  float chain[NCOL], summs[AFF || K45 ? NCOL : 1];   // K45: the mins' chain (q4_K lanes 0-3, q5_K lane 0)
 #pragma unroll
   for (int c = 0; c < NCOL; ++c) {
     chain[c] = 0.f;
-    if constexpr (AFF) summs[c] = 0.f;
+    if constexpr (AFF || K45) summs[c] = 0.f;
   }
   const uint32_t* arow = &sa[rloc * SEGW];
 
@@ -172,6 +185,14 @@ __global__ __launch_bounds__(RR * 8) void ref_kernel(GemvArgs p) {
           }
         }
         if (part == 0) sd[c * KCH + k] = ok ? __builtin_bit_cast(float, bload4(rb, base)) : 0.f;
+        if (MINS && part == 1) {   // the 16 int16 bsums (bytes 260 .. 291) as 8 dwords
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            const u32x4 v = bload16(rb, ok ? base + 260 + 16 * i : 0x7ffffff0u);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) sbs[(c * KCH + k) * 8 + 4 * i + e] = v[e];
+          }
+        }
       }
     }
     __syncthreads();
@@ -180,13 +201,50 @@ __global__ __launch_bounds__(RR * 8) void ref_kernel(GemvArgs p) {
       for (int k0 = 0; k0 < nu; k0 += U) {
         uint32_t aq[U][QW];
         int sc[U][QW];
-        float da[U], ma[U];
+        float da[U], ma[U], dm[U];
+        int mn[U][K45 ? 8 : 2];   // q2_K: this lane's two min nibbles; q4_K / q5_K: the 8 mins
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const int ub = (k0 + u) * F::BPB;   // this unit's bytes in the row's LDS image
-          da[u] = h2f(lds32(arow, ub + (KQ ? 208 : 0)) & 0xffffu);
+          da[u] = h2f(lds32(arow, ub + F::D) & 0xffffu);
           ma[u] = AFF ? h2f(lds32(arow, ub + (AFF ? F::M : 0)) & 0xffffu) : 0.f;
-          if constexpr (!KQ) {
+          dm[u] = MINS ? h2f(lds32(arow, ub + (MINS ? F::DM : 0)) & 0xffffu) : 0.f;
+          if constexpr (K2) {
+            // group h = elements 32 h ..: quants (qs[32 (h / 4) + e] >> 2 (h % 4)) & 3, scale nibble
+            // sc[2 h + (e >= 16)] (lane l: e = 4 l .. 4 l + 3)
+            const uint32_t s4[4] = {lds32(arow, ub), lds32(arow, ub + 4), lds32(arow, ub + 8), lds32(arow, ub + 12)};
+#pragma unroll
+            for (int h = 0; h < 8; ++h) {
+              const uint32_t w = lds32(arow, ub + F::QS + 32 * (h >> 2) + 4 * l);
+              static_assert(F::QH < 0 && F::OFF == 0, "q2_K: two-bit unsigned quants, no high bits");
+              aq[u][h] = to_signed<F::OFF>((w >> (2 * (h & 3))) & 0x03030303u);
+              const int si = 2 * h + (l < 4 ? 0 : 1);
+              sc[u][h] = (int)((s4[si >> 2] >> (8 * (si & 3))) & 0xfu);
+            }
+            const uint32_t mw = (s4[l >> 1] >> (16 * (l & 1))) & 0xffffu;   // bytes 2l, 2l + 1
+            mn[u][0] = (int)((mw >> 4) & 0xfu);
+            mn[u][1] = (int)((mw >> 12) & 0xfu);
+          } else if constexpr (K45) {
+            // ggml's utmp unpacking of the 12 scale bytes (LC/ggml-quants.c:7093-7098): 8 six-bit scales
+            // and mins; group h = elements 32 h ..: nibble (h odd: high) of qs[32 (h / 2) + e] (+ 16 x
+            // bit h of qh[e] for q5_K)
+            uint32_t u0 = lds32(arow, ub + 4), u1 = lds32(arow, ub + 8), u2 = lds32(arow, ub + 12), u3;
+            u3 = ((u2 >> 4) & 0x0f0f0f0fu) | (((u1 >> 6) & 0x03030303u) << 4);
+            const uint32_t uaux = u1 & 0x3f3f3f3fu;
+            u1 = (u2 & 0x0f0f0f0fu) | (((u0 >> 6) & 0x03030303u) << 4);
+            u2 = uaux;
+            u0 &= 0x3f3f3f3fu;
+            const uint32_t qh = F::QH >= 0 ? lds32(arow, ub + (F::QH >= 0 ? F::QH : 0) + 4 * l) : 0u;
+#pragma unroll
+            for (int h = 0; h < 8; ++h) {
+              const uint32_t w = lds32(arow, ub + F::QS + 32 * (h >> 1) + 4 * l);
+              uint32_t q = ((h & 1) ? w >> 4 : w) & 0x0f0f0f0fu;
+              if constexpr (F::QH >= 0) q |= ((qh >> h) & 0x01010101u) << 4;
+              aq[u][h] = to_signed<F::OFF>(q);
+              sc[u][h] = (int)((((h < 4) ? u0 : u1) >> (8 * (h & 3))) & 0xffu);
+              mn[u][h] = (int)((((h < 4) ? u2 : u3) >> (8 * (h & 3))) & 0xffu);
+            }
+          } else if constexpr (!KQ) {
             const uint32_t qw = lds32(arow, ub + F::QS + 4 * (l & 3));
             uint32_t q = l < 4 ? qw & 0x0f0f0f0fu : (qw >> 4) & 0x0f0f0f0fu;
             if constexpr (F::QH >= 0) {
@@ -215,12 +273,31 @@ __global__ __launch_bounds__(RR * 8) void ref_kernel(GemvArgs p) {
         for (int c = 0; c < NCOL; ++c) {
           uint32_t bq[U][QW];
           float db[U], sb[U];
+          int ym[U];   // q2_K: Y_l; q4_K: prod_l (lanes 0-3); q5_K: the four prods' sum
 #pragma unroll
           for (int u = 0; u < U; ++u) {
 #pragma unroll
             for (int h = 0; h < QW; ++h) bq[u][h] = sq[((c * 8 + l) * KCH + k0 + u) * QW + h];
             db[u] = sd[c * KCH + k0 + u];
             sb[u] = AFF ? ss[c * KCH + k0 + u] : 0.f;
+            ym[u] = 0;
+            if constexpr (MINS) {
+              const uint32_t* bs = &sbs[(c * KCH + k0 + u) * 8];
+              auto lo16 = [](uint32_t x) { return (int)(int16_t)(x & 0xffffu); };
+              auto hi16 = [](uint32_t x) { return (int)(int16_t)(x >> 16); };
+              if constexpr (K2) {   // madd_epi16(mins, bsums), lane l: bsums 2l, 2l + 1
+                const uint32_t w = bs[l];
+                ym[u] = mn[u][0] * lo16(w) + mn[u][1] * hi16(w);
+              } else {   // prod_q = mn[2q] (bs[4q] + bs[4q+1]) + mn[2q+1] (bs[4q+2] + bs[4q+3])
+                auto prod = [&](int q) {
+                  const uint32_t w0 = bs[2 * q], w1 = bs[2 * q + 1];
+                  return mn[u][2 * q] * (int)(int16_t)(lo16(w0) + hi16(w0)) +
+                         mn[u][2 * q + 1] * (int)(int16_t)(lo16(w1) + hi16(w1));
+                };
+                if constexpr (T == kQ4_K) ym[u] = l < 4 ? prod(l & 3) : 0;
+                else ym[u] = (prod(0) + prod(1)) + (prod(2) + prod(3));
+              }
+            }
           }
 #pragma unroll
           for (int u = 0; u < U; ++u) {
@@ -240,6 +317,22 @@ __global__ __launch_bounds__(RR * 8) void ref_kernel(GemvArgs p) {
               asm("" : "+v"(pm));
               summs[c] = summs[c] + pm;
             }
+            if constexpr (K2) {   // lamm: acc = fma(-fp32(dmin_a) * d_b, prod, acc) after the d term
+              float d2 = -dm[u] * db[u];
+              asm("" : "+v"(d2));
+              chain[c] = __builtin_fmaf(d2, (float)ym[u], chain[c]);
+            }
+            if constexpr (K45) {   // ggml: dmin = -y.d * fp32(x.dmin)
+              float d2 = -db[u] * dm[u];
+              asm("" : "+v"(d2));
+              if constexpr (T == kQ4_K) {
+                if (l < 4) summs[c] = __builtin_fmaf(d2, (float)ym[u], summs[c]);
+              } else if (l == 0) {
+                float pm = d2 * (float)ym[u];
+                asm("" : "+v"(pm));
+                summs[c] = summs[c] + pm;
+              }
+            }
           }
         }
       }
@@ -256,6 +349,12 @@ __global__ __launch_bounds__(RR * 8) void ref_kernel(GemvArgs p) {
       v = v + __shfl_down(v, 2, 8);   // lanes 0, 1: x_l + x_{l+2}
       v = v + __shfl_down(v, 1, 8);   // lane 0: (x0 + x2) + (x1 + x3)
       if constexpr (AFF) v = v + summs[c];
+      if constexpr (T == kQ4_K) {   // the mins' 4-lane chain: (m0 + m2) + (m1 + m3)
+        float m = summs[c] + __shfl_down(summs[c], 2, 8);
+        m = m + __shfl_down(m, 1, 8);
+        v = v + m;
+      }
+      if constexpr (T == kQ5_K) v = v + summs[c];
     }
     if (l == 0 && row < p.M && c < ncols) Cz[(int64_t)(n0 + c) * p.ldc + row] = v;
   }
@@ -1340,7 +1439,7 @@ bool ref_order_supported(int type, int btype) {
   switch (type) {
     case kQ4_0: case kQ5_0: return btype == kQ8_0;
     case kQ4_1: case kQ5_1: return btype == kQ8_1;
-    case kQ6_K: return btype == kQ8_K;
+    case kQ2_K: case kQ4_K: case kQ5_K: case kQ6_K: return btype == kQ8_K;
     case kF16: return btype == kF16;
     default: return false;
   }
@@ -1412,7 +1511,7 @@ hipError_t launch_ref(int type, const GemvArgs& p, hipStream_t s) {
     else hipLaunchKernelGGL((ref_mfma_kq_kernel<2, false>), gm, dim3(MNT), 0, s, p);
     return hipGetLastError();
   }
-  if (p.N > 8 && type != kQ6_K) {
+  if (p.N > 8 && type != kQ6_K && type != kQ2_K && type != kQ4_K && type != kQ5_K) {
     // ref_mfma2_kernel, 2 column groups per wave (LAMM_REF_MFMA=4: 4 groups, one wave per SIMD; =1:
     // the unpipelined ref_mfma_kernel)
     // default per format (tools/ref_ab.py, profiles/r04/ref_order/pk_fma/, profiles/r05/ref_pipe/):
@@ -1477,6 +1576,9 @@ hipError_t launch_ref(int type, const GemvArgs& p, hipStream_t s) {
     case kQ4_1: go(std::integral_constant<int, kQ4_1>{}); break;
     case kQ5_0: go(std::integral_constant<int, kQ5_0>{}); break;
     case kQ5_1: go(std::integral_constant<int, kQ5_1>{}); break;
+    case kQ2_K: go(std::integral_constant<int, kQ2_K>{}); break;
+    case kQ4_K: go(std::integral_constant<int, kQ4_K>{}); break;
+    case kQ5_K: go(std::integral_constant<int, kQ5_K>{}); break;
     case kQ6_K: go(std::integral_constant<int, kQ6_K>{}); break;
     default: return hipErrorInvalidValue;
   }

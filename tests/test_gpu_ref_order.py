@@ -1,9 +1,9 @@
 """The reference's x86 float order on the GPU (csrc/lamm_ref.hip, lamm_hip_matmul_ex with
-LAMM_ORDER_REFERENCE): BIT-EXACT against the reference's own lamm opt-3 AVX2 output (golden
+LAMM_ORDER_REFERENCE; q2_K / q4_K / q5_K since round 6): BIT-EXACT against the reference's own
+lamm opt-3 AVX2 output (golden
 C_lamm3, tools/gen_golden.py) and against the oracle's restatement of that order
 (lo_mul_mat_avx, itself pinned to C_lamm3 in tests/test_oracle_golden.py), on ragged shapes,
-strided operands and batch slices; and through the ggml boundary, which runs this order by
-default (LAMM_HIP_ORDER)."""
+strided operands and batch slices; and through the ggml boundary under LAMM_HIP_ORDER=reference."""
 import os
 
 import numpy as np
@@ -18,7 +18,7 @@ import lamm_amd as la  # noqa: E402
 from test_gpu_parity import dev_bytes, pitch_blocks, pitched_A  # noqa: E402
 
 ORACLE = ol.Oracle()
-REF_TYPES = [ol.Q4_0, ol.Q4_1, ol.Q5_0, ol.Q5_1, ol.Q6_K]
+REF_TYPES = [ol.Q4_0, ol.Q4_1, ol.Q5_0, ol.Q5_1, ol.Q2_K, ol.Q4_K, ol.Q5_K, ol.Q6_K]
 
 
 def ref_mul_mat(t, A_q, B_q, M, N, K):
@@ -36,7 +36,8 @@ def bits(x):
     return np.ascontiguousarray(x, dtype=np.float32).view(np.uint32)
 
 
-GOLD = [p for p in fixture_paths() if p.rsplit("/", 1)[-1].rsplit("_", 1)[0] in ("q4_0", "q4_1", "q5_0", "q5_1", "q6_k")]
+GOLD = [p for p in fixture_paths()
+        if p.rsplit("/", 1)[-1].rsplit("_", 1)[0] in ("q4_0", "q4_1", "q5_0", "q5_1", "q2_k", "q4_k", "q5_k", "q6_k")]
 
 
 @pytest.mark.parametrize("path", GOLD, ids=[p.rsplit("/", 1)[-1][:-4] for p in GOLD])
@@ -46,7 +47,7 @@ def test_reference_order_matches_lamm3_golden(path):
     z = load_fixture(path)
     t, M, N, K = int(z["type"]), int(z["M"]), int(z["N"]), int(z["K"])
     c = ref_mul_mat(t, z["A_q"], z["B_avx"], M, N, K)[:N * M].reshape(N, M)
-    done = M if t == ol.Q6_K else 4 * (M // 4)
+    done = M if t in (ol.Q4_K, ol.Q5_K, ol.Q6_K) else 4 * (M // 4)   # ggml's own loop: every row
     assert np.array_equal(bits(c[:, :done]), bits(z["C_lamm3"][:, :done]))
 
 
@@ -59,7 +60,7 @@ SHAPES = [(1, 1, 256), (17, 3, 512), (31, 9, 768), (67, 1, 4096), (33, 18, 4096)
 def random_blocks(t, M, N, K, seed):
     rng = np.random.default_rng(seed)
     vt = la.vec_dot_type(t)
-    if t == ol.Q6_K:
+    if t in (ol.Q4_K, ol.Q5_K, ol.Q6_K):
         A_q = ol.random_kq_blocks(t, M, K, rng)
     else:
         A_q = ORACLE.quantize(t, rng.standard_normal((M, K), dtype=np.float32), ol.QUANT_REF)
@@ -80,7 +81,7 @@ def test_reference_order_vs_oracle_bit_exact(t, shape):
     assert np.array_equal(bits(c), bits(want)), f"{(c != want).sum()} of {c.size} differ"
 
 
-@pytest.mark.parametrize("t", [ol.Q4_0, ol.Q6_K], ids=["q4_0", "q6_k"])
+@pytest.mark.parametrize("t", [ol.Q4_0, ol.Q2_K, ol.Q4_K, ol.Q5_K, ol.Q6_K], ids=["q4_0", "q2_k", "q4_k", "q5_k", "q6_k"])
 def test_reference_order_strides_and_slices(t):
     """Pitched A rows, ldc > M, and 3 x 2 batch slices broadcasting one A slice over 3 B slices
     (ggml's r2 = ne12 / ne02): every slice bit-exact."""
@@ -220,8 +221,11 @@ def test_reference_order_f16_vs_oracle(shape):
 
 
 def test_reference_order_rejects_other_types():
+    """q8_0: lamm's AVX2 q8_0 kernel is SURVEY §8a defect 2 (signed weights through maddubs), an
+    order not worth reproducing -- the reference-order flag refuses it (the boundary then keeps the
+    fast engines for it)."""
     M, N, K = 16, 2, 256
-    for t, vt in ((ol.Q8_0, ol.Q8_0), (ol.Q2_K, ol.Q8_K), (ol.Q4_K, ol.Q8_K)):
+    for t, vt in ((ol.Q8_0, ol.Q8_0),):
         A = torch.zeros(M * la.row_bytes(t, K) + 64, dtype=torch.uint8, device="cuda")
         B = torch.zeros(N * la.row_bytes(vt, K) + 64, dtype=torch.uint8, device="cuda")
         C = torch.zeros(N * M, dtype=torch.float32, device="cuda")
@@ -245,6 +249,25 @@ def test_reference_order_prefill_kernels_bit_exact(variant, t, shape, monkeypatc
     c = ref_mul_mat(t, A_q, B_q, M, N, K)[:N * M].reshape(N, M)
     want = ORACLE.mul_mat_avx(t, M, N, K, A_q, B_q)
     assert np.array_equal(bits(c), bits(want)), f"{(c != want).sum()} of {c.size} differ"
+
+
+KQ_REF = [ol.Q2_K, ol.Q4_K, ol.Q5_K]
+
+
+@pytest.mark.parametrize("t", KQ_REF, ids=[ol.NAMES[t] for t in KQ_REF])
+@pytest.mark.parametrize("shape", [(300, 64, 1024), (4096, 32, 4096)], ids=["300x64x1024", "4096x32x4096"])
+def test_reference_order_kquants_prefill_bit_exact(t, shape):
+    """q2_K (lamm's AVX2 block kernel) / q4_K / q5_K (ggml's AVX2 vec_dot) at prefill-sized N through
+    ref_kernel's 8-column tiles: sampled rows bit for bit against the oracle's restatement."""
+    M, N, K = shape
+    A_q, B_q = random_blocks(t, M, N, K, seed=M + N + K + t)
+    c = ref_mul_mat(t, A_q, B_q, M, N, K)[:N * M].reshape(N, M)
+    rows = np.unique(np.r_[np.random.default_rng(M).choice(M, 64, replace=False), [0, M - 1]])
+    arow = la.row_bytes(t, K)
+    A_s = np.concatenate([A_q[r * arow:(r + 1) * arow] for r in rows])
+    want = ORACLE.mul_mat_avx(t, len(rows), N, K, A_s, B_q)
+    got = c[:, rows]
+    assert np.array_equal(bits(got), bits(want)), f"{(got != want).sum()} of {got.size} differ"
 
 
 FULL_SHAPES = [(4096, 512, 4096), (11008, 512, 4096)]

@@ -988,14 +988,18 @@ __global__ __launch_bounds__((F6Waves<WJ, SI, SJ, KG>::NT)) void gemm_fp6_kernel
 // operands (scale MFMA / f16 MFMA), assembled from the two 16-byte planes at use.
 // AB (ablations, tools/prep_probe.hip only): 1 loads only; 2 compute only (no loads after the first
 // P blocks); 3 compute only with half the FMAs; 4 compute only, one FMA per unit.
-template <int T, int P, int AB = 0>
+// AD (probe): the weight fragments by buffer loads straight into VGPRs (both half-waves load the same
+// rows; the L1 merges the duplicate addresses) instead of the LDS-DMA ring.
+template <int T, int P, int AB = 0, int AD = 0>
 __global__ __launch_bounds__(512) void gemm_fp6_kv_kernel(GemvArgs p, const unsigned char* wsA,
                                                           const unsigned char* wsB) {
   using F = F6<T>;
   constexpr bool AFF = F::AFF;
   constexpr int WP = F::WP;   // weight code planes (q8_0: hi, lo)
   constexpr int KG = 4, TI = 128, TJ = 64, NW = 8, WJ = 2, UPB = 2 * WJ;
-  constexpr int LPB = 2 * WP + 2 * WJ;   // vmem ops per block: 2 weight DMA pieces per plane, WJ x 2 activation loads
+  // vmem ops per block: 2 weight DMA pieces per plane (AD: 2 sub-tiles x 2 loads per plane), WJ x 2
+  // activation loads
+  constexpr int LPB = (AD ? 4 * WP : 2 * WP) + 2 * WJ;
   constexpr int RING = P * 2 * WP * F6_PIECE;   // bytes of a wave's weight ring
   constexpr int ABY = WP * F6_A_BYTES;          // bytes of a K-step's A chunk
   static_assert(P >= 2 && P <= 6, "blocks in flight");
@@ -1033,6 +1037,8 @@ __global__ __launch_bounds__(512) void gemm_fp6_kv_kernel(GemvArgs p, const unsi
   unsigned char* ring = smem + w * RING;
 
   u32x4 rb_[P][WJ][2];   // activation ring: sub-tile x, plane
+  u32x4 ra_[AD ? P : 1][2][2 * WP];   // AD: weight fragments: sub-tile y, (code plane, 16-byte plane)
+  const uint32_t arow = (uint32_t)(ri0 + 64 * wi + lr) * 16;   // AD: the lane's weight row
   // block u of this wave (K-step g + KG (u / KB), block u % KB) into ring slot S; past the end the
   // last block is fetched again (unused) so every slot's wait count stays the same
   auto issue = [&](int u, auto S_) {
@@ -1040,18 +1046,40 @@ __global__ __launch_bounds__(512) void gemm_fp6_kv_kernel(GemvArgs p, const unsi
     const int uu = min(u, nbw - 1);
     const int ks = g + KG * (uu / F6_KB), b = uu % F6_KB;
     const int ka = ks * ABY, kb = ks * F6_B_BYTES;
+    if constexpr (AD) {
 #pragma unroll
-    for (int pl = 0; pl < 2 * WP; ++pl) {   // (code plane pl / 2) x (16-byte plane pl % 2)
-      auto* d = (__attribute__((address_space(3))) void*)(ring + (S * 2 * WP + pl) * F6_PIECE);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, d, 16, lane * 16,
-                                               ka + (pl / 2) * F6_A_BYTES + a0 + ((pl % 2) * F6_KB + b) * F6_TI * 16, 0, 0);
+      for (int y = 0; y < 2; ++y)
+#pragma unroll
+        for (int pl = 0; pl < 2 * WP; ++pl) {
+          const uint32_t o = arow + (uint32_t)((pl / 2) * F6_A_BYTES + ((pl % 2) * F6_KB + b) * F6_TI * 16 + 32 * y * 16);
+          // a second plane without m (all but q4_1 / q5_1): its last dword is 0, 12 bytes suffice
+          if (pl % 2 == 1 && !AFF) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b96(ra, o, ka, 0);
+            ra_[S][y][pl] = u32x4{v[0], v[1], v[2], 0u};
+          } else {
+            ra_[S][y][pl] = __builtin_amdgcn_raw_buffer_load_b128(ra, o, ka, 0);
+          }
+        }
+    } else {
+#pragma unroll
+      for (int pl = 0; pl < 2 * WP; ++pl) {   // (code plane pl / 2) x (16-byte plane pl % 2)
+        auto* d = (__attribute__((address_space(3))) void*)(ring + (S * 2 * WP + pl) * F6_PIECE);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, d, 16, lane * 16,
+                                                 ka + (pl / 2) * F6_A_BYTES + a0 + ((pl % 2) * F6_KB + b) * F6_TI * 16, 0, 0);
+      }
     }
 #pragma unroll
     for (int x = 0; x < WJ; ++x)
 #pragma unroll
-      for (int pl = 0; pl < 2; ++pl)
-        rb_[S][x][pl] = __builtin_amdgcn_raw_buffer_load_b128(
-            rb, b0 + (uint32_t)((((pl * F6_KB + b) * 2) * F6_TJ + 32 * x) * 16), kb, 0);
+      for (int pl = 0; pl < 2; ++pl) {
+        const uint32_t o = b0 + (uint32_t)((((pl * F6_KB + b) * 2) * F6_TJ + 32 * x) * 16);
+        if (AD && pl == 1 && F::VBPB != 36) {   // q8_0 activations: no s, the plane's last dword is 0
+          const auto v = __builtin_amdgcn_raw_buffer_load_b96(rb, o, kb, 0);
+          rb_[S][x][pl] = u32x4{v[0], v[1], v[2], 0u};
+        } else {
+          rb_[S][x][pl] = __builtin_amdgcn_raw_buffer_load_b128(rb, o, kb, 0);
+        }
+      }
   };
 
   const int sc_a = h ? SCALE_LO : SCALE_HI;
@@ -1107,14 +1135,35 @@ __global__ __launch_bounds__(512) void gemm_fp6_kv_kernel(GemvArgs p, const unsi
     f6_wait_vm<LPB * (P - 1)>();   // block u's activations landed; the P - 1 younger may fly
     if constexpr (AB == 1) {
 #pragma unroll
-      for (int x = 0; x < WJ; ++x) sink ^= (int)(rb_[S][x][0][0] ^ rb_[S][x][1][3]);
-      sink ^= *(const int*)(ring + S * 2 * F6_PIECE + lane * 4);
+      for (int x = 0; x < WJ; ++x) sink ^= (int)(rb_[S][x][0][0] ^ rb_[S][x][1][0]);
+      if constexpr (AD) {   // every load's first dword (a load whose value is unused would be dropped)
+#pragma unroll
+        for (int y = 0; y < 2; ++y)
+#pragma unroll
+          for (int pl = 0; pl < 2 * WP; ++pl) sink ^= (int)ra_[S][y][pl][0];
+      } else {
+        sink ^= *(const int*)(ring + S * 2 * F6_PIECE + lane * 4);
+      }
       issue(u + P, S_);
       return;
     }
     if constexpr (AB >= 2) {
 #pragma unroll
       for (int x = 0; x < WJ; ++x) asm volatile("" : "+v"(rb_[S][x][0]), "+v"(rb_[S][x][1]));
+      if constexpr (AD) {
+#pragma unroll
+        for (int y = 0; y < 2; ++y)
+#pragma unroll
+          for (int pl = 0; pl < 2 * WP; ++pl) asm volatile("" : "+v"(ra_[S][y][pl]));
+      }
+    }
+    if constexpr (AD) {   // this block's weight fragments: landed with its activations
+#pragma unroll
+      for (int y = 0; y < 2; ++y) {
+        wc.d[y] = i32x2{(int)ra_[S][y][1][2], (int)ra_[S][y][1][3]};
+        wc.c[y] = codes(ra_[S][y][0], ra_[S][y][1]);
+        if constexpr (WP == 2) wc.c2[y] = codes(ra_[S][y][2], ra_[S][y][3]);
+      }
     }
     WFrag wn;   // the next block's, read half-way through this one
     // unit n: S = the exact block dots (scale MFMA), P = 2 d_b d_a (f16 MFMA), then acc += S * P.
@@ -1164,8 +1213,8 @@ __global__ __launch_bounds__(512) void gemm_fp6_kv_kernel(GemvArgs p, const unsi
          [&] { if (pend) epi(UPB - 1, rr[(UPB - 1) % 2], 1); });
     unroll<UPB - 1>([&](auto NN) {
       constexpr int n = NN;
-      if constexpr (n == 1) {   // the next block's weights: its DMA pieces landed (the oldest vmem ops
-        // but this block's activation loads are older still -- all landed at the top)
+      if constexpr (n == 1 && !AD) {   // the next block's weights: its DMA pieces landed (the oldest vmem
+        // ops but this block's activation loads are older still -- all landed at the top)
         if constexpr (AB < 2) f6_wait_vm<LPB * (P - 2) + 2 * WJ>();
         wread(SN, wn);
         sb();
@@ -1213,14 +1262,16 @@ __global__ __launch_bounds__(512) void gemm_fp6_kv_kernel(GemvArgs p, const unsi
     // this slot's registers were read by the MFMAs above and its LDS by the ds_reads they waited
     // for: refill it P blocks ahead
     if constexpr (AB < 2) issue(u + P, S_);
-    wc = wn;
+    if constexpr (!AD) wc = wn;
   };
   if (nbw > 0) {
     // whole rounds of the ring without branches (the wait-count pass stays exact), then the
     // remaining nbw % P blocks (a multiple of KB = 2)
     unroll<P>([&](auto K) { issue(K, K); });
-    f6_wait_vm<LPB * (P - 1) + 2 * WJ>();   // block 0's weight pieces
-    wread(0, wc);
+    if constexpr (!AD) {
+      f6_wait_vm<LPB * (P - 1) + 2 * WJ>();   // block 0's weight pieces
+      wread(0, wc);
+    }
     int u0 = 0;
     for (; u0 + P <= nbw; u0 += P) unroll<P>([&](auto K) { block(u0 + K, K); });
     unroll<P - 1>([&](auto K) {
@@ -1434,7 +1485,11 @@ hipError_t launch_fp6_t(const GemvArgs& p, const void* prepA, void* ws, hipStrea
 #endif
   if (plan.sub == 1 && knobs().fp6_av) {   // LAMM_FP6_AV=0: the LDS-staged form below
     constexpr size_t lds = (size_t)4 * 64 * (128 + 8) * 4;   // the epilogue's parked tiles
-    auto kern = gemm_fp6_kv_kernel<T, F6<T>::AFF || F6<T>::WP == 2 ? 2 : 3>;   // more in flight spills
+    // two blocks in flight per wave: config 3 whole launch 27.84-28.12 us against 27.94-28.34 with three
+    // (q4_0; q5_0 28.22 vs 28.39; alternating processes, profiles/r06/kv_p/); the affine formats and
+    // q8_0 spill with three.  LAMM_FP6_KV_P=3: three (A/B, q4_0 / q5_0 only)
+    constexpr bool P3OK = !F6<T>::AFF && F6<T>::WP == 1;
+    auto kern = knobs().fp6_kv_p == 3 && P3OK ? gemm_fp6_kv_kernel<T, P3OK ? 3 : 2> : gemm_fp6_kv_kernel<T, 2>;
     set_max_lds((const void*)kern, (int)lds);
     hipLaunchKernelGGL(kern, dim3((unsigned)plan.grid), dim3(512), lds, s, p, kA, static_cast<const unsigned char*>(wsB));
     return hipGetLastError();

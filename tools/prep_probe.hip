@@ -127,16 +127,35 @@ int main(int argc, char** argv) {
     if (N == 512) {
       constexpr size_t lds = (size_t)4 * 64 * (128 + 8) * 4;
       const int grid = (M / 128) * (N / 64);
-#define KV(NAME, PP, AB)                                                                              \
-  set_max_lds((const void*)gemm_fp6_kv_kernel<kQ4_0, PP, AB>, (int)lds);                              \
+#define KV(NAME, PP, AB, AD)                                                                          \
+  set_max_lds((const void*)gemm_fp6_kv_kernel<kQ4_0, PP, AB, AD>, (int)lds);                          \
   snprintf(n, sizeof n, NAME "_N%d", N);                                                              \
-  run(n, 2.0 * M * N * K / 1e3, [&] { gemm_fp6_kv_kernel<kQ4_0, PP, AB><<<grid, 512, lds, s>>>(p, wA, wsAll); });
-      KV("gemm_kvmain_p3", 3, 0)
-      KV("gemm_kvmain_p2", 2, 0)
-      KV("gemm_kvmain_loadsonly_p3", 3, 1)
-      KV("gemm_kvmain_computeonly_p3", 3, 2)
-      KV("gemm_kvmain_co_halffma_p3", 3, 3)
-      KV("gemm_kvmain_co_1fma_p3", 3, 4)
+  run(n, 2.0 * M * N * K / 1e3, [&] { gemm_fp6_kv_kernel<kQ4_0, PP, AB, AD><<<grid, 512, lds, s>>>(p, wA, wsAll); });
+      KV("gemm_kvmain_p3", 3, 0, 0)
+      KV("gemm_kvmain_p2", 2, 0, 0)
+      KV("gemm_kvmain_ad_p3", 3, 0, 1)
+      KV("gemm_kvmain_ad_p2", 2, 0, 1)
+      KV("gemm_kvmain_ad_p4", 4, 0, 1)
+      KV("gemm_kvmain_loadsonly_p3", 3, 1, 0)
+      KV("gemm_kvmain_ad_loadsonly_p3", 3, 1, 1)
+      KV("gemm_kvmain_computeonly_p3", 3, 2, 0)
+      KV("gemm_kvmain_ad_computeonly_p3", 3, 2, 1)
+      KV("gemm_kvmain_co_halffma_p3", 3, 3, 0)
+      KV("gemm_kvmain_co_1fma_p3", 3, 4, 0)
+      {   // the AD variant's C against the production kernel's, bit for bit
+        std::vector<float> c0((size_t)M * N), c1((size_t)M * N);
+        CK(hipMemset(dC, 0, (size_t)M * N * 4));
+        gemm_fp6_kv_kernel<kQ4_0, 3, 0, 0><<<grid, 512, lds, s>>>(p, wA, wsAll);
+        CK(hipStreamSynchronize(s));
+        CK(hipMemcpy(c0.data(), dC, c0.size() * 4, hipMemcpyDeviceToHost));
+        CK(hipMemset(dC, 0, (size_t)M * N * 4));
+        gemm_fp6_kv_kernel<kQ4_0, 3, 0, 1><<<grid, 512, lds, s>>>(p, wA, wsAll);
+        CK(hipStreamSynchronize(s));
+        CK(hipMemcpy(c1.data(), dC, c1.size() * 4, hipMemcpyDeviceToHost));
+        size_t bad = 0;
+        for (size_t i = 0; i < c0.size(); ++i) bad += memcmp(&c0[i], &c1[i], 4) != 0;
+        printf(", \"ad_vs_production_mismatches\": %zu", bad);
+      }
     }
     CK(hipFree(dA));
     CK(hipFree(wA));

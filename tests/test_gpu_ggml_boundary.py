@@ -448,13 +448,23 @@ def test_boundary_prefill_value_range(t):
     assert rel_err(got[fin], want[fin], absdot[fin]).max() < 1e-3
 
 
-def test_sibling_calls(monkeypatch):
+SIBLING_MODES = {"default": {}, "kernel_signal": {"LAMM_HIP_KERNEL_SIGNAL": "1"},
+                 "watch_coherent": {"LAMM_HIP_C_WATCH": "1"}, "watch_noncoherent": {"LAMM_HIP_C_WATCH": "2"}}
+
+
+@pytest.mark.parametrize("mode", list(SIBLING_MODES))
+def test_sibling_calls(mode, monkeypatch):
     """Sibling decode calls (lamm_hip.cpp Siblings): three weights multiplied by the same src1
     tensor one after another, as llama.cpp's wq / wk / wv, over several tokens.  With the prediction
     on, the first call of each token runs the other two GEMVs ahead and their calls take the kept
     results; every output must be the bits of the prediction-off run.  Token 2 changes src1 between
     the first and second call (the kept result must be discarded), token 3 rewrites the third
-    weight in place (its fingerprint changes: discarded, re-uploaded, recomputed)."""
+    weight in place (its fingerprint changes: discarded, re-uploaded, recomputed).  Over the
+    completion modes: with a C watch no group is formed (the watch sees only the
+    leader's words) and none with the kernel-written completion signal either (lamm_hip.cpp sib_form), so
+    the calls run one by one -- still the same bits."""
+    for k, v in SIBLING_MODES[mode].items():
+        monkeypatch.setenv(k, v)
     M, K, t = 4096, 4096, ol.Q4_0
     rng = np.random.default_rng(77)
     As = [ORACLE.quantize(t, rng.standard_normal((M, K), dtype=np.float32)) for _ in range(3)]
@@ -485,10 +495,15 @@ def test_sibling_calls(monkeypatch):
         on, l_on, t_on = run("1")
     finally:
         monkeypatch.delenv("LAMM_HIP_SIBLINGS", raising=False)
+        for k in SIBLING_MODES[mode]:
+            monkeypatch.delenv(k, raising=False)
         la.boundary_reset()
     assert (l_off, t_off) == (0, 0)
-    assert l_on >= 8 and t_on >= 6, (l_on, t_on)   # tokens 1..5 lead with 2 siblings each; 2 discarded
-    assert t_on < l_on
+    if mode != "default":
+        assert (l_on, t_on) == (0, 0)
+    else:
+        assert l_on >= 8 and t_on >= 6, (l_on, t_on)   # tokens 1..5 lead with 2 siblings each; 2 discarded
+        assert t_on < l_on
     for i, (a, b) in enumerate(zip(off, on)):
         assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), f"call {i}"
     # and against the oracle: the second call of token 2 used x_alt, the third of tokens >= 3 A_new

@@ -358,8 +358,8 @@ def time_direct(ctx, mats, R, Bm, Cm, steps, warmup, flags=0):
     for f0, n0 in ((0, first), (first, steps)):
         n = lib.lamm_steps_direct(ctypes.cast(arr, ctypes.c_void_p), R, ctypes.byref(Bm), ctypes.byref(Cm), f0,
                                   n0, dev, flags, ctypes.byref(wall_us))
-        if n != n0:
-            log("direct dispatch unavailable:", n, la.last_error())
+        if n != n0:   # e.g. config 4's q2_K GEMV: only the flat GEMV kernels have a direct form
+            log(f"direct dispatch not taken ({n} of {n0} calls direct):", la.last_error())
             return None
     flush_caches(torch)
     ctx.barrier()

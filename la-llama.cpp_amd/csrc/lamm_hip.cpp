@@ -166,7 +166,6 @@ struct lamm_weights {
   size_t nba2, nba3;
   void* packed = nullptr;    // fp6 GEMM form of A (q4_0 / q4_1 / q5_0), null otherwise
   size_t packed_bytes = 0;
-  void* packed_i8 = nullptr; // int8 K-group form (LAMM_I8KV, q4_0 / q5_0 / q8_0), null otherwise
 };
 
 namespace {
@@ -362,11 +361,6 @@ int matmul_impl_(const lamm_matrix* A, const lamm_matrix* B, const lamm_matrix* 
       break;
     }
     case kEngFp6: {
-      // the int8 form with no activation prep (LAMM_I8KV): same plan, same bits
-      if (W && W->packed_i8 && !p.b_f32 && gemm_fp6_kv_plan(p) && launch_gemm_i8kv(A->type, p, W->packed_i8, s) == hipSuccess) {
-        e = hipGetLastError();
-        break;
-      }
       const void* prepA = W ? W->packed : nullptr;
       const size_t wsb = gemm_fp6_workspace_bytes(A->type, p, prepA != nullptr);
       void* ws = workspace(wsb, s);
@@ -489,17 +483,6 @@ extern "C" int lamm_hip_weights_create(const lamm_matrix* A, int64_t ne02, int64
       W->packed = nullptr;
       W->packed_bytes = 0;
     }
-    if (knobs().i8kv && gemm_i8kv_supported(A->type) && W->packed) {
-      const size_t nb = gemm_i8kv_weight_bytes(A->type, p);
-      if (hipMalloc(&W->packed_i8, nb) == hipSuccess) {
-        if (prepare_i8kv_weights(A->type, p, W->packed_i8, static_cast<hipStream_t>(hip_stream)) == hipSuccess) {
-          W->packed_bytes += nb;
-        } else {
-          (void)hipFree(W->packed_i8);
-          W->packed_i8 = nullptr;
-        }
-      }
-    }
   }
   *out = W;
   return LAMM_OK;
@@ -521,10 +504,9 @@ extern "C" size_t lamm_hip_weights_bytes(const lamm_weights* W) { return W ? W->
 
 extern "C" void lamm_hip_weights_destroy(lamm_weights* W) {
   if (!W) return;
-  if (W->packed || W->packed_i8) {
-    (void)hipDeviceSynchronize();   // no launch may still read the packed forms
-    if (W->packed) (void)hipFree(W->packed);
-    if (W->packed_i8) (void)hipFree(W->packed_i8);
+  if (W->packed) {
+    (void)hipDeviceSynchronize();   // no launch may still read the packed form
+    (void)hipFree(W->packed);
   }
   delete W;
 }

@@ -115,12 +115,6 @@ bool gemm_fp6_supported(int type);   // q4_0 / q4_1 / q5_0 / q5_1 / q8_0 (q5_1, 
 // the call runs on the 128 x 64 K-group plan (gemm_fp6_kv_kernel) -- the only one q8_0's two weight
 // code planes have
 bool gemm_fp6_kv_plan(const GemvArgs& p);
-// the same K-group plan with the block dots on the int8 MFMA and ggml's q8_0 activation rows read as
-// stored -- no activation prep launch (lamm_gemm_i8kv.hip; q4_0 / q5_0 / q8_0, prepared weights only)
-bool gemm_i8kv_supported(int type);
-size_t gemm_i8kv_weight_bytes(int type, const GemvArgs& p);
-hipError_t prepare_i8kv_weights(int type, const GemvArgs& p, void* ws, hipStream_t s);
-hipError_t launch_gemm_i8kv(int type, const GemvArgs& p, const void* prepA, hipStream_t s);
 int gemm_fp6_tiles(const GemvArgs& p);   // 256x128 output tiles of the fp6 GEMM (before K-splits)
 int gemm_fp6_grid(const GemvArgs& p);    // its main-kernel workgroups (tiles x K-splits)
 

@@ -18,8 +18,6 @@ struct Knobs {
   int fp6_sub = -1;            // LAMM_FP6_SUB: 0 split-K plan, 1 4-group K-group plan, 2 2-group plan
   bool fp6_fused_reduce = false;   // LAMM_FP6_FUSED_REDUCE=1: split-K partials summed in-launch
   int fp6_wj = 2;              // LAMM_FP6_WJ=1: 16 waves of 32x64 on the 256x128 plan
-  bool i8kv = false;           // LAMM_I8KV=1: prepared q4_0 / q5_0 / q8_0 weights on the K-group plan run the
-                               // int8 form with no activation prep (lamm_gemm_i8kv.hip)
   int fp6_kv_p = 0;            // LAMM_FP6_KV_P=3: three blocks in flight per wave of gemm_fp6_kv_kernel
                                // (A/B, q4_0 / q5_0; default two)
   bool fp6_av = true;          // LAMM_FP6_AV=0: the K-group plan's barrier-staged LDS form instead

@@ -280,7 +280,6 @@ constexpr int KQC_A = 35840;    // 35 KiB: 32768 + 256 + 256 + 2048 (+ pad)
 constexpr int KQC_B = 37888;    // 37 KiB: 32768 + 512 + 4096 (+ pad)
 constexpr int KQ_PIECES = (KQC_A + KQC_B) / 1024;   // 72 LDS-DMA pieces per step
 constexpr int KQ_PA = KQC_A / 1024;
-constexpr int KQ_PPW = KQ_PIECES / 4;               // per wave (4 waves)
 static_assert(KQ_PIECES % 4 == 0, "pieces split evenly over the 4 waves");
 
 struct KQLayout {
@@ -481,11 +480,16 @@ __global__ __launch_bounds__(KQ_T) void gemm_kq_kernel(GemvArgs p, const unsigne
   const auto rb = make_rsrc(gb, (uint32_t)((int64_t)L.nsb * KQC_B));
   const int nsb = L.nsb;
 
+  // q2_K (no hi plane: q * sc <= 45 fits int8) skips the A chunk's hi-plane pieces 16..31 -- 56 instead
+  // of 72 KiB per step
+  constexpr int SKIP = KQ<T>::HI ? 0 : 16, PPW = (KQ_PIECES - SKIP) / 4;
+  static_assert((KQ_PIECES - SKIP) % 4 == 0, "pieces split evenly over the 4 waves");
   auto issue = [&](int sb) {
     unsigned char* dst = smem + (sb & 1) * (KQC_A + KQC_B);
 #pragma unroll
-    for (int k = 0; k < KQ_PPW; ++k) {
-      const int pc = k * 4 + w;   // wave-uniform
+    for (int k = 0; k < PPW; ++k) {
+      const int pc0 = k * 4 + w;   // wave-uniform
+      const int pc = pc0 < 16 ? pc0 : pc0 + SKIP;
       if (pc < KQ_PA)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (__attribute__((address_space(3))) void*)(dst + pc * 1024), 16,
                                                  (uint32_t)(sb * KQC_A + pc * 1024 + lane * 16), 0, 0, 0);
@@ -506,7 +510,7 @@ __global__ __launch_bounds__(KQ_T) void gemm_kq_kernel(GemvArgs p, const unsigne
   if (k1 - k0 > 1) issue(k0 + 1);
   const int ia = 32 * wi + lr;
   for (int sb = k0; sb < k1; ++sb) {
-    if (sb + 1 < k1) kq_wait_vm<KQ_PPW>(); else kq_wait_vm<0>();
+    if (sb + 1 < k1) kq_wait_vm<PPW>(); else kq_wait_vm<0>();
     kq_barrier();   // step sb's chunks visible to every wave
     const unsigned char* sA = smem + (sb & 1) * (KQC_A + KQC_B);
     const unsigned char* sB = sA + KQC_A;

@@ -206,6 +206,72 @@ __global__ __launch_bounds__(DG_NT) void gemm_dense_kernel(GemvArgs p, int nspli
     }
 }
 
+// Small F32 GEMMs (BASELINE config 1: 512^3 is 16 of the 128 x 128 tiles above, which needed split-K
+// partials and a reduce launch, 18.3 us): one 32 x 32 output tile per 256-thread workgroup -- 256
+// workgroups for 512^3 -- whose 4 waves take a quarter of K each (K-groups), every operand straight
+// from HBM / L2 into VGPRs (lane (r, h) takes row r's elements [128 c + 64 h, + 64) of chunk c: 16
+// b128 loads per operand, no LDS staging), one v_mfma_f32_32x32x2_f32 chain per wave, and the four
+// partial tiles summed through LDS in group order before one store per output.  No partials in HBM,
+// no second launch.  K % 4 == 0 (whole 16-byte pieces; the tail past K is zeroed per piece).
+constexpr int SF_CH = 128;   // floats of K per chunk (lane half h: 64 of them)
+
+__global__ __launch_bounds__(256) void gemm_f32_small_kernel(GemvArgs p) {
+  __shared__ float red[4][32][33];
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int lr = lane & 31, h = lane >> 5;
+  const int nit = (p.M + 31) / 32, njt = (p.N + 31) / 32;
+  const int per = nit * njt, z = blockIdx.x / per, r = blockIdx.x % per;
+  const int it = r % nit, jt = r / nit;
+  const int i12 = z % p.ne12, i13 = z / p.ne12;
+  const unsigned char* Az = p.A + (int64_t)(i12 / p.r2) * p.sa2 + (int64_t)(i13 / p.r3) * p.sa3;
+  const unsigned char* Bz = p.B + (int64_t)i12 * p.sb2 + (int64_t)i13 * p.sb3;
+  float* Cz = p.C + (int64_t)i12 * p.sc2 + (int64_t)i13 * p.sc3;
+  const int K = p.K, i0 = it * 32, j0 = jt * 32;
+  const int mrows = min(32, p.M - i0), ncols = min(32, p.N - j0);
+  const int64_t abytes = (int64_t)(mrows - 1) * p.lda + (int64_t)K * 4;
+  const int64_t bbytes = (int64_t)(ncols - 1) * p.ldb + (int64_t)K * 4;
+  const auto ra = make_rsrc(Az + (int64_t)i0 * p.lda, (uint32_t)min(abytes, (int64_t)0x7fffffff));
+  const auto rb = make_rsrc(Bz + (int64_t)j0 * p.ldb, (uint32_t)min(bbytes, (int64_t)0x7fffffff));
+  const int nch = (K + SF_CH - 1) / SF_CH, c0 = w * nch / 4, c1 = (w + 1) * nch / 4;
+  f32x16 acc = {};
+  for (int c = c0; c < c1; ++c) {
+    u32x4 a[16], b[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int e = c * SF_CH + 64 * h + 4 * q;   // the piece's first element
+      const bool in = e < K;                       // K % 4 == 0: a piece is all in or all out
+      a[q] = __builtin_amdgcn_raw_buffer_load_b128(
+          ra, in && lr < mrows ? (uint32_t)(lr * p.lda + 4 * e) : 0x7ffffff0u, 0, 0);
+      b[q] = __builtin_amdgcn_raw_buffer_load_b128(
+          rb, in && lr < ncols ? (uint32_t)(lr * p.ldb + 4 * e) : 0x7ffffff0u, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q)
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(__uint_as_float(b[q][k]), __uint_as_float(a[q][k]), acc, 0, 0, 0);
+  }
+  // D layout (srcA = activation rows j, srcB = weight rows i): lane -> i = lr, e -> j = (e & 3) + 8 (e >> 2) + 4 h
+#pragma unroll
+  for (int e = 0; e < 16; ++e) red[w][(e & 3) + 8 * (e >> 2) + 4 * h][lr] = acc[e];
+  __syncthreads();
+  const int jl = t >> 3, il = 4 * (t & 7);   // 4 consecutive outputs of row jl per thread
+  float v[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) v[k] = ((red[0][jl][il + k] + red[1][jl][il + k]) + red[2][jl][il + k]) + red[3][jl][il + k];
+  if (jl < ncols) {
+    float* o = Cz + (int64_t)(j0 + jl) * p.ldc + i0 + il;
+    if (il + 3 < mrows && ((uintptr_t)o & 15) == 0) {
+      *reinterpret_cast<f32x4*>(o) = f32x4{v[0], v[1], v[2], v[3]};
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (il + k < mrows) o[k] = v[k];
+    }
+  }
+}
+
 // K-splits: double until the grid covers 256 CUs, keeping >= 4 K-steps per split
 // (LAMM_DENSE_SPLIT=n forces n)
 int dg_nsplit(const GemvArgs& p, int eb) {
@@ -221,8 +287,22 @@ int dg_nsplit(const GemvArgs& p, int eb) {
   return n < 1 ? 1 : (n > nsteps ? (nsteps < 1 ? 1 : nsteps) : n);
 }
 
+// the small-tile F32 form: grids the 128 x 128 tiles would split (fewer than 64 of them), K % 4 == 0
+bool f32_small(const GemvArgs& p) {
+  const int64_t tiles = (int64_t)((p.M + DG_T - 1) / DG_T) * ((p.N + DG_T - 1) / DG_T) * p.ne12 * p.ne13;
+  const int64_t small = (int64_t)((p.M + 31) / 32) * ((p.N + 31) / 32) * p.ne12 * p.ne13;
+  return knobs().dense_split <= 0 && tiles < 64 && p.K % 4 == 0 && small <= 4096 && (p.lda & 15) == 0 &&
+         (p.ldb & 15) == 0 && ((uintptr_t)p.A & 15) == 0 && ((uintptr_t)p.B & 15) == 0 && (p.sa2 & 15) == 0 &&
+         (p.sa3 & 15) == 0 && (p.sb2 & 15) == 0 && (p.sb3 & 15) == 0;
+}
+
 template <int T, bool BAL>
 hipError_t launch_dg(const GemvArgs& p, void* ws, hipStream_t s) {
+  if (T == kF32 && f32_small(p)) {
+    const int64_t nwg = (int64_t)((p.M + 31) / 32) * ((p.N + 31) / 32) * p.ne12 * p.ne13;
+    hipLaunchKernelGGL(gemm_f32_small_kernel, dim3((unsigned)nwg), dim3(256), 0, s, p);
+    return hipGetLastError();
+  }
   const int nit = (p.M + DG_T - 1) / DG_T, njt = (p.N + DG_T - 1) / DG_T;
   const int nsplit = dg_nsplit(p, DenseG<T>::EB);
   const int64_t nwg = (int64_t)nit * njt * p.ne12 * p.ne13 * nsplit;
@@ -240,6 +320,7 @@ hipError_t launch_dg(const GemvArgs& p, void* ws, hipStream_t s) {
 bool gemm_dense_supported(int type) { return type == kF32 || type == kF16; }
 
 size_t gemm_dense_workspace_bytes(int type, const GemvArgs& p) {
+  if (type == kF32 && f32_small(p)) return 0;
   const int n = dg_nsplit(p, type == kF32 ? 4 : 2);
   return n > 1 ? (size_t)n * p.ne12 * p.ne13 * (size_t)p.N * p.M * sizeof(float) + 256 : 0;
 }

@@ -458,11 +458,7 @@ __device__ __forceinline__ void kq_barrier() {
   asm volatile("" ::: "memory");
 }
 
-// RAWB (round 6, the default): the B chunk is DMA'd straight from ggml's q8_K rows (292-byte blocks,
-// dword aligned) into the same LDS image prep_b_kq would have written -- the quants' 16-byte slots
-// by source addresses that apply the swizzle, d_b by 4-byte pieces, the 16 int16 bsums raw (made
-// fp16 at their read) -- so the prep launch goes away.  Same image, same arithmetic, same bits.
-template <int T, bool RAWB>
+template <int T>
 __global__ __launch_bounds__(KQ_T) void gemm_kq_kernel(GemvArgs p, const unsigned char* wsA,
                                                        const unsigned char* wsB, int nsplit, float* part) {
   constexpr bool MIN = KQ<T>::MIN;
@@ -483,44 +479,16 @@ __global__ __launch_bounds__(KQ_T) void gemm_kq_kernel(GemvArgs p, const unsigne
   const auto ra = make_rsrc(ga, (uint32_t)((int64_t)L.nsb * KQC_A));
   const auto rb = make_rsrc(gb, (uint32_t)((int64_t)L.nsb * KQC_B));
   const int nsb = L.nsb;
-  // RAWB: the tile's q8_K rows from row j0 (wave-uniform base); rows past N read as zeros
-  const int64_t j0 = (int64_t)jt * KQ_TJ;
-  const int64_t ncols = min((int64_t)KQ_TJ, (int64_t)p.N - j0);
-  const unsigned char* Bz = p.B + (int64_t)i12 * p.sb2 + (int64_t)i13 * p.sb3 + j0 * p.ldb;
-  const auto rr_ = make_rsrc(Bz, RAWB ? (uint32_t)min((ncols - 1) * p.ldb + (int64_t)nsb * 292, (int64_t)0x7fffffff) : 0u);
 
   // q2_K (no hi plane: q * sc <= 45 fits int8) skips the A chunk's hi-plane pieces 16..31 -- 56 instead
   // of 72 KiB per step
-  constexpr int SKIP = KQ<T>::HI ? 0 : 16;
-  // RAWB: the A pieces, then 32 quant pieces, 2 d pieces, 4 bsums pieces; padded to a multiple of the 4
-  // waves by re-issuing the last piece (every wave then counts the same vmem ops per step)
-  constexpr int NA = KQ_PA - SKIP, NPC = RAWB ? NA + 38 : KQ_PIECES - SKIP, PPW = (NPC + 3) / 4;
-  static_assert(RAWB || NPC % 4 == 0, "pieces split evenly over the 4 waves");
+  constexpr int SKIP = KQ<T>::HI ? 0 : 16, PPW = (KQ_PIECES - SKIP) / 4;
+  static_assert((KQ_PIECES - SKIP) % 4 == 0, "pieces split evenly over the 4 waves");
   auto issue = [&](int sb) {
     unsigned char* dst = smem + (sb & 1) * (KQC_A + KQC_B);
 #pragma unroll
     for (int k = 0; k < PPW; ++k) {
-      const int pcr = min(k * 4 + w, NPC - 1);   // wave-uniform
-      if (RAWB && pcr >= NA) {
-        unsigned char* bdst = dst + KQC_A;
-        const int q = pcr - NA;
-        const uint32_t blk = (uint32_t)sb * 292u;
-        if (q < 32) {   // quants: LDS row r = 4 q + lane / 16, position lane % 16 holds slot (lane % 16) ^ (r & 15)
-          const int r = 4 * q + (lane >> 4), c = (lane & 15) ^ (r & 15);
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(rr_, (__attribute__((address_space(3))) void*)(bdst + q * 1024), 16,
-                                                   (uint32_t)(r * p.ldb) + blk + 4u + 16u * c, 0, 0, 0);
-        } else if (q < 34) {   // d_b (f32) of rows 64 (q - 32) + lane
-          const int r = 64 * (q - 32) + lane;
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(rr_, (__attribute__((address_space(3))) void*)(bdst + 32768 + (q - 32) * 256),
-                                                   4, (uint32_t)(r * p.ldb) + blk, 0, 0, 0);
-        } else {   // bsums (16 x int16): row 32 (q - 34) + lane / 2, half lane % 2
-          const int r = 32 * (q - 34) + (lane >> 1);
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(rr_, (__attribute__((address_space(3))) void*)(bdst + 33280 + (q - 34) * 1024),
-                                                   16, (uint32_t)(r * p.ldb) + blk + 260u + 16u * (lane & 1), 0, 0, 0);
-        }
-        continue;
-      }
-      const int pc0 = pcr;
+      const int pc0 = k * 4 + w;   // wave-uniform
       const int pc = pc0 < 16 ? pc0 : pc0 + SKIP;
       if (pc < KQ_PA)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (__attribute__((address_space(3))) void*)(dst + pc * 1024), 16,
@@ -574,14 +542,7 @@ __global__ __launch_bounds__(KQ_T) void gemm_kq_kernel(GemvArgs p, const unsigne
       const int jb = 64 * wj + 32 * rt;
       f32x16 mins = {};
       if constexpr (MIN) {
-        half8 bsf;
-        if constexpr (RAWB) {   // the raw int16 bsums, exact in fp16 (|bsum| <= 16 x 128)
-          const i32x4 raw = *(const i32x4*)(sB + 33280 + 32 * (jb + lr) + 16 * h);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) bsf[e] = (_Float16)(int16_t)((uint32_t)raw[e >> 1] >> (16 * (e & 1)));
-        } else {
-          bsf = *(const half8*)(sB + 33280 + 32 * (jb + lr) + 16 * h);
-        }
+        const half8 bsf = *(const half8*)(sB + 33280 + 32 * (jb + lr) + 16 * h);
         mins = __builtin_amdgcn_mfma_f32_32x32x16_f16(bsf, mnf, mins, 0, 0, 0);
       }
 #pragma unroll
@@ -650,19 +611,15 @@ hipError_t launch_kq(const GemvArgs& p, const void* prepA, void* ws, hipStream_t
   unsigned char* wsA = prepA ? nullptr : w;
   unsigned char* wsB = w + (prepA ? 0 : L.a_bytes);
   if (!prepA) launch_prep_w_kq<T>(p, wsA, s);
-  const bool rawb = knobs().kq_rawb;   // LAMM_KQ_RAWB=0: the prep_b_kq launch (A/B)
-  if (!rawb) {
-    const int64_t nb = (int64_t)L.njt * KQ_TJ * L.nsb * 18;
-    hipLaunchKernelGGL(prep_b_kq, dim3((unsigned)((nb + 255) / 256), (unsigned)(p.ne12 * p.ne13)), dim3(256), 0, s, p,
-                       wsB);
-  }
+  const int64_t nb = (int64_t)L.njt * KQ_TJ * L.nsb * 18;
+  hipLaunchKernelGGL(prep_b_kq, dim3((unsigned)((nb + 255) / 256), (unsigned)(p.ne12 * p.ne13)), dim3(256), 0, s, p,
+                     wsB);
   constexpr size_t lds = 2 * (KQC_A + KQC_B);
   static_assert(lds <= 160 * 1024, "LDS");
-  auto kern = rawb ? gemm_kq_kernel<T, true> : gemm_kq_kernel<T, false>;
-  set_max_lds((const void*)kern, (int)lds);
+  set_max_lds((const void*)gemm_kq_kernel<T>, (int)lds);
   const int nsplit = kq_nsplit(p);
   float* part = reinterpret_cast<float*>(w + kq_part_offset(p, prepA != nullptr));
-  hipLaunchKernelGGL(kern, dim3((unsigned)L.nit, (unsigned)L.njt, (unsigned)(p.ne12 * p.ne13 * nsplit)),
+  hipLaunchKernelGGL(gemm_kq_kernel<T>, dim3((unsigned)L.nit, (unsigned)L.njt, (unsigned)(p.ne12 * p.ne13 * nsplit)),
                      dim3(KQ_T), lds, s, p, prepA ? static_cast<const unsigned char*>(prepA) : wsA,
                      static_cast<const unsigned char*>(wsB), nsplit, part);
   if (nsplit > 1) launch_splitk_reduce(p, nsplit, part, s);

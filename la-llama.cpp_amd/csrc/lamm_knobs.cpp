@@ -39,7 +39,6 @@ Knobs* read_env() {
   k->fp6_wj = env_int("LAMM_FP6_WJ", 2);
   k->fp6_av = !env_off("LAMM_FP6_AV");
   k->fp6_kv_p = env_int("LAMM_FP6_KV_P", 0);
-  k->kq_rawb = !env_off("LAMM_KQ_RAWB");
   k->i8_split = env_int("LAMM_I8_SPLIT", 0);
   k->dense_split = env_int("LAMM_DENSE_SPLIT", 0);
   k->kq_split = env_int("LAMM_KQ_SPLIT", 0);

@@ -25,8 +25,6 @@ struct Knobs {
   int dense_split = 0;         // LAMM_DENSE_SPLIT=n
   int kq_split = 0;            // LAMM_KQ_SPLIT=n
   int kq_variant = 0;          // LAMM_KQ_VARIANT=1: single-pass super-block kernel
-  bool kq_rawb = true;         // LAMM_KQ_RAWB=0: the super-block GEMM's q8_K rows through the prep_b_kq launch
-                               // instead of DMA'd raw into its LDS image
   int gemv_variant = 0;        // LAMM_GEMV_VARIANT: 7 segmented, 8 DMA 4x4, 10 VGPR stream, 12 flat, 13 staged seg
   int gemv_rpw = -1;           // LAMM_GEMV_RPW: 0 off, 4 / 8 / 16 waves forced
   bool gemv_laneb = false;     // LAMM_GEMV_LANEB=1: per-lane activation blocks in the row-per-wave GEMV

@@ -987,7 +987,9 @@ __global__ __launch_bounds__((F6Waves<WJ, SI, SJ, KG>::NT)) void gemm_fp6_kernel
 // P blocks in flight per wave.  A fragment's six code dwords and its {d, m / s} pair are separate
 // operands (scale MFMA / f16 MFMA), assembled from the two 16-byte planes at use.
 // AB (ablations, tools/prep_probe.hip only): 1 loads only; 2 compute only (no loads after the first
-// P blocks); 3 compute only with half the FMAs; 4 compute only, one FMA per unit.
+// P blocks); 3 compute only with half the FMAs; 4 compute only, one FMA per unit; 5 / 6 / 7 the
+// production loop without the activations' / the weights' / both second 16-byte planes (the
+// operand bytes' share of the time; the results are not meaningful).
 // AD (probe): the weight fragments by buffer loads straight into VGPRs (both half-waves load the same
 // rows; the L1 merges the duplicate addresses) instead of the LDS-DMA ring.
 template <int T, int P, int AB = 0, int AD = 0>
@@ -999,7 +1001,10 @@ __global__ __launch_bounds__(512) void gemm_fp6_kv_kernel(GemvArgs p, const unsi
   constexpr int KG = 4, TI = 128, TJ = 64, NW = 8, WJ = 2, UPB = 2 * WJ;
   // vmem ops per block: 2 weight DMA pieces per plane (AD: 2 sub-tiles x 2 loads per plane), WJ x 2
   // activation loads
-  constexpr int LPB = (AD ? 4 * WP : 2 * WP) + 2 * WJ;
+  constexpr bool CO = AB >= 2 && AB <= 4;            // compute-only ablations
+  constexpr bool SKA = AB == 5 || AB == 7, SKW = AB == 6 || AB == 7;
+  constexpr int APB = (SKA ? 1 : 2) * WJ;             // activation loads per block
+  constexpr int LPB = (AD ? 4 * WP : (SKW ? 1 : 2) * WP) + APB;
   constexpr int RING = P * 2 * WP * F6_PIECE;   // bytes of a wave's weight ring
   constexpr int ABY = WP * F6_A_BYTES;          // bytes of a K-step's A chunk
   static_assert(P >= 2 && P <= 6, "blocks in flight");
@@ -1037,6 +1042,9 @@ __global__ __launch_bounds__(512) void gemm_fp6_kv_kernel(GemvArgs p, const unsi
   unsigned char* ring = smem + w * RING;
 
   u32x4 rb_[P][WJ][2];   // activation ring: sub-tile x, plane
+  if constexpr (SKA)
+    for (int s_ = 0; s_ < P; ++s_)
+      for (int x = 0; x < WJ; ++x) rb_[s_][x][1] = u32x4{0u, 0u, 0u, 0u};
   u32x4 ra_[AD ? P : 1][2][2 * WP];   // AD: weight fragments: sub-tile y, (code plane, 16-byte plane)
   const uint32_t arow = (uint32_t)(ri0 + 64 * wi + lr) * 16;   // AD: the lane's weight row
   // block u of this wave (K-step g + KG (u / KB), block u % KB) into ring slot S; past the end the
@@ -1063,6 +1071,7 @@ __global__ __launch_bounds__(512) void gemm_fp6_kv_kernel(GemvArgs p, const unsi
     } else {
 #pragma unroll
       for (int pl = 0; pl < 2 * WP; ++pl) {   // (code plane pl / 2) x (16-byte plane pl % 2)
+        if (SKW && pl % 2 == 1) continue;
         auto* d = (__attribute__((address_space(3))) void*)(ring + (S * 2 * WP + pl) * F6_PIECE);
         __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, d, 16, lane * 16,
                                                  ka + (pl / 2) * F6_A_BYTES + a0 + ((pl % 2) * F6_KB + b) * F6_TI * 16, 0, 0);
@@ -1072,6 +1081,7 @@ __global__ __launch_bounds__(512) void gemm_fp6_kv_kernel(GemvArgs p, const unsi
     for (int x = 0; x < WJ; ++x)
 #pragma unroll
       for (int pl = 0; pl < 2; ++pl) {
+        if (SKA && pl == 1) continue;
         const uint32_t o = b0 + (uint32_t)((((pl * F6_KB + b) * 2) * F6_TJ + 32 * x) * 16);
         if (AD && pl == 1 && F::VBPB != 36) {   // q8_0 activations: no s, the plane's last dword is 0
           const auto v = __builtin_amdgcn_raw_buffer_load_b96(rb, o, kb, 0);
@@ -1147,7 +1157,7 @@ __global__ __launch_bounds__(512) void gemm_fp6_kv_kernel(GemvArgs p, const unsi
       issue(u + P, S_);
       return;
     }
-    if constexpr (AB >= 2) {
+    if constexpr (CO || SKA) {
 #pragma unroll
       for (int x = 0; x < WJ; ++x) asm volatile("" : "+v"(rb_[S][x][0]), "+v"(rb_[S][x][1]));
       if constexpr (AD) {
@@ -1215,7 +1225,7 @@ __global__ __launch_bounds__(512) void gemm_fp6_kv_kernel(GemvArgs p, const unsi
       constexpr int n = NN;
       if constexpr (n == 1 && !AD) {   // the next block's weights: its DMA pieces landed (the oldest vmem
         // ops but this block's activation loads are older still -- all landed at the top)
-        if constexpr (AB < 2) f6_wait_vm<LPB * (P - 2) + 2 * WJ>();
+        if constexpr (!CO) f6_wait_vm<LPB * (P - 2) + APB>();
         wread(SN, wn);
         sb();
       }
@@ -1261,7 +1271,7 @@ __global__ __launch_bounds__(512) void gemm_fp6_kv_kernel(GemvArgs p, const unsi
     sb();
     // this slot's registers were read by the MFMAs above and its LDS by the ds_reads they waited
     // for: refill it P blocks ahead
-    if constexpr (AB < 2) issue(u + P, S_);
+    if constexpr (!CO) issue(u + P, S_);
     if constexpr (!AD) wc = wn;
   };
   if (nbw > 0) {
@@ -1269,7 +1279,7 @@ __global__ __launch_bounds__(512) void gemm_fp6_kv_kernel(GemvArgs p, const unsi
     // remaining nbw % P blocks (a multiple of KB = 2)
     unroll<P>([&](auto K) { issue(K, K); });
     if constexpr (!AD) {
-      f6_wait_vm<LPB * (P - 1) + 2 * WJ>();   // block 0's weight pieces
+      f6_wait_vm<LPB * (P - 1) + APB>();   // block 0's weight pieces
       wread(0, wc);
     }
     int u0 = 0;

@@ -142,6 +142,10 @@ int main(int argc, char** argv) {
       KV("gemm_kvmain_ad_computeonly_p3", 3, 2, 1)
       KV("gemm_kvmain_co_halffma_p3", 3, 3, 0)
       KV("gemm_kvmain_co_1fma_p3", 3, 4, 0)
+      KV("gemm_kvmain_noactp1_p2", 2, 5, 0)
+      KV("gemm_kvmain_nowp1_p2", 2, 6, 0)
+      KV("gemm_kvmain_nop1_p2", 2, 7, 0)
+      KV("gemm_kvmain_p2_again", 2, 0, 0)
       {   // the AD variant's C against the production kernel's, bit for bit
         std::vector<float> c0((size_t)M * N), c1((size_t)M * N);
         CK(hipMemset(dC, 0, (size_t)M * N * 4));

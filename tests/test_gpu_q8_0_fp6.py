@@ -99,3 +99,24 @@ def test_q8_0_fp6_value_range():
     rows = np.random.default_rng(0).choice(M, 256, replace=False)
     err, _ = check(c, A_q, B_q, M, N, K, rows)
     assert err < TOL
+
+
+RAGGED = [(4000, 500, 4160), (4032, 456, 4128)]
+
+
+@pytest.mark.parametrize("shape", RAGGED, ids=[f"{m}x{n}x{k}" for m, n, k in RAGGED])
+def test_q8_0_fp6_ragged_vs_oracle(shape):
+    """Shapes off every tile edge on the same exact engine: rows past the last 128-row tile, columns
+    past the last 64-column tile and an odd number of blocks (a K-step of one block at the end, the
+    two weight code planes' last chunk half empty) -- every row the oracle checks, nothing written
+    past C."""
+    M, N, K = shape
+    assert la.gemm_engine(T, M, N, K, 1, stationary=True) == "fp6"
+    rng = np.random.default_rng(M * 7 + N + K)
+    A_q = ORACLE.quantize(T, rng.standard_normal((M, K), dtype=np.float32))
+    B_q = ORACLE.quantize(T, rng.standard_normal((N, K), dtype=np.float32), ol.QUANT_AVX)
+    c, _ = stationary(A_q, B_q, M, N, K)
+    rows = np.unique(np.r_[np.arange(0, M, 7), np.arange(M - 40, M)])
+    err, _ = check(c, A_q, B_q, M, N, K, rows)
+    print(f"q8_0 fp6 ragged {M}x{N}x{K}: max rel err {err:.2e}")
+    assert err < TOL

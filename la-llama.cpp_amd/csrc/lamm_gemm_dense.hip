@@ -318,6 +318,10 @@ hipError_t launch_dg(const GemvArgs& p, void* ws, hipStream_t s) {
 }  // namespace
 
 bool gemm_dense_supported(int type) { return type == kF32 || type == kF16; }
+// a 128-row tile's bytes addressable by the kernels' 32-bit buffer offsets (other calls: grouped GEMV)
+bool gemm_dense_args_ok(const GemvArgs& p) {
+  return (int64_t)DG_T * p.lda < 0x7fffffff && (int64_t)DG_T * p.ldb < 0x7fffffff;
+}
 
 size_t gemm_dense_workspace_bytes(int type, const GemvArgs& p) {
   if (type == kF32 && f32_small(p)) return 0;

@@ -220,7 +220,7 @@ bool use_dq(int type, const GemvArgs& p, bool stationary) {
 }
 Engine pick_engine(int type, const GemvArgs& p, bool stationary, bool b_al4) {
   if (p.N <= gemv_max_n(type) || (p.b_f32 && p.N <= 8)) return kEngGemv;
-  if (gemm_dense_supported(type) && knobs().dense_gemm) return kEngDense;
+  if (gemm_dense_supported(type) && knobs().dense_gemm && gemm_dense_args_ok(p)) return kEngDense;
   if (gemm_kq_supported(type) && knobs().kq_gemm && b_al4) return kEngKq;
   if (use_dq(type, p, stationary)) return kEngDq;
   if (gemm_fp6_supported(type) && (type != kQ5_1 || stationary) && gemm_path(p, stationary) == 0 &&

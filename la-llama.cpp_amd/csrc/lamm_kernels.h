@@ -58,6 +58,7 @@ hipError_t prepare_kq_weights(int type, const GemvArgs& p, void* wsA, hipStream_
 hipError_t launch_gemm_dense(int type, const GemvArgs& p, void* workspace, hipStream_t s);
 size_t gemm_dense_workspace_bytes(int type, const GemvArgs& p);
 bool gemm_dense_supported(int type);
+bool gemm_dense_args_ok(const GemvArgs& p);   // strides the 32-bit tile offsets reach
 
 // C (slice z, row j, col i) = sum_{s < nsplit} part[s][z][j][i] in split order (deterministic)
 void launch_splitk_reduce(const GemvArgs& p, int nsplit, const float* part, hipStream_t s);

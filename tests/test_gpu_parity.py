@@ -624,6 +624,30 @@ def test_dense_gemm_vs_oracle(t, shape, bal):
 
 
 @pytest.mark.parametrize("t", [ol.F32, ol.F16], ids=["f32", "f16"])
+def test_dense_huge_row_pitch(t):
+    """F32 / F16 prefill-sized call whose weight rows lie 2^24 + 64 bytes apart (a ggml view into a
+    large tensor): 128 such rows are past the tiled GEMM's 32-bit buffer offsets, so the call runs on
+    the grouped GEMV, which rebases per row -- within the bar, every row."""
+    M, N, K = 9, 16, 256
+    eb = la.type_size(t)
+    lda = ((1 << 24) + 64) // eb
+    rng = np.random.default_rng(3)
+    A_q = ORACLE.quantize(t, rng.standard_normal((M, K), dtype=np.float32))
+    B_q = ORACLE.quantize(t, rng.standard_normal((N, K), dtype=np.float32))
+    A = torch.zeros(M * lda * eb + 64, dtype=torch.uint8, device="cuda")
+    A[:M * lda * eb].view(M, lda * eb)[:, :K * eb] = \
+        torch.from_numpy(np.ascontiguousarray(A_q).view(np.uint8).reshape(M, K * eb).copy()).cuda()
+    B = dev_bytes(B_q)
+    C = torch.full((N * M + 16,), float("nan"), dtype=torch.float32, device="cuda")
+    la.mul_mat_torch(t, A, B, C, M, N, K, lda=lda)
+    torch.cuda.synchronize()
+    c = C.cpu().numpy()
+    assert np.isnan(c[N * M:]).all()
+    ref = ORACLE.mul_mat(t, M, N, K, A_q, B_q)
+    assert rel_err(c[:N * M].reshape(N, M), ref, absdot(t, A_q, B_q, M, N, K)).max() < TOL
+
+
+@pytest.mark.parametrize("t", [ol.F32, ol.F16], ids=["f32", "f16"])
 def test_dense_gemm_batched_broadcast(t):
     """ggml batch dims on the dense GEMM: 2 weight slices broadcast over 2x3 activation slices
     (r2 = 1, r3 = 3 -- the GQA-style sharing of a KV-cache slice by several query heads)."""
